@@ -1,0 +1,130 @@
+// Pool (sparse down/up-sample) SpMM and the mini-batch feature swap, gfx950.
+//
+// Reference: Pool (model.py:50-55) = index_select(x, 1, col) * value, then
+// torch_scatter.scatter_add(.., row, dim_size=M).  Here: row-sorted CSR whose
+// per-row entry order is the COO file order, so each output is the same
+// sequence of fp32 mul/add roundings as the reference's sequential
+// scatter_add (multiply and add are issued un-fused on purpose).
+//
+// SwapFeatures (swap_batch_transform.py:13-52): bs base meshes -> bs^2 meshes,
+// out[i*bs + j] = mesh i with the swapped region's feature vertices from j.
+#include "cfsd_common.h"
+
+namespace cfsd {
+
+// One thread per (b, r, 4-channel chunk).  Consecutive threads walk the
+// channel chunks of one row, so a row of C fp32 is read/written as C/4
+// 16-B accesses by C/4 adjacent lanes.
+__global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_ptr,
+                                                  const int* __restrict__ col,
+                                                  const float* __restrict__ val,
+                                                  const float* __restrict__ x,
+                                                  const float* __restrict__ elu_y,
+                                                  float* __restrict__ y, int m, int n, int c4,
+                                                  long total) {
+  // hipcc contracts a*b+c into fma by default; the reference rounds the
+  // product and the sum separately (index_select*value, then scatter_add).
+#pragma clang fp contract(off)
+  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int q = (int)(t % c4);
+  const long br = t / c4;
+  const int r = (int)(br % m);
+  const int b = (int)(br / m);
+  const float* xb = x + (long)b * n * c4 * 4 + 4 * q;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int beg = row_ptr[r], end = row_ptr[r + 1];
+  for (int e = beg; e < end; ++e) {
+    const float v = val[e];
+    f32x4 xv = ld4(xb + (long)col[e] * c4 * 4);
+    acc.x = acc.x + xv.x * v;
+    acc.y = acc.y + xv.y * v;
+    acc.z = acc.z + xv.z * v;
+    acc.w = acc.w + xv.w * v;
+  }
+  if (elu_y) {
+    f32x4 g = ld4(elu_y + t * 4);
+    acc.x *= elu_grad_from_out(g.x);
+    acc.y *= elu_grad_from_out(g.y);
+    acc.z *= elu_grad_from_out(g.z);
+    acc.w *= elu_grad_from_out(g.w);
+  }
+  st4(y + t * 4, acc);
+}
+
+// out[(i*bs + j), v, :] = x[mesh(i or j), v, :]; one thread per (out mesh,
+// vertex); c <= 4 channels per vertex (xyz) are copied as scalars, larger c
+// in 16-B chunks.
+__global__ __launch_bounds__(256) void swap_k(const float* __restrict__ x,
+                                              const int* __restrict__ batch_idx,
+                                              const unsigned char* __restrict__ mask,
+                                              const int* __restrict__ key, float* __restrict__ out,
+                                              int bs, int nv, int c, long total) {
+  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int v = (int)(t % nv);
+  const int ob = (int)(t / nv);
+  const int i = ob / bs, j = ob % bs;
+  const int k = *key;
+  const bool take = (i != j) && mask[(long)k * nv + v];
+  const long src_mesh = batch_idx[take ? j : i];
+  const float* src = x + (src_mesh * nv + v) * c;
+  float* dst = out + t * c;
+  for (int q = 0; q < c; ++q) dst[q] = src[q];
+}
+
+__global__ void scale_k(float* __restrict__ y, long n, float alpha) {
+  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) y[t] *= alpha;
+}
+
+__global__ void elu_bwd_k(const float* __restrict__ dy, const float* __restrict__ y,
+                          float* dx, long n) {
+  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) dx[t] = dy[t] * elu_grad_from_out(y[t]);
+}
+
+}  // namespace cfsd
+
+using namespace cfsd;
+
+extern "C" int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const float* val,
+                             const float* x, const float* elu_y, float* y, int batch, int m,
+                             int n, int c, void* stream) {
+  if (!row_ptr || !col || !val || !x || !y) return set_error(CFSD_EINVAL, "spmm_csr: null pointer");
+  if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
+    return set_error(CFSD_EINVAL, "spmm_csr: bad sizes batch=%d m=%d n=%d c=%d", batch, m, n, c);
+  const long total = (long)batch * m * (c / 4);
+  hipLaunchKernelGGL(spmm_csr_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, row_ptr, col, val, x, elu_y, y, m, n, c / 4, total);
+  return launch_status("spmm_csr");
+}
+
+extern "C" int cfsd_swap_features(const float* x, const int32_t* batch_idx,
+                                  const uint8_t* region_mask, const int32_t* key, float* out,
+                                  int bs, int nv, int c, int n_meshes, void* stream) {
+  if (!x || !batch_idx || !region_mask || !key || !out)
+    return set_error(CFSD_EINVAL, "swap_features: null pointer");
+  if (bs <= 0 || nv <= 0 || c <= 0 || n_meshes <= 0)
+    return set_error(CFSD_EINVAL, "swap_features: bad sizes");
+  const long total = (long)bs * bs * nv;
+  hipLaunchKernelGGL(swap_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, batch_idx, region_mask, key, out, bs, nv, c, total);
+  return launch_status("swap_features");
+}
+
+extern "C" int cfsd_scale(float* y, size_t n, float alpha, void* stream) {
+  if (!y) return set_error(CFSD_EINVAL, "scale: null pointer");
+  if (n == 0) return CFSD_OK;
+  hipLaunchKernelGGL(scale_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, y, (long)n, alpha);
+  return launch_status("scale");
+}
+
+extern "C" int cfsd_elu_bwd(const float* dy, const float* y, float* dx, size_t n, void* stream) {
+  if (!dy || !y || !dx) return set_error(CFSD_EINVAL, "elu_bwd: null pointer");
+  if (n == 0) return CFSD_OK;
+  hipLaunchKernelGGL(elu_bwd_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, dy, y, dx, (long)n);
+  return launch_status("elu_bwd");
+}

@@ -1,0 +1,429 @@
+"""The SD-VAE training step as an explicit launch sequence on libcfsd.
+
+Reference call stack being replaced: ``ModelManager._do_iteration``
+(``model_manager.py:274-326``) -> ``Model.forward`` (``model.py:175-182``) ->
+losses -> ``loss_tot.backward()`` -> ``Adam.step()``, with the batch built by
+``SwapFeatures`` in DataLoader workers (``swap_batch_transform.py:13-42``).
+
+MI355X design:
+* parameters, gradients and Adam moments live in ONE flat fp32 buffer each
+  (named views keep the reference ``state_dict`` keys), so data-parallel
+  training all-reduces one contiguous bucket and Adam is one launch;
+* every activation/gradient buffer is allocated once per batch size, so the
+  whole step (swap -> forward -> 4 losses -> backward -> Adam) is a fixed
+  sequence of ~60 kernel launches that is captured once into a hipGraph and
+  replayed; nothing in the step synchronises with the host (losses are
+  accumulated on device, unlike the reference's seven ``.item()`` calls);
+* the backward is hand-derived and fused (ELU backward in the producer's
+  epilogue, deterministic gather-based transposes, no atomics).
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+from .ops import ACT_ELU, ACT_NONE
+
+
+class ModelSpec:
+    """Architecture of ``Model`` (``model.py:88-137``)."""
+
+    def __init__(self, in_channels=3, out_channels=(32, 32, 32, 64), latent_size=75,
+                 is_vae=True, pre_z_sigmoid=False):
+        self.in_ch = int(in_channels)
+        self.out_ch = [int(c) for c in out_channels]
+        self.latent = int(latent_size)
+        self.is_vae = bool(is_vae)
+        self.sigmoid = bool(pre_z_sigmoid) and not self.is_vae
+        self.n = len(self.out_ch)
+
+    def enc_layers(self):
+        """(cin, cout, level) of the Enblock convs."""
+        return [((self.in_ch if i == 0 else self.out_ch[i - 1]), self.out_ch[i], i)
+                for i in range(self.n)]
+
+    def dec_layers(self):
+        """(cin, cout, level, up_index) of de_layers[1..n] (model.py:125-134)."""
+        out = []
+        for idx in range(self.n):
+            if idx == 0:
+                cin, cout = self.out_ch[-1], self.out_ch[-1]
+            else:
+                cin, cout = self.out_ch[-idx], self.out_ch[-idx - 1]
+            level = self.n - 1 - idx
+            out.append((cin, cout, level, self.n - (idx + 1)))
+        return out
+
+    def param_specs(self, num_vert, seq):
+        """(name, shape) in FLAT-BUFFER order.  The two encoder Linears are
+        stacked [logvar; mu] so one GEMM produces both (mu = en_layers[-1],
+        logvar = en_layers[-2], model.py:153-156)."""
+        n, lat, c_last = self.n, self.latent, self.out_ch[-1]
+        flat_in = num_vert * c_last
+        specs = []
+        for (cin, cout, lv) in self.enc_layers():
+            specs.append((f"en_layers.{lv}.conv.layer.weight", (cout, seq[lv] * cin)))
+            specs.append((f"en_layers.{lv}.conv.layer.bias", (cout,)))
+        if self.is_vae:
+            specs += [(f"en_layers.{n}.weight", (lat, flat_in)), (f"en_layers.{n + 1}.weight", (lat, flat_in)),
+                      (f"en_layers.{n}.bias", (lat,)), (f"en_layers.{n + 1}.bias", (lat,))]
+        else:
+            specs += [(f"en_layers.{n}.weight", (lat, flat_in)), (f"en_layers.{n}.bias", (lat,))]
+        specs += [("de_layers.0.weight", (flat_in, lat)), ("de_layers.0.bias", (flat_in,))]
+        for i, (cin, cout, lv, _) in enumerate(self.dec_layers()):
+            specs.append((f"de_layers.{i + 1}.conv.layer.weight", (cout, seq[lv] * cin)))
+            specs.append((f"de_layers.{i + 1}.conv.layer.bias", (cout,)))
+        specs.append((f"de_layers.{n + 1}.layer.weight", (self.in_ch, seq[0] * self.out_ch[0])))
+        specs.append((f"de_layers.{n + 1}.layer.bias", (self.in_ch,)))
+        return specs
+
+    def reference_order(self, num_vert, seq):
+        """Parameter names in the reference ``named_parameters`` order."""
+        n = self.n
+        names = [k for k, _ in self.param_specs(num_vert, seq)]
+        enc_lin = [f"en_layers.{n}.weight", f"en_layers.{n}.bias"]
+        if self.is_vae:
+            enc_lin += [f"en_layers.{n + 1}.weight", f"en_layers.{n + 1}.bias"]
+        convs = [k for k in names if k.startswith("en_layers") and ".conv." in k]
+        rest = [k for k in names if k.startswith("de_layers")]
+        return convs + enc_lin + rest
+
+
+class FlatParams:
+    """One contiguous fp32 buffer for params / grads / Adam moments."""
+
+    def __init__(self, specs, device):
+        self.specs = list(specs)
+        self.offsets = {}
+        off = 0
+        for name, shape in self.specs:
+            self.offsets[name] = (off, tuple(shape))
+            off += int(np.prod(shape))
+        self.numel = off
+        self.data = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=device)
+        self.exp_avg = torch.zeros(off, dtype=torch.float32, device=device)
+        self.exp_avg_sq = torch.zeros(off, dtype=torch.float32, device=device)
+        self.step = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def view(self, name, buf=None):
+        off, shape = self.offsets[name]
+        b = self.data if buf is None else buf
+        return b[off:off + int(np.prod(shape))].view(shape)
+
+    def gview(self, name):
+        return self.view(name, self.grad)
+
+    def span(self, first, last, buf=None):
+        """Contiguous view from the start of ``first`` to the end of ``last``."""
+        b = self.data if buf is None else buf
+        o0, _ = self.offsets[first]
+        o1, s1 = self.offsets[last]
+        return b[o0:o1 + int(np.prod(s1))]
+
+
+class _Buffers:
+    pass
+
+
+class SDVAEEngine:
+    """Forward/backward/Adam of the SD-VAE on one device, for a fixed
+    topology and any number of batch sizes (buffers cached per batch)."""
+
+    def __init__(self, topo, spec=None, lr=1e-4, weight_decay=0.0, w_kl=1e-4, w_lc=0.5,
+                 w_lap=0.1, eta1=0.5, eta2=0.5, swap_bs=4, seed=0, device="cuda"):
+        self.topo = topo
+        self.spec = spec or ModelSpec()
+        self.device = torch.device(device)
+        self.lr, self.weight_decay = float(lr), float(weight_decay)
+        self.w_kl = float(w_kl) if self.spec.is_vae else 0.0
+        self.w_lc, self.w_lap = float(w_lc), float(w_lap)
+        self.eta1, self.eta2 = float(eta1), float(eta2)
+        self.swap_bs = int(swap_bs)
+        self.seed = int(seed)
+        if topo.n_levels != self.spec.n:
+            raise ValueError(f"topology has {topo.n_levels} levels, model {self.spec.n}")
+        self.num_vert = topo.n_verts[-1]
+        self.params = FlatParams(self.spec.param_specs(self.num_vert, topo.seq), self.device)
+        n_reg = topo.n_regions if topo.n_regions else 1
+        self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
+        if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
+            raise ValueError("latent_size must be a multiple of the number of regions")
+        self.reset_parameters()
+        self._bufs = {}
+        self.loss_acc = torch.zeros(6, dtype=torch.float32, device=self.device)
+
+    # ----------------------------------------------------------- parameters
+    def reset_parameters(self, generator=None):
+        """``Model.reset_parameters`` (model.py:139-144): xavier-uniform
+        weights, zero biases."""
+        for name, shape in self.params.specs:
+            v = self.params.view(name)
+            if name.endswith("bias"):
+                v.zero_()
+            else:
+                fan_out, fan_in = shape
+                a = math.sqrt(6.0 / (fan_in + fan_out))
+                v.uniform_(-a, a, generator=generator)
+
+    def state_dict(self):
+        n, order = self.spec.n, self.spec.reference_order(self.num_vert, self.topo.seq)
+        return {k: self.params.view(k).detach().clone() for k in order}
+
+    def load_state_dict(self, sd):
+        for name, shape in self.params.specs:
+            t = sd[name]
+            if tuple(t.shape) != tuple(shape):
+                raise ValueError(f"{name}: shape {tuple(t.shape)} != {shape}")
+            self.params.view(name).copy_(t.to(self.device, torch.float32))
+
+    def grads(self):
+        return {k: self.params.gview(k) for k, _ in self.params.specs}
+
+    # ----------------------------------------------------------- buffers
+    def buffers(self, bsz):
+        if bsz in self._bufs:
+            return self._bufs[bsz]
+        T, S, dev = self.topo, self.spec, self.device
+        f = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731
+        b = _Buffers()
+        b.bsz = bsz
+        nv = T.n_verts
+        lat = S.latent
+        b.x = f(bsz, nv[0], S.in_ch)
+        b.enc_full = [None] * S.n     # full-resolution conv outputs (non-selection path)
+        b.enc_out = []                # pooled Enblock outputs [B, V_{i+1}, C_i]
+        for (cin, cout, lv) in S.enc_layers():
+            if not T.enc_select[lv]:
+                b.enc_full[lv] = f(bsz, nv[lv], cout)
+            b.enc_out.append(f(bsz, nv[lv + 1], cout))
+        nmulv = 2 * lat if S.is_vae else lat
+        b.mulv, b.z = f(bsz, nmulv), f(bsz, lat)
+        b.dlat, b.terms = f(bsz, 3 * lat), f(2)
+        b.eps = f(bsz, lat)
+        b.key = torch.zeros(1, dtype=torch.int32, device=dev)
+        b.h = f(bsz, self.num_vert, S.out_ch[-1])
+        b.dec_up, b.dec_out = [], []
+        for (cin, cout, lv, ui) in S.dec_layers():
+            b.dec_up.append(f(bsz, nv[lv], cin))
+            b.dec_out.append(f(bsz, nv[lv], cout))
+        b.out = f(bsz, nv[0], S.in_ch)
+        b.unit = f(bsz, nv[0], S.in_ch)
+        b.partials = f(2 * ops.recon_lap_blocks(bsz, nv[0]))
+        b.losses = f(5)
+        # backward
+        b.dout = f(bsz, nv[0], S.in_ch)
+        b.g_dec_up = [torch.empty_like(t) for t in b.dec_up]    # grad wrt dec_up (conv dx)
+        b.dpre_dec = [torch.empty_like(t) for t in b.dec_out]   # grad wrt pre-ELU dec conv
+        b.dh = torch.empty_like(b.h)
+        b.dz = f(bsz, lat)
+        b.dmulv = torch.empty_like(b.mulv)
+        b.dpre_enc = [f(bsz, (nv[lv + 1] if T.enc_select[lv] else nv[lv]), cout)
+                      for (cin, cout, lv) in S.enc_layers()]
+        b.g_enc_in = [None] + [f(bsz, nv[lv], cin) if not T.enc_select[lv - 1] else None
+                               for (cin, cout, lv) in S.enc_layers()[1:]]
+        b.g_pooled = [f(bsz, nv[lv + 1], cout) if not T.enc_select[lv] else None
+                      for (cin, cout, lv) in S.enc_layers()]
+        ws = 0
+        for (cin, cout, lv) in S.enc_layers():
+            rows = nv[lv + 1] if T.enc_select[lv] else nv[lv]
+            ws = max(ws, ops.spiral_conv_bwd_weight_workspace(bsz, rows, T.seq[lv], cin, cout))
+        for (cin, cout, lv, _) in S.dec_layers():
+            ws = max(ws, ops.spiral_conv_bwd_weight_workspace(bsz, nv[lv], T.seq[lv], cin, cout))
+        ws = max(ws, ops.spiral_conv_bwd_weight_workspace(bsz, nv[0], T.seq[0], S.out_ch[0], S.in_ch))
+        b.ws = torch.empty(ws // 4 + 64, dtype=torch.float32, device=dev)
+        # step bookkeeping for the resident-dataset path
+        b.batch_idx = torch.zeros(self.swap_bs, dtype=torch.int32, device=dev)
+        self._bufs[bsz] = b
+        return b
+
+    # ----------------------------------------------------------- names
+    def _enc_w(self, i):
+        return (self.params.view(f"en_layers.{i}.conv.layer.weight"),
+                self.params.view(f"en_layers.{i}.conv.layer.bias"))
+
+    def _dec_w(self, i):  # de_layers[i + 1]
+        return (self.params.view(f"de_layers.{i + 1}.conv.layer.weight"),
+                self.params.view(f"de_layers.{i + 1}.conv.layer.bias"))
+
+    def _lin_names(self):
+        n = self.spec.n
+        if self.spec.is_vae:
+            return (f"en_layers.{n}.weight", f"en_layers.{n + 1}.weight",
+                    f"en_layers.{n}.bias", f"en_layers.{n + 1}.bias")
+        return (f"en_layers.{n}.weight", f"en_layers.{n}.weight",
+                f"en_layers.{n}.bias", f"en_layers.{n}.bias")
+
+    def _enc_lin(self, buf=None):
+        w0, w1, b0, b1 = self._lin_names()
+        P = self.params
+        flat_in = self.num_vert * self.spec.out_ch[-1]
+        nout = self.spec.latent * (2 if self.spec.is_vae else 1)
+        W = P.span(w0, w1, buf).view(nout, flat_in)
+        B = P.span(b0, b1, buf)
+        return W, B
+
+    # ----------------------------------------------------------- forward
+    def encode(self, b):
+        """Enblocks + stacked mu/logvar Linear (model.py:146-160)."""
+        T, S = self.topo, self.spec
+        h = b.x
+        for (cin, cout, lv) in S.enc_layers():
+            w, bias = self._enc_w(lv)
+            if T.enc_select[lv]:
+                ops.spiral_conv_fwd(h, T.enc_rows[lv], w, bias, ACT_ELU, out=b.enc_out[lv])
+            else:
+                ops.spiral_conv_fwd(h, T.spiral[lv], w, bias, ACT_ELU, out=b.enc_full[lv])
+                ops.spmm(T.down_csr[lv], b.enc_full[lv], T.n_verts[lv + 1], out=b.enc_out[lv])
+            h = b.enc_out[lv]
+        W, B = self._enc_lin()
+        ops.linear_fwd(h.view(b.bsz, -1), W, B, out=b.mulv)
+
+    def _lc_on(self, b):
+        """Latent consistency needs a swapped bs x bs group (model_manager.py:360-367)."""
+        return bool(self.region_size) and self.w_lc != 0.0 and b.bsz == self.swap_bs ** 2
+
+    def latent(self, b, train):
+        S = self.spec
+        lc = self._lc_on(b)
+        ops.latent_fwd(b.mulv, b.eps if (train and S.is_vae) else None,
+                       b.key if lc else None, b.z, b.dlat, b.terms, S.latent,
+                       self.region_size if lc else 0, train, S.is_vae, S.sigmoid, self.w_kl,
+                       self.w_lc if lc else 0.0, self.eta1, self.eta2)
+
+    def decode(self, b, z=None):
+        """de_layers: Linear -> 4x (Pool up -> conv -> ELU) -> conv (model.py:162-173)."""
+        T, S = self.topo, self.spec
+        ops.linear_fwd(b.z if z is None else z, self.params.view("de_layers.0.weight"),
+                       self.params.view("de_layers.0.bias"), out=b.h.view(b.bsz, -1))
+        h = b.h
+        for i, (cin, cout, lv, ui) in enumerate(S.dec_layers()):
+            ops.spmm(T.up_csr[ui], h, T.n_verts[lv], out=b.dec_up[i])
+            w, bias = self._dec_w(i)
+            ops.spiral_conv_fwd(b.dec_up[i], T.spiral[lv], w, bias, ACT_ELU, out=b.dec_out[i])
+            h = b.dec_out[i]
+        n = S.n
+        ops.spiral_conv_fwd(h, T.spiral[0], self.params.view(f"de_layers.{n + 1}.layer.weight"),
+                            self.params.view(f"de_layers.{n + 1}.layer.bias"), ACT_NONE, out=b.out)
+
+    def losses_fwd(self, b, acc=None):
+        T = self.topo
+        ops.recon_lap_fwd(b.out, b.x, T.lap_csr, b.unit, b.partials)
+        ops.loss_finalize(b.partials, b.terms, b.losses, acc, b.bsz, T.n_verts[0], self.spec.in_ch,
+                          self.w_kl, self.w_lc if self._lc_on(b) else 0.0, self.w_lap)
+
+    def forward(self, b, train=True, acc=None):
+        self.encode(b)
+        self.latent(b, train)
+        self.decode(b)
+        if self.topo.lap_csr is not None:
+            self.losses_fwd(b, acc)
+
+    # ----------------------------------------------------------- backward
+    def backward(self, b):
+        T, S, P = self.topo, self.spec, self.params
+        n = S.n
+        ops.recon_lap_bwd(b.out, b.x, b.unit, T.lapT_csr, b.dout, 1.0, self.w_lap)
+        # final SpiralConv (no activation): dpre = dout
+        last_in = b.dec_out[-1]
+        ops.spiral_conv_bwd_weight(last_in, T.spiral[0], b.dout, P.gview(f"de_layers.{n + 1}.layer.weight"),
+                                   P.gview(f"de_layers.{n + 1}.layer.bias"), b.ws)
+        ops.spiral_conv_bwd_data(b.dout, T.spiral_inv[0], P.view(f"de_layers.{n + 1}.layer.weight"),
+                                 T.n_verts[0], elu_y=last_in, out=b.dpre_dec[-1])
+        dec = S.dec_layers()
+        for i in reversed(range(len(dec))):
+            cin, cout, lv, ui = dec[i]
+            w, _ = self._dec_w(i)
+            ops.spiral_conv_bwd_weight(b.dec_up[i], T.spiral[lv], b.dpre_dec[i],
+                                       P.gview(f"de_layers.{i + 1}.conv.layer.weight"),
+                                       P.gview(f"de_layers.{i + 1}.conv.layer.bias"), b.ws)
+            ops.spiral_conv_bwd_data(b.dpre_dec[i], T.spiral_inv[lv], w, T.n_verts[lv],
+                                     out=b.g_dec_up[i])
+            if i > 0:  # through Pool(up) into the previous Deblock's ELU
+                ops.spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], elu_y=b.dec_out[i - 1],
+                         out=b.dpre_dec[i - 1])
+            else:
+                ops.spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh)
+        # decoder Linear
+        ops.linear_bwd(b.z, P.view("de_layers.0.weight"), b.dh.view(b.bsz, -1), dx=b.dz,
+                       dw=P.gview("de_layers.0.weight"), db=P.gview("de_layers.0.bias"))
+        ops.latent_bwd(b.mulv, b.eps, b.z, b.dz, b.dlat, b.dmulv, S.latent, True, S.is_vae, S.sigmoid)
+        # stacked encoder Linear; ELU of the last Enblock folded into dx
+        W, _ = self._enc_lin()
+        gW, gB = self._enc_lin(P.grad)
+        enc = S.enc_layers()
+        last = enc[-1][2]
+        flat = b.enc_out[last].view(b.bsz, -1)
+        if T.enc_select[last]:
+            ops.linear_bwd(flat, W, b.dmulv, dx=b.dpre_enc[last].view(b.bsz, -1), dw=gW.view(W.shape),
+                           db=gB, elu_y=flat)
+        else:
+            ops.linear_bwd(flat, W, b.dmulv, dx=b.g_pooled[last].view(b.bsz, -1), dw=gW.view(W.shape),
+                           db=gB)
+            ops.spmm(T.downT_csr[last], b.g_pooled[last], T.n_verts[last], elu_y=b.enc_full[last],
+                     out=b.dpre_enc[last])
+        for (cin, cout, lv) in reversed(enc):
+            w, _ = self._enc_w(lv)
+            x_in = b.x if lv == 0 else b.enc_out[lv - 1]
+            rows_tab = T.enc_rows[lv]
+            ops.spiral_conv_bwd_weight(x_in, rows_tab, b.dpre_enc[lv],
+                                       P.gview(f"en_layers.{lv}.conv.layer.weight"),
+                                       P.gview(f"en_layers.{lv}.conv.layer.bias"), b.ws)
+            if lv == 0:
+                break
+            prev = lv - 1
+            if T.enc_select[prev]:
+                # input of this conv IS the ELU output of the previous Enblock
+                ops.spiral_conv_bwd_data(b.dpre_enc[lv], T.enc_inv[lv], w, T.n_verts[lv],
+                                         elu_y=b.enc_out[prev], out=b.dpre_enc[prev])
+            else:
+                ops.spiral_conv_bwd_data(b.dpre_enc[lv], T.enc_inv[lv], w, T.n_verts[lv],
+                                         out=b.g_pooled[prev])
+                ops.spmm(T.downT_csr[prev], b.g_pooled[prev], T.n_verts[prev], elu_y=b.enc_full[prev],
+                         out=b.dpre_enc[prev])
+
+    def adam_step(self):
+        P = self.params
+        ops.adam(P.data, P.grad, P.exp_avg, P.exp_avg_sq, P.step, self.lr,
+                 weight_decay=self.weight_decay)
+
+    def advance_step(self):
+        """t += 1 on device (the Adam bias-correction step)."""
+        ops.step_begin(self.params.step, self.seed)
+
+    # ----------------------------------------------------------- entry points
+    def set_batch(self, x, key_index=None, eps=None):
+        """Copy an already-swapped batch [B, V, C] (+ injected key / eps)."""
+        b = self.buffers(x.shape[0])
+        b.x.copy_(x)
+        if key_index is not None:
+            b.key.fill_(int(key_index))
+        if eps is not None:
+            b.eps.copy_(eps)
+        return b
+
+    def train_step_on(self, b, acc=None, grad_hook=None):
+        """forward + losses + backward + (grad_hook, e.g. all-reduce) + Adam."""
+        self.forward(b, train=True, acc=acc)
+        self.backward(b)
+        if grad_hook is not None:
+            grad_hook(self.params.grad)
+        self.advance_step()
+        self.adam_step()
+
+    def resident_step(self, b, dataset, perm, n_batches, acc=None, grad_hook=None):
+        """Full reference step from a resident dataset: device-side batch
+        pick + swap key + VAE noise (cfsd_step_begin), on-device feature swap,
+        then train_step_on.  No host input -> graph-capturable."""
+        T = self.topo
+        ops.step_begin(self._step_counter(b), self.seed, eps=b.eps, key=b.key,
+                       n_regions=max(T.n_regions, 1), batch_idx=b.batch_idx, bs=self.swap_bs,
+                       n_batches=n_batches, perm=perm)
+        ops.swap_features(dataset, b.batch_idx, T.region_mask, b.key, self.swap_bs, out=b.x)
+        self.train_step_on(b, acc=acc, grad_hook=grad_hook)
+
+    def _step_counter(self, b):
+        if not hasattr(b, "counter"):
+            b.counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+        return b.counter

@@ -1,0 +1,251 @@
+"""Typed host wrappers over the libcfsd C ABI.
+
+Every wrapper validates shapes/dtypes/devices on the host BEFORE launching
+(an out-of-range launch on the GPU would fault the device), then launches on
+the current torch stream with no synchronisation.  Outputs may be passed in
+(pre-allocated, graph-capture friendly) or are allocated with ``torch.empty``.
+"""
+import ctypes
+
+import torch
+
+from . import _abi
+from ._abi import call, ptr, stream_ptr
+
+ACT_NONE = 0
+ACT_ELU = 1
+
+
+def _need(t, shape, dtype=torch.float32, name="tensor"):
+    if t is None:
+        raise ValueError(f"{name} is required")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+    return t
+
+
+def _out(out, shape, like, name="out"):
+    if out is None:
+        return torch.empty(shape, dtype=torch.float32, device=like.device)
+    return _need(out, shape, name=name)
+
+
+# ------------------------------------------------------------------ spiral conv
+def spiral_conv_fwd(x, idx, w, b, act=ACT_NONE, out=None):
+    """y[b, r] = act(b + W . concat_s x[b, idx[r, s]])  (model.py:27-41)."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = w.shape[0]
+    _need(x, None, name="x")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(w, (cout, seq * cin), name="w")
+    if b is not None:
+        _need(b, (cout,), name="bias")
+    y = _out(out, (bsz, rows, cout), x)
+    call("cfsd_spiral_conv_fwd", ptr(x), ptr(idx), ptr(w), ptr(b), ptr(y), bsz, vsrc, rows, seq,
+         cin, cout, act, stream_ptr())
+    return y
+
+
+def spiral_conv_bwd_data(dpre, inv, w, vsrc, elu_y=None, out=None):
+    """dx[b, u] = g * sum_{(r,s) in inv(u)} W_s^T dpre[b, r]."""
+    bsz, rows, cout = dpre.shape
+    inv_ptr, inv_row = inv
+    seq = (inv_ptr.numel() - 1) // vsrc
+    cin = w.shape[1] // seq
+    _need(dpre, None, name="dpre")
+    _need(inv_ptr, (vsrc * seq + 1,), torch.int32, "inv_ptr")
+    _need(inv_row, (rows * seq,), torch.int32, "inv_row")
+    _need(w, (cout, seq * cin), name="w")
+    if elu_y is not None:
+        _need(elu_y, (bsz, vsrc, cin), name="elu_y")
+    dx = _out(out, (bsz, vsrc, cin), dpre)
+    call("cfsd_spiral_conv_bwd_data", ptr(dpre), ptr(inv_ptr), ptr(inv_row), ptr(w), ptr(elu_y),
+         ptr(dx), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    return dx
+
+
+def spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout):
+    return int(_abi.lib().cfsd_spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout))
+
+
+def spiral_conv_bwd_weight(x, idx, dpre, dw, db, workspace):
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = dpre.shape[2]
+    _need(x, None, name="x")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(dpre, (bsz, rows, cout), name="dpre")
+    _need(dw, (cout, seq * cin), name="dw")
+    _need(db, (cout,), name="db")
+    _need(workspace, None, name="workspace")
+    need = spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout)
+    nbytes = workspace.numel() * workspace.element_size()
+    if nbytes < need:
+        raise ValueError(f"workspace {nbytes} < {need} bytes")
+    call("cfsd_spiral_conv_bwd_weight", ptr(x), ptr(idx), ptr(dpre), ptr(dw), ptr(db),
+         ptr(workspace), ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+
+
+def spiral_gather(x, idx, out=None):
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    _need(x, None, name="x")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    g = _out(out, (bsz, rows, seq * cin), x)
+    call("cfsd_spiral_gather", ptr(x), ptr(idx), ptr(g), bsz, vsrc, rows, seq, cin, stream_ptr())
+    return g
+
+
+# ------------------------------------------------------------------ pool / swap
+def spmm(csr, x, m, elu_y=None, out=None):
+    """y[b, r] = g * sum_{k in row r} val[k] x[b, col[k]]   (Pool, model.py:50-55)."""
+    row_ptr, col, val = csr
+    bsz, n, c = x.shape
+    _need(x, None, name="x")
+    _need(row_ptr, (m + 1,), torch.int32, "row_ptr")
+    _need(col, None, torch.int32, "col")
+    _need(val, (col.numel(),), name="val")
+    if elu_y is not None:
+        _need(elu_y, (bsz, m, c), name="elu_y")
+    y = _out(out, (bsz, m, c), x)
+    call("cfsd_spmm_csr", ptr(row_ptr), ptr(col), ptr(val), ptr(x), ptr(elu_y), ptr(y), bsz, m, n,
+         c, stream_ptr())
+    return y
+
+
+def swap_features(x_all, batch_idx, region_mask, key, bs, out=None):
+    n_meshes, nv, c = x_all.shape
+    _need(x_all, None, name="x_all")
+    _need(batch_idx, (bs,), torch.int32, "batch_idx")
+    _need(region_mask, (region_mask.shape[0], nv), torch.uint8, "region_mask")
+    _need(key, (1,), torch.int32, "key")
+    y = _out(out, (bs * bs, nv, c), x_all)
+    call("cfsd_swap_features", ptr(x_all), ptr(batch_idx), ptr(region_mask), ptr(key), ptr(y), bs,
+         nv, c, n_meshes, stream_ptr())
+    return y
+
+
+def elu_bwd(dy, y, out=None):
+    _need(dy, None, name="dy")
+    _need(y, tuple(dy.shape), name="y")
+    dx = _out(out, tuple(dy.shape), dy)
+    call("cfsd_elu_bwd", ptr(dy), ptr(y), ptr(dx), ctypes.c_size_t(dy.numel()), stream_ptr())
+    return dx
+
+
+# ------------------------------------------------------------------ dense
+def linear_fwd(x, w, b, out=None):
+    m, k = x.shape
+    n = w.shape[0]
+    _need(x, None, name="x")
+    _need(w, (n, k), name="w")
+    if b is not None:
+        _need(b, (n,), name="b")
+    y = _out(out, (m, n), x)
+    call("cfsd_linear_fwd", ptr(x), ptr(w), ptr(b), ptr(y), m, k, n, stream_ptr())
+    return y
+
+
+def linear_bwd(x, w, dy, dx=None, dw=None, db=None, elu_y=None, accumulate=False):
+    m, n = dy.shape
+    k = w.shape[1] if w is not None else x.shape[1]
+    _need(dy, None, name="dy")
+    if dx is not None:
+        _need(dx, (m, k), name="dx")
+        _need(w, (n, k), name="w")
+    if dw is not None:
+        _need(dw, (n, k), name="dw")
+        _need(x, (m, k), name="x")
+    if db is not None:
+        _need(db, (n,), name="db")
+    if elu_y is not None:
+        _need(elu_y, (m, k), name="elu_y")
+    call("cfsd_linear_bwd", ptr(x), ptr(w), ptr(dy), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), m, k,
+         n, int(accumulate), stream_ptr())
+
+
+# ------------------------------------------------------------------ losses
+def recon_lap_blocks(bsz, nv):
+    return int(_abi.lib().cfsd_recon_lap_blocks(bsz, nv))
+
+
+def recon_lap_fwd(pred, gt, lap_csr, unit, partials):
+    bsz, nv, c = pred.shape
+    _need(pred, None, name="pred")
+    _need(gt, (bsz, nv, c), name="gt")
+    _need(unit, (bsz, nv, c), name="unit")
+    _need(partials, (2 * recon_lap_blocks(bsz, nv),), name="partials")
+    _need(lap_csr[0], (nv + 1,), torch.int32, "l_ptr")
+    call("cfsd_recon_lap_fwd", ptr(pred), ptr(gt), ptr(lap_csr[0]), ptr(lap_csr[1]),
+         ptr(lap_csr[2]), ptr(unit), ptr(partials), bsz, nv, c, stream_ptr())
+
+
+def recon_lap_bwd(pred, gt, unit, lapT_csr, dpred, w_rec, w_lap):
+    bsz, nv, c = pred.shape
+    _need(dpred, (bsz, nv, c), name="dpred")
+    _need(lapT_csr[0], (nv + 1,), torch.int32, "lt_ptr")
+    call("cfsd_recon_lap_bwd", ptr(pred), ptr(gt), ptr(unit), ptr(lapT_csr[0]),
+         ptr(lapT_csr[1]), ptr(lapT_csr[2]), ptr(dpred), bsz, nv, c, float(w_rec), float(w_lap),
+         stream_ptr())
+
+
+def latent_fwd(mulv, eps, key, z, dlat, terms, latent, region_size, train, is_vae, sigmoid,
+               w_kl, w_lc, eta1, eta2):
+    bsz = z.shape[0]
+    _need(mulv, (bsz, 2 * latent if is_vae else latent), name="mulv")
+    _need(z, (bsz, latent), name="z")
+    _need(dlat, (bsz, 3 * latent), name="dlat")
+    _need(terms, (2,), name="terms")
+    if eps is not None:
+        _need(eps, (bsz, latent), name="eps")
+    if key is not None:
+        _need(key, (1,), torch.int32, "key")
+    call("cfsd_latent_fwd", ptr(mulv), ptr(eps), ptr(key), ptr(z), ptr(dlat), ptr(terms), bsz,
+         latent, region_size, int(train), int(is_vae), int(sigmoid), float(w_kl), float(w_lc),
+         float(eta1), float(eta2), stream_ptr())
+
+
+def latent_bwd(mulv, eps, z, dz_dec, dlat, dmulv, latent, train, is_vae, sigmoid):
+    bsz = dz_dec.shape[0]
+    _need(dz_dec, (bsz, latent), name="dz_dec")
+    _need(dmulv, tuple(mulv.shape), name="dmulv")
+    call("cfsd_latent_bwd", ptr(mulv), ptr(eps), ptr(z), ptr(dz_dec), ptr(dlat), ptr(dmulv), bsz,
+         latent, int(train), int(is_vae), int(sigmoid), stream_ptr())
+
+
+def loss_finalize(partials, terms, out, acc, bsz, nv, c, w_kl, w_lc, w_lap):
+    _need(out, (5,), name="out")
+    if acc is not None:
+        _need(acc, (6,), name="acc")
+    call("cfsd_loss_finalize", ptr(partials), partials.numel() // 2, ptr(terms), ptr(out),
+         ptr(acc), bsz, nv, c, float(w_kl), float(w_lc), float(w_lap), stream_ptr())
+
+
+# ------------------------------------------------------------------ optimiser
+def adam(param, grad, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):
+    n = param.numel()
+    for t, nm in ((param, "param"), (grad, "grad"), (m, "m"), (v, "v")):
+        _need(t, (n,), name=nm)
+    _need(step, (1,), torch.int32, "step")
+    call("cfsd_adam", ptr(param), ptr(grad), ptr(m), ptr(v), ptr(step), ctypes.c_size_t(n),
+         float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), stream_ptr())
+
+
+def step_begin(counter, seed, eps=None, key=None, n_regions=0, batch_idx=None, bs=0,
+               n_batches=0, perm=None):
+    _need(counter, (1,), torch.int32, "counter")
+    call("cfsd_step_begin", ptr(counter), ctypes.c_ulonglong(seed), ptr(eps),
+         eps.numel() if eps is not None else 0, ptr(key), n_regions, ptr(batch_idx), bs,
+         n_batches, ptr(perm), stream_ptr())
+
+
+def scale(y, alpha):
+    _need(y, None, name="y")
+    call("cfsd_scale", ptr(y), ctypes.c_size_t(y.numel()), float(alpha), stream_ptr())

@@ -1,0 +1,208 @@
+"""Mesh-hierarchy index tables, laid out for the gfx950 kernels.
+
+The reference keeps its static geometry as int64 spiral tensors
+(``spirals.pkl``), torch sparse-COO down/up transforms (``transforms.pkl``)
+and a COO random-walk Laplacian (``utils.py:88-89``), and consumes them with
+``index_select`` / ``scatter_add`` / ``sparse.mm`` every step
+(``model_manager.py:176-230``).  Here they are converted ONCE into the int32
+tables the kernels read:
+
+* spirals -> int32 ``[V, S]`` plus the inverse-spiral CSR (rows r with
+  ``idx[r, s] == u`` for every (u, s)) that makes the spiral backward a
+  deterministic gather instead of an atomic scatter;
+* a down transform that is a 0/1 row selection (the QEM decimation matrices,
+  one nnz of value 1.0 per row) becomes a *row subset*: the Enblock conv is
+  evaluated only at the kept vertices, bit-identical to conv -> Pool(down);
+* other transforms -> CSR (row-sorted, per-row order = COO file order, i.e.
+  the reference's sequential ``scatter_add`` order) and the transpose CSR
+  for the backward;
+* the Laplacian -> CSR in coalesced (row, col) order + transpose CSR;
+* the feature-swap regions -> a ``[n_regions, V]`` uint8 membership mask.
+"""
+import numpy as np
+import torch
+
+
+def _i32(a):
+    a = np.asarray(a)
+    if a.size and (a.min() < np.iinfo(np.int32).min or a.max() > np.iinfo(np.int32).max):
+        raise ValueError("index out of int32 range")
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def csr_from_coo(row, col, val, m):
+    """Row-sorted CSR keeping, inside each row, the COO (file) order."""
+    row = np.asarray(row, np.int64)
+    order = np.argsort(row, kind="stable")
+    ptr = np.zeros(m + 1, np.int64)
+    np.add.at(ptr, row + 1, 1)
+    ptr = np.cumsum(ptr)
+    return _i32(ptr), _i32(np.asarray(col)[order]), np.ascontiguousarray(np.asarray(val, np.float32)[order])
+
+
+def csr_transpose_from_coo(row, col, val, n):
+    """CSR of the transpose (grouped by column), per-group order = COO order.
+    Matches the accumulation order of ``index_add_`` over the nnz sequence
+    (the autograd of ``index_select`` at ``model.py:53``)."""
+    return csr_from_coo(col, row, val, n)
+
+
+def inverse_spiral(idx, vsrc):
+    """CSR over keys (u, s): rows r with ``idx[r, s] == u``, r ascending."""
+    idx = np.asarray(idx, np.int64)
+    r_count, s_len = idx.shape
+    if idx.size and (idx.min() < 0 or idx.max() >= vsrc):
+        raise ValueError("spiral index out of range")
+    keys = (idx * s_len + np.arange(s_len)[None, :]).reshape(-1)  # r-major
+    rows = np.repeat(np.arange(r_count), s_len)
+    order = np.argsort(keys, kind="stable")
+    ptr = np.zeros(vsrc * s_len + 1, np.int64)
+    np.add.at(ptr, keys + 1, 1)
+    return _i32(np.cumsum(ptr)), _i32(rows[order])
+
+
+def selection_rows(row, col, val, m):
+    """Return the kept-vertex list if the COO transform is a 0/1 row
+    selection (exactly one entry of value 1.0 per row), else None."""
+    row = np.asarray(row)
+    if len(row) != m:
+        return None
+    if not np.array_equal(np.sort(row), np.arange(m)):
+        return None
+    if not np.all(np.asarray(val) == 1.0):
+        return None
+    sel = np.empty(m, np.int64)
+    sel[row] = np.asarray(col)
+    return sel
+
+
+def coalesced_csr(row, col, val, n):
+    """torch ``coalesce`` order (row, then col), duplicates summed."""
+    row = np.asarray(row, np.int64)
+    col = np.asarray(col, np.int64)
+    lin = row * n + col
+    uniq, inv = np.unique(lin, return_inverse=True)
+    v = np.zeros(len(uniq), np.float32)
+    np.add.at(v, inv, np.asarray(val, np.float32))
+    r, c = uniq // n, uniq % n
+    return r, c, v
+
+
+class Level:
+    """Device tables of one resolution level."""
+
+
+def _dev(a, device):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+class DeviceTopology:
+    """All static tables of a mesh hierarchy, resident on one device.
+
+    ``spirals[l]`` int [V_l, S]; ``down[l]``/``up[l]`` COO triples
+    ``(row, col, val, (M, N))``; ``lap`` optional COO triple of level 0;
+    ``regions`` optional list of feature-vertex index arrays (swap keys).
+    """
+
+    def __init__(self, spirals, down, up, lap=None, regions=None, region_keys=None,
+                 device="cuda"):
+        self.device = torch.device(device)
+        self.n_levels = len(spirals)
+        self.seq = [int(np.asarray(s).shape[1]) for s in spirals]
+        self.n_verts = [int(np.asarray(spirals[0]).shape[0])] + [int(d[3][0]) for d in down]
+        self.region_keys = list(region_keys) if region_keys is not None else None
+        self.spiral = []        # full spiral tables [V_l, S]
+        self.spiral_inv = []    # inverse CSR of the full table
+        self.enc_rows = []      # per Enblock: evaluated spiral table (subset or full)
+        self.enc_inv = []
+        self.enc_select = []    # True when Pool(down) folds into the row subset
+        self.down_csr, self.downT_csr = [], []
+        self.up_csr, self.upT_csr = [], []
+        self.np_spirals = [np.asarray(s, np.int64) for s in spirals]
+        for l in range(self.n_levels):
+            sp = np.asarray(spirals[l], np.int64)
+            v = sp.shape[0]
+            self.spiral.append(_dev(_i32(sp), self.device))
+            ip, ir = inverse_spiral(sp, v)
+            self.spiral_inv.append((_dev(ip, self.device), _dev(ir, self.device)))
+            drow, dcol, dval, dshape = down[l]
+            sel = selection_rows(drow, dcol, dval, dshape[0])
+            if dshape[1] != v:
+                raise ValueError(f"down[{l}] has {dshape[1]} columns, level has {v} vertices")
+            if sel is not None:
+                sub = sp[sel]
+                self.enc_select.append(True)
+                self.enc_rows.append(_dev(_i32(sub), self.device))
+                sp_ip, sp_ir = inverse_spiral(sub, v)
+                self.enc_inv.append((_dev(sp_ip, self.device), _dev(sp_ir, self.device)))
+            else:
+                self.enc_select.append(False)
+                self.enc_rows.append(self.spiral[-1])
+                self.enc_inv.append(self.spiral_inv[-1])
+            self.down_csr.append(self._csr(csr_from_coo(drow, dcol, dval, dshape[0])))
+            self.downT_csr.append(self._csr(csr_transpose_from_coo(drow, dcol, dval, dshape[1])))
+            urow, ucol, uval, ushape = up[l]
+            self.up_csr.append(self._csr(csr_from_coo(urow, ucol, uval, ushape[0])))
+            self.upT_csr.append(self._csr(csr_transpose_from_coo(urow, ucol, uval, ushape[1])))
+        self.lap_csr = self.lapT_csr = None
+        if lap is not None:
+            lr, lc, lv, lshape = lap
+            r, c, v = coalesced_csr(lr, lc, lv, lshape[1])
+            self.lap_csr = self._csr(csr_from_coo(r, c, v, lshape[0]))
+            self.lapT_csr = self._csr(csr_transpose_from_coo(r, c, v, lshape[1]))
+        self.region_mask = None
+        self.n_regions = 0
+        if regions is not None:
+            mask = np.zeros((len(regions), self.n_verts[0]), np.uint8)
+            for k, feat in enumerate(regions):
+                mask[k, np.asarray(feat, np.int64)] = 1
+            self.region_mask = _dev(mask, self.device)
+            self.n_regions = len(regions)
+
+    def _csr(self, t):
+        ptr, col, val = t
+        return (_dev(ptr, self.device), _dev(col, self.device), _dev(val, self.device))
+
+    # ------------------------------------------------------------- builders
+    @classmethod
+    def from_npz(cls, npz, device="cuda"):
+        """From the arrays of ``tests/golden/topology_craniofacial.npz``."""
+        n = int(npz["n_levels"])
+        spirals = [npz[f"spiral_{l}"] for l in range(n)]
+
+        def coo(name, l):
+            return (npz[f"{name}_{l}_row"], npz[f"{name}_{l}_col"], npz[f"{name}_{l}_val"],
+                    tuple(int(s) for s in npz[f"{name}_{l}_shape"]))
+
+        down = [coo("down", l) for l in range(n)]
+        up = [coo("up", l) for l in range(n)]
+        nv = spirals[0].shape[0]
+        lap = None
+        if "lap_row" in npz:
+            lap = (npz["lap_row"], npz["lap_col"], npz["lap_val"], (nv, nv))
+        regions = keys = None
+        if "region_keys" in npz:
+            keys = [str(k) for k in npz["region_keys"]]
+            regions = [npz[f"region_{i}_feature"] for i in range(len(keys))]
+        return cls(spirals, down, up, lap, regions, keys, device)
+
+    @classmethod
+    def from_torch(cls, spiral_indices, down_transform, up_transform, laplacian=None,
+                   feat_and_cont=None, device="cuda"):
+        """From the objects the reference passes to ``Model`` (int64 spiral
+        tensors, torch sparse-COO transforms) and, optionally, the template's
+        ``laplacian`` and ``feat_and_cont`` (``utils.load_template``)."""
+        def coo_of(t):
+            t = t.cpu()
+            idx = t._indices().numpy()
+            return (idx[0], idx[1], t._values().numpy(), tuple(t.shape))
+
+        spirals = [s.cpu().numpy() for s in spiral_indices]
+        down = [coo_of(d) for d in down_transform]
+        up = [coo_of(u) for u in up_transform]
+        lap = coo_of(laplacian) if laplacian is not None else None
+        regions = keys = None
+        if feat_and_cont is not None:
+            keys = list(feat_and_cont.keys())
+            regions = [np.asarray(feat_and_cont[k]["feature"]) for k in keys]
+        return cls(spirals, down, up, lap, regions, keys, device)

@@ -1,0 +1,183 @@
+/*
+ * cfsd.h — C ABI of libcfsd.so, the MI355X (gfx950) kernels of the
+ * spiral-convolution mesh-VAE training step (CraniofacialSD-VAE).
+ *
+ * The reference has no FFI: its hot path is the Python module API of
+ * model.py / swap_batch_transform.py / model_manager.py running on ATen and
+ * torch-scatter.  Each entry point below names the reference interface whose
+ * arithmetic it replaces (path:line in simofoti/CraniofacialSD-VAE).
+ *
+ * Conventions (all entry points):
+ *  - every pointer is a DEVICE pointer owned by the caller; the library never
+ *    allocates device memory (workspaces are passed in);
+ *  - tensors are dense row-major fp32, activations [batch, vertices, channels];
+ *    index tables are int32;
+ *  - launches are asynchronous on `stream` (a hipStream_t, may be NULL for the
+ *    default stream) with no host synchronisation, so calls can be captured
+ *    into a hipGraph;
+ *  - the return value is CFSD_OK (0), a negative CFSD_E* code for invalid
+ *    arguments, or a positive hipError_t; cfsd_last_error_string() gives text
+ *    (per calling thread).  Nothing aborts and no C++ exception crosses the ABI.
+ *  - stateless and re-entrant.
+ */
+#ifndef CFSD_H
+#define CFSD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CFSD_OK 0
+#define CFSD_EINVAL (-1)      /* bad shape / null pointer / unsupported size */
+#define CFSD_EWORKSPACE (-2)  /* workspace too small */
+
+#define CFSD_ACT_NONE 0
+#define CFSD_ACT_ELU 1
+
+/* ABI version: (major << 16) | minor. */
+int cfsd_version(void);
+const char* cfsd_last_error_string(void);
+
+/* ---------------------------------------------------------------- SpiralConv
+ * Replaces SpiralConv.forward (model.py:27-41) + F.elu (model.py:68,84):
+ *   y[b,r,o] = act( bias[o] + sum_{s,c} w[o, s*cin + c] * x[b, idx[r*seq+s], c] )
+ * x [batch, vsrc, cin], idx [rows, seq] (values in [0, vsrc)), w [cout, seq*cin],
+ * y [batch, rows, cout].  `rows` may be a subset of the mesh's vertices (the
+ * Enblock evaluates the conv only where the 0/1 down-sample selects, which is
+ * bit-identical to conv -> Pool(down) for a selection transform). */
+int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const float* w, const float* bias,
+                         float* y, int batch, int vsrc, int rows, int seq, int cin, int cout,
+                         int act, void* stream);
+
+/* Replaces the autograd of model.py:34 (IndexSelectBackward = index_add_) and
+ * :40 (AddmmBackward dX = dY.W), deterministically (no atomics):
+ *   dx[b,u,c] = g(b,u,c) * sum_{(r,s): idx[r,s]=u} sum_o dpre[b,r,o] w[o, s*cin+c]
+ * where g = elu'(elu_y[b,u,c]) computed from the ELU output when elu_y != NULL
+ * (fuses the previous layer's ELU backward), else 1.
+ * inv_ptr [vsrc*seq + 1] / inv_row [rows*seq]: CSR of the inverse spiral,
+ * entry list of (u, s) = rows r with idx[r*seq+s] == u. */
+int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_ptr, const int32_t* inv_row,
+                              const float* w, const float* elu_y, float* dx, int batch, int vsrc,
+                              int rows, int seq, int cin, int cout, void* stream);
+
+/* Replaces AddmmBackward's dW = G^T.dY and db = sum dY (model.py:40):
+ *   dw[o, s*cin+c] = sum_{b,r} dpre[b,r,o] x[b, idx[r,s], c],  db[o] = sum_{b,r} dpre[b,r,o]
+ * Deterministic two-stage reduction through `workspace`
+ * (cfsd_spiral_conv_bwd_weight_workspace() bytes). */
+int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, const float* dpre, float* dw,
+                                float* db, float* workspace, size_t workspace_bytes, int batch,
+                                int vsrc, int rows, int seq, int cin, int cout, void* stream);
+size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int seq, int cin, int cout);
+
+/* Materialising spiral gather, g[b,r,s*cin+c] = x[b, idx[r,s], c]
+ * (model.py:34 index_select + view).  Used as the HBM-roofline probe. */
+int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, int batch, int vsrc, int rows,
+                       int seq, int cin, void* stream);
+
+/* ---------------------------------------------------------------- Pool
+ * Replaces Pool (model.py:50-55: index_select * value, torch_scatter.scatter_add)
+ * and its autograd, as a row-sorted CSR SpMM whose per-row order is the COO
+ * file order (so the fp32 sum order equals the reference's sequential
+ * scatter_add):
+ *   y[b,r,:] = g(b,r,:) * sum_{k in row r} val[k] * x[b, col[k], :]
+ * with g = elu'(elu_y) when elu_y != NULL (fuses the ELU backward of the
+ * tensor the transpose product returns a gradient for), else 1.
+ * x [batch, n, c], y [batch, m, c]; c % 4 == 0. */
+int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const float* val, const float* x,
+                  const float* elu_y, float* y, int batch, int m, int n, int c, void* stream);
+
+/* ---------------------------------------------------------------- feature swap
+ * Replaces SwapFeatures.__call__ / swap (swap_batch_transform.py:13-52):
+ *   out[i*bs+j, v, :] = x[mesh[(i != j && mask[key*nv + v]) ? j : i], v, :]
+ * x [n_meshes, nv, c] resident dataset, batch_idx [bs] device indices of the
+ * base meshes, region_mask [n_regions, nv] (1 = feature vertex of the region),
+ * key: device int32 scalar (region index).  Bit-exact copy. */
+int cfsd_swap_features(const float* x, const int32_t* batch_idx, const uint8_t* region_mask,
+                       const int32_t* key, float* out, int bs, int nv, int c, int n_meshes,
+                       void* stream);
+
+/* ---------------------------------------------------------------- dense layers
+ * nn.Linear of the latent bottleneck (model.py:114-124, 153-156, 167):
+ *   y[i,n] = bias[n] + sum_k x[i,k] w[n,k]      x [m,k], w [n,k], y [m,n] */
+int cfsd_linear_fwd(const float* x, const float* w, const float* bias, float* y, int m, int k,
+                    int n, void* stream);
+/* Linear backward: dx = dy.w (+ optional elu' scale from elu_y [m,k]; accumulate
+ * into dx when accumulate != 0), dw = dy^T.x, db = sum_i dy.  dx/dw/db may be NULL. */
+int cfsd_linear_bwd(const float* x, const float* w, const float* dy, const float* elu_y, float* dx,
+                    float* dw, float* db, int m, int k, int n, int accumulate, void* stream);
+
+/* ---------------------------------------------------------------- losses
+ * compute_mse_loss + _compute_laplacian_regularizer (model_manager.py:333-349,
+ * utils.py:153-165) fused.  Pass 1 computes, per (b,v), Lx = sum_k L[v,k] pred[b,k,:]
+ * (CSR of the random-walk Laplacian, per-row order = COO order), stores the
+ * unit vector Lx/|Lx| in unit_lx [batch, nv, c] and writes per-block partial
+ * sums {sum (pred-gt)^2, sum |Lx|} to partials[2*nblocks] (nblocks from
+ * cfsd_recon_lap_blocks).  Pass 2 writes the gradient of
+ *   w_rec * mse + w_lap * sum|Lx| / (nv*batch)
+ * w.r.t. pred into dpred using the transpose CSR (lt_*). */
+int cfsd_recon_lap_blocks(int batch, int nv);
+int cfsd_recon_lap_fwd(const float* pred, const float* gt, const int32_t* l_ptr,
+                       const int32_t* l_col, const float* l_val, float* unit_lx, float* partials,
+                       int batch, int nv, int c, void* stream);
+int cfsd_recon_lap_bwd(const float* pred, const float* gt, const float* unit_lx,
+                       const int32_t* lt_ptr, const int32_t* lt_col, const float* lt_val,
+                       float* dpred, int batch, int nv, int c, float w_rec, float w_lap,
+                       void* stream);
+
+/* Latent head, forward (model.py:146-160, 184-188; model_manager.py:352-393).
+ * mulv [batch, 2*latent] = [logvar | mu] when is_vae (the two encoder Linears
+ * stacked, logvar = en_layers[-2], mu = en_layers[-1]), else mu [batch, latent].
+ * z = mu + eps*exp(0.5*logvar) (train && is_vae), sigmoid(mu) (!is_vae && sigmoid),
+ * else mu.  KL and the latent-consistency hinge for the swapped region
+ * [key*region_size, +region_size) (key: device scalar; bs = sqrt(batch)).
+ * Writes z [batch, latent]; terms[2] = {kl, lc}; and the head's own gradient
+ * parts dlat [batch, 3*latent] = {w_lc*dLC/dz | w_kl*dKL/dmu | w_kl*dKL/dlogvar}.
+ * Single workgroup (batch <= 64, latent <= 256). */
+int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_t* key, float* z,
+                    float* dlat, float* terms, int batch, int latent, int region_size, int train,
+                    int is_vae, int sigmoid, float w_kl, float w_lc, float eta1, float eta2,
+                    void* stream);
+/* Latent head, backward: dmulv (same layout as mulv) from dz_dec (gradient of
+ * the decoder input) + dlat.  z is only read for the sigmoid AE variant. */
+int cfsd_latent_bwd(const float* mulv, const float* eps, const float* z, const float* dz_dec,
+                    const float* dlat, float* dmulv, int batch, int latent, int train, int is_vae,
+                    int sigmoid, void* stream);
+/* Reduce the recon partials + latent terms into out[5] = {rec, kl, lc, lap, tot}
+ * (tot = rec + w_kl*kl + w_lc*lc + w_lap*lap, model_manager.py:308-312) and,
+ * when acc != NULL, add them to acc[0..4] and 1 to acc[5] (per-epoch sums on
+ * device: no per-step host sync, unlike the reference's 7 .item() calls). */
+int cfsd_loss_finalize(const float* partials, int nblocks, const float* terms, float* out,
+                       float* acc, int batch, int nv, int c, float w_kl, float w_lc, float w_lap,
+                       void* stream);
+
+/* ---------------------------------------------------------------- optimiser
+ * torch.optim.Adam step (model_manager.py:69-72, 316) over one flat fp32
+ * parameter buffer.  `step` is a device int32 holding the 1-based step number
+ * t used for the bias corrections (advanced by cfsd_step_begin). */
+int cfsd_adam(float* param, const float* grad, float* m, float* v, const int32_t* step, size_t n,
+              float lr, float beta1, float beta2, float eps, float weight_decay, void* stream);
+
+/* Per-step device bookkeeping (graph-replayable, no host input):
+ * t = ++*counter; key = hash(seed, t) % n_regions (replaces random.choice,
+ * swap_batch_transform.py:26); eps[n_eps] ~ N(0,1) (replaces randn_like,
+ * model.py:187); batch_idx[q] = perm[((t-1) % n_batches)*bs + q] (or the
+ * identity when perm == NULL) — the shuffled, drop_last batch order of
+ * MeshLoader (data_loading.py:40-42).  Any of eps/key/batch_idx may be NULL. */
+int cfsd_step_begin(int32_t* counter, unsigned long long seed, float* eps, int n_eps,
+                    int32_t* key, int n_regions, int32_t* batch_idx, int bs, int n_batches,
+                    const int32_t* perm, void* stream);
+
+/* F.elu backward written from the ELU output (model.py:68,84 autograd):
+ * dx = dy * (y > 0 ? 1 : y + 1).  dx may alias dy. */
+int cfsd_elu_bwd(const float* dy, const float* y, float* dx, size_t n, void* stream);
+
+/* Element-wise y *= alpha (gradient averaging after an all-reduce). */
+int cfsd_scale(float* y, size_t n, float alpha, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFSD_H */

@@ -1,0 +1,262 @@
+"""HIP path vs the CPU oracle and the reference goldens (needs an MI355X).
+
+Tolerances (fp32 everywhere):
+* per-vertex L1 of reconstructions <= 1e-4 (BASELINE north_star), z <= 1e-4;
+* per-op results: |hip - oracle| <= 1e-5 * (1 + max|oracle|) unless stated;
+* Pool forward / backward and the feature swap: bit-exact (same fp32
+  operation order as the reference's sequential scatter_add / index_add_).
+"""
+import numpy as np
+import pytest
+import torch
+
+import cfsd_loader
+import recipe
+from oracle import cfsd_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+cfsd_loader.load()
+from craniofacialsd_vae_amd import engine as E  # noqa: E402
+from craniofacialsd_vae_amd import ops, topology  # noqa: E402
+
+DEV = "cuda"
+torch.set_num_threads(1)
+
+
+def close(a, b, rel=1e-5, what=""):
+    a = a.detach().cpu().double().numpy() if torch.is_tensor(a) else np.asarray(a, np.float64)
+    b = b.detach().cpu().double().numpy() if torch.is_tensor(b) else np.asarray(b, np.float64)
+    tol = rel * (1.0 + np.abs(b).max())
+    err = np.abs(a - b).max()
+    assert err <= tol, f"{what}: max err {err:.3e} > tol {tol:.3e}"
+
+
+@pytest.fixture(scope="module")
+def dtopo(topo_npz):
+    return topology.DeviceTopology.from_npz(topo_npz, device=DEV)
+
+
+# --------------------------------------------------------------- spiral conv
+CONV_CASES = [(3, 32, 3), (32, 32, 3), (32, 64, 3), (64, 32, 2), (64, 64, 2), (32, 3, 1),
+              (32, 32, 1), (3, 32, 0), (32, 3, 0)]
+
+
+@pytest.mark.parametrize("cin,cout,level", CONV_CASES)
+@pytest.mark.parametrize("act", [0, 1])
+def test_spiral_conv_fwd(otopo, dtopo, cin, cout, level, act):
+    g = torch.Generator().manual_seed(cin * 100 + cout + level)
+    sp = otopo.spirals[level]
+    v = sp.shape[0]
+    bsz = 3 if v < 2000 else 2
+    x = torch.randn(bsz, v, cin, generator=g)
+    w = torch.randn(cout, 9 * cin, generator=g) * 0.1
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = O.spiral_conv(x, sp, w, b)
+    if act:
+        ref = O.elu(ref)
+    y = ops.spiral_conv_fwd(x.to(DEV), dtopo.spiral[level], w.to(DEV), b.to(DEV), act)
+    close(y, ref, 1e-5, "conv fwd")
+
+
+@pytest.mark.parametrize("cin,cout,level", [c for c in CONV_CASES if c[0] != 3])
+@pytest.mark.parametrize("use_elu_y", [False, True])
+def test_spiral_conv_bwd(otopo, dtopo, cin, cout, level, use_elu_y):
+    g = torch.Generator().manual_seed(7 + cin + cout + level)
+    sp = otopo.spirals[level]
+    v = sp.shape[0]
+    bsz = 3 if v < 2000 else 2
+    x = torch.randn(bsz, v, cin, generator=g).requires_grad_()
+    xin = O.elu(x) if use_elu_y else x
+    w = (torch.randn(cout, 9 * cin, generator=g) * 0.1).requires_grad_()
+    b = (torch.randn(cout, generator=g) * 0.1).requires_grad_()
+    xin_leaf = xin.detach().requires_grad_()
+    y = O.spiral_conv(xin_leaf, sp, w, b)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy)
+    dx_ref = xin_leaf.grad
+    if use_elu_y:
+        dx_ref = torch.autograd.grad(xin, x, dx_ref)[0]
+    dpre = dy.to(DEV)
+    dx = ops.spiral_conv_bwd_data(dpre, dtopo.spiral_inv[level], w.detach().to(DEV), v,
+                                  elu_y=xin.detach().to(DEV) if use_elu_y else None)
+    close(dx, dx_ref, 1e-5, "conv dx")
+    dw = torch.empty(cout, 9 * cin, device=DEV)
+    db = torch.empty(cout, device=DEV)
+    ws = torch.empty(ops.spiral_conv_bwd_weight_workspace(bsz, v, 9, cin, cout) // 4 + 1, device=DEV)
+    ops.spiral_conv_bwd_weight(xin.detach().to(DEV).contiguous(), dtopo.spiral[level], dpre, dw, db, ws)
+    close(dw, w.grad, 1e-5, "conv dw")
+    close(db, b.grad, 1e-5, "conv db")
+
+
+def test_spiral_conv_e0_weight_grad(otopo, dtopo):
+    g = torch.Generator().manual_seed(3)
+    sp = otopo.spirals[0]
+    x = torch.randn(2, sp.shape[0], 3, generator=g)
+    w = (torch.randn(32, 27, generator=g) * 0.1).requires_grad_()
+    b = torch.zeros(32).requires_grad_()
+    sel = torch.from_numpy(otopo.down[0][1])
+    y = O.spiral_conv(x, sp, w, b)[:, sel]
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy)
+    dw = torch.empty(32, 27, device=DEV)
+    db = torch.empty(32, device=DEV)
+    ws = torch.empty(ops.spiral_conv_bwd_weight_workspace(2, 4260, 9, 3, 32) // 4 + 1, device=DEV)
+    ops.spiral_conv_bwd_weight(x.to(DEV), dtopo.enc_rows[0], dy.to(DEV), dw, db, ws)
+    close(dw, w.grad, 1e-5, "E0 dw")
+    close(db, b.grad, 1e-5, "E0 db")
+
+
+def test_enblock_row_subset_equals_conv_then_pool(otopo, dtopo):
+    """Pool(down) of a selection transform == conv evaluated at kept rows."""
+    g = torch.Generator().manual_seed(5)
+    for level in range(4):
+        sp = otopo.spirals[level]
+        cin = 3 if level == 0 else 32
+        x = torch.randn(2, sp.shape[0], cin, generator=g)
+        w = torch.randn(32, 9 * cin, generator=g) * 0.1
+        b = torch.randn(32, generator=g) * 0.1
+        ref = O.pool(O.elu(O.spiral_conv(x, sp, w, b)), otopo.down[level])
+        y = ops.spiral_conv_fwd(x.to(DEV), dtopo.enc_rows[level], w.to(DEV), b.to(DEV), 1)
+        close(y, ref, 1e-5, f"enblock level {level}")
+
+
+# --------------------------------------------------------------- pool
+@pytest.mark.parametrize("level", [0, 1, 2, 3])
+@pytest.mark.parametrize("kind", ["up", "down"])
+def test_pool_bit_exact(otopo, dtopo, level, kind):
+    coo = (otopo.up if kind == "up" else otopo.down)[level]
+    csr = (dtopo.up_csr if kind == "up" else dtopo.down_csr)[level]
+    csrT = (dtopo.upT_csr if kind == "up" else dtopo.downT_csr)[level]
+    m, n = coo[3]
+    g = torch.Generator().manual_seed(level)
+    x = torch.randn(2, n, 32, generator=g).requires_grad_()
+    out = O.pool(x, coo)
+    dout = torch.randn(out.shape, generator=g)
+    out.backward(dout)
+    y = ops.spmm(csr, x.detach().to(DEV), m)
+    np.testing.assert_array_equal(y.cpu().numpy(), out.detach().numpy())
+    dx = ops.spmm(csrT, dout.to(DEV), n)
+    np.testing.assert_array_equal(dx.cpu().numpy(), x.grad.numpy())
+
+
+def test_pool_golden(dtopo):
+    gops = np.load(f"{recipe.HERE}/golden_ops.npz")
+    for name, level, kind in (("down3", 3, "down"), ("up3", 3, "up"), ("up2", 2, "up")):
+        csr = (dtopo.up_csr if kind == "up" else dtopo.down_csr)[level]
+        csrT = (dtopo.upT_csr if kind == "up" else dtopo.downT_csr)[level]
+        x = torch.from_numpy(gops[f"pool_{name}_x"]).to(DEV)
+        out = gops[f"pool_{name}_out"]
+        y = ops.spmm(csr, x, out.shape[1])
+        np.testing.assert_array_equal(y.cpu().numpy(), out)
+        dx = ops.spmm(csrT, torch.from_numpy(gops[f"pool_{name}_dout"]).to(DEV), x.shape[1])
+        close(dx, gops[f"pool_{name}_dx"], 1e-6, "pool golden dx")
+
+
+def test_conv_golden(dtopo):
+    gops = np.load(f"{recipe.HERE}/golden_ops.npz")
+    x = torch.from_numpy(gops["conv_x"]).to(DEV)
+    w = torch.from_numpy(gops["conv_w"]).to(DEV)
+    b = torch.from_numpy(gops["conv_b"]).to(DEV)
+    y = ops.spiral_conv_fwd(x, dtopo.spiral[3], w, b, 0)
+    close(y, gops["conv_y"], 1e-5, "golden conv y")
+    dy = torch.from_numpy(gops["conv_dy"]).to(DEV)
+    dx = ops.spiral_conv_bwd_data(dy, dtopo.spiral_inv[3], w, 267)
+    close(dx, gops["conv_dx"], 1e-5, "golden conv dx")
+    dw = torch.empty_like(w)
+    db = torch.empty_like(b)
+    ws = torch.empty(ops.spiral_conv_bwd_weight_workspace(2, 267, 9, 32, 64) // 4 + 1, device=DEV)
+    ops.spiral_conv_bwd_weight(x, dtopo.spiral[3], dy, dw, db, ws)
+    close(dw, gops["conv_dw"], 1e-5, "golden conv dw")
+    close(db, gops["conv_db"], 1e-5, "golden conv db")
+
+
+# --------------------------------------------------------------- swap
+def test_swap_bit_exact(otopo, dtopo):
+    gsw = np.load(f"{recipe.HERE}/golden_swap.npz")
+    base = torch.from_numpy(recipe.normalized_meshes(4)).to(DEV)
+    bidx = torch.arange(4, dtype=torch.int32, device=DEV)
+    key = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for k in range(dtopo.n_regions):
+        key.fill_(k)
+        out = ops.swap_features(base, bidx, dtopo.region_mask, key, 4)
+        assert recipe.sha256(out.cpu().numpy()) == str(gsw["sha"][k]), k
+
+
+# --------------------------------------------------------------- full model
+def make_engine(dtopo, weights, bs=4):
+    eng = E.SDVAEEngine(dtopo, E.ModelSpec(), swap_bs=bs, device=DEV)
+    eng.load_state_dict({k: torch.from_numpy(v) for k, v in weights.items()})
+    return eng
+
+
+def test_state_dict_keys_match_reference(dtopo):
+    eng = make_engine(dtopo, recipe.golden_weights())
+    assert list(eng.state_dict().keys()) == [k for k, _ in recipe.param_shapes()]
+
+
+def test_eval_c1_golden(dtopo):
+    """C1: encode+decode of the first 8 demo meshes, eval mode (z = mu)."""
+    g = np.load(f"{recipe.HERE}/golden_eval.npz")
+    eng = make_engine(dtopo, recipe.golden_weights())
+    b = eng.set_batch(torch.from_numpy(recipe.normalized_meshes(8)).to(DEV))
+    eng.forward(b, train=False)
+    torch.cuda.synchronize()
+    d = np.abs(b.out.cpu().numpy() - g["recon"]).sum(-1)
+    assert d.max() <= 1e-4, f"max per-vertex L1 {d.max():.3e}"
+    assert np.abs(b.z.cpu().numpy() - g["z"]).max() <= 1e-4
+    assert np.abs(b.mulv[:, 75:].cpu().numpy() - g["mu"]).max() <= 1e-4
+    assert np.abs(b.mulv[:, :75].cpu().numpy() - g["logvar"]).max() <= 1e-4
+
+
+def test_train_three_steps_golden(otopo, dtopo):
+    """C2: three reference train steps (swap, fwd, 4 losses, bwd, Adam)."""
+    g = np.load(f"{recipe.HERE}/golden_train.npz")
+    w = recipe.golden_weights()
+    eng = make_engine(dtopo, w)
+    # oracle in lock-step for full-tensor gradient comparison
+    P = O.make_params(w)
+    opt = O.Adam(P)
+    meshes = recipe.normalized_meshes(12)
+    data = torch.from_numpy(meshes).to(DEV)
+    for step in range(3):
+        p = f"s{step}_"
+        key = recipe.train_key_index(step)
+        eps = torch.from_numpy(recipe.train_eps(step))
+        out, grads, x16 = O.train_step(P, opt, meshes[4 * step:4 * step + 4], otopo, key, eps.numpy())
+        b = eng.buffers(16)
+        b.key.fill_(key)
+        b.eps.copy_(eps)
+        b.batch_idx.copy_(torch.arange(4 * step, 4 * step + 4, dtype=torch.int32))
+        ops.swap_features(data, b.batch_idx, dtopo.region_mask, b.key, 4, out=b.x)
+        eng.train_step_on(b)
+        torch.cuda.synchronize()
+        assert recipe.sha256(b.x.cpu().numpy()) == str(g[p + "x_sha"])
+        got = b.losses.cpu().numpy()
+        np.testing.assert_allclose(got, g[p + "losses"], rtol=1e-4)
+        np.testing.assert_allclose(b.z.cpu().numpy(), g[p + "z"], atol=1e-4)
+        hip_grads = {k: v.cpu() for k, v in eng.grads().items()}
+        for name in w:
+            close(hip_grads[name], grads[name], 1e-4, f"step {step} grad {name}")
+        sd = eng.state_dict()
+        for name in w:
+            close(sd[name], P[name].detach(), 2e-5, f"step {step} param {name}")
+            ps = sd[name].cpu().numpy().ravel()
+            np.testing.assert_allclose(ps[recipe.sample_idx(ps.size)], g[p + "param_sample_" + name],
+                                       atol=2e-5)
+
+
+def test_train_step_deterministic(dtopo):
+    w = recipe.golden_weights()
+    outs = []
+    for _ in range(2):
+        eng = make_engine(dtopo, w)
+        b = eng.set_batch(torch.from_numpy(
+            O.swap_features(recipe.normalized_meshes(4), [np.asarray(r) for r in
+                                                          O.Topology(recipe.load_topology()).region_features], 2)).to(DEV),
+            key_index=2, eps=torch.from_numpy(recipe.train_eps(0)).to(DEV))
+        eng.train_step_on(b)
+        torch.cuda.synchronize()
+        outs.append((eng.params.data.cpu().clone(), eng.params.grad.cpu().clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

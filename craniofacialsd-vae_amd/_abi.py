@@ -25,14 +25,15 @@ SIGNATURES = {
     "cfsd_version": (_I, []),
     "cfsd_last_error_string": (ctypes.c_char_p, []),
     "cfsd_spiral_conv_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
-    "cfsd_spiral_conv_bwd_data": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "cfsd_spiral_conv_bwd_data": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_weight": (_I, [_P, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_weight_workspace": (_Z, [_I, _I, _I, _I, _I]),
     "cfsd_spiral_gather": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spmm_csr": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "cfsd_swap_features": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
-    "cfsd_linear_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
-    "cfsd_linear_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "cfsd_linear_workspace": (_Z, [_I, _I, _I]),
+    "cfsd_linear_fwd": (_I, [_P, _P, _P, _P, _P, _Z, _I, _I, _I, _P]),
+    "cfsd_linear_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _P]),
     "cfsd_recon_lap_blocks": (_I, [_I, _I]),
     "cfsd_recon_lap_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "cfsd_recon_lap_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P]),

@@ -6,473 +6,665 @@
 // contraction: every 32-row output tile is one v_mfma_f32_32x32x2_f32
 // accumulator chain whose A operand is gathered straight from HBM/L2 into
 // VGPRs (each lane pair reads one 128-B neighbour row with 16-B loads) and
-// whose B operand (the weights) is staged once per workgroup in LDS.
+// whose B operand (the weights) is staged once per persistent workgroup in LDS.
 //
 // K ordering inside one spiral slot is permuted (lane half h owns channels
 // [h*C/2, h*C/2 + C/2)): MFMA step j sums A[i][h]*B[h][n] over h, so slot s's
 // dot product is accumulated as pairs (j, j + C/2).  This is exact f32 (the
 // f32 MFMA is a k-ordered fmaf chain), only the summation order differs from
 // ATen's sgemm.
+//
+// Channel counts of 3 (xyz in/out: the first Enblock and the last decoder
+// conv) would waste 29/32 of an MFMA tile, so those layers run on VALU
+// kernels shaped for them (lane-per-output-channel or 8-lanes-per-row).
 #include "cfsd_common.h"
 
 namespace cfsd {
 
-// --------------------------------------------------------------------------
-// Forward, MFMA path: CIN in {32, 64}, COUT in {32, 64}.
-// Block = 256 threads = 4 waves; wave w owns output rows [m0 + 32w, +32) of
-// the flattened (b, r) row space and all COUT columns.
-// W staged in LDS as [COUT][K + 4] (pad 4 floats: 16-lane ds_read_b128
-// groups hit distinct 16-B slots for K = 288 and 576).
+constexpr int kSeq = 9;  // spiral length of every configuration (craniofacial/body/default.yaml)
+
+// Persistent-grid geometry: enough blocks for ~4 per CU, tiles spread evenly.
+static inline unsigned persistent_blocks(long n_tiles, int tiles_per_block_unit, long max_blocks) {
+  long units = (n_tiles + tiles_per_block_unit - 1) / tiles_per_block_unit;
+  if (units <= max_blocks) return (unsigned)(units > 0 ? units : 1);
+  long per = (units + max_blocks - 1) / max_blocks;
+  return (unsigned)((units + per - 1) / per);
+}
+
+// ==========================================================================
+// Forward, MFMA path: CIN, COUT in {32, 64}.  Each wave owns 32-row tiles of
+// the flattened (b, r) row space (all COUT columns) and loops over them.
+// W staged in LDS as [COUT][K + 4] (pad: 16-lane ds_read_b128 groups hit
+// distinct 16-B slots for K = 288 and 576).
+// Occupancy target per channel shape (min waves per SIMD -> VGPR budget).
+constexpr int mfma_occ(int cin, int cout) { return (cin == 32 && cout == 32) ? 4 : 2; }
+
 template <int CIN, int COUT, int ACT, bool W_LDS>
-__global__ __launch_bounds__(256) void conv_fwd_mfma(const float* __restrict__ x,
+__global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(const float* __restrict__ x,
                                                      const int* __restrict__ idx,
                                                      const float* __restrict__ w,
                                                      const float* __restrict__ bias,
                                                      float* __restrict__ y, int vsrc, int rows,
-                                                     int seq, long total_rows) {
-  constexpr int HALF = CIN / 2;   // channels per lane half
-  constexpr int NT = COUT / 32;   // 32-wide output tiles
+                                                     long total_rows) {
+  constexpr int HALF = CIN / 2;
+  constexpr int NT = COUT / 32;
+  constexpr int K = kSeq * CIN;
+  constexpr int KP = K + 4;
   extern __shared__ float lds_w[];
-  const int K = seq * CIN;
-  const int KP = K + 4;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-
   if (W_LDS) {
-    for (int i = threadIdx.x; i < COUT * (K / 4); i += 256) {
-      int n = i / (K / 4), k4 = i % (K / 4);
+    for (int e = threadIdx.x; e < COUT * (K / 4); e += 256) {
+      const int n = e / (K / 4), k4 = e % (K / 4);
       st4(&lds_w[n * KP + 4 * k4], ld4(&w[(long)n * K + 4 * k4]));
     }
     __syncthreads();
   }
-
-  const long m0 = (long)blockIdx.x * 128 + wave * 32;
-  if (m0 >= total_rows) return;
   const int i = lane & 31, h = lane >> 5;
-  long m = m0 + i;
-  if (m >= total_rows) m = total_rows - 1;  // clamp loads, stores are masked
-  const int b = (int)(m / rows), r = (int)(m % rows);
-  const float* xb = x + (long)b * vsrc * CIN + h * HALF;
-  const int* irow = idx + (long)r * seq;
-
-  f32x16 acc[NT];
+  float bn[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = (f32x16){0.f};
-
-  float a[HALF], an[HALF];
-  {
-    const float* src = xb + (long)irow[0] * CIN;
+  for (int t = 0; t < NT; ++t) bn[t] = bias ? bias[t * 32 + i] : 0.f;
+  const long n_tiles = (total_rows + 31) / 32;
+  for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
+    const long m0 = tile * 32;
+    long m = m0 + i;
+    if (m >= total_rows) m = total_rows - 1;  // clamp loads, stores are masked
+    const int b = (int)(m / rows), r = (int)(m % rows);
+    const float* xb = x + (long)b * vsrc * CIN + h * HALF;
+    const int* ir = idx + (long)r * kSeq;
+    f32x16 acc[NT];
 #pragma unroll
-    for (int q = 0; q < HALF / 4; ++q) {
-      f32x4 v = ld4(src + 4 * q);
-      a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-    }
-  }
-  for (int s = 0; s < seq; ++s) {
-    if (s + 1 < seq) {  // prefetch next slot's neighbour row
-      const float* src = xb + (long)irow[s + 1] * CIN;
+    for (int t = 0; t < NT; ++t) acc[t] = (f32x16){0.f};
+    // software pipeline: neighbour row of slot s+1 and index of slot s+2 are
+    // in flight while slot s runs its MFMAs (loop kept rolled: a full unroll
+    // makes hipcc hoist all nine gathers and spill).
+    f32x4 a[HALF / 4], an[HALF / 4];
+    int src_n = ir[1];
 #pragma unroll
-      for (int q = 0; q < HALF / 4; ++q) {
-        f32x4 v = ld4(src + 4 * q);
-        an[4 * q] = v.x; an[4 * q + 1] = v.y; an[4 * q + 2] = v.z; an[4 * q + 3] = v.w;
+    for (int q = 0; q < HALF / 4; ++q) a[q] = ld4(xb + (long)ir[0] * CIN + 4 * q);
+#pragma unroll 1
+    for (int s = 0; s < kSeq; ++s) {
+      if (s + 1 < kSeq) {
+        const int src_nn = (s + 2 < kSeq) ? ir[s + 2] : 0;
+#pragma unroll
+        for (int q = 0; q < HALF / 4; ++q) an[q] = ld4(xb + (long)src_n * CIN + 4 * q);
+        src_n = src_nn;
       }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = t * 32 + i;
+        const float* wr = W_LDS ? &lds_w[n * KP + s * CIN + h * HALF]
+                                : &w[(long)n * K + s * CIN + h * HALF];
+#pragma unroll
+        for (int q = 0; q < HALF / 4; ++q) {
+          const f32x4 bw = ld4(wr + 4 * q);
+          acc[t] = mfma32(a[q].x, bw.x, acc[t]);
+          acc[t] = mfma32(a[q].y, bw.y, acc[t]);
+          acc[t] = mfma32(a[q].z, bw.z, acc[t]);
+          acc[t] = mfma32(a[q].w, bw.w, acc[t]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < HALF / 4; ++q) a[q] = an[q];
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int n = t * 32 + i;
-      const float* wr = W_LDS ? &lds_w[n * KP + s * CIN + h * HALF]
-                              : &w[(long)n * K + s * CIN + h * HALF];
 #pragma unroll
-      for (int q = 0; q < HALF / 4; ++q) {
-        f32x4 bw = ld4(wr + 4 * q);
-        acc[t] = mfma32(a[4 * q + 0], bw.x, acc[t]);
-        acc[t] = mfma32(a[4 * q + 1], bw.y, acc[t]);
-        acc[t] = mfma32(a[4 * q + 2], bw.z, acc[t]);
-        acc[t] = mfma32(a[4 * q + 3], bw.w, acc[t]);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < HALF; ++q) a[q] = an[q];
-  }
-
-  // epilogue: bias + activation, lanes 0..31 / 32..63 each store one
-  // 128-B row segment per register.
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int n = t * 32 + i;
-    const float bn = bias ? bias[n] : 0.f;
-#pragma unroll
-    for (int rr = 0; rr < 16; ++rr) {
-      long mo = m0 + acc_row(rr, lane);
-      if (mo < total_rows) {
-        float v = acc[t][rr] + bn;
-        if (ACT == CFSD_ACT_ELU) v = elu_f(v);
-        y[mo * COUT + n] = v;
+      for (int rr = 0; rr < 16; ++rr) {
+        const long mo = m0 + acc_row(rr, lane);
+        if (mo < total_rows) {
+          float v = acc[t][rr] + bn[t];
+          if (ACT == CFSD_ACT_ELU) v = elu_f(v);
+          y[mo * COUT + n] = v;
+        }
       }
     }
   }
 }
 
-// --------------------------------------------------------------------------
-// Forward, VALU path for tiny channel counts (E0: CIN = 3; Dout: COUT = 3).
-// One thread per output row; weights are read with wave-uniform addresses
-// (scalar loads), neighbour rows with plain loads.
-template <int CIN, int COUT, int ACT>
-__global__ __launch_bounds__(256) void conv_fwd_small(const float* __restrict__ x,
-                                                      const int* __restrict__ idx,
-                                                      const float* __restrict__ w,
-                                                      const float* __restrict__ bias,
-                                                      float* __restrict__ y, int vsrc, int rows,
-                                                      int seq, long total_rows) {
-  long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
+// Forward, small input (CS <= 4 channels, e.g. the xyz input of the first
+// Enblock): one lane per (row, output channel).  The CS*kSeq gathered inputs
+// of a row are the same for its COUT lanes (broadcast loads); each lane keeps
+// its weight row in registers.
+template <int CS, int COUT, int ACT>
+__global__ __launch_bounds__(256) void conv_fwd_in_small(const float* __restrict__ x,
+                                                         const int* __restrict__ idx,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ bias,
+                                                         float* __restrict__ y, int vsrc,
+                                                         int rows, long total_rows) {
+  constexpr int K = kSeq * CS;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int o = (int)(t % COUT);
+  const long m = t / COUT;
   if (m >= total_rows) return;
+  float wr[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) wr[k] = w[o * K + k];
   const int b = (int)(m / rows), r = (int)(m % rows);
-  const float* xb = x + (long)b * vsrc * CIN;
-  const int K = seq * CIN;
-  float acc[COUT];
+  const float* xb = x + (long)b * vsrc * CS;
+  float acc = bias ? bias[o] : 0.f;
 #pragma unroll
-  for (int o = 0; o < COUT; ++o) acc[o] = 0.f;
-  for (int s = 0; s < seq; ++s) {
-    const float* src = xb + (long)idx[(long)r * seq + s] * CIN;
-    float xv[CIN];
-    if (CIN % 4 == 0) {
+  for (int s = 0; s < kSeq; ++s) {
+    const float* p = xb + (long)idx[(long)r * kSeq + s] * CS;
 #pragma unroll
-      for (int q = 0; q < CIN / 4; ++q) {
-        f32x4 v = ld4(src + 4 * q);
-        xv[4 * q] = v.x; xv[4 * q + 1] = v.y; xv[4 * q + 2] = v.z; xv[4 * q + 3] = v.w;
-      }
-    } else {
+    for (int c = 0; c < CS; ++c) acc = fmaf(p[c], wr[s * CS + c], acc);
+  }
+  if (ACT == CFSD_ACT_ELU) acc = elu_f(acc);
+  y[m * COUT + o] = acc;
+}
+
+// Forward, small output (CO <= 4 channels, e.g. the xyz output conv):
+// L = CIN/4 lanes per row, each lane owns a float4 of input channels of every
+// neighbour row (so a neighbour row is one coalesced 16*L-byte read), then
+// the CO partial dots are reduced across the L lanes with xor shuffles.
+template <int CIN, int CO, int ACT>
+__global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restrict__ x,
+                                                          const int* __restrict__ idx,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ y, int vsrc,
+                                                          int rows, long total_rows) {
+  constexpr int L = CIN / 4;
+  constexpr int K = kSeq * CIN;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = (int)(t % L);
+  long m = t / L;
+  const bool valid = m < total_rows;
+  if (!valid) m = total_rows - 1;
+  f32x4 wr[kSeq][CO];
 #pragma unroll
-      for (int c = 0; c < CIN; ++c) xv[c] = src[c];
-    }
+  for (int s = 0; s < kSeq; ++s)
 #pragma unroll
-    for (int o = 0; o < COUT; ++o) {
-      const float* wr = w + (long)o * K + s * CIN;
+    for (int o = 0; o < CO; ++o) wr[s][o] = ld4(w + (long)o * K + s * CIN + 4 * q);
+  const int b = (int)(m / rows), r = (int)(m % rows);
+  const float* xb = x + (long)b * vsrc * CIN + 4 * q;
+  float acc[CO];
 #pragma unroll
-      for (int c = 0; c < CIN; ++c) acc[o] = fmaf(xv[c], wr[c], acc[o]);
+  for (int o = 0; o < CO; ++o) acc[o] = 0.f;
+#pragma unroll
+  for (int s = 0; s < kSeq; ++s) {
+    const f32x4 v = ld4(xb + (long)idx[(long)r * kSeq + s] * CIN);
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      acc[o] = fmaf(v.x, wr[s][o].x, acc[o]);
+      acc[o] = fmaf(v.y, wr[s][o].y, acc[o]);
+      acc[o] = fmaf(v.z, wr[s][o].z, acc[o]);
+      acc[o] = fmaf(v.w, wr[s][o].w, acc[o]);
     }
   }
 #pragma unroll
-  for (int o = 0; o < COUT; ++o) {
-    float v = acc[o] + (bias ? bias[o] : 0.f);
-    if (ACT == CFSD_ACT_ELU) v = elu_f(v);
-    y[m * COUT + o] = v;
+  for (int o = 0; o < CO; ++o)
+#pragma unroll
+    for (int d = L / 2; d >= 1; d >>= 1) acc[o] += __shfl_xor(acc[o], d);
+  if (valid && q == 0) {
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      float v = acc[o] + (bias ? bias[o] : 0.f);
+      if (ACT == CFSD_ACT_ELU) v = elu_f(v);
+      y[m * CO + o] = v;
+    }
   }
 }
 
-// --------------------------------------------------------------------------
+// ==========================================================================
 // Backward data, MFMA path.  dx rows are source vertices u (flattened with
 // b).  For slot s the A operand is T_s[u, :] = sum_{r in inv(u,s)} dpre[r, :]
-// (gather-sum through the inverse-spiral CSR, fixed order -> deterministic),
-// the B operand is W_s^T staged in LDS as [s][c][COUT + 4].
+// (gather-sum through the inverse spiral, fixed order -> deterministic); the
+// B operand is W_s^T staged in LDS as [s][c][COUT + 4].
+// inv_pair[u*S + s] = the first two rows of inv(u,s) (-1 if absent): those
+// loads are issued unconditionally one slot ahead; the rare further entries
+// (inv_ptr/inv_row from offset 2) are summed in a short loop.
 template <int CIN, int COUT, bool W_LDS>
-__global__ __launch_bounds__(256) void conv_dx_mfma(const float* __restrict__ dpre,
+__global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(const float* __restrict__ dpre,
                                                     const int* __restrict__ inv_ptr,
                                                     const int* __restrict__ inv_row,
+                                                    const int2* __restrict__ inv_pair,
                                                     const float* __restrict__ w,
                                                     const float* __restrict__ elu_y,
                                                     float* __restrict__ dx, int vsrc, int rows,
-                                                    int seq, long total_rows) {
-  constexpr int HALF = COUT / 2;  // reduction channels (o) per lane half
-  constexpr int NT = CIN / 32;    // output tiles over c
+                                                    long total_rows) {
+  constexpr int HALF = COUT / 2;
+  constexpr int NT = CIN / 32;
   constexpr int OP = COUT + 4;
+  constexpr int K = kSeq * CIN;
   extern __shared__ float lds_wt[];
-  const int K = seq * CIN;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-
   if (W_LDS) {
-    // lds_wt[(s*CIN + c) * OP + o] = w[o, s*CIN + c]
     for (int e = threadIdx.x; e < COUT * K; e += 256) {
-      int o = e / K, k = e % K;
+      const int o = e / K, k = e % K;
       lds_wt[k * OP + o] = w[e];
     }
     __syncthreads();
   }
-
-  const long m0 = (long)blockIdx.x * 128 + wave * 32;
-  if (m0 >= total_rows) return;
   const int i = lane & 31, h = lane >> 5;
-  long m = m0 + i;
-  if (m >= total_rows) m = total_rows - 1;
-  const int b = (int)(m / vsrc), u = (int)(m % vsrc);
-  const float* db_ = dpre + (long)b * rows * COUT + h * HALF;
-  const int* pu = inv_ptr + (long)u * seq;
-
-  f32x16 acc[NT];
+  const long n_tiles = (total_rows + 31) / 32;
+  for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
+    const long m0 = tile * 32;
+    long m = m0 + i;
+    if (m >= total_rows) m = total_rows - 1;
+    const int b = (int)(m / vsrc), u = (int)(m % vsrc);
+    const float* db_ = dpre + (long)b * rows * COUT + h * HALF;
+    const int2* pu = inv_pair + (long)u * kSeq;
+    f32x16 acc[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = (f32x16){0.f};
-
-  for (int s = 0; s < seq; ++s) {
-    float a[HALF];
+    for (int t = 0; t < NT; ++t) acc[t] = (f32x16){0.f};
+    // slot pipeline: rows r0/r1 of slot s+1 and the pair of slot s+2 are in
+    // flight while slot s computes (rolled loop, see conv_fwd_mfma).
+    f32x4 c0[HALF / 4], c1[HALF / 4];
+    int2 pc = pu[0], pn = pu[1];
 #pragma unroll
-    for (int q = 0; q < HALF; ++q) a[q] = 0.f;
-    const int beg = pu[s], end = pu[s + 1];
-    for (int e = beg; e < end; ++e) {
-      const float* src = db_ + (long)inv_row[e] * COUT;
+    for (int q = 0; q < HALF / 4; ++q) {
+      c0[q] = ld4(db_ + (long)max(pc.x, 0) * COUT + 4 * q);
+      c1[q] = ld4(db_ + (long)max(pc.y, 0) * COUT + 4 * q);
+    }
+#pragma unroll 1
+    for (int s = 0; s < kSeq; ++s) {
+      f32x4 a[HALF / 4];
+      const float f0 = pc.x >= 0 ? 1.f : 0.f, f1 = pc.y >= 0 ? 1.f : 0.f;
 #pragma unroll
-      for (int q = 0; q < HALF / 4; ++q) {
-        f32x4 v = ld4(src + 4 * q);
-        a[4 * q] += v.x; a[4 * q + 1] += v.y; a[4 * q + 2] += v.z; a[4 * q + 3] += v.w;
+      for (int q = 0; q < HALF / 4; ++q) a[q] = c0[q] * f0 + c1[q] * f1;
+      const bool more = pc.y >= 0;
+      if (s + 1 < kSeq) {
+        const int2 pnn = (s + 2 < kSeq) ? pu[s + 2] : make_int2(-1, -1);
+#pragma unroll
+        for (int q = 0; q < HALF / 4; ++q) {
+          c0[q] = ld4(db_ + (long)max(pn.x, 0) * COUT + 4 * q);
+          c1[q] = ld4(db_ + (long)max(pn.y, 0) * COUT + 4 * q);
+        }
+        pc = pn;
+        pn = pnn;
+      }
+      if (more) {  // rare: entries beyond the first two
+        const int beg = inv_ptr[(long)u * kSeq + s] + 2, end = inv_ptr[(long)u * kSeq + s + 1];
+        for (int e = beg; e < end; ++e) {
+          const float* p = db_ + (long)inv_row[e] * COUT;
+#pragma unroll
+          for (int q = 0; q < HALF / 4; ++q) a[q] += ld4(p + 4 * q);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int c = t * 32 + i;
+        if (W_LDS) {
+          const float* wr = &lds_wt[(s * CIN + c) * OP + h * HALF];
+#pragma unroll
+          for (int q = 0; q < HALF / 4; ++q) {
+            const f32x4 bw = ld4(wr + 4 * q);
+            acc[t] = mfma32(a[q].x, bw.x, acc[t]);
+            acc[t] = mfma32(a[q].y, bw.y, acc[t]);
+            acc[t] = mfma32(a[q].z, bw.z, acc[t]);
+            acc[t] = mfma32(a[q].w, bw.w, acc[t]);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < HALF / 4; ++q) {
+            const long wo = (long)(h * HALF + 4 * q) * K + s * CIN + c;
+            acc[t] = mfma32(a[q].x, w[wo], acc[t]);
+            acc[t] = mfma32(a[q].y, w[wo + K], acc[t]);
+            acc[t] = mfma32(a[q].z, w[wo + 2 * K], acc[t]);
+            acc[t] = mfma32(a[q].w, w[wo + 3 * K], acc[t]);
+          }
+        }
       }
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int c = t * 32 + i;
-      if (W_LDS) {
-        const float* wr = &lds_wt[(s * CIN + c) * OP + h * HALF];
 #pragma unroll
-        for (int q = 0; q < HALF / 4; ++q) {
-          f32x4 bw = ld4(wr + 4 * q);
-          acc[t] = mfma32(a[4 * q + 0], bw.x, acc[t]);
-          acc[t] = mfma32(a[4 * q + 1], bw.y, acc[t]);
-          acc[t] = mfma32(a[4 * q + 2], bw.z, acc[t]);
-          acc[t] = mfma32(a[4 * q + 3], bw.w, acc[t]);
+      for (int rr = 0; rr < 16; ++rr) {
+        const long mo = m0 + acc_row(rr, lane);
+        if (mo < total_rows) {
+          float v = acc[t][rr];
+          if (elu_y) v *= elu_grad_from_out(elu_y[mo * CIN + c]);
+          dx[mo * CIN + c] = v;
         }
-      } else {
-#pragma unroll
-        for (int q = 0; q < HALF; ++q)
-          acc[t] = mfma32(a[q], w[(long)(h * HALF + q) * K + s * CIN + c], acc[t]);
-      }
-    }
-  }
-
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int c = t * 32 + i;
-#pragma unroll
-    for (int rr = 0; rr < 16; ++rr) {
-      long mo = m0 + acc_row(rr, lane);
-      if (mo < total_rows) {
-        float v = acc[t][rr];
-        if (elu_y) v *= elu_grad_from_out(elu_y[mo * CIN + c]);
-        dx[mo * CIN + c] = v;
       }
     }
   }
 }
 
-// Backward data, VALU path for COUT = 3 (Dout): one thread per source row.
-template <int CIN, int COUT>
-__global__ __launch_bounds__(256) void conv_dx_small(const float* __restrict__ dpre,
-                                                     const int* __restrict__ inv_ptr,
-                                                     const int* __restrict__ inv_row,
-                                                     const float* __restrict__ w,
-                                                     const float* __restrict__ elu_y,
-                                                     float* __restrict__ dx, int vsrc, int rows,
-                                                     int seq, long total_rows) {
-  long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
+// Backward data, small dpre (CO <= 4 channels; the xyz output conv):
+// L = CIN/4 lanes per source row u, lane q owns dx channels [4q, 4q+4).
+template <int CIN, int CO>
+__global__ __launch_bounds__(256) void conv_dx_out_small(const float* __restrict__ dpre,
+                                                         const int* __restrict__ inv_ptr,
+                                                         const int* __restrict__ inv_row,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ elu_y,
+                                                         float* __restrict__ dx, int vsrc,
+                                                         int rows, long total_rows) {
+  constexpr int L = CIN / 4;
+  constexpr int K = kSeq * CIN;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = (int)(t % L);
+  const long m = t / L;
   if (m >= total_rows) return;
   const int b = (int)(m / vsrc), u = (int)(m % vsrc);
-  const int K = seq * CIN;
-  const float* db_ = dpre + (long)b * rows * COUT;
-  float acc[CIN];
+  const float* db_ = dpre + (long)b * rows * CO;
+  int p[kSeq + 1];
 #pragma unroll
-  for (int c = 0; c < CIN; ++c) acc[c] = 0.f;
-  for (int s = 0; s < seq; ++s) {
-    float t[COUT];
+  for (int s = 0; s <= kSeq; ++s) p[s] = inv_ptr[(long)u * kSeq + s];
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int o = 0; o < COUT; ++o) t[o] = 0.f;
-    const int beg = inv_ptr[(long)u * seq + s], end = inv_ptr[(long)u * seq + s + 1];
-    for (int e = beg; e < end; ++e) {
-      const float* src = db_ + (long)inv_row[e] * COUT;
+  for (int s = 0; s < kSeq; ++s) {
+    float tt[CO];
 #pragma unroll
-      for (int o = 0; o < COUT; ++o) t[o] += src[o];
+    for (int o = 0; o < CO; ++o) tt[o] = 0.f;
+    for (int e = p[s]; e < p[s + 1]; ++e) {
+      const float* src = db_ + (long)inv_row[e] * CO;
+#pragma unroll
+      for (int o = 0; o < CO; ++o) tt[o] += src[o];
     }
 #pragma unroll
-    for (int o = 0; o < COUT; ++o) {
-      const float* wr = w + (long)o * K + s * CIN;
-#pragma unroll
-      for (int c = 0; c < CIN; ++c) acc[c] = fmaf(t[o], wr[c], acc[c]);
+    for (int o = 0; o < CO; ++o) {
+      const f32x4 wv = ld4(w + (long)o * K + s * CIN + 4 * q);
+      acc.x = fmaf(tt[o], wv.x, acc.x);
+      acc.y = fmaf(tt[o], wv.y, acc.y);
+      acc.z = fmaf(tt[o], wv.z, acc.z);
+      acc.w = fmaf(tt[o], wv.w, acc.w);
     }
   }
-  float* out = dx + m * CIN;
-  const float* ey = elu_y ? elu_y + m * CIN : nullptr;
-#pragma unroll
-  for (int c = 0; c < CIN; ++c) out[c] = ey ? acc[c] * elu_grad_from_out(ey[c]) : acc[c];
+  if (elu_y) {
+    const f32x4 g = ld4(elu_y + m * CIN + 4 * q);
+    acc.x *= elu_grad_from_out(g.x);
+    acc.y *= elu_grad_from_out(g.y);
+    acc.z *= elu_grad_from_out(g.z);
+    acc.w *= elu_grad_from_out(g.w);
+  }
+  st4(dx + m * CIN + 4 * q, acc);
 }
 
-// --------------------------------------------------------------------------
-// Backward weight, MFMA path.  Units u = (s, ot, ct): output tile
-// dW[ot*32 .. +32][s*CIN + ct*32 .. +32].  Each wave owns UPW units and a
-// strided set of 32-row blocks; lane half h takes rows j + 16h of a block
-// (MFMA step j reduces the pair).  A = dpre^T (o on lanes), B = gathered x
-// (c on lanes).  The block's 4 wave partials are summed through LDS in
-// wave order and written as one slab: ws[(blockIdx.x * gridDim.y + y) * UPW * 1024].
-// db partials (sum over rows of dpre) go to ws_db[blockIdx.x * COUT + o] from
-// the y == 0 blocks.
-template <int CIN, int COUT, int UPW>
-__global__ __launch_bounds__(256) void conv_dw_mfma(const float* __restrict__ x,
-                                                    const int* __restrict__ idx,
-                                                    const float* __restrict__ dpre,
-                                                    float* __restrict__ ws,
-                                                    float* __restrict__ ws_db, int vsrc,
-                                                    int rows, int seq, long total_rows) {
+// ==========================================================================
+// Backward weight, MFMA path, LDS-staged.  A block owns 32-row tiles in a
+// persistent loop.  Per tile, all threads stage dpre[32][COUT] and the
+// gathered x for every slot, x_lds[s][32][CIN], into LDS (coalesced 16-B
+// loads, the NEXT tile's loads are in flight in registers during this tile's
+// MFMAs).  The U = kSeq*(COUT/32)*(CIN/32) output tiles (s, ot, ct) of
+// dW[32 o][32 c] are split evenly over the block's WAVES waves, each keeping
+// its UPW accumulators across all tiles: A = dpre^T (o on lanes), B = x
+// (c on lanes), MFMA step j reduces rows (j, j+16).  The block writes one
+// slab [U][32][32] + db partial; cfsd_dw_reduce sums slabs in fixed order.
+template <int CIN, int COUT>
+struct DwCfg {
+  static constexpr int U = kSeq * (COUT / 32) * (CIN / 32);
+  static constexpr int WAVES = (U % 4 == 0) ? 4 : 3;
+  static constexpr int UPW = U / WAVES;
+  static constexpr int THREADS = WAVES * 64;
+  static constexpr int XF4 = kSeq * 32 * CIN / 4;  // float4s of gathered x per tile
+  static constexpr int DF4 = 32 * COUT / 4;        // float4s of dpre per tile
+  static constexpr int XPT = (XF4 + THREADS - 1) / THREADS;
+  static constexpr int DPT = (DF4 + THREADS - 1) / THREADS;
+  static constexpr int LDS_FLOATS = 32 * COUT + kSeq * 32 * CIN;
+  static_assert(U % WAVES == 0, "unit split");
+};
+
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void conv_dw_mfma(
+    const float* __restrict__ x, const int* __restrict__ idx, const float* __restrict__ dpre,
+    float* __restrict__ ws, float* __restrict__ ws_db, int vsrc, int rows, long total_rows) {
+  using C = DwCfg<CIN, COUT>;
   constexpr int OT = COUT / 32, CT = CIN / 32;
-  __shared__ float red[UPW * 1024];
-  __shared__ float redb[COUT];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  extern __shared__ float lds[];
+  float* dp_lds = lds;               // [32][COUT]
+  float* x_lds = lds + 32 * COUT;    // [kSeq][32][CIN]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
   const int i = lane & 31, h = lane >> 5;
-  const int n_units = seq * OT * CT;
-  const int u0 = blockIdx.y * UPW;
+  const long n_tiles = (total_rows + 31) / 32;
 
-  f32x16 acc[UPW];
+  f32x16 acc[C::UPW];
 #pragma unroll
-  for (int q = 0; q < UPW; ++q) acc[q] = (f32x16){0.f};
-  float dbs[OT];
-#pragma unroll
-  for (int t = 0; t < OT; ++t) dbs[t] = 0.f;
+  for (int q = 0; q < C::UPW; ++q) acc[q] = (f32x16){0.f};
+  float db_acc = 0.f;
 
-  const long nblk = (total_rows + 31) / 32;
-  const long stride = (long)gridDim.x * 4;
-  for (long blk = (long)blockIdx.x * 4 + wave; blk < nblk; blk += stride) {
-    const long mbase = blk * 32;
-    // this lane's row for the index broadcast: row mbase + i
-    long mi = mbase + i;
-    const bool mi_ok = mi < total_rows;
-    if (!mi_ok) mi = total_rows - 1;
-    const int bi = (int)(mi / rows), ri = (int)(mi % rows);
-    // dpre fragments: rows mbase + 16h + j, column o = ot*32 + i
-    float dp[OT][16];
+  f32x4 xs[C::XPT], ds[C::DPT];
+  auto load_tile = [&](long tile) {
+    const long m0 = tile * 32;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      long mj = mbase + 16 * h + j;
-      bool ok = mj < total_rows;
-      long mc = ok ? mj : total_rows - 1;
-#pragma unroll
-      for (int t = 0; t < OT; ++t) {
-        float v = dpre[mc * COUT + t * 32 + i];
-        dp[t][j] = ok ? v : 0.f;
+    for (int e = 0; e < C::XPT; ++e) {
+      const int f = tid + e * C::THREADS;  // f in [0, XF4): (s, row, c4)
+      if (f < C::XF4) {
+        const int c4 = f % (CIN / 4);
+        const int row = (f / (CIN / 4)) % 32;
+        const int s = f / (32 * CIN / 4);
+        long m = m0 + row;
+        if (m >= total_rows) m = total_rows - 1;
+        const int b = (int)(m / rows), r = (int)(m % rows);
+        const int src = idx[(long)r * kSeq + s];
+        xs[e] = ld4(x + ((long)b * vsrc + src) * CIN + 4 * c4);
       }
     }
-    if (blockIdx.y == 0) {
 #pragma unroll
-      for (int t = 0; t < OT; ++t)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) dbs[t] += dp[t][j];
-    }
-#pragma unroll
-    for (int q = 0; q < UPW; ++q) {
-      const int un = u0 + q;
-      if (un >= n_units) break;
-      const int s = un / (OT * CT);
-      const int ot = (un / CT) % OT;
-      const int ct = un % CT;
-      const int my_src = idx[(long)ri * seq + s];
-      const long my_base = ((long)bi * vsrc + my_src) * CIN + ct * 32;
-      float xv[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        // row mbase + 16h + j lives in lane (16h + j) for the index broadcast
-        long base = __shfl(my_base, 16 * h + j);
-        xv[j] = x[base + i];
+    for (int e = 0; e < C::DPT; ++e) {
+      const int f = tid + e * C::THREADS;  // (row, o4)
+      if (f < C::DF4) {
+        const int row = f / (COUT / 4);
+        const long m = m0 + row;
+        ds[e] = m < total_rows ? ld4(dpre + m * COUT + 4 * (f % (COUT / 4)))
+                               : (f32x4){0.f, 0.f, 0.f, 0.f};
       }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc[q] = mfma32(dp[ot][j], xv[j], acc[q]);
     }
-  }
+  };
 
-  // block reduction in fixed wave order (deterministic)
-  for (int wv = 0; wv < 4; ++wv) {
-    if (wave == wv) {
+  long tile = blockIdx.x;
+  if (tile < n_tiles) load_tile(tile);
+  for (; tile < n_tiles; tile += gridDim.x) {
 #pragma unroll
-      for (int q = 0; q < UPW; ++q)
+    for (int e = 0; e < C::XPT; ++e) {
+      const int f = tid + e * C::THREADS;
+      if (f < C::XF4) st4(&x_lds[4 * f], xs[e]);
+    }
 #pragma unroll
-        for (int rr = 0; rr < 16; ++rr) {
-          int e = q * 1024 + acc_row(rr, lane) * 32 + i;  // [o][c]
-          red[e] = (wv == 0) ? acc[q][rr] : red[e] + acc[q][rr];
-        }
-      if (blockIdx.y == 0) {
+    for (int e = 0; e < C::DPT; ++e) {
+      const int f = tid + e * C::THREADS;
+      if (f < C::DF4) st4(&dp_lds[4 * f], ds[e]);
+    }
+    __syncthreads();
+    const long next = tile + gridDim.x;
+    if (next < n_tiles) load_tile(next);
+    if (tid < COUT) {
+#pragma unroll 8
+      for (int row = 0; row < 32; ++row) db_acc += dp_lds[row * COUT + tid];
+    }
 #pragma unroll
-        for (int t = 0; t < OT; ++t) {
-          float v = dbs[t] + __shfl_xor(dbs[t], 32);
-          if (h == 0) redb[t * 32 + i] = (wv == 0) ? v : redb[t * 32 + i] + v;
-        }
-      }
+    for (int q = 0; q < C::UPW; ++q) {
+      const int un = wave * C::UPW + q;
+      const int s = un / (OT * CT), ot = (un / CT) % OT, ct = un % CT;
+      const float* ap = dp_lds + (16 * h) * COUT + ot * 32 + i;
+      const float* bp = x_lds + (s * 32 + 16 * h) * CIN + ct * 32 + i;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[q] = mfma32(ap[j * COUT], bp[j * CIN], acc[q]);
     }
     __syncthreads();
   }
-  float* slab = ws + ((long)blockIdx.x * gridDim.y + blockIdx.y) * (UPW * 1024);
-  for (int e = threadIdx.x; e < UPW * 1024; e += 256) slab[e] = red[e];
-  if (blockIdx.y == 0)
-    for (int o = threadIdx.x; o < COUT; o += 256) ws_db[(long)blockIdx.x * COUT + o] = redb[o];
+  float* slab = ws + (long)blockIdx.x * (C::U * 1024);
+#pragma unroll
+  for (int q = 0; q < C::UPW; ++q) {
+    const int un = wave * C::UPW + q;
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) slab[un * 1024 + acc_row(rr, lane) * 32 + i] = acc[q][rr];
+  }
+  if (tid < COUT) ws_db[(long)blockIdx.x * COUT + tid] = db_acc;
 }
 
-// Reduce the dw slabs: dw[o, s*CIN + ct*32 + c] = sum_p slab_p[unit][o%32][c].
-// 16 threads per output element, each sums a strided subset of slabs, then a
-// fixed-order xor-shuffle tree (deterministic).
-template <int CIN, int COUT, int UPW>
+// dw[o, s*CIN + c] = sum_p slab_p[unit(s, o/32, c/32)][o%32][c%32]; 16
+// threads per output element, fixed-order xor tree (deterministic).
+template <int CIN, int COUT>
 __global__ __launch_bounds__(256) void conv_dw_reduce(const float* __restrict__ ws,
                                                       const float* __restrict__ ws_db,
                                                       float* __restrict__ dw,
-                                                      float* __restrict__ db, int seq,
-                                                      int n_slabs, int gy) {
+                                                      float* __restrict__ db, int n_slabs) {
   constexpr int OT = COUT / 32, CT = CIN / 32;
-  const long n_out = (long)COUT * seq * CIN;
-  long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int U = DwCfg<CIN, COUT>::U;
+  constexpr long n_out = (long)COUT * kSeq * CIN;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long e = tid >> 4;
   const int sub = threadIdx.x & 15;
-  const bool is_db = e >= n_out;
-  if (e >= n_out + COUT) e = n_out + COUT - 1;  // keep lanes alive for the shuffle
+  const bool valid = e < n_out + COUT;
+  if (!valid) e = n_out + COUT - 1;
   float sum = 0.f;
-  if (!is_db) {
-    const int o = (int)(e / (seq * CIN));
-    const int k = (int)(e % (seq * CIN));
+  if (e < n_out) {
+    const int o = (int)(e / (kSeq * CIN));
+    const int k = (int)(e % (kSeq * CIN));
     const int s = k / CIN, cc = k % CIN;
-    const int ot = o / 32, ct = cc / 32;
-    const int un = (s * OT + ot) * CT + ct;
-    const int y = un / UPW, q = un % UPW;
-    const long off = (long)q * 1024 + (o % 32) * 32 + (cc % 32);
-    for (int p = sub; p < n_slabs; p += 16) sum += ws[((long)p * gy + y) * (UPW * 1024) + off];
+    const int un = (s * OT + o / 32) * CT + cc / 32;
+    const long off = (long)un * 1024 + (o % 32) * 32 + (cc % 32);
+    for (int p = sub; p < n_slabs; p += 16) sum += ws[(long)p * (U * 1024) + off];
   } else {
     const int o = (int)(e - n_out);
     for (int p = sub; p < n_slabs; p += 16) sum += ws_db[(long)p * COUT + o];
   }
 #pragma unroll
   for (int d = 8; d >= 1; d >>= 1) sum += __shfl_xor(sum, d);
-  if (sub == 0 && (tid >> 4) < n_out + COUT) {
-    if (!is_db) dw[e] = sum;
+  if (sub == 0 && valid) {
+    if (e < n_out) dw[e] = sum;
     else db[e - n_out] = sum;
   }
 }
 
-// Backward weight, VALU path for tiny channels: one output weight column
-// group per thread block.  Thread t of a block owns (o, k) pairs; rows are
-// split across blocks and partial sums go to slabs [block][COUT*K + COUT].
-template <int CIN, int COUT>
-__global__ __launch_bounds__(256) void conv_dw_small(const float* __restrict__ x,
-                                                     const int* __restrict__ idx,
-                                                     const float* __restrict__ dpre,
-                                                     float* __restrict__ ws, int vsrc, int rows,
-                                                     int seq, long total_rows, int rows_per_blk) {
-  // element e in [0, COUT*K + COUT): weights then biases
-  const int K = seq * CIN;
-  const int n_el = COUT * K + COUT;
-  const long r0 = (long)blockIdx.x * rows_per_blk;
-  const long r1 = min(total_rows, r0 + rows_per_blk);
-  for (int e = threadIdx.x; e < n_el; e += blockDim.x) {
-    float sum = 0.f;
-    if (e < COUT * K) {
-      const int o = e / K, k = e % K;
-      const int s = k / CIN, c = k % CIN;
-      for (long m = r0; m < r1; ++m) {
-        const int b = (int)(m / rows), r = (int)(m % rows);
-        const float xv = x[((long)b * vsrc + idx[(long)r * seq + s]) * CIN + c];
-        sum = fmaf(dpre[m * COUT + o], xv, sum);
-      }
-    } else {
-      const int o = e - COUT * K;
-      for (long m = r0; m < r1; ++m) sum += dpre[m * COUT + o];
+// Backward weight, small input (CS <= 4; first Enblock): lane = output
+// channel o, 64/COUT rows per wave in flight; each lane accumulates its
+// kSeq*CS weight partials over a strided row range; waves are combined in
+// LDS in fixed order; one slab [COUT*K + COUT] per block.
+template <int CS, int COUT>
+__global__ __launch_bounds__(256) void conv_dw_in_small(const float* __restrict__ x,
+                                                        const int* __restrict__ idx,
+                                                        const float* __restrict__ dpre,
+                                                        float* __restrict__ ws, int vsrc,
+                                                        int rows, long total_rows) {
+  constexpr int K = kSeq * CS;
+  constexpr int RPW = 64 / COUT;  // row slots per wave
+  constexpr int NEL = COUT * K + COUT;
+  __shared__ float red[NEL];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int o = lane % COUT, slot = lane / COUT;
+  float acc[K + 1];
+#pragma unroll
+  for (int k = 0; k <= K; ++k) acc[k] = 0.f;
+  const long stride = (long)gridDim.x * 4 * RPW;
+  for (long m = ((long)blockIdx.x * 4 + wave) * RPW + slot; m < total_rows; m += stride) {
+    const int b = (int)(m / rows), r = (int)(m % rows);
+    const float d = dpre[m * COUT + o];
+    const float* xb = x + (long)b * vsrc * CS;
+#pragma unroll
+    for (int s = 0; s < kSeq; ++s) {
+      const float* p = xb + (long)idx[(long)r * kSeq + s] * CS;
+#pragma unroll
+      for (int c = 0; c < CS; ++c) acc[s * CS + c] = fmaf(d, p[c], acc[s * CS + c]);
     }
-    ws[(long)blockIdx.x * n_el + e] = sum;
+    acc[K] += d;
   }
+  // combine row slots inside the wave (lanes with equal o)
+#pragma unroll
+  for (int k = 0; k <= K; ++k)
+#pragma unroll
+    for (int d = COUT; d < 64; d <<= 1) acc[k] += __shfl_xor(acc[k], d);
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv && slot == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int e = o * K + k;
+        red[e] = wv == 0 ? acc[k] : red[e] + acc[k];
+      }
+      const int e = COUT * K + o;
+      red[e] = wv == 0 ? acc[K] : red[e] + acc[K];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < NEL; e += 256) ws[(long)blockIdx.x * NEL + e] = red[e];
+}
+
+// Backward weight, small output (CO <= 4; last decoder conv): L = CIN/4
+// lanes per row; lane q accumulates dW[o][s*CIN + 4q .. +4] for all o, s.
+template <int CIN, int CO>
+__global__ __launch_bounds__(256) void conv_dw_out_small(const float* __restrict__ x,
+                                                         const int* __restrict__ idx,
+                                                         const float* __restrict__ dpre,
+                                                         float* __restrict__ ws, int vsrc,
+                                                         int rows, long total_rows) {
+  constexpr int L = CIN / 4;
+  constexpr int K = kSeq * CIN;
+  constexpr int RPW = 64 / L;
+  constexpr int NEL = CO * K + CO;
+  __shared__ float red[NEL];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int q = lane % L, slot = lane / L;
+  f32x4 acc[kSeq][CO];
+  float dbs[CO];
+#pragma unroll
+  for (int s = 0; s < kSeq; ++s)
+#pragma unroll
+    for (int o = 0; o < CO; ++o) acc[s][o] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int o = 0; o < CO; ++o) dbs[o] = 0.f;
+  const long stride = (long)gridDim.x * 4 * RPW;
+  for (long m = ((long)blockIdx.x * 4 + wave) * RPW + slot; m < total_rows; m += stride) {
+    const int b = (int)(m / rows), r = (int)(m % rows);
+    float d[CO];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) d[o] = dpre[m * CO + o];
+    const float* xb = x + (long)b * vsrc * CIN + 4 * q;
+#pragma unroll
+    for (int s = 0; s < kSeq; ++s) {
+      const f32x4 v = ld4(xb + (long)idx[(long)r * kSeq + s] * CIN);
+#pragma unroll
+      for (int o = 0; o < CO; ++o) {
+        acc[s][o].x = fmaf(d[o], v.x, acc[s][o].x);
+        acc[s][o].y = fmaf(d[o], v.y, acc[s][o].y);
+        acc[s][o].z = fmaf(d[o], v.z, acc[s][o].z);
+        acc[s][o].w = fmaf(d[o], v.w, acc[s][o].w);
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < CO; ++o) dbs[o] += d[o];
+  }
+#pragma unroll
+  for (int s = 0; s < kSeq; ++s)
+#pragma unroll
+    for (int o = 0; o < CO; ++o)
+#pragma unroll
+      for (int dd = L; dd < 64; dd <<= 1) {
+        acc[s][o].x += __shfl_xor(acc[s][o].x, dd);
+        acc[s][o].y += __shfl_xor(acc[s][o].y, dd);
+        acc[s][o].z += __shfl_xor(acc[s][o].z, dd);
+        acc[s][o].w += __shfl_xor(acc[s][o].w, dd);
+      }
+#pragma unroll
+  for (int o = 0; o < CO; ++o)
+#pragma unroll
+    for (int dd = L; dd < 64; dd <<= 1) dbs[o] += __shfl_xor(dbs[o], dd);
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv && slot == 0) {
+#pragma unroll
+      for (int s = 0; s < kSeq; ++s)
+#pragma unroll
+        for (int o = 0; o < CO; ++o) {
+          const int e = o * K + s * CIN + 4 * q;
+          const f32x4 v = acc[s][o];
+          if (wv == 0) {
+            red[e] = v.x; red[e + 1] = v.y; red[e + 2] = v.z; red[e + 3] = v.w;
+          } else {
+            red[e] += v.x; red[e + 1] += v.y; red[e + 2] += v.z; red[e + 3] += v.w;
+          }
+        }
+      if (q == 0)
+#pragma unroll
+        for (int o = 0; o < CO; ++o) red[CO * K + o] = wv == 0 ? dbs[o] : red[CO * K + o] + dbs[o];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < NEL; e += 256) ws[(long)blockIdx.x * NEL + e] = red[e];
 }
 
 __global__ __launch_bounds__(256) void slab_reduce(const float* __restrict__ ws, int n_slabs,
                                                    int n_el, float* __restrict__ out_a, int n_a,
                                                    float* __restrict__ out_b) {
-  long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long e = tid >> 4;
   const int sub = threadIdx.x & 15;
   const bool valid = e < n_el;
@@ -487,17 +679,17 @@ __global__ __launch_bounds__(256) void slab_reduce(const float* __restrict__ ws,
   }
 }
 
-// Materialising gather (roofline probe): g[m, s*CIN + c] = x[b, idx[r,s], c].
+// Materialising gather (HBM roofline probe): g[m, s*cin + c] = x[b, idx[r,s], c].
 // One thread per 16-B chunk of the output.
 __global__ __launch_bounds__(256) void spiral_gather_k(const float* __restrict__ x,
                                                        const int* __restrict__ idx,
                                                        float* __restrict__ g, int vsrc, int rows,
                                                        int seq, int cin, long total_chunks) {
-  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total_chunks) return;
   const int c4 = cin / 4;
   const int q = (int)(t % c4);
-  long rs = t / c4;
+  const long rs = t / c4;
   const int s = (int)(rs % seq);
   const long m = rs / seq;
   const int b = (int)(m / rows), r = (int)(m % rows);
@@ -516,34 +708,26 @@ static int check_conv_args(const void* a, const void* b, const void* c, int batc
   if (batch <= 0 || vsrc <= 0 || rows <= 0 || seq <= 0 || cin <= 0 || cout <= 0)
     return set_error(CFSD_EINVAL, "non-positive size (batch=%d vsrc=%d rows=%d seq=%d cin=%d cout=%d)",
                      batch, vsrc, rows, seq, cin, cout);
+  if (seq != kSeq) return set_error(CFSD_EINVAL, "spiral length %d unsupported (built for %d)", seq, kSeq);
   return CFSD_OK;
 }
 
+static const long kMaxPersistentBlocks = 1024;  // 4 per CU on 256 CUs
+
 template <int CIN, int COUT, int ACT>
 static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const float* bias,
-                           float* y, int vsrc, int rows, int seq, long M, hipStream_t st) {
-  const size_t lds = (size_t)COUT * (seq * CIN + 4) * sizeof(float);
-  dim3 grid((unsigned)((M + 127) / 128));
+                           float* y, int vsrc, int rows, long M, hipStream_t st) {
+  const size_t lds = (size_t)COUT * (kSeq * CIN + 4) * sizeof(float);
+  const long n_tiles = (M + 31) / 32;
+  dim3 grid(persistent_blocks(n_tiles, 4, kMaxPersistentBlocks));
   if (lds <= 64 * 1024)
     hipLaunchKernelGGL((conv_fwd_mfma<CIN, COUT, ACT, true>), grid, dim3(256), lds, st, x, idx, w,
-                       bias, y, vsrc, rows, seq, M);
+                       bias, y, vsrc, rows, M);
   else
     hipLaunchKernelGGL((conv_fwd_mfma<CIN, COUT, ACT, false>), grid, dim3(256), 0, st, x, idx, w,
-                       bias, y, vsrc, rows, seq, M);
+                       bias, y, vsrc, rows, M);
   return launch_status("spiral_conv_fwd");
 }
-
-template <int CIN, int COUT, int ACT>
-static int launch_fwd_small(const float* x, const int* idx, const float* w, const float* bias,
-                            float* y, int vsrc, int rows, int seq, long M, hipStream_t st) {
-  dim3 grid((unsigned)((M + 255) / 256));
-  hipLaunchKernelGGL((conv_fwd_small<CIN, COUT, ACT>), grid, dim3(256), 0, st, x, idx, w, bias, y,
-                     vsrc, rows, seq, M);
-  return launch_status("spiral_conv_fwd_small");
-}
-
-#define CFSD_DISPATCH_MFMA(CIN_, COUT_, CALL) \
-  if (cin == CIN_ && cout == COUT_) return CALL;
 
 extern "C" int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const float* w,
                                     const float* bias, float* y, int batch, int vsrc, int rows,
@@ -554,94 +738,110 @@ extern "C" int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const fl
   if (act != CFSD_ACT_NONE && act != CFSD_ACT_ELU) return set_error(CFSD_EINVAL, "bad act %d", act);
   hipStream_t st = (hipStream_t)stream;
   const long M = (long)batch * rows;
-#define FWD(CIN_, COUT_)                                                                       \
-  if (cin == CIN_ && cout == COUT_) {                                                          \
-    return act == CFSD_ACT_ELU                                                                 \
-               ? launch_fwd_mfma<CIN_, COUT_, CFSD_ACT_ELU>(x, idx, w, bias, y, vsrc, rows, seq, M, st) \
-               : launch_fwd_mfma<CIN_, COUT_, CFSD_ACT_NONE>(x, idx, w, bias, y, vsrc, rows, seq, M, st); \
-  }
+#define FWD(CIN_, COUT_)                                                                              \
+  if (cin == CIN_ && cout == COUT_)                                                                   \
+    return act == CFSD_ACT_ELU                                                                        \
+               ? launch_fwd_mfma<CIN_, COUT_, CFSD_ACT_ELU>(x, idx, w, bias, y, vsrc, rows, M, st)     \
+               : launch_fwd_mfma<CIN_, COUT_, CFSD_ACT_NONE>(x, idx, w, bias, y, vsrc, rows, M, st);
   FWD(32, 32) FWD(32, 64) FWD(64, 32) FWD(64, 64)
 #undef FWD
-#define FWDS(CIN_, COUT_)                                                                      \
-  if (cin == CIN_ && cout == COUT_) {                                                          \
-    return act == CFSD_ACT_ELU                                                                 \
-               ? launch_fwd_small<CIN_, COUT_, CFSD_ACT_ELU>(x, idx, w, bias, y, vsrc, rows, seq, M, st) \
-               : launch_fwd_small<CIN_, COUT_, CFSD_ACT_NONE>(x, idx, w, bias, y, vsrc, rows, seq, M, st); \
+#define FWD_IN(CS_, COUT_)                                                                            \
+  if (cin == CS_ && cout == COUT_) {                                                                  \
+    dim3 g((unsigned)((M * COUT_ + 255) / 256));                                                      \
+    if (act == CFSD_ACT_ELU)                                                                          \
+      hipLaunchKernelGGL((conv_fwd_in_small<CS_, COUT_, CFSD_ACT_ELU>), g, dim3(256), 0, st, x, idx, \
+                         w, bias, y, vsrc, rows, M);                                                  \
+    else                                                                                              \
+      hipLaunchKernelGGL((conv_fwd_in_small<CS_, COUT_, CFSD_ACT_NONE>), g, dim3(256), 0, st, x,     \
+                         idx, w, bias, y, vsrc, rows, M);                                             \
+    return launch_status("spiral_conv_fwd_in_small");                                                 \
   }
-  FWDS(3, 32) FWDS(3, 64) FWDS(32, 3) FWDS(64, 3) FWDS(3, 16) FWDS(16, 3) FWDS(16, 16)
-#undef FWDS
+  FWD_IN(3, 16) FWD_IN(3, 32) FWD_IN(3, 64)
+#undef FWD_IN
+#define FWD_OUT(CIN_, CO_)                                                                            \
+  if (cin == CIN_ && cout == CO_) {                                                                   \
+    dim3 g((unsigned)((M * (CIN_ / 4) + 255) / 256));                                                 \
+    if (act == CFSD_ACT_ELU)                                                                          \
+      hipLaunchKernelGGL((conv_fwd_out_small<CIN_, CO_, CFSD_ACT_ELU>), g, dim3(256), 0, st, x, idx, \
+                         w, bias, y, vsrc, rows, M);                                                  \
+    else                                                                                              \
+      hipLaunchKernelGGL((conv_fwd_out_small<CIN_, CO_, CFSD_ACT_NONE>), g, dim3(256), 0, st, x,     \
+                         idx, w, bias, y, vsrc, rows, M);                                             \
+    return launch_status("spiral_conv_fwd_out_small");                                                \
+  }
+  FWD_OUT(16, 3) FWD_OUT(32, 3) FWD_OUT(64, 3)
+#undef FWD_OUT
   return set_error(CFSD_EINVAL, "spiral_conv_fwd: unsupported channels %d -> %d", cin, cout);
 }
 
 extern "C" int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_ptr,
-                                         const int32_t* inv_row, const float* w,
-                                         const float* elu_y, float* dx, int batch, int vsrc,
-                                         int rows, int seq, int cin, int cout, void* stream) {
+                                         const int32_t* inv_row, const int32_t* inv_pair,
+                                         const float* w, const float* elu_y, float* dx, int batch,
+                                         int vsrc, int rows, int seq, int cin, int cout,
+                                         void* stream) {
   int rc = check_conv_args(dpre, inv_ptr, inv_row, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
   if (!w || !dx) return set_error(CFSD_EINVAL, "null w/dx");
   hipStream_t st = (hipStream_t)stream;
   const long M = (long)batch * vsrc;
-#define DXM(CIN_, COUT_)                                                                         \
-  if (cin == CIN_ && cout == COUT_) {                                                            \
-    const size_t lds = (size_t)seq * CIN_ * (COUT_ + 4) * sizeof(float);                         \
-    dim3 grid((unsigned)((M + 127) / 128));                                                      \
-    if (lds <= 80 * 1024)                                                                        \
-      hipLaunchKernelGGL((conv_dx_mfma<CIN_, COUT_, true>), grid, dim3(256), lds, st, dpre,      \
-                         inv_ptr, inv_row, w, elu_y, dx, vsrc, rows, seq, M);                    \
-    else                                                                                         \
-      hipLaunchKernelGGL((conv_dx_mfma<CIN_, COUT_, false>), grid, dim3(256), 0, st, dpre,       \
-                         inv_ptr, inv_row, w, elu_y, dx, vsrc, rows, seq, M);                    \
-    return launch_status("spiral_conv_bwd_data");                                                \
+#define DXM(CIN_, COUT_)                                                                           \
+  if (cin == CIN_ && cout == COUT_) {                                                              \
+    if (!inv_pair) return set_error(CFSD_EINVAL, "null inv_pair");                                 \
+    const size_t lds = (size_t)kSeq * CIN_ * (COUT_ + 4) * sizeof(float);                          \
+    dim3 grid(persistent_blocks((M + 31) / 32, 4, kMaxPersistentBlocks));                          \
+    if (lds <= 80 * 1024)                                                                          \
+      hipLaunchKernelGGL((conv_dx_mfma<CIN_, COUT_, true>), grid, dim3(256), lds, st, dpre,        \
+                         inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M);    \
+    else                                                                                           \
+      hipLaunchKernelGGL((conv_dx_mfma<CIN_, COUT_, false>), grid, dim3(256), 0, st, dpre,         \
+                         inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M);    \
+    return launch_status("spiral_conv_bwd_data");                                                  \
   }
   DXM(32, 32) DXM(32, 64) DXM(64, 32) DXM(64, 64)
 #undef DXM
-#define DXS(CIN_, COUT_)                                                                        \
-  if (cin == CIN_ && cout == COUT_) {                                                           \
-    hipLaunchKernelGGL((conv_dx_small<CIN_, COUT_>), dim3((unsigned)((M + 255) / 256)),         \
-                       dim3(256), 0, st, dpre, inv_ptr, inv_row, w, elu_y, dx, vsrc, rows, seq, M); \
-    return launch_status("spiral_conv_bwd_data_small");                                        \
+#define DXS(CIN_, CO_)                                                                           \
+  if (cin == CIN_ && cout == CO_) {                                                              \
+    hipLaunchKernelGGL((conv_dx_out_small<CIN_, CO_>), dim3((unsigned)((M * (CIN_ / 4) + 255) / 256)), \
+                       dim3(256), 0, st, dpre, inv_ptr, inv_row, w, elu_y, dx, vsrc, rows, M);   \
+    return launch_status("spiral_conv_bwd_data_small");                                         \
   }
-  DXS(32, 3) DXS(64, 3) DXS(3, 32) DXS(3, 64) DXS(16, 3) DXS(3, 16) DXS(16, 16)
+  DXS(16, 3) DXS(32, 3) DXS(64, 3)
 #undef DXS
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_data: unsupported channels %d -> %d", cin, cout);
 }
 
-// ---- bwd weight: launch geometry shared by workspace query and launch
+// ---- bwd weight: launch geometry shared by the workspace query and the launch
 namespace {
+enum DwKind { kDwMfma, kDwInSmall, kDwOutSmall, kDwNone };
 struct DwGeom {
-  bool mfma;
-  int gx, gy, upw;
-  long rows_per_blk;
+  DwKind kind;
+  int gx;
   size_t ws_floats;
 };
 
-DwGeom dw_geom(int batch, int rows, int seq, int cin, int cout) {
-  DwGeom g{};
+size_t dw_units(int cin, int cout) { return (size_t)kSeq * (cout / 32) * (cin / 32); }
+
+DwGeom dw_geom(int batch, int rows, int cin, int cout) {
+  DwGeom g{kDwNone, 0, 0};
   const long M = (long)batch * rows;
-  const bool mfma = (cin % 32 == 0) && (cout % 32 == 0) && cin <= 64 && cout <= 64;
-  g.mfma = mfma;
-  if (mfma) {
-    const int units = seq * (cout / 32) * (cin / 32);
-    g.upw = 9;
-    g.gy = (units + g.upw - 1) / g.upw;
-    const long nblk = (M + 31) / 32;
-    long gx = (nblk + 31) / 32;  // ~8 row-blocks per wave
-    if (gx > 256) gx = 256;
-    if (gx < 1) gx = 1;
-    g.gx = (int)gx;
-    g.ws_floats = (size_t)g.gx * g.gy * g.upw * 1024 + (size_t)g.gx * cout;
-  } else {
-    long per = 512;
-    long gx = (M + per - 1) / per;
-    if (gx > 512) {
-      gx = 512;
-      per = (M + gx - 1) / gx;
-    }
-    g.gx = (int)gx;
-    g.gy = 1;
-    g.rows_per_blk = per;
-    g.ws_floats = (size_t)g.gx * ((size_t)cout * seq * cin + cout);
+  if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64)) {
+    g.kind = kDwMfma;
+    const long n_tiles = (M + 31) / 32;
+    long gx = n_tiles < 512 ? n_tiles : 512;
+    g.gx = (int)(gx > 0 ? gx : 1);
+    g.ws_floats = (size_t)g.gx * dw_units(cin, cout) * 1024 + (size_t)g.gx * cout;
+  } else if (cin <= 4 && (cout == 16 || cout == 32 || cout == 64)) {
+    g.kind = kDwInSmall;
+    const long per_blk = 4 * (64 / cout);
+    long gx = (M + per_blk * 8 - 1) / (per_blk * 8);  // >= 8 rows per row slot
+    g.gx = (int)(gx > 512 ? 512 : (gx < 1 ? 1 : gx));
+    g.ws_floats = (size_t)g.gx * ((size_t)cout * kSeq * cin + cout);
+  } else if (cout <= 4 && (cin == 16 || cin == 32 || cin == 64)) {
+    g.kind = kDwOutSmall;
+    const long per_blk = 4 * (64 / (cin / 4));
+    long gx = (M + per_blk * 8 - 1) / (per_blk * 8);
+    g.gx = (int)(gx > 512 ? 512 : (gx < 1 ? 1 : gx));
+    g.ws_floats = (size_t)g.gx * ((size_t)cout * kSeq * cin + cout);
   }
   return g;
 }
@@ -649,8 +849,8 @@ DwGeom dw_geom(int batch, int rows, int seq, int cin, int cout) {
 
 extern "C" size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int seq, int cin,
                                                         int cout) {
-  if (batch <= 0 || rows <= 0 || seq <= 0 || cin <= 0 || cout <= 0) return 0;
-  return dw_geom(batch, rows, seq, cin, cout).ws_floats * sizeof(float);
+  if (batch <= 0 || rows <= 0 || seq != kSeq || cin <= 0 || cout <= 0) return 0;
+  return dw_geom(batch, rows, cin, cout).ws_floats * sizeof(float);
 }
 
 extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, const float* dpre,
@@ -660,51 +860,57 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
   int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
   if (!dw || !db || !workspace) return set_error(CFSD_EINVAL, "null dw/db/workspace");
-  DwGeom g = dw_geom(batch, rows, seq, cin, cout);
+  DwGeom g = dw_geom(batch, rows, cin, cout);
+  if (g.kind == kDwNone)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight: unsupported channels %d -> %d", cin, cout);
   if (workspace_bytes < g.ws_floats * sizeof(float))
     return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes,
                      g.ws_floats * sizeof(float));
   hipStream_t st = (hipStream_t)stream;
   const long M = (long)batch * rows;
-  if (g.mfma) {
-    float* ws_db = workspace + (size_t)g.gx * g.gy * g.upw * 1024;
-    const long n_out = (long)cout * seq * cin + cout;
-    dim3 rg((unsigned)((n_out * 16 + 255) / 256));
-#define DWM(CIN_, COUT_)                                                                       \
-  if (cin == CIN_ && cout == COUT_) {                                                          \
-    hipLaunchKernelGGL((conv_dw_mfma<CIN_, COUT_, 9>), dim3(g.gx, g.gy), dim3(256), 0, st, x,  \
-                       idx, dpre, workspace, ws_db, vsrc, rows, seq, M);                      \
-    rc = launch_status("spiral_conv_bwd_weight");                                              \
-    if (rc) return rc;                                                                         \
-    hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_, 9>), rg, dim3(256), 0, st, workspace,      \
-                       ws_db, dw, db, seq, g.gx, g.gy);                                        \
-    return launch_status("spiral_conv_bwd_weight_reduce");                                     \
+  const int n_el = cout * kSeq * cin + cout;
+  const dim3 rg((unsigned)(((long)n_el * 16 + 255) / 256));
+  if (g.kind == kDwMfma) {
+    float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
+#define DWM(CIN_, COUT_)                                                                        \
+  if (cin == CIN_ && cout == COUT_) {                                                           \
+    using C = DwCfg<CIN_, COUT_>;                                                               \
+    hipLaunchKernelGGL((conv_dw_mfma<CIN_, COUT_>), dim3(g.gx), dim3(C::THREADS),               \
+                       C::LDS_FLOATS * sizeof(float), st, x, idx, dpre, workspace, ws_db, vsrc, \
+                       rows, M);                                                                \
+    rc = launch_status("spiral_conv_bwd_weight");                                               \
+    if (rc) return rc;                                                                          \
+    hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), rg, dim3(256), 0, st, workspace, ws_db,   \
+                       dw, db, g.gx);                                                           \
+    return launch_status("spiral_conv_bwd_weight_reduce");                                      \
   }
     DWM(32, 32) DWM(32, 64) DWM(64, 32) DWM(64, 64)
 #undef DWM
-  } else {
-    const int n_el = cout * seq * cin + cout;
-#define DWS(CIN_, COUT_)                                                                          \
-  if (cin == CIN_ && cout == COUT_) {                                                             \
-    hipLaunchKernelGGL((conv_dw_small<CIN_, COUT_>), dim3(g.gx), dim3(256), 0, st, x, idx, dpre,  \
-                       workspace, vsrc, rows, seq, M, (int)g.rows_per_blk);                       \
+  }
+#define DWS(KERNEL, A_, B_)                                                                       \
+  if (cin == A_ && cout == B_) {                                                                  \
+    hipLaunchKernelGGL((KERNEL<A_, B_>), dim3(g.gx), dim3(256), 0, st, x, idx, dpre, workspace,   \
+                       vsrc, rows, M);                                                            \
     rc = launch_status("spiral_conv_bwd_weight_small");                                           \
     if (rc) return rc;                                                                            \
-    hipLaunchKernelGGL(slab_reduce, dim3((unsigned)(((long)n_el * 16 + 255) / 256)), dim3(256), 0, \
-                       st, workspace, g.gx, n_el, dw, cout * seq * cin, db);                      \
+    hipLaunchKernelGGL(slab_reduce, rg, dim3(256), 0, st, workspace, g.gx, n_el, dw,              \
+                       cout * kSeq * cin, db);                                                    \
     return launch_status("spiral_conv_bwd_weight_small_reduce");                                  \
   }
-    DWS(3, 32) DWS(3, 64) DWS(32, 3) DWS(64, 3) DWS(3, 16) DWS(16, 3) DWS(16, 16)
-#undef DWS
+  if (g.kind == kDwInSmall) {
+    DWS(conv_dw_in_small, 3, 16) DWS(conv_dw_in_small, 3, 32) DWS(conv_dw_in_small, 3, 64)
+  } else {
+    DWS(conv_dw_out_small, 16, 3) DWS(conv_dw_out_small, 32, 3) DWS(conv_dw_out_small, 64, 3)
   }
+#undef DWS
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight: unsupported channels %d -> %d", cin, cout);
 }
 
 extern "C" int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, int batch,
                                   int vsrc, int rows, int seq, int cin, void* stream) {
-  int rc = check_conv_args(x, idx, g, batch, vsrc, rows, seq, cin, 1);
-  if (rc) return rc;
-  if (cin % 4) return set_error(CFSD_EINVAL, "spiral_gather: cin %% 4 != 0");
+  if (!x || !idx || !g) return set_error(CFSD_EINVAL, "spiral_gather: null pointer");
+  if (batch <= 0 || vsrc <= 0 || rows <= 0 || seq <= 0 || cin <= 0 || (cin % 4))
+    return set_error(CFSD_EINVAL, "spiral_gather: bad sizes");
   const long chunks = (long)batch * rows * seq * (cin / 4);
   hipLaunchKernelGGL(spiral_gather_k, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, x, idx, g, vsrc, rows, seq, cin, chunks);

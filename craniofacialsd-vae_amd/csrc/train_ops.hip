@@ -265,112 +265,122 @@ __global__ void loss_finalize_k(const float* __restrict__ partials, int nblocks,
 }
 
 // ----------------------------------------------------------- dense Linear
-// y[i,n] = bias[n] + sum_k x[i,k] w[n,k], rows processed in chunks of 16.
-// One workgroup (NW waves) per output column n; lanes stride k.
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void linear_fwd_k(const float* __restrict__ x,
+// The bottleneck Linears are [16 x 4288] x [4288 x 150] (encoder, stacked
+// mu/logvar) and [16 x 75] x [75 x 4288] (decoder): tiny GEMMs whose cost is
+// parallelism and latency, not FLOPs.  Long reductions are split across
+// workgroups into a workspace and summed in a second fixed-order pass.
+constexpr int kLinKC = 256;   // k per split-K workgroup (64 lanes x 4)
+constexpr int kLinNC = 128;   // n per split-n chunk (dx of the decoder Linear)
+
+// Split-K partials: block (col n, chunk ks), one wave; lane l owns k =
+// ks*256 + 4l .. +3.  ws[(ks*m + i)*n + col].
+__global__ __launch_bounds__(64) void linear_fwd_splitk(const float* __restrict__ x,
                                                         const float* __restrict__ w,
-                                                        const float* __restrict__ bias,
-                                                        float* __restrict__ y, int m, int k,
+                                                        float* __restrict__ ws, int m, int k,
                                                         int n) {
-  __shared__ float red[NW][16];
-  const int col = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float* wr = w + (long)col * k;
+  const int col = blockIdx.x, ks = blockIdx.y, lane = threadIdx.x;
+  const int k0 = ks * kLinKC + 4 * lane;
+  float wv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) wv[q] = (k0 + q < k) ? w[(long)col * k + k0 + q] : 0.f;
   for (int i0 = 0; i0 < m; i0 += 16) {
-    const int mr = min(16, m - i0);
     float acc[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    for (int kk = threadIdx.x; kk < k; kk += NW * 64) {
-      const float wv = wr[kk];
+    for (int i = 0; i < 16; ++i) {
+      acc[i] = 0.f;
+      if (i0 + i < m) {
+        const float* xr = x + (long)(i0 + i) * k;
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (i < mr) acc[i] = fmaf(x[(long)(i0 + i) * k + kk], wv, acc[i]);
+        for (int q = 0; q < 4; ++q)
+          if (k0 + q < k) acc[i] = fmaf(xr[k0 + q], wv[q], acc[i]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       float v = acc[i];
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-      if (lane == 0) red[wave][i] = v;
+      if (lane == i && i0 + i < m) ws[((long)ks * m + i0 + i) * n + col] = v;
     }
-    __syncthreads();
-    if (threadIdx.x < mr) {
-      float s = 0.f;
-      for (int wv = 0; wv < NW; ++wv) s += red[wv][threadIdx.x];
-      y[(long)(i0 + threadIdx.x) * n + col] = s + (bias ? bias[col] : 0.f);
-    }
-    __syncthreads();
   }
 }
 
-// dx[i,k] = g * sum_n dy[i,n] w[n,k]  (n small): one thread per k, 16 rows.
-__global__ __launch_bounds__(256) void linear_dx_k(const float* __restrict__ dy,
-                                                   const float* __restrict__ w,
-                                                   const float* __restrict__ elu_y,
-                                                   float* __restrict__ dx, int m, int k, int n,
-                                                   int accumulate) {
-  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void linear_fwd_reduce(const float* __restrict__ ws,
+                                                         const float* __restrict__ bias,
+                                                         float* __restrict__ y, int m, int n,
+                                                         int nks) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)m * n) return;
+  float s = 0.f;
+  for (int q = 0; q < nks; ++q) s += ws[(long)q * m * n + e];
+  y[e] = s + (bias ? bias[e % n] : 0.f);
+}
+
+// Short k: one thread per (i, n); 16 consecutive threads share n (broadcast W).
+__global__ __launch_bounds__(256) void linear_fwd_smallk(const float* __restrict__ x,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ bias,
+                                                         float* __restrict__ y, int m, int k,
+                                                         int n) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = (int)(t % 16);
+  const long col = t / 16;
+  if (col >= n) return;
+  const float* wr = w + col * k;
+  for (int ii = i; ii < m; ii += 16) {
+    const float* xr = x + (long)ii * k;
+    float acc = 0.f;
+    for (int kk = 0; kk < k; ++kk) acc = fmaf(xr[kk], wr[kk], acc);
+    y[(long)ii * n + col] = acc + (bias ? bias[col] : 0.f);
+  }
+}
+
+// dx for short n (encoder Linear, n = 150): block = one wave of 64 k's for
+// row i = blockIdx.y (wave-uniform -> dy is read with scalar loads).
+__global__ __launch_bounds__(64) void linear_dx_rows(const float* __restrict__ dy,
+                                                     const float* __restrict__ w,
+                                                     const float* __restrict__ elu_y,
+                                                     float* __restrict__ dx, int m, int k, int n,
+                                                     int accumulate) {
+  const int kk = blockIdx.x * 64 + threadIdx.x;
+  const int i = blockIdx.y;
   if (kk >= k) return;
-  for (int i0 = 0; i0 < m; i0 += 16) {
-    const int mr = min(16, m - i0);
-    float acc[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    for (int nn = 0; nn < n; ++nn) {
-      const float wv = w[(long)nn * k + kk];
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (i < mr) acc[i] = fmaf(dy[(long)(i0 + i) * n + nn], wv, acc[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (i >= mr) break;
-      const long o = (long)(i0 + i) * k + kk;
-      float v = acc[i];
-      if (elu_y) v *= elu_grad_from_out(elu_y[o]);
-      dx[o] = accumulate ? dx[o] + v : v;
-    }
-  }
+  const float* dyr = dy + (long)i * n;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int nn = 0; nn < n; ++nn) acc = fmaf(dyr[nn], w[(long)nn * k + kk], acc);
+  const long o = (long)i * k + kk;
+  if (elu_y) acc *= elu_grad_from_out(elu_y[o]);
+  dx[o] = accumulate ? dx[o] + acc : acc;
 }
 
-// dx for large n (k small): one workgroup per k, threads stride n.
-__global__ __launch_bounds__(256) void linear_dx_wide_k(const float* __restrict__ dy,
+// dx for long n (decoder Linear, n = 4288): split-n partials, thread per
+// (i, k) pair, ws[ns][i*k + kk].
+__global__ __launch_bounds__(256) void linear_dx_splitn(const float* __restrict__ dy,
                                                         const float* __restrict__ w,
+                                                        float* __restrict__ ws, int m, int k,
+                                                        int n) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= (long)m * k) return;
+  const int i = (int)(p / k), kk = (int)(p % k);
+  const int n0 = blockIdx.y * kLinNC, n1 = min(n, n0 + kLinNC);
+  const float* dyr = dy + (long)i * n;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int nn = n0; nn < n1; ++nn) acc = fmaf(dyr[nn], w[(long)nn * k + kk], acc);
+  ws[(long)blockIdx.y * m * k + p] = acc;
+}
+
+__global__ __launch_bounds__(256) void linear_dx_reduce(const float* __restrict__ ws,
                                                         const float* __restrict__ elu_y,
-                                                        float* __restrict__ dx, int m, int k,
-                                                        int n, int accumulate) {
-  __shared__ float red[4][16];
-  const int kk = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i0 = 0; i0 < m; i0 += 16) {
-    const int mr = min(16, m - i0);
-    float acc[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    for (int nn = threadIdx.x; nn < n; nn += 256) {
-      const float wv = w[(long)nn * k + kk];
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (i < mr) acc[i] = fmaf(dy[(long)(i0 + i) * n + nn], wv, acc[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float v = acc[i];
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-      if (lane == 0) red[wave][i] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < mr) {
-      const long o = (long)(i0 + threadIdx.x) * k + kk;
-      float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-      if (elu_y) v *= elu_grad_from_out(elu_y[o]);
-      dx[o] = accumulate ? dx[o] + v : v;
-    }
-    __syncthreads();
-  }
+                                                        float* __restrict__ dx, long mk, int nns,
+                                                        int accumulate) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= mk) return;
+  float s = 0.f;
+  for (int q = 0; q < nns; ++q) s += ws[(long)q * mk + p];
+  if (elu_y) s *= elu_grad_from_out(elu_y[p]);
+  dx[p] = accumulate ? dx[p] + s : s;
 }
 
 // dw[n,k] = sum_i dy[i,n] x[i,k] (thread per element), db[n] = sum_i dy[i,n].
@@ -535,34 +545,72 @@ extern "C" int cfsd_loss_finalize(const float* partials, int nblocks, const floa
   return launch_status("loss_finalize");
 }
 
-extern "C" int cfsd_linear_fwd(const float* x, const float* w, const float* bias, float* y, int m,
-                               int k, int n, void* stream) {
+static size_t linear_ws_floats(int m, int k, int n) {
+  size_t f = 0;
+  if (k >= 512) f = (size_t)((k + kLinKC - 1) / kLinKC) * m * n;
+  if (n > 512) {
+    const size_t g = (size_t)((n + kLinNC - 1) / kLinNC) * m * k;
+    if (g > f) f = g;
+  }
+  return f;
+}
+
+extern "C" size_t cfsd_linear_workspace(int m, int k, int n) {
+  if (m <= 0 || k <= 0 || n <= 0) return 0;
+  return linear_ws_floats(m, k, n) * sizeof(float);
+}
+
+extern "C" int cfsd_linear_fwd(const float* x, const float* w, const float* bias, float* y,
+                               float* workspace, size_t workspace_bytes, int m, int k, int n,
+                               void* stream) {
   if (!x || !w || !y) return set_error(CFSD_EINVAL, "linear_fwd: null pointer");
   if (m <= 0 || k <= 0 || n <= 0) return set_error(CFSD_EINVAL, "linear_fwd: bad sizes");
-  if (k >= 1024)
-    hipLaunchKernelGGL(linear_fwd_k<4>, dim3(n), dim3(256), 0, (hipStream_t)stream, x, w, bias, y,
-                       m, k, n);
-  else
-    hipLaunchKernelGGL(linear_fwd_k<1>, dim3(n), dim3(64), 0, (hipStream_t)stream, x, w, bias, y,
-                       m, k, n);
-  return launch_status("linear_fwd");
+  hipStream_t st = (hipStream_t)stream;
+  if (k >= 512) {
+    const int nks = (k + kLinKC - 1) / kLinKC;
+    if (!workspace || workspace_bytes < (size_t)nks * m * n * sizeof(float))
+      return set_error(CFSD_EWORKSPACE, "linear_fwd: workspace too small");
+    hipLaunchKernelGGL(linear_fwd_splitk, dim3(n, nks), dim3(64), 0, st, x, w, workspace, m, k, n);
+    int rc = launch_status("linear_fwd_splitk");
+    if (rc) return rc;
+    const long mn = (long)m * n;
+    hipLaunchKernelGGL(linear_fwd_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, st,
+                       workspace, bias, y, m, n, nks);
+    return launch_status("linear_fwd_reduce");
+  }
+  const long t = (long)n * 16;
+  hipLaunchKernelGGL(linear_fwd_smallk, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, x, w,
+                     bias, y, m, k, n);
+  return launch_status("linear_fwd_smallk");
 }
 
 extern "C" int cfsd_linear_bwd(const float* x, const float* w, const float* dy, const float* elu_y,
-                               float* dx, float* dw, float* db, int m, int k, int n,
-                               int accumulate, void* stream) {
+                               float* dx, float* dw, float* db, float* workspace,
+                               size_t workspace_bytes, int m, int k, int n, int accumulate,
+                               void* stream) {
   if (!dy) return set_error(CFSD_EINVAL, "linear_bwd: null dy");
   if (m <= 0 || k <= 0 || n <= 0) return set_error(CFSD_EINVAL, "linear_bwd: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   if (dx) {
     if (!w) return set_error(CFSD_EINVAL, "linear_bwd: null w");
-    if (n <= 512)
-      hipLaunchKernelGGL(linear_dx_k, dim3((k + 255) / 256), dim3(256), 0, st, dy, w, elu_y, dx,
+    int rc;
+    if (n <= 512) {
+      hipLaunchKernelGGL(linear_dx_rows, dim3((k + 63) / 64, m), dim3(64), 0, st, dy, w, elu_y, dx,
                          m, k, n, accumulate);
-    else
-      hipLaunchKernelGGL(linear_dx_wide_k, dim3(k), dim3(256), 0, st, dy, w, elu_y, dx, m, k, n,
-                         accumulate);
-    int rc = launch_status("linear_bwd_dx");
+      rc = launch_status("linear_dx_rows");
+    } else {
+      const int nns = (n + kLinNC - 1) / kLinNC;
+      const long mk = (long)m * k;
+      if (!workspace || workspace_bytes < (size_t)nns * mk * sizeof(float))
+        return set_error(CFSD_EWORKSPACE, "linear_bwd: workspace too small");
+      hipLaunchKernelGGL(linear_dx_splitn, dim3((unsigned)((mk + 255) / 256), nns), dim3(256), 0,
+                         st, dy, w, workspace, m, k, n);
+      rc = launch_status("linear_dx_splitn");
+      if (rc) return rc;
+      hipLaunchKernelGGL(linear_dx_reduce, dim3((unsigned)((mk + 255) / 256)), dim3(256), 0, st,
+                         workspace, elu_y, dx, mk, nns, accumulate);
+      rc = launch_status("linear_dx_reduce");
+    }
     if (rc) return rc;
   }
   if (dw || db) {

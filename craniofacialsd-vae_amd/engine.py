@@ -233,6 +233,10 @@ class SDVAEEngine:
             ws = max(ws, ops.spiral_conv_bwd_weight_workspace(bsz, nv[lv], T.seq[lv], cin, cout))
         ws = max(ws, ops.spiral_conv_bwd_weight_workspace(bsz, nv[0], T.seq[0], S.out_ch[0], S.in_ch))
         b.ws = torch.empty(ws // 4 + 64, dtype=torch.float32, device=dev)
+        flat_in = self.num_vert * S.out_ch[-1]
+        nmu = lat * (2 if S.is_vae else 1)
+        lws = max(ops.linear_workspace(bsz, flat_in, nmu), ops.linear_workspace(bsz, lat, flat_in))
+        b.lin_ws = torch.empty(lws // 4 + 64, dtype=torch.float32, device=dev)
         # step bookkeeping for the resident-dataset path
         b.batch_idx = torch.zeros(self.swap_bs, dtype=torch.int32, device=dev)
         self._bufs[bsz] = b
@@ -278,7 +282,7 @@ class SDVAEEngine:
                 ops.spmm(T.down_csr[lv], b.enc_full[lv], T.n_verts[lv + 1], out=b.enc_out[lv])
             h = b.enc_out[lv]
         W, B = self._enc_lin()
-        ops.linear_fwd(h.view(b.bsz, -1), W, B, out=b.mulv)
+        ops.linear_fwd(h.view(b.bsz, -1), W, B, out=b.mulv, workspace=b.lin_ws)
 
     def _lc_on(self, b):
         """Latent consistency needs a swapped bs x bs group (model_manager.py:360-367)."""
@@ -296,7 +300,8 @@ class SDVAEEngine:
         """de_layers: Linear -> 4x (Pool up -> conv -> ELU) -> conv (model.py:162-173)."""
         T, S = self.topo, self.spec
         ops.linear_fwd(b.z if z is None else z, self.params.view("de_layers.0.weight"),
-                       self.params.view("de_layers.0.bias"), out=b.h.view(b.bsz, -1))
+                       self.params.view("de_layers.0.bias"), out=b.h.view(b.bsz, -1),
+                       workspace=b.lin_ws)
         h = b.h
         for i, (cin, cout, lv, ui) in enumerate(S.dec_layers()):
             ops.spmm(T.up_csr[ui], h, T.n_verts[lv], out=b.dec_up[i])
@@ -347,7 +352,8 @@ class SDVAEEngine:
                 ops.spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh)
         # decoder Linear
         ops.linear_bwd(b.z, P.view("de_layers.0.weight"), b.dh.view(b.bsz, -1), dx=b.dz,
-                       dw=P.gview("de_layers.0.weight"), db=P.gview("de_layers.0.bias"))
+                       dw=P.gview("de_layers.0.weight"), db=P.gview("de_layers.0.bias"),
+                       workspace=b.lin_ws)
         ops.latent_bwd(b.mulv, b.eps, b.z, b.dz, b.dlat, b.dmulv, S.latent, True, S.is_vae, S.sigmoid)
         # stacked encoder Linear; ELU of the last Enblock folded into dx
         W, _ = self._enc_lin()
@@ -357,10 +363,10 @@ class SDVAEEngine:
         flat = b.enc_out[last].view(b.bsz, -1)
         if T.enc_select[last]:
             ops.linear_bwd(flat, W, b.dmulv, dx=b.dpre_enc[last].view(b.bsz, -1), dw=gW.view(W.shape),
-                           db=gB, elu_y=flat)
+                           db=gB, elu_y=flat, workspace=b.lin_ws)
         else:
             ops.linear_bwd(flat, W, b.dmulv, dx=b.g_pooled[last].view(b.bsz, -1), dw=gW.view(W.shape),
-                           db=gB)
+                           db=gB, workspace=b.lin_ws)
             ops.spmm(T.downT_csr[last], b.g_pooled[last], T.n_verts[last], elu_y=b.enc_full[last],
                      out=b.dpre_enc[last])
         for (cin, cout, lv) in reversed(enc):

@@ -54,20 +54,22 @@ def spiral_conv_fwd(x, idx, w, b, act=ACT_NONE, out=None):
 
 
 def spiral_conv_bwd_data(dpre, inv, w, vsrc, elu_y=None, out=None):
-    """dx[b, u] = g * sum_{(r,s) in inv(u)} W_s^T dpre[b, r]."""
+    """dx[b, u] = g * sum_{(r,s) in inv(u)} W_s^T dpre[b, r]; ``inv`` is the
+    (inv_ptr, inv_row, inv_pair) triple of ``topology.inverse_spiral``."""
     bsz, rows, cout = dpre.shape
-    inv_ptr, inv_row = inv
+    inv_ptr, inv_row, inv_pair = inv
     seq = (inv_ptr.numel() - 1) // vsrc
     cin = w.shape[1] // seq
     _need(dpre, None, name="dpre")
     _need(inv_ptr, (vsrc * seq + 1,), torch.int32, "inv_ptr")
     _need(inv_row, (rows * seq,), torch.int32, "inv_row")
+    _need(inv_pair, (vsrc * seq, 2), torch.int32, "inv_pair")
     _need(w, (cout, seq * cin), name="w")
     if elu_y is not None:
         _need(elu_y, (bsz, vsrc, cin), name="elu_y")
     dx = _out(out, (bsz, vsrc, cin), dpre)
-    call("cfsd_spiral_conv_bwd_data", ptr(dpre), ptr(inv_ptr), ptr(inv_row), ptr(w), ptr(elu_y),
-         ptr(dx), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    call("cfsd_spiral_conv_bwd_data", ptr(dpre), ptr(inv_ptr), ptr(inv_row), ptr(inv_pair), ptr(w),
+         ptr(elu_y), ptr(dx), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
     return dx
 
 
@@ -141,7 +143,22 @@ def elu_bwd(dy, y, out=None):
 
 
 # ------------------------------------------------------------------ dense
-def linear_fwd(x, w, b, out=None):
+def linear_workspace(m, k, n):
+    return int(_abi.lib().cfsd_linear_workspace(m, k, n))
+
+
+def _ws(workspace, need):
+    if need == 0:
+        return None, 0
+    if workspace is None:
+        raise ValueError(f"linear: workspace of {need} bytes required")
+    nbytes = workspace.numel() * workspace.element_size()
+    if nbytes < need:
+        raise ValueError(f"linear: workspace {nbytes} < {need} bytes")
+    return workspace, nbytes
+
+
+def linear_fwd(x, w, b, out=None, workspace=None):
     m, k = x.shape
     n = w.shape[0]
     _need(x, None, name="x")
@@ -149,11 +166,15 @@ def linear_fwd(x, w, b, out=None):
     if b is not None:
         _need(b, (n,), name="b")
     y = _out(out, (m, n), x)
-    call("cfsd_linear_fwd", ptr(x), ptr(w), ptr(b), ptr(y), m, k, n, stream_ptr())
+    if workspace is None and linear_workspace(m, k, n):
+        workspace = torch.empty(linear_workspace(m, k, n) // 4, device=x.device)
+    ws, nb = _ws(workspace, linear_workspace(m, k, n))
+    call("cfsd_linear_fwd", ptr(x), ptr(w), ptr(b), ptr(y), ptr(ws), ctypes.c_size_t(nb), m, k, n,
+         stream_ptr())
     return y
 
 
-def linear_bwd(x, w, dy, dx=None, dw=None, db=None, elu_y=None, accumulate=False):
+def linear_bwd(x, w, dy, dx=None, dw=None, db=None, elu_y=None, accumulate=False, workspace=None):
     m, n = dy.shape
     k = w.shape[1] if w is not None else x.shape[1]
     _need(dy, None, name="dy")
@@ -167,8 +188,12 @@ def linear_bwd(x, w, dy, dx=None, dw=None, db=None, elu_y=None, accumulate=False
         _need(db, (n,), name="db")
     if elu_y is not None:
         _need(elu_y, (m, k), name="elu_y")
-    call("cfsd_linear_bwd", ptr(x), ptr(w), ptr(dy), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), m, k,
-         n, int(accumulate), stream_ptr())
+    need = linear_workspace(m, k, n) if dx is not None else 0
+    if workspace is None and need:
+        workspace = torch.empty(need // 4, device=dy.device)
+    ws, nb = _ws(workspace, need)
+    call("cfsd_linear_bwd", ptr(x), ptr(w), ptr(dy), ptr(elu_y), ptr(dx), ptr(dw), ptr(db),
+         ptr(ws), ctypes.c_size_t(nb), m, k, n, int(accumulate), stream_ptr())
 
 
 # ------------------------------------------------------------------ losses

@@ -48,7 +48,9 @@ def csr_transpose_from_coo(row, col, val, n):
 
 
 def inverse_spiral(idx, vsrc):
-    """CSR over keys (u, s): rows r with ``idx[r, s] == u``, r ascending."""
+    """CSR over keys (u, s): rows r with ``idx[r, s] == u``, r ascending.
+    Returns (ptr [vsrc*S + 1], rows [R*S], pair [vsrc*S, 2]) where ``pair``
+    holds the first two rows of every list (-1 when absent)."""
     idx = np.asarray(idx, np.int64)
     r_count, s_len = idx.shape
     if idx.size and (idx.min() < 0 or idx.max() >= vsrc):
@@ -58,7 +60,15 @@ def inverse_spiral(idx, vsrc):
     order = np.argsort(keys, kind="stable")
     ptr = np.zeros(vsrc * s_len + 1, np.int64)
     np.add.at(ptr, keys + 1, 1)
-    return _i32(np.cumsum(ptr)), _i32(rows[order])
+    ptr = np.cumsum(ptr)
+    rows_sorted = rows[order]
+    cnt = np.diff(ptr)
+    pair = -np.ones((vsrc * s_len, 2), np.int64)
+    has1 = cnt >= 1
+    pair[has1, 0] = rows_sorted[ptr[:-1][has1]]
+    has2 = cnt >= 2
+    pair[has2, 1] = rows_sorted[ptr[:-1][has2] + 1]
+    return _i32(ptr), _i32(rows_sorted), _i32(pair)
 
 
 def selection_rows(row, col, val, m):
@@ -123,8 +133,7 @@ class DeviceTopology:
             sp = np.asarray(spirals[l], np.int64)
             v = sp.shape[0]
             self.spiral.append(_dev(_i32(sp), self.device))
-            ip, ir = inverse_spiral(sp, v)
-            self.spiral_inv.append((_dev(ip, self.device), _dev(ir, self.device)))
+            self.spiral_inv.append(tuple(_dev(a, self.device) for a in inverse_spiral(sp, v)))
             drow, dcol, dval, dshape = down[l]
             sel = selection_rows(drow, dcol, dval, dshape[0])
             if dshape[1] != v:
@@ -133,8 +142,7 @@ class DeviceTopology:
                 sub = sp[sel]
                 self.enc_select.append(True)
                 self.enc_rows.append(_dev(_i32(sub), self.device))
-                sp_ip, sp_ir = inverse_spiral(sub, v)
-                self.enc_inv.append((_dev(sp_ip, self.device), _dev(sp_ir, self.device)))
+                self.enc_inv.append(tuple(_dev(a, self.device) for a in inverse_spiral(sub, v)))
             else:
                 self.enc_select.append(False)
                 self.enc_rows.append(self.spiral[-1])

@@ -58,10 +58,14 @@ int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const float* w, con
  * where g = elu'(elu_y[b,u,c]) computed from the ELU output when elu_y != NULL
  * (fuses the previous layer's ELU backward), else 1.
  * inv_ptr [vsrc*seq + 1] / inv_row [rows*seq]: CSR of the inverse spiral,
- * entry list of (u, s) = rows r with idx[r*seq+s] == u. */
+ * entry list of (u, s) = rows r with idx[r*seq+s] == u (r ascending);
+ * inv_pair [vsrc*seq][2]: the first two entries of each list (-1 if absent),
+ * read up front so the gathers are issued one slot ahead (may be NULL for the
+ * 3-channel VALU path).  The spiral length must be 9 (all reference configs). */
 int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_ptr, const int32_t* inv_row,
-                              const float* w, const float* elu_y, float* dx, int batch, int vsrc,
-                              int rows, int seq, int cin, int cout, void* stream);
+                              const int32_t* inv_pair, const float* w, const float* elu_y,
+                              float* dx, int batch, int vsrc, int rows, int seq, int cin, int cout,
+                              void* stream);
 
 /* Replaces AddmmBackward's dW = G^T.dY and db = sum dY (model.py:40):
  *   dw[o, s*cin+c] = sum_{b,r} dpre[b,r,o] x[b, idx[r,s], c],  db[o] = sum_{b,r} dpre[b,r,o]
@@ -101,13 +105,17 @@ int cfsd_swap_features(const float* x, const int32_t* batch_idx, const uint8_t* 
 
 /* ---------------------------------------------------------------- dense layers
  * nn.Linear of the latent bottleneck (model.py:114-124, 153-156, 167):
- *   y[i,n] = bias[n] + sum_k x[i,k] w[n,k]      x [m,k], w [n,k], y [m,n] */
-int cfsd_linear_fwd(const float* x, const float* w, const float* bias, float* y, int m, int k,
-                    int n, void* stream);
-/* Linear backward: dx = dy.w (+ optional elu' scale from elu_y [m,k]; accumulate
- * into dx when accumulate != 0), dw = dy^T.x, db = sum_i dy.  dx/dw/db may be NULL. */
+ *   y[i,n] = bias[n] + sum_k x[i,k] w[n,k]      x [m,k], w [n,k], y [m,n]
+ * Long reductions are split across workgroups through `workspace`
+ * (cfsd_linear_workspace(m,k,n) bytes; may be 0 -> NULL allowed). */
+size_t cfsd_linear_workspace(int m, int k, int n);
+int cfsd_linear_fwd(const float* x, const float* w, const float* bias, float* y, float* workspace,
+                    size_t workspace_bytes, int m, int k, int n, void* stream);
+/* Linear backward: dx = dy.w (times elu'(elu_y) when elu_y [m,k] != NULL; added
+ * to dx when accumulate != 0), dw = dy^T.x, db = sum_i dy.  dx/dw/db may be NULL. */
 int cfsd_linear_bwd(const float* x, const float* w, const float* dy, const float* elu_y, float* dx,
-                    float* dw, float* db, int m, int k, int n, int accumulate, void* stream);
+                    float* dw, float* db, float* workspace, size_t workspace_bytes, int m, int k,
+                    int n, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------- losses
  * compute_mse_loss + _compute_laplacian_regularizer (model_manager.py:333-349,

@@ -24,8 +24,10 @@ _U64 = ctypes.c_ulonglong
 SIGNATURES = {
     "cfsd_version": (_I, []),
     "cfsd_last_error_string": (ctypes.c_char_p, []),
-    "cfsd_spiral_conv_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
-    "cfsd_spiral_conv_bwd_data": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "cfsd_spiral_conv_workspace": (_Z, [_I, _I, _I, _I, _I, _I]),
+    "cfsd_spiral_conv_fwd": (_I, [_P, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "cfsd_spiral_conv_bwd_data": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _I,
+                                       _P]),
     "cfsd_spiral_conv_bwd_weight": (_I, [_P, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_weight_workspace": (_Z, [_I, _I, _I, _I, _I]),
     "cfsd_spiral_gather": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),

@@ -31,39 +31,40 @@ static inline unsigned persistent_blocks(long n_tiles, int tiles_per_block_unit,
   return (unsigned)((units + per - 1) / per);
 }
 
-// ==========================================================================
-// Forward, MFMA path: CIN, COUT in {32, 64}.  Each wave owns 32-row tiles of
-// the flattened (b, r) row space (all COUT columns) and loops over them.
-// W staged in LDS as [COUT][K + 4] (pad: 16-lane ds_read_b128 groups hit
-// distinct 16-B slots for K = 288 and 576).
 // Occupancy target per channel shape (min waves per SIMD -> VGPR budget).
 constexpr int mfma_occ(int cin, int cout) { return (cin == 32 && cout == 32) ? 4 : 2; }
 
-template <int CIN, int COUT, int ACT, bool W_LDS>
-__global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(const float* __restrict__ x,
-                                                     const int* __restrict__ idx,
-                                                     const float* __restrict__ w,
-                                                     const float* __restrict__ bias,
-                                                     float* __restrict__ y, int vsrc, int rows,
-                                                     long total_rows) {
+// ==========================================================================
+// Forward, MFMA path: CIN, COUT in {32, 64}.  Each wave owns 32-row tiles of
+// the flattened (b, r) row space (all COUT columns) and loops over them.
+// Slot groups: blockIdx.y = g handles spiral slots [g*SPG, g*SPG + SPG); with
+// SPG < 9 (layers with few rows) the partial sums go to ws[g][m][COUT] and
+// conv_combine adds the groups (fixed order), bias and activation.
+// W slice staged in LDS as [COUT][SPG*CIN + 4] (pad: 16-lane ds_read_b128
+// groups hit distinct 16-B slots).
+template <int CIN, int COUT, int ACT, int SPG>
+__global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(
+    const float* __restrict__ x, const int* __restrict__ idx, const float* __restrict__ w,
+    const float* __restrict__ bias, float* __restrict__ y, float* __restrict__ ws, int vsrc,
+    int rows, long total_rows) {
   constexpr int HALF = CIN / 2;
   constexpr int NT = COUT / 32;
   constexpr int K = kSeq * CIN;
-  constexpr int KP = K + 4;
+  constexpr int KG = SPG * CIN;
+  constexpr int KP = KG + 4;
   extern __shared__ float lds_w[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  if (W_LDS) {
-    for (int e = threadIdx.x; e < COUT * (K / 4); e += 256) {
-      const int n = e / (K / 4), k4 = e % (K / 4);
-      st4(&lds_w[n * KP + 4 * k4], ld4(&w[(long)n * K + 4 * k4]));
-    }
-    __syncthreads();
+  const int g = blockIdx.y, s0 = g * SPG;
+  for (int e = threadIdx.x; e < COUT * (KG / 4); e += 256) {
+    const int n = e / (KG / 4), k4 = e % (KG / 4);
+    st4(&lds_w[n * KP + 4 * k4], ld4(&w[(long)n * K + s0 * CIN + 4 * k4]));
   }
+  __syncthreads();
   const int i = lane & 31, h = lane >> 5;
   float bn[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) bn[t] = bias ? bias[t * 32 + i] : 0.f;
+  for (int t = 0; t < NT; ++t) bn[t] = (SPG == kSeq && bias) ? bias[t * 32 + i] : 0.f;
   const long n_tiles = (total_rows + 31) / 32;
   for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
     const long m0 = tile * 32;
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(const 
     if (m >= total_rows) m = total_rows - 1;  // clamp loads, stores are masked
     const int b = (int)(m / rows), r = (int)(m % rows);
     const float* xb = x + (long)b * vsrc * CIN + h * HALF;
-    const int* ir = idx + (long)r * kSeq;
+    const int* ir = idx + (long)r * kSeq + s0;
     f32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x16){0.f};
@@ -79,22 +80,20 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(const 
     // in flight while slot s runs its MFMAs (loop kept rolled: a full unroll
     // makes hipcc hoist all nine gathers and spill).
     f32x4 a[HALF / 4], an[HALF / 4];
-    int src_n = ir[1];
+    int src_n = SPG > 1 ? ir[1] : 0;
 #pragma unroll
     for (int q = 0; q < HALF / 4; ++q) a[q] = ld4(xb + (long)ir[0] * CIN + 4 * q);
 #pragma unroll 1
-    for (int s = 0; s < kSeq; ++s) {
-      if (s + 1 < kSeq) {
-        const int src_nn = (s + 2 < kSeq) ? ir[s + 2] : 0;
+    for (int s = 0; s < SPG; ++s) {
+      if (s + 1 < SPG) {
+        const int src_nn = (s + 2 < SPG) ? ir[s + 2] : 0;
 #pragma unroll
         for (int q = 0; q < HALF / 4; ++q) an[q] = ld4(xb + (long)src_n * CIN + 4 * q);
         src_n = src_nn;
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const int n = t * 32 + i;
-        const float* wr = W_LDS ? &lds_w[n * KP + s * CIN + h * HALF]
-                                : &w[(long)n * K + s * CIN + h * HALF];
+        const float* wr = &lds_w[(t * 32 + i) * KP + s * CIN + h * HALF];
 #pragma unroll
         for (int q = 0; q < HALF / 4; ++q) {
           const f32x4 bw = ld4(wr + 4 * q);
@@ -104,9 +103,12 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(const 
           acc[t] = mfma32(a[q].w, bw.w, acc[t]);
         }
       }
+      if (s + 1 < SPG) {
 #pragma unroll
-      for (int q = 0; q < HALF / 4; ++q) a[q] = an[q];
+        for (int q = 0; q < HALF / 4; ++q) a[q] = an[q];
+      }
     }
+    float* dst = (SPG == kSeq) ? y : ws + (long)g * total_rows * COUT;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int n = t * 32 + i;
@@ -114,19 +116,49 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(const 
       for (int rr = 0; rr < 16; ++rr) {
         const long mo = m0 + acc_row(rr, lane);
         if (mo < total_rows) {
-          float v = acc[t][rr] + bn[t];
-          if (ACT == CFSD_ACT_ELU) v = elu_f(v);
-          y[mo * COUT + n] = v;
+          float v = acc[t][rr];
+          if (SPG == kSeq) {
+            v += bn[t];
+            if (ACT == CFSD_ACT_ELU) v = elu_f(v);
+          }
+          dst[mo * COUT + n] = v;
         }
       }
     }
   }
 }
 
+// Slot-group combine: out = act(sum_g ws[g] + bias) (fwd) or
+// out = (sum_g ws[g]) * elu'(elu_y) (bwd data); one thread per float4.
+template <int ACT>
+__global__ __launch_bounds__(256) void conv_combine(const float* __restrict__ ws,
+                                                    const float* __restrict__ bias,
+                                                    const float* __restrict__ elu_y,
+                                                    float* __restrict__ out, int groups,
+                                                    int cols, long n4) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n4) return;
+  f32x4 v = ld4(ws + 4 * t);
+  for (int g = 1; g < groups; ++g) v += ld4(ws + (long)g * n4 * 4 + 4 * t);
+  if (bias) {
+    const int c = (int)((4 * t) % cols);
+    v.x += bias[c]; v.y += bias[c + 1]; v.z += bias[c + 2]; v.w += bias[c + 3];
+  }
+  if (ACT == CFSD_ACT_ELU) {
+    v.x = elu_f(v.x); v.y = elu_f(v.y); v.z = elu_f(v.z); v.w = elu_f(v.w);
+  }
+  if (elu_y) {
+    const f32x4 e = ld4(elu_y + 4 * t);
+    v.x *= elu_grad_from_out(e.x); v.y *= elu_grad_from_out(e.y);
+    v.z *= elu_grad_from_out(e.z); v.w *= elu_grad_from_out(e.w);
+  }
+  st4(out + 4 * t, v);
+}
+
 // Forward, small input (CS <= 4 channels, e.g. the xyz input of the first
-// Enblock): one lane per (row, output channel).  The CS*kSeq gathered inputs
-// of a row are the same for its COUT lanes (broadcast loads); each lane keeps
-// its weight row in registers.
+// Enblock): one lane per (row, output channel), persistent over rows.  The
+// CS*kSeq gathered inputs of a row are the same for its COUT lanes
+// (broadcast loads); each lane keeps its weight row in registers.
 template <int CS, int COUT, int ACT>
 __global__ __launch_bounds__(256) void conv_fwd_in_small(const float* __restrict__ x,
                                                          const int* __restrict__ idx,
@@ -135,30 +167,34 @@ __global__ __launch_bounds__(256) void conv_fwd_in_small(const float* __restrict
                                                          float* __restrict__ y, int vsrc,
                                                          int rows, long total_rows) {
   constexpr int K = kSeq * CS;
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int o = (int)(t % COUT);
-  const long m = t / COUT;
-  if (m >= total_rows) return;
+  constexpr int RPW = 64 / COUT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int o = lane % COUT, slot = lane / COUT;
   float wr[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) wr[k] = w[o * K + k];
-  const int b = (int)(m / rows), r = (int)(m % rows);
-  const float* xb = x + (long)b * vsrc * CS;
-  float acc = bias ? bias[o] : 0.f;
+  const float bo = bias ? bias[o] : 0.f;
+  const long stride = (long)gridDim.x * 4 * RPW;
+  for (long m = ((long)blockIdx.x * 4 + wave) * RPW + slot; m < total_rows; m += stride) {
+    const int b = (int)(m / rows), r = (int)(m % rows);
+    const float* xb = x + (long)b * vsrc * CS;
+    const int* ir = idx + (long)r * kSeq;
+    float acc = bo;
 #pragma unroll
-  for (int s = 0; s < kSeq; ++s) {
-    const float* p = xb + (long)idx[(long)r * kSeq + s] * CS;
+    for (int s = 0; s < kSeq; ++s) {
+      const float* p = xb + (long)ir[s] * CS;
 #pragma unroll
-    for (int c = 0; c < CS; ++c) acc = fmaf(p[c], wr[s * CS + c], acc);
+      for (int c = 0; c < CS; ++c) acc = fmaf(p[c], wr[s * CS + c], acc);
+    }
+    if (ACT == CFSD_ACT_ELU) acc = elu_f(acc);
+    y[m * COUT + o] = acc;
   }
-  if (ACT == CFSD_ACT_ELU) acc = elu_f(acc);
-  y[m * COUT + o] = acc;
 }
 
-// Forward, small output (CO <= 4 channels, e.g. the xyz output conv):
-// L = CIN/4 lanes per row, each lane owns a float4 of input channels of every
-// neighbour row (so a neighbour row is one coalesced 16*L-byte read), then
-// the CO partial dots are reduced across the L lanes with xor shuffles.
+// Forward, small output (CO <= 4 channels, e.g. the xyz output conv),
+// persistent over rows: L = CIN/4 lanes per row, each lane owns a float4 of
+// input channels of every neighbour row (one coalesced 16*L-byte read per
+// neighbour), the CO partial dots are reduced across the L lanes.
 template <int CIN, int CO, int ACT>
 __global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restrict__ x,
                                                           const int* __restrict__ idx,
@@ -167,43 +203,51 @@ __global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restric
                                                           float* __restrict__ y, int vsrc,
                                                           int rows, long total_rows) {
   constexpr int L = CIN / 4;
+  constexpr int RPW = 64 / L;
   constexpr int K = kSeq * CIN;
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int q = (int)(t % L);
-  long m = t / L;
-  const bool valid = m < total_rows;
-  if (!valid) m = total_rows - 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane % L, slot = lane / L;
   f32x4 wr[kSeq][CO];
 #pragma unroll
   for (int s = 0; s < kSeq; ++s)
 #pragma unroll
     for (int o = 0; o < CO; ++o) wr[s][o] = ld4(w + (long)o * K + s * CIN + 4 * q);
-  const int b = (int)(m / rows), r = (int)(m % rows);
-  const float* xb = x + (long)b * vsrc * CIN + 4 * q;
-  float acc[CO];
+  float bo[CO];
 #pragma unroll
-  for (int o = 0; o < CO; ++o) acc[o] = 0.f;
+  for (int o = 0; o < CO; ++o) bo[o] = bias ? bias[o] : 0.f;
+  const long n_rows_pad = (total_rows + RPW - 1) / RPW * RPW;  // whole waves stay in the loop
+  const long stride = (long)gridDim.x * 4 * RPW;
+  for (long mm = ((long)blockIdx.x * 4 + wave) * RPW + slot; mm < n_rows_pad; mm += stride) {
+    const bool valid = mm < total_rows;
+    const long m = valid ? mm : total_rows - 1;
+    const int b = (int)(m / rows), r = (int)(m % rows);
+    const float* xb = x + (long)b * vsrc * CIN + 4 * q;
+    const int* ir = idx + (long)r * kSeq;
+    float acc[CO];
 #pragma unroll
-  for (int s = 0; s < kSeq; ++s) {
-    const f32x4 v = ld4(xb + (long)idx[(long)r * kSeq + s] * CIN);
+    for (int o = 0; o < CO; ++o) acc[o] = 0.f;
 #pragma unroll
-    for (int o = 0; o < CO; ++o) {
-      acc[o] = fmaf(v.x, wr[s][o].x, acc[o]);
-      acc[o] = fmaf(v.y, wr[s][o].y, acc[o]);
-      acc[o] = fmaf(v.z, wr[s][o].z, acc[o]);
-      acc[o] = fmaf(v.w, wr[s][o].w, acc[o]);
+    for (int s = 0; s < kSeq; ++s) {
+      const f32x4 v = ld4(xb + (long)ir[s] * CIN);
+#pragma unroll
+      for (int o = 0; o < CO; ++o) {
+        acc[o] = fmaf(v.x, wr[s][o].x, acc[o]);
+        acc[o] = fmaf(v.y, wr[s][o].y, acc[o]);
+        acc[o] = fmaf(v.z, wr[s][o].z, acc[o]);
+        acc[o] = fmaf(v.w, wr[s][o].w, acc[o]);
+      }
     }
-  }
 #pragma unroll
-  for (int o = 0; o < CO; ++o)
+    for (int o = 0; o < CO; ++o)
 #pragma unroll
-    for (int d = L / 2; d >= 1; d >>= 1) acc[o] += __shfl_xor(acc[o], d);
-  if (valid && q == 0) {
+      for (int d = L / 2; d >= 1; d >>= 1) acc[o] += __shfl_xor(acc[o], d);
+    if (valid && q == 0) {
 #pragma unroll
-    for (int o = 0; o < CO; ++o) {
-      float v = acc[o] + (bias ? bias[o] : 0.f);
-      if (ACT == CFSD_ACT_ELU) v = elu_f(v);
-      y[m * CO + o] = v;
+      for (int o = 0; o < CO; ++o) {
+        float v = acc[o] + bo[o];
+        if (ACT == CFSD_ACT_ELU) v = elu_f(v);
+        y[m * CO + o] = v;
+      }
     }
   }
 }
@@ -216,15 +260,13 @@ __global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restric
 // inv_pair[u*S + s] = the first two rows of inv(u,s) (-1 if absent): those
 // loads are issued unconditionally one slot ahead; the rare further entries
 // (inv_ptr/inv_row from offset 2) are summed in a short loop.
-template <int CIN, int COUT, bool W_LDS>
-__global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(const float* __restrict__ dpre,
-                                                    const int* __restrict__ inv_ptr,
-                                                    const int* __restrict__ inv_row,
-                                                    const int2* __restrict__ inv_pair,
-                                                    const float* __restrict__ w,
-                                                    const float* __restrict__ elu_y,
-                                                    float* __restrict__ dx, int vsrc, int rows,
-                                                    long total_rows) {
+// Slot groups as in conv_fwd_mfma (partials -> ws, conv_combine).
+template <int CIN, int COUT, int SPG>
+__global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
+    const float* __restrict__ dpre, const int* __restrict__ inv_ptr,
+    const int* __restrict__ inv_row, const int2* __restrict__ inv_pair,
+    const float* __restrict__ w, const float* __restrict__ elu_y, float* __restrict__ dx,
+    float* __restrict__ ws, int vsrc, int rows, long total_rows) {
   constexpr int HALF = COUT / 2;
   constexpr int NT = CIN / 32;
   constexpr int OP = COUT + 4;
@@ -232,13 +274,13 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(const f
   extern __shared__ float lds_wt[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  if (W_LDS) {
-    for (int e = threadIdx.x; e < COUT * K; e += 256) {
-      const int o = e / K, k = e % K;
-      lds_wt[k * OP + o] = w[e];
-    }
-    __syncthreads();
+  const int g = blockIdx.y, s0 = g * SPG;
+  // lds_wt[(sl*CIN + c) * OP + o] = w[o, (s0+sl)*CIN + c]
+  for (int e = threadIdx.x; e < COUT * SPG * CIN; e += 256) {
+    const int o = e / (SPG * CIN), k = e % (SPG * CIN);
+    lds_wt[k * OP + o] = w[(long)o * K + s0 * CIN + k];
   }
+  __syncthreads();
   const int i = lane & 31, h = lane >> 5;
   const long n_tiles = (total_rows + 31) / 32;
   for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
@@ -247,28 +289,28 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(const f
     if (m >= total_rows) m = total_rows - 1;
     const int b = (int)(m / vsrc), u = (int)(m % vsrc);
     const float* db_ = dpre + (long)b * rows * COUT + h * HALF;
-    const int2* pu = inv_pair + (long)u * kSeq;
+    const int2* pu = inv_pair + (long)u * kSeq + s0;
     f32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x16){0.f};
     // slot pipeline: rows r0/r1 of slot s+1 and the pair of slot s+2 are in
     // flight while slot s computes (rolled loop, see conv_fwd_mfma).
     f32x4 c0[HALF / 4], c1[HALF / 4];
-    int2 pc = pu[0], pn = pu[1];
+    int2 pc = pu[0], pn = SPG > 1 ? pu[1] : make_int2(-1, -1);
 #pragma unroll
     for (int q = 0; q < HALF / 4; ++q) {
       c0[q] = ld4(db_ + (long)max(pc.x, 0) * COUT + 4 * q);
       c1[q] = ld4(db_ + (long)max(pc.y, 0) * COUT + 4 * q);
     }
 #pragma unroll 1
-    for (int s = 0; s < kSeq; ++s) {
+    for (int s = 0; s < SPG; ++s) {
       f32x4 a[HALF / 4];
       const float f0 = pc.x >= 0 ? 1.f : 0.f, f1 = pc.y >= 0 ? 1.f : 0.f;
 #pragma unroll
       for (int q = 0; q < HALF / 4; ++q) a[q] = c0[q] * f0 + c1[q] * f1;
       const bool more = pc.y >= 0;
-      if (s + 1 < kSeq) {
-        const int2 pnn = (s + 2 < kSeq) ? pu[s + 2] : make_int2(-1, -1);
+      if (s + 1 < SPG) {
+        const int2 pnn = (s + 2 < SPG) ? pu[s + 2] : make_int2(-1, -1);
 #pragma unroll
         for (int q = 0; q < HALF / 4; ++q) {
           c0[q] = ld4(db_ + (long)max(pn.x, 0) * COUT + 4 * q);
@@ -278,7 +320,8 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(const f
         pn = pnn;
       }
       if (more) {  // rare: entries beyond the first two
-        const int beg = inv_ptr[(long)u * kSeq + s] + 2, end = inv_ptr[(long)u * kSeq + s + 1];
+        const long key = (long)u * kSeq + s0 + s;
+        const int beg = inv_ptr[key] + 2, end = inv_ptr[key + 1];
         for (int e = beg; e < end; ++e) {
           const float* p = db_ + (long)inv_row[e] * COUT;
 #pragma unroll
@@ -287,29 +330,18 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(const f
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const int c = t * 32 + i;
-        if (W_LDS) {
-          const float* wr = &lds_wt[(s * CIN + c) * OP + h * HALF];
+        const float* wr = &lds_wt[(s * CIN + t * 32 + i) * OP + h * HALF];
 #pragma unroll
-          for (int q = 0; q < HALF / 4; ++q) {
-            const f32x4 bw = ld4(wr + 4 * q);
-            acc[t] = mfma32(a[q].x, bw.x, acc[t]);
-            acc[t] = mfma32(a[q].y, bw.y, acc[t]);
-            acc[t] = mfma32(a[q].z, bw.z, acc[t]);
-            acc[t] = mfma32(a[q].w, bw.w, acc[t]);
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < HALF / 4; ++q) {
-            const long wo = (long)(h * HALF + 4 * q) * K + s * CIN + c;
-            acc[t] = mfma32(a[q].x, w[wo], acc[t]);
-            acc[t] = mfma32(a[q].y, w[wo + K], acc[t]);
-            acc[t] = mfma32(a[q].z, w[wo + 2 * K], acc[t]);
-            acc[t] = mfma32(a[q].w, w[wo + 3 * K], acc[t]);
-          }
+        for (int q = 0; q < HALF / 4; ++q) {
+          const f32x4 bw = ld4(wr + 4 * q);
+          acc[t] = mfma32(a[q].x, bw.x, acc[t]);
+          acc[t] = mfma32(a[q].y, bw.y, acc[t]);
+          acc[t] = mfma32(a[q].z, bw.z, acc[t]);
+          acc[t] = mfma32(a[q].w, bw.w, acc[t]);
         }
       }
     }
+    float* dst = (SPG == kSeq) ? dx : ws + (long)g * total_rows * CIN;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int c = t * 32 + i;
@@ -318,63 +350,82 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(const f
         const long mo = m0 + acc_row(rr, lane);
         if (mo < total_rows) {
           float v = acc[t][rr];
-          if (elu_y) v *= elu_grad_from_out(elu_y[mo * CIN + c]);
-          dx[mo * CIN + c] = v;
+          if (SPG == kSeq && elu_y) v *= elu_grad_from_out(elu_y[mo * CIN + c]);
+          dst[mo * CIN + c] = v;
         }
       }
     }
   }
 }
 
-// Backward data, small dpre (CO <= 4 channels; the xyz output conv):
-// L = CIN/4 lanes per source row u, lane q owns dx channels [4q, 4q+4).
+// Backward data, small dpre (CO <= 4 channels; the xyz output conv),
+// persistent over source rows: L = CIN/4 lanes per row u, lane q owns dx
+// channels [4q, 4q+4).  W (CO x kSeq*CIN) is staged once in LDS; the first
+// two inverse entries of every slot come from inv_pair so all their dpre
+// loads are issued together; further entries (rare) are looped.
 template <int CIN, int CO>
 __global__ __launch_bounds__(256) void conv_dx_out_small(const float* __restrict__ dpre,
                                                          const int* __restrict__ inv_ptr,
                                                          const int* __restrict__ inv_row,
+                                                         const int2* __restrict__ inv_pair,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ elu_y,
                                                          float* __restrict__ dx, int vsrc,
                                                          int rows, long total_rows) {
   constexpr int L = CIN / 4;
+  constexpr int RPW = 64 / L;
   constexpr int K = kSeq * CIN;
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int q = (int)(t % L);
-  const long m = t / L;
-  if (m >= total_rows) return;
-  const int b = (int)(m / vsrc), u = (int)(m % vsrc);
-  const float* db_ = dpre + (long)b * rows * CO;
-  int p[kSeq + 1];
+  __shared__ float wl[CO * K];
+  for (int e = threadIdx.x; e < CO * K; e += blockDim.x) wl[e] = w[e];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane % L, slot = lane / L;
+  const long stride = (long)gridDim.x * 4 * RPW;
+  for (long m = ((long)blockIdx.x * 4 + wave) * RPW + slot; m < total_rows; m += stride) {
+    const int b = (int)(m / vsrc), u = (int)(m % vsrc);
+    const float* db_ = dpre + (long)b * rows * CO;
+    const int2* pu = inv_pair + (long)u * kSeq;
+    float tt[kSeq][CO];
 #pragma unroll
-  for (int s = 0; s <= kSeq; ++s) p[s] = inv_ptr[(long)u * kSeq + s];
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < kSeq; ++s) {
+      const int2 pr = pu[s];
+      const float* p0 = db_ + (long)max(pr.x, 0) * CO;
+      const float* p1 = db_ + (long)max(pr.y, 0) * CO;
+      const float f0 = pr.x >= 0 ? 1.f : 0.f, f1 = pr.y >= 0 ? 1.f : 0.f;
 #pragma unroll
-  for (int s = 0; s < kSeq; ++s) {
-    float tt[CO];
-#pragma unroll
-    for (int o = 0; o < CO; ++o) tt[o] = 0.f;
-    for (int e = p[s]; e < p[s + 1]; ++e) {
-      const float* src = db_ + (long)inv_row[e] * CO;
-#pragma unroll
-      for (int o = 0; o < CO; ++o) tt[o] += src[o];
+      for (int o = 0; o < CO; ++o) tt[s][o] = p0[o] * f0 + p1[o] * f1;
     }
 #pragma unroll
-    for (int o = 0; o < CO; ++o) {
-      const f32x4 wv = ld4(w + (long)o * K + s * CIN + 4 * q);
-      acc.x = fmaf(tt[o], wv.x, acc.x);
-      acc.y = fmaf(tt[o], wv.y, acc.y);
-      acc.z = fmaf(tt[o], wv.z, acc.z);
-      acc.w = fmaf(tt[o], wv.w, acc.w);
+    for (int s = 0; s < kSeq; ++s) {
+      if (pu[s].y >= 0) {
+        const long key = (long)u * kSeq + s;
+        for (int e = inv_ptr[key] + 2; e < inv_ptr[key + 1]; ++e) {
+          const float* p = db_ + (long)inv_row[e] * CO;
+#pragma unroll
+          for (int o = 0; o < CO; ++o) tt[s][o] += p[o];
+        }
+      }
     }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kSeq; ++s)
+#pragma unroll
+      for (int o = 0; o < CO; ++o) {
+        const f32x4 wv = ld4(&wl[o * K + s * CIN + 4 * q]);
+        acc.x = fmaf(tt[s][o], wv.x, acc.x);
+        acc.y = fmaf(tt[s][o], wv.y, acc.y);
+        acc.z = fmaf(tt[s][o], wv.z, acc.z);
+        acc.w = fmaf(tt[s][o], wv.w, acc.w);
+      }
+    if (elu_y) {
+      const f32x4 g = ld4(elu_y + m * CIN + 4 * q);
+      acc.x *= elu_grad_from_out(g.x);
+      acc.y *= elu_grad_from_out(g.y);
+      acc.z *= elu_grad_from_out(g.z);
+      acc.w *= elu_grad_from_out(g.w);
+    }
+    st4(dx + m * CIN + 4 * q, acc);
   }
-  if (elu_y) {
-    const f32x4 g = ld4(elu_y + m * CIN + 4 * q);
-    acc.x *= elu_grad_from_out(g.x);
-    acc.y *= elu_grad_from_out(g.y);
-    acc.z *= elu_grad_from_out(g.z);
-    acc.w *= elu_grad_from_out(g.w);
-  }
-  st4(dx + m * CIN + 4 * q, acc);
 }
 
 // ==========================================================================
@@ -390,7 +441,7 @@ __global__ __launch_bounds__(256) void conv_dx_out_small(const float* __restrict
 template <int CIN, int COUT>
 struct DwCfg {
   static constexpr int U = kSeq * (COUT / 32) * (CIN / 32);
-  static constexpr int WAVES = (U % 4 == 0) ? 4 : 3;
+  static constexpr int WAVES = (U % 12 == 0) ? 12 : 9;  // 36 units -> 12 x 3, else 9 x U/9
   static constexpr int UPW = U / WAVES;
   static constexpr int THREADS = WAVES * 64;
   static constexpr int XF4 = kSeq * 32 * CIN / 4;  // float4s of gathered x per tile
@@ -402,7 +453,7 @@ struct DwCfg {
 };
 
 template <int CIN, int COUT>
-__global__ __launch_bounds__(256) void conv_dw_mfma(
+__global__ __launch_bounds__(768) void conv_dw_mfma(
     const float* __restrict__ x, const int* __restrict__ idx, const float* __restrict__ dpre,
     float* __restrict__ ws, float* __restrict__ ws_db, int vsrc, int rows, long total_rows) {
   using C = DwCfg<CIN, COUT>;
@@ -713,97 +764,157 @@ static int check_conv_args(const void* a, const void* b, const void* c, int batc
 }
 
 static const long kMaxPersistentBlocks = 1024;  // 4 per CU on 256 CUs
+static const unsigned kSmallBlocks = 1024;       // persistent VALU kernels
+
+// Slots per group for the MFMA fwd / bwd-data kernels: few rows -> split the
+// 9 spiral slots over more waves (partials combined by conv_combine).
+static int pick_spg(long m_rows, size_t ws_floats_avail, long out_cols) {
+  const long tiles = (m_rows + 31) / 32;
+  int spg = tiles >= 2048 ? 9 : (tiles >= 400 ? 3 : 1);
+  while (spg < 9 && (size_t)(kSeq / spg) * m_rows * out_cols > ws_floats_avail) spg = spg == 1 ? 3 : 9;
+  return spg;
+}
+
+static size_t slot_group_ws_floats(long m_rows, long out_cols) {
+  return (size_t)kSeq * m_rows * out_cols;  // worst case: 9 groups of one slot
+}
+
+template <int CIN, int COUT, int ACT, int SPG>
+static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const float* bias,
+                           float* y, float* ws, int vsrc, int rows, long M, hipStream_t st) {
+  constexpr size_t lds = (size_t)COUT * (SPG * CIN + 4) * sizeof(float);
+  static_assert(lds <= 80 * 1024, "W slice must fit LDS");
+  const long n_tiles = (M + 31) / 32;
+  dim3 grid(persistent_blocks(n_tiles, 4, kMaxPersistentBlocks / (kSeq / SPG) + 1), kSeq / SPG);
+  hipLaunchKernelGGL((conv_fwd_mfma<CIN, COUT, ACT, SPG>), grid, dim3(256), lds, st, x, idx, w,
+                     bias, y, ws, vsrc, rows, M);
+  int rc = launch_status("spiral_conv_fwd");
+  if (rc || SPG == kSeq) return rc;
+  const long n4 = M * COUT / 4;
+  hipLaunchKernelGGL((conv_combine<ACT>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, ws,
+                     bias, (const float*)nullptr, y, kSeq / SPG, COUT, n4);
+  return launch_status("spiral_conv_fwd_combine");
+}
 
 template <int CIN, int COUT, int ACT>
-static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const float* bias,
-                           float* y, int vsrc, int rows, long M, hipStream_t st) {
-  const size_t lds = (size_t)COUT * (kSeq * CIN + 4) * sizeof(float);
-  const long n_tiles = (M + 31) / 32;
-  dim3 grid(persistent_blocks(n_tiles, 4, kMaxPersistentBlocks));
-  if (lds <= 64 * 1024)
-    hipLaunchKernelGGL((conv_fwd_mfma<CIN, COUT, ACT, true>), grid, dim3(256), lds, st, x, idx, w,
-                       bias, y, vsrc, rows, M);
-  else
-    hipLaunchKernelGGL((conv_fwd_mfma<CIN, COUT, ACT, false>), grid, dim3(256), 0, st, x, idx, w,
-                       bias, y, vsrc, rows, M);
-  return launch_status("spiral_conv_fwd");
+static int dispatch_fwd_mfma(const float* x, const int* idx, const float* w, const float* bias,
+                             float* y, float* ws, size_t ws_floats, int vsrc, int rows, long M,
+                             hipStream_t st) {
+  constexpr bool big = (size_t)COUT * (kSeq * CIN + 4) * sizeof(float) > 80 * 1024;
+  int spg = ws ? pick_spg(M, ws_floats, COUT) : 9;
+  if (big && spg == 9) spg = 3;  // whole W does not fit LDS
+  if (spg != 9 && !ws) return set_error(CFSD_EWORKSPACE, "spiral_conv_fwd: workspace required");
+  if (spg == 9)
+    return launch_fwd_mfma<CIN, COUT, ACT, (big ? 3 : 9)>(x, idx, w, bias, y, ws, vsrc, rows, M, st);
+  if (spg == 3) return launch_fwd_mfma<CIN, COUT, ACT, 3>(x, idx, w, bias, y, ws, vsrc, rows, M, st);
+  return launch_fwd_mfma<CIN, COUT, ACT, 1>(x, idx, w, bias, y, ws, vsrc, rows, M, st);
+}
+
+extern "C" size_t cfsd_spiral_conv_workspace(int batch, int vsrc, int rows, int seq, int cin,
+                                             int cout) {
+  if (batch <= 0 || vsrc <= 0 || rows <= 0 || seq != kSeq || cin <= 0 || cout <= 0) return 0;
+  const size_t a = slot_group_ws_floats((long)batch * rows, cout);
+  const size_t b = slot_group_ws_floats((long)batch * vsrc, cin);
+  return (a > b ? a : b) * sizeof(float);
 }
 
 extern "C" int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const float* w,
-                                    const float* bias, float* y, int batch, int vsrc, int rows,
-                                    int seq, int cin, int cout, int act, void* stream) {
+                                    const float* bias, float* y, float* workspace,
+                                    size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
+                                    int cin, int cout, int act, void* stream) {
   int rc = check_conv_args(x, idx, w, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
   if (!y) return set_error(CFSD_EINVAL, "null y");
   if (act != CFSD_ACT_NONE && act != CFSD_ACT_ELU) return set_error(CFSD_EINVAL, "bad act %d", act);
   hipStream_t st = (hipStream_t)stream;
   const long M = (long)batch * rows;
-#define FWD(CIN_, COUT_)                                                                              \
-  if (cin == CIN_ && cout == COUT_)                                                                   \
-    return act == CFSD_ACT_ELU                                                                        \
-               ? launch_fwd_mfma<CIN_, COUT_, CFSD_ACT_ELU>(x, idx, w, bias, y, vsrc, rows, M, st)     \
-               : launch_fwd_mfma<CIN_, COUT_, CFSD_ACT_NONE>(x, idx, w, bias, y, vsrc, rows, M, st);
+  const size_t wsf = workspace ? workspace_bytes / sizeof(float) : 0;
+#define FWD(CIN_, COUT_)                                                                         \
+  if (cin == CIN_ && cout == COUT_)                                                              \
+    return act == CFSD_ACT_ELU                                                                   \
+               ? dispatch_fwd_mfma<CIN_, COUT_, CFSD_ACT_ELU>(x, idx, w, bias, y, workspace, wsf, \
+                                                              vsrc, rows, M, st)                 \
+               : dispatch_fwd_mfma<CIN_, COUT_, CFSD_ACT_NONE>(x, idx, w, bias, y, workspace,    \
+                                                               wsf, vsrc, rows, M, st);
   FWD(32, 32) FWD(32, 64) FWD(64, 32) FWD(64, 64)
 #undef FWD
-#define FWD_IN(CS_, COUT_)                                                                            \
-  if (cin == CS_ && cout == COUT_) {                                                                  \
-    dim3 g((unsigned)((M * COUT_ + 255) / 256));                                                      \
-    if (act == CFSD_ACT_ELU)                                                                          \
-      hipLaunchKernelGGL((conv_fwd_in_small<CS_, COUT_, CFSD_ACT_ELU>), g, dim3(256), 0, st, x, idx, \
-                         w, bias, y, vsrc, rows, M);                                                  \
-    else                                                                                              \
-      hipLaunchKernelGGL((conv_fwd_in_small<CS_, COUT_, CFSD_ACT_NONE>), g, dim3(256), 0, st, x,     \
-                         idx, w, bias, y, vsrc, rows, M);                                             \
-    return launch_status("spiral_conv_fwd_in_small");                                                 \
+#define FWD_SMALL(KERNEL, A_, B_)                                                                \
+  if (cin == A_ && cout == B_) {                                                                 \
+    if (act == CFSD_ACT_ELU)                                                                     \
+      hipLaunchKernelGGL((KERNEL<A_, B_, CFSD_ACT_ELU>), dim3(kSmallBlocks), dim3(256), 0, st, x, \
+                         idx, w, bias, y, vsrc, rows, M);                                        \
+    else                                                                                         \
+      hipLaunchKernelGGL((KERNEL<A_, B_, CFSD_ACT_NONE>), dim3(kSmallBlocks), dim3(256), 0, st,  \
+                         x, idx, w, bias, y, vsrc, rows, M);                                     \
+    return launch_status("spiral_conv_fwd_small");                                               \
   }
-  FWD_IN(3, 16) FWD_IN(3, 32) FWD_IN(3, 64)
-#undef FWD_IN
-#define FWD_OUT(CIN_, CO_)                                                                            \
-  if (cin == CIN_ && cout == CO_) {                                                                   \
-    dim3 g((unsigned)((M * (CIN_ / 4) + 255) / 256));                                                 \
-    if (act == CFSD_ACT_ELU)                                                                          \
-      hipLaunchKernelGGL((conv_fwd_out_small<CIN_, CO_, CFSD_ACT_ELU>), g, dim3(256), 0, st, x, idx, \
-                         w, bias, y, vsrc, rows, M);                                                  \
-    else                                                                                              \
-      hipLaunchKernelGGL((conv_fwd_out_small<CIN_, CO_, CFSD_ACT_NONE>), g, dim3(256), 0, st, x,     \
-                         idx, w, bias, y, vsrc, rows, M);                                             \
-    return launch_status("spiral_conv_fwd_out_small");                                                \
-  }
-  FWD_OUT(16, 3) FWD_OUT(32, 3) FWD_OUT(64, 3)
-#undef FWD_OUT
+  FWD_SMALL(conv_fwd_in_small, 3, 16) FWD_SMALL(conv_fwd_in_small, 3, 32)
+  FWD_SMALL(conv_fwd_in_small, 3, 64) FWD_SMALL(conv_fwd_out_small, 16, 3)
+  FWD_SMALL(conv_fwd_out_small, 32, 3) FWD_SMALL(conv_fwd_out_small, 64, 3)
+#undef FWD_SMALL
   return set_error(CFSD_EINVAL, "spiral_conv_fwd: unsupported channels %d -> %d", cin, cout);
+}
+
+template <int CIN, int COUT, int SPG>
+static int launch_dx_mfma(const float* dpre, const int* inv_ptr, const int* inv_row,
+                          const int* inv_pair, const float* w, const float* elu_y, float* dx,
+                          float* ws, int vsrc, int rows, long M, hipStream_t st) {
+  constexpr size_t lds = (size_t)SPG * CIN * (COUT + 4) * sizeof(float);
+  static_assert(lds <= 80 * 1024, "W slice must fit LDS");
+  dim3 grid(persistent_blocks((M + 31) / 32, 4, kMaxPersistentBlocks / (kSeq / SPG) + 1),
+            kSeq / SPG);
+  hipLaunchKernelGGL((conv_dx_mfma<CIN, COUT, SPG>), grid, dim3(256), lds, st, dpre, inv_ptr,
+                     inv_row, (const int2*)inv_pair, w, elu_y, dx, ws, vsrc, rows, M);
+  int rc = launch_status("spiral_conv_bwd_data");
+  if (rc || SPG == kSeq) return rc;
+  const long n4 = M * CIN / 4;
+  hipLaunchKernelGGL((conv_combine<CFSD_ACT_NONE>), dim3((unsigned)((n4 + 255) / 256)), dim3(256),
+                     0, st, ws, (const float*)nullptr, elu_y, dx, kSeq / SPG, CIN, n4);
+  return launch_status("spiral_conv_bwd_data_combine");
+}
+
+template <int CIN, int COUT>
+static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* inv_row,
+                            const int* inv_pair, const float* w, const float* elu_y, float* dx,
+                            float* ws, size_t ws_floats, int vsrc, int rows, long M,
+                            hipStream_t st) {
+  constexpr bool big = (size_t)kSeq * CIN * (COUT + 4) * sizeof(float) > 80 * 1024;
+  int spg = ws ? pick_spg(M, ws_floats, CIN) : 9;
+  if (big && spg == 9) spg = 3;
+  if (spg != 9 && !ws) return set_error(CFSD_EWORKSPACE, "spiral_conv_bwd_data: workspace required");
+  if (spg == 9)
+    return launch_dx_mfma<CIN, COUT, (big ? 3 : 9)>(dpre, inv_ptr, inv_row, inv_pair, w, elu_y, dx,
+                                                    ws, vsrc, rows, M, st);
+  if (spg == 3)
+    return launch_dx_mfma<CIN, COUT, 3>(dpre, inv_ptr, inv_row, inv_pair, w, elu_y, dx, ws, vsrc,
+                                        rows, M, st);
+  return launch_dx_mfma<CIN, COUT, 1>(dpre, inv_ptr, inv_row, inv_pair, w, elu_y, dx, ws, vsrc,
+                                      rows, M, st);
 }
 
 extern "C" int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_ptr,
                                          const int32_t* inv_row, const int32_t* inv_pair,
-                                         const float* w, const float* elu_y, float* dx, int batch,
+                                         const float* w, const float* elu_y, float* dx,
+                                         float* workspace, size_t workspace_bytes, int batch,
                                          int vsrc, int rows, int seq, int cin, int cout,
                                          void* stream) {
   int rc = check_conv_args(dpre, inv_ptr, inv_row, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
-  if (!w || !dx) return set_error(CFSD_EINVAL, "null w/dx");
+  if (!w || !dx || !inv_pair) return set_error(CFSD_EINVAL, "null w/dx/inv_pair");
   hipStream_t st = (hipStream_t)stream;
   const long M = (long)batch * vsrc;
-#define DXM(CIN_, COUT_)                                                                           \
-  if (cin == CIN_ && cout == COUT_) {                                                              \
-    if (!inv_pair) return set_error(CFSD_EINVAL, "null inv_pair");                                 \
-    const size_t lds = (size_t)kSeq * CIN_ * (COUT_ + 4) * sizeof(float);                          \
-    dim3 grid(persistent_blocks((M + 31) / 32, 4, kMaxPersistentBlocks));                          \
-    if (lds <= 80 * 1024)                                                                          \
-      hipLaunchKernelGGL((conv_dx_mfma<CIN_, COUT_, true>), grid, dim3(256), lds, st, dpre,        \
-                         inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M);    \
-    else                                                                                           \
-      hipLaunchKernelGGL((conv_dx_mfma<CIN_, COUT_, false>), grid, dim3(256), 0, st, dpre,         \
-                         inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M);    \
-    return launch_status("spiral_conv_bwd_data");                                                  \
-  }
+  const size_t wsf = workspace ? workspace_bytes / sizeof(float) : 0;
+#define DXM(CIN_, COUT_)                                                                       \
+  if (cin == CIN_ && cout == COUT_)                                                            \
+    return dispatch_dx_mfma<CIN_, COUT_>(dpre, inv_ptr, inv_row, inv_pair, w, elu_y, dx,       \
+                                         workspace, wsf, vsrc, rows, M, st);
   DXM(32, 32) DXM(32, 64) DXM(64, 32) DXM(64, 64)
 #undef DXM
-#define DXS(CIN_, CO_)                                                                           \
-  if (cin == CIN_ && cout == CO_) {                                                              \
-    hipLaunchKernelGGL((conv_dx_out_small<CIN_, CO_>), dim3((unsigned)((M * (CIN_ / 4) + 255) / 256)), \
-                       dim3(256), 0, st, dpre, inv_ptr, inv_row, w, elu_y, dx, vsrc, rows, M);   \
-    return launch_status("spiral_conv_bwd_data_small");                                         \
+#define DXS(CIN_, CO_)                                                                          \
+  if (cin == CIN_ && cout == CO_) {                                                             \
+    hipLaunchKernelGGL((conv_dx_out_small<CIN_, CO_>), dim3(kSmallBlocks), dim3(256), 0, st,    \
+                       dpre, inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M); \
+    return launch_status("spiral_conv_bwd_data_small");                                        \
   }
   DXS(16, 3) DXS(32, 3) DXS(64, 3)
 #undef DXS
@@ -827,7 +938,8 @@ DwGeom dw_geom(int batch, int rows, int cin, int cout) {
   if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64)) {
     g.kind = kDwMfma;
     const long n_tiles = (M + 31) / 32;
-    long gx = n_tiles < 512 ? n_tiles : 512;
+    long gx = (n_tiles + 3) / 4;  // >= 4 tiles per block keeps the slab traffic bounded
+    if (gx > 768) gx = 768;       // 3 blocks of 9 waves per CU
     g.gx = (int)(gx > 0 ? gx : 1);
     g.ws_floats = (size_t)g.gx * dw_units(cin, cout) * 1024 + (size_t)g.gx * cout;
   } else if (cin <= 4 && (cout == 16 || cout == 32 || cout == 64)) {

@@ -232,6 +232,12 @@ class SDVAEEngine:
         for (cin, cout, lv, _) in S.dec_layers():
             ws = max(ws, ops.spiral_conv_bwd_weight_workspace(bsz, nv[lv], T.seq[lv], cin, cout))
         ws = max(ws, ops.spiral_conv_bwd_weight_workspace(bsz, nv[0], T.seq[0], S.out_ch[0], S.in_ch))
+        for (cin, cout, lv) in S.enc_layers():
+            rows = nv[lv + 1] if T.enc_select[lv] else nv[lv]
+            ws = max(ws, ops.spiral_conv_workspace(bsz, nv[lv], rows, T.seq[lv], cin, cout))
+        for (cin, cout, lv, _) in S.dec_layers():
+            ws = max(ws, ops.spiral_conv_workspace(bsz, nv[lv], nv[lv], T.seq[lv], cin, cout))
+        ws = max(ws, ops.spiral_conv_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
         b.ws = torch.empty(ws // 4 + 64, dtype=torch.float32, device=dev)
         flat_in = self.num_vert * S.out_ch[-1]
         nmu = lat * (2 if S.is_vae else 1)
@@ -276,9 +282,11 @@ class SDVAEEngine:
         for (cin, cout, lv) in S.enc_layers():
             w, bias = self._enc_w(lv)
             if T.enc_select[lv]:
-                ops.spiral_conv_fwd(h, T.enc_rows[lv], w, bias, ACT_ELU, out=b.enc_out[lv])
+                ops.spiral_conv_fwd(h, T.enc_rows[lv], w, bias, ACT_ELU, out=b.enc_out[lv],
+                                    workspace=b.ws)
             else:
-                ops.spiral_conv_fwd(h, T.spiral[lv], w, bias, ACT_ELU, out=b.enc_full[lv])
+                ops.spiral_conv_fwd(h, T.spiral[lv], w, bias, ACT_ELU, out=b.enc_full[lv],
+                                    workspace=b.ws)
                 ops.spmm(T.down_csr[lv], b.enc_full[lv], T.n_verts[lv + 1], out=b.enc_out[lv])
             h = b.enc_out[lv]
         W, B = self._enc_lin()
@@ -306,11 +314,13 @@ class SDVAEEngine:
         for i, (cin, cout, lv, ui) in enumerate(S.dec_layers()):
             ops.spmm(T.up_csr[ui], h, T.n_verts[lv], out=b.dec_up[i])
             w, bias = self._dec_w(i)
-            ops.spiral_conv_fwd(b.dec_up[i], T.spiral[lv], w, bias, ACT_ELU, out=b.dec_out[i])
+            ops.spiral_conv_fwd(b.dec_up[i], T.spiral[lv], w, bias, ACT_ELU, out=b.dec_out[i],
+                                workspace=b.ws)
             h = b.dec_out[i]
         n = S.n
         ops.spiral_conv_fwd(h, T.spiral[0], self.params.view(f"de_layers.{n + 1}.layer.weight"),
-                            self.params.view(f"de_layers.{n + 1}.layer.bias"), ACT_NONE, out=b.out)
+                            self.params.view(f"de_layers.{n + 1}.layer.bias"), ACT_NONE, out=b.out,
+                            workspace=b.ws)
 
     def losses_fwd(self, b, acc=None):
         T = self.topo
@@ -335,7 +345,7 @@ class SDVAEEngine:
         ops.spiral_conv_bwd_weight(last_in, T.spiral[0], b.dout, P.gview(f"de_layers.{n + 1}.layer.weight"),
                                    P.gview(f"de_layers.{n + 1}.layer.bias"), b.ws)
         ops.spiral_conv_bwd_data(b.dout, T.spiral_inv[0], P.view(f"de_layers.{n + 1}.layer.weight"),
-                                 T.n_verts[0], elu_y=last_in, out=b.dpre_dec[-1])
+                                 T.n_verts[0], elu_y=last_in, out=b.dpre_dec[-1], workspace=b.ws)
         dec = S.dec_layers()
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]
@@ -344,7 +354,7 @@ class SDVAEEngine:
                                        P.gview(f"de_layers.{i + 1}.conv.layer.weight"),
                                        P.gview(f"de_layers.{i + 1}.conv.layer.bias"), b.ws)
             ops.spiral_conv_bwd_data(b.dpre_dec[i], T.spiral_inv[lv], w, T.n_verts[lv],
-                                     out=b.g_dec_up[i])
+                                     out=b.g_dec_up[i], workspace=b.ws)
             if i > 0:  # through Pool(up) into the previous Deblock's ELU
                 ops.spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], elu_y=b.dec_out[i - 1],
                          out=b.dpre_dec[i - 1])
@@ -382,10 +392,10 @@ class SDVAEEngine:
             if T.enc_select[prev]:
                 # input of this conv IS the ELU output of the previous Enblock
                 ops.spiral_conv_bwd_data(b.dpre_enc[lv], T.enc_inv[lv], w, T.n_verts[lv],
-                                         elu_y=b.enc_out[prev], out=b.dpre_enc[prev])
+                                         elu_y=b.enc_out[prev], out=b.dpre_enc[prev], workspace=b.ws)
             else:
                 ops.spiral_conv_bwd_data(b.dpre_enc[lv], T.enc_inv[lv], w, T.n_verts[lv],
-                                         out=b.g_pooled[prev])
+                                         out=b.g_pooled[prev], workspace=b.ws)
                 ops.spmm(T.downT_csr[prev], b.g_pooled[prev], T.n_verts[prev], elu_y=b.enc_full[prev],
                          out=b.dpre_enc[prev])
 

@@ -37,7 +37,21 @@ def _out(out, shape, like, name="out"):
 
 
 # ------------------------------------------------------------------ spiral conv
-def spiral_conv_fwd(x, idx, w, b, act=ACT_NONE, out=None):
+def spiral_conv_workspace(bsz, vsrc, rows, seq, cin, cout):
+    return int(_abi.lib().cfsd_spiral_conv_workspace(bsz, vsrc, rows, seq, cin, cout))
+
+
+def _conv_ws(workspace, device, need):
+    if workspace is None:
+        workspace = torch.empty(need // 4 + 1, dtype=torch.float32, device=device)
+    _need(workspace, None, name="workspace")
+    nbytes = workspace.numel() * workspace.element_size()
+    if nbytes < need:
+        raise ValueError(f"conv workspace {nbytes} < {need} bytes")
+    return workspace, nbytes
+
+
+def spiral_conv_fwd(x, idx, w, b, act=ACT_NONE, out=None, workspace=None):
     """y[b, r] = act(b + W . concat_s x[b, idx[r, s]])  (model.py:27-41)."""
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape
@@ -48,12 +62,13 @@ def spiral_conv_fwd(x, idx, w, b, act=ACT_NONE, out=None):
     if b is not None:
         _need(b, (cout,), name="bias")
     y = _out(out, (bsz, rows, cout), x)
-    call("cfsd_spiral_conv_fwd", ptr(x), ptr(idx), ptr(w), ptr(b), ptr(y), bsz, vsrc, rows, seq,
-         cin, cout, act, stream_ptr())
+    ws, nb = _conv_ws(workspace, x.device, spiral_conv_workspace(bsz, vsrc, rows, seq, cin, cout))
+    call("cfsd_spiral_conv_fwd", ptr(x), ptr(idx), ptr(w), ptr(b), ptr(y), ptr(ws),
+         ctypes.c_size_t(nb), bsz, vsrc, rows, seq, cin, cout, act, stream_ptr())
     return y
 
 
-def spiral_conv_bwd_data(dpre, inv, w, vsrc, elu_y=None, out=None):
+def spiral_conv_bwd_data(dpre, inv, w, vsrc, elu_y=None, out=None, workspace=None):
     """dx[b, u] = g * sum_{(r,s) in inv(u)} W_s^T dpre[b, r]; ``inv`` is the
     (inv_ptr, inv_row, inv_pair) triple of ``topology.inverse_spiral``."""
     bsz, rows, cout = dpre.shape
@@ -68,8 +83,10 @@ def spiral_conv_bwd_data(dpre, inv, w, vsrc, elu_y=None, out=None):
     if elu_y is not None:
         _need(elu_y, (bsz, vsrc, cin), name="elu_y")
     dx = _out(out, (bsz, vsrc, cin), dpre)
+    ws, nb = _conv_ws(workspace, dpre.device, spiral_conv_workspace(bsz, vsrc, rows, seq, cin, cout))
     call("cfsd_spiral_conv_bwd_data", ptr(dpre), ptr(inv_ptr), ptr(inv_row), ptr(inv_pair), ptr(w),
-         ptr(elu_y), ptr(dx), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+         ptr(elu_y), ptr(dx), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, seq, cin, cout,
+         stream_ptr())
     return dx
 
 

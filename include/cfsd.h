@@ -49,8 +49,14 @@ const char* cfsd_last_error_string(void);
  * Enblock evaluates the conv only where the 0/1 down-sample selects, which is
  * bit-identical to conv -> Pool(down) for a selection transform). */
 int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const float* w, const float* bias,
-                         float* y, int batch, int vsrc, int rows, int seq, int cin, int cout,
-                         int act, void* stream);
+                         float* y, float* workspace, size_t workspace_bytes, int batch, int vsrc,
+                         int rows, int seq, int cin, int cout, int act, void* stream);
+
+/* Workspace (bytes) that lets cfsd_spiral_conv_fwd / _bwd_data split the
+ * spiral slots of layers with few rows over more workgroups (partial sums
+ * combined in a fixed order).  NULL/0 workspace is allowed for 32-channel
+ * layers (no split); 64x64 layers require it. */
+size_t cfsd_spiral_conv_workspace(int batch, int vsrc, int rows, int seq, int cin, int cout);
 
 /* Replaces the autograd of model.py:34 (IndexSelectBackward = index_add_) and
  * :40 (AddmmBackward dX = dY.W), deterministically (no atomics):
@@ -64,8 +70,8 @@ int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const float* w, con
  * 3-channel VALU path).  The spiral length must be 9 (all reference configs). */
 int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_ptr, const int32_t* inv_row,
                               const int32_t* inv_pair, const float* w, const float* elu_y,
-                              float* dx, int batch, int vsrc, int rows, int seq, int cin, int cout,
-                              void* stream);
+                              float* dx, float* workspace, size_t workspace_bytes, int batch,
+                              int vsrc, int rows, int seq, int cin, int cout, void* stream);
 
 /* Replaces AddmmBackward's dW = G^T.dY and db = sum dY (model.py:40):
  *   dw[o, s*cin+c] = sum_{b,r} dpre[b,r,o] x[b, idx[r,s], c],  db[o] = sum_{b,r} dpre[b,r,o]

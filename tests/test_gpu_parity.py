@@ -38,17 +38,19 @@ def dtopo(topo_npz):
 
 
 # --------------------------------------------------------------- spiral conv
-CONV_CASES = [(3, 32, 3), (32, 32, 3), (32, 64, 3), (64, 32, 2), (64, 64, 2), (32, 3, 1),
-              (32, 32, 1), (3, 32, 0), (32, 3, 0)]
+# (cin, cout, level, batch): batches chosen so every slot-group split of the
+# MFMA kernels is exercised (<400 tiles -> 1 slot/group, 400-2047 -> 3, >=2048 -> 9).
+CONV_CASES = [(3, 32, 3, 3), (32, 32, 3, 3), (32, 64, 3, 3), (64, 32, 2, 3), (64, 64, 2, 3),
+              (32, 3, 1, 2), (32, 32, 1, 2), (3, 32, 0, 2), (32, 3, 0, 2), (32, 32, 0, 2),
+              (32, 32, 0, 4), (64, 32, 0, 4), (32, 64, 1, 16), (64, 64, 1, 16)]
 
 
-@pytest.mark.parametrize("cin,cout,level", CONV_CASES)
+@pytest.mark.parametrize("cin,cout,level,bsz", CONV_CASES)
 @pytest.mark.parametrize("act", [0, 1])
-def test_spiral_conv_fwd(otopo, dtopo, cin, cout, level, act):
+def test_spiral_conv_fwd(otopo, dtopo, cin, cout, level, bsz, act):
     g = torch.Generator().manual_seed(cin * 100 + cout + level)
     sp = otopo.spirals[level]
     v = sp.shape[0]
-    bsz = 3 if v < 2000 else 2
     x = torch.randn(bsz, v, cin, generator=g)
     w = torch.randn(cout, 9 * cin, generator=g) * 0.1
     b = torch.randn(cout, generator=g) * 0.1
@@ -59,13 +61,12 @@ def test_spiral_conv_fwd(otopo, dtopo, cin, cout, level, act):
     close(y, ref, 1e-5, "conv fwd")
 
 
-@pytest.mark.parametrize("cin,cout,level", [c for c in CONV_CASES if c[0] != 3])
+@pytest.mark.parametrize("cin,cout,level,bsz", [c for c in CONV_CASES if c[0] != 3])
 @pytest.mark.parametrize("use_elu_y", [False, True])
-def test_spiral_conv_bwd(otopo, dtopo, cin, cout, level, use_elu_y):
+def test_spiral_conv_bwd(otopo, dtopo, cin, cout, level, bsz, use_elu_y):
     g = torch.Generator().manual_seed(7 + cin + cout + level)
     sp = otopo.spirals[level]
     v = sp.shape[0]
-    bsz = 3 if v < 2000 else 2
     x = torch.randn(bsz, v, cin, generator=g).requires_grad_()
     xin = O.elu(x) if use_elu_y else x
     w = (torch.randn(cout, 9 * cin, generator=g) * 0.1).requires_grad_()

@@ -1,0 +1,115 @@
+"""CPU tests of the host side: C-ABI exports, index-table builders, engine
+parameter layout.  No kernel is launched here (no GPU in the build container)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import cfsd_loader
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+cfsd_loader.load()
+from craniofacialsd_vae_amd import _abi, topology  # noqa: E402
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "cfsd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cfsd_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_abi.LIB_PATH):
+        pytest.skip("libcfsd.so not built (run __graft_entry__.build())")
+    return _abi.load()
+
+
+def test_library_exports_every_header_symbol(lib):
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_abi.SIGNATURES), set(names) ^ set(_abi.SIGNATURES)
+
+
+def test_version_and_error_reporting(lib):
+    assert lib.cfsd_version() >> 16 == 1
+    # argument validation happens before any HIP call: safe without a GPU
+    rc = lib.cfsd_spiral_conv_fwd(None, None, None, None, None, None, 0, 1, 1, 1, 9, 32, 32, 0, None)
+    assert rc == -1
+    assert b"null" in lib.cfsd_last_error_string()
+    rc = lib.cfsd_spiral_conv_fwd(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16), None,
+                                  ctypes.c_void_p(16), None, 0, 1, 10, 10, 7, 32, 32, 0, None)
+    assert rc == -1 and b"spiral length" in lib.cfsd_last_error_string()
+    assert lib.cfsd_spiral_conv_bwd_weight_workspace(16, 17039, 9, 32, 32) > 0
+    assert lib.cfsd_spiral_conv_bwd_weight_workspace(16, 17039, 9, 7, 5) == 0
+
+
+def test_inverse_spiral_matches_bruteforce():
+    rs = np.random.RandomState(0)
+    idx = rs.randint(0, 50, size=(80, 9))
+    ptr, rows, pair = topology.inverse_spiral(idx, 50)
+    for u in range(50):
+        for s in range(9):
+            k = u * 9 + s
+            got = rows[ptr[k]:ptr[k + 1]].tolist()
+            exp = [r for r in range(80) if idx[r, s] == u]
+            assert got == exp
+            assert pair[k, 0] == (exp[0] if exp else -1)
+            assert pair[k, 1] == (exp[1] if len(exp) > 1 else -1)
+
+
+def test_csr_keeps_file_order_and_transpose():
+    row = np.array([2, 0, 2, 1, 0, 2])
+    col = np.array([5, 1, 0, 3, 4, 2])
+    val = np.arange(6, dtype=np.float32)
+    ptr, c, v = topology.csr_from_coo(row, col, val, 3)
+    assert ptr.tolist() == [0, 2, 3, 6]
+    assert c.tolist() == [1, 4, 3, 5, 0, 2] and v.tolist() == [1, 4, 3, 0, 2, 5]
+    tp, tc, tv = topology.csr_transpose_from_coo(row, col, val, 6)
+    assert tp.tolist() == [0, 1, 2, 3, 4, 5, 6]
+    assert tc.tolist() == [2, 0, 2, 1, 0, 2]
+
+
+def test_selection_detection(topo_npz):
+    for l in range(4):
+        sel = topology.selection_rows(topo_npz[f"down_{l}_row"], topo_npz[f"down_{l}_col"],
+                                      topo_npz[f"down_{l}_val"], int(topo_npz[f"down_{l}_shape"][0]))
+        assert sel is not None and len(np.unique(sel)) == len(sel)
+        up = topology.selection_rows(topo_npz[f"up_{l}_row"], topo_npz[f"up_{l}_col"],
+                                     topo_npz[f"up_{l}_val"], int(topo_npz[f"up_{l}_shape"][0]))
+        assert up is None
+
+
+def test_device_topology_tables_on_cpu(topo_npz):
+    T = topology.DeviceTopology.from_npz(topo_npz, device="cpu")
+    assert T.n_verts == [17039, 4260, 1065, 267, 67]
+    assert all(T.enc_select)
+    assert T.n_regions == 15 and tuple(T.region_mask.shape) == (15, 17039)
+    # row subset of level 0 == spiral rows of the kept vertices
+    sel = topology.selection_rows(topo_npz["down_0_row"], topo_npz["down_0_col"],
+                                  topo_npz["down_0_val"], 4260)
+    np.testing.assert_array_equal(T.enc_rows[0].numpy(), topo_npz["spiral_0"][sel])
+    # Laplacian rows sum to zero (random walk: 1 - sum 1/deg)
+    ptr, col, val = (t.numpy() for t in T.lap_csr)
+    sums = np.add.reduceat(val.astype(np.float64), ptr[:-1])
+    assert np.abs(sums).max() < 1e-6
+
+
+def test_engine_parameter_layout():
+    from craniofacialsd_vae_amd.engine import ModelSpec
+    import recipe
+    spec = ModelSpec()
+    specs = spec.param_specs(67, [9, 9, 9, 9])
+    ref = recipe.param_shapes()
+    assert sorted(specs) == sorted(ref)
+    assert spec.reference_order(67, [9, 9, 9, 9]) == [k for k, _ in ref]
+    names = [k for k, _ in specs]
+    # stacked encoder Linears: logvar (en_layers.4) then mu (en_layers.5), adjacent
+    i = names.index("en_layers.4.weight")
+    assert names[i + 1] == "en_layers.5.weight"
+    assert names[i + 2: i + 4] == ["en_layers.4.bias", "en_layers.5.bias"]
+    assert sum(int(np.prod(s)) for _, s in specs) == 1081881

@@ -33,6 +33,50 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 }
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
+// v_mfma_f32_16x16x4_f32: lane l holds A[l&15][l>>4], B[l>>4][l&15];
+// D: col = l&15, row = 4*(l>>4) + r.  32-cycle issue, 40-cycle dependent latency.
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
 constexpr int kMaxBatch = 1 << 20;
+
+// Workgroups of `kernel` that can be resident on the whole device at once
+// (occupancy API x CU count).  Persistent grids are sized to this so no
+// workgroup runs in a second, mostly idle, round.  Cached per kernel.
+int resident_blocks(const void* kernel, int block_threads, size_t dyn_lds);
+template <typename K>
+inline int resident_blocks_of(K kernel, int block_threads, size_t dyn_lds) {
+  return resident_blocks(reinterpret_cast<const void*>(kernel), block_threads, dyn_lds);
+}
+
+// Balanced persistent grid: `units` work items, `per_block` processed per
+// block-iteration, at most `max_blocks` blocks.
+inline unsigned balanced_blocks(long units, int per_block, long max_blocks) {
+  long need = (units + per_block - 1) / per_block;
+  if (need < 1) need = 1;
+  if (need <= max_blocks) return (unsigned)need;
+  const long iters = (need + max_blocks - 1) / max_blocks;
+  return (unsigned)((need + iters - 1) / iters);
+}
+
+// Gather load hidden from hipcc's waitcnt bookkeeping (cdna_hip_programming.md
+// §5.7 form (ii)): issue with gload4_async, then retire with a vm_wait4<N>
+// naming the destinations before the first consumer.  Used where hipcc's own
+// waitcnt placement would drain a prefetch one slot too early.
+__device__ __forceinline__ void gload4_async(f32x4& d, const float* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait4(f32x4& a, f32x4& b, f32x4& c, f32x4& d) {
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void vm_wait8(f32x4& a, f32x4& b, f32x4& c, f32x4& d, f32x4& e,
+                                         f32x4& f, f32x4& g, f32x4& h) {
+  asm volatile("s_waitcnt vmcnt(%8)"
+               : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h)
+               : "n"(N));
+}
 
 }  // namespace cfsd

@@ -23,35 +23,54 @@ namespace cfsd {
 
 constexpr int kSeq = 9;  // spiral length of every configuration (craniofacial/body/default.yaml)
 
-// Persistent-grid geometry: enough blocks for ~4 per CU, tiles spread evenly.
-static inline unsigned persistent_blocks(long n_tiles, int tiles_per_block_unit, long max_blocks) {
-  long units = (n_tiles + tiles_per_block_unit - 1) / tiles_per_block_unit;
-  if (units <= max_blocks) return (unsigned)(units > 0 ? units : 1);
-  long per = (units + max_blocks - 1) / max_blocks;
-  return (unsigned)((units + per - 1) / per);
+// XCD-aware persistent tile schedule.  Blocks b and b+8 share an XCD (and
+// its 4 MB L2) under the dispatcher's round-robin placement, so the blocks of
+// group g = b % G sweep ONE contiguous 1/G of the tile range: neighbouring
+// tiles gather neighbouring vertices, which then hit the same L2.  Placement
+// only changes speed, never results.
+struct TileSweep {
+  long begin, end, step;
+};
+__device__ __forceinline__ TileSweep xcd_sweep(long n_tiles, int lanes_per_block, int lane_id) {
+  const int nb = gridDim.x;
+  const int G = nb < 8 ? nb : 8;
+  const int grp = blockIdx.x % G, lb = blockIdx.x / G;
+  const int nb_g = (nb - grp + G - 1) / G;  // blocks in this group
+  const long per = (n_tiles + G - 1) / G;
+  TileSweep t;
+  t.begin = grp * per + (long)lb * lanes_per_block + lane_id;
+  t.end = min(n_tiles, (grp + 1) * per);
+  t.step = (long)nb_g * lanes_per_block;
+  return t;
 }
 
 // Occupancy target per channel shape (min waves per SIMD -> VGPR budget).
 constexpr int mfma_occ(int cin, int cout) { return (cin == 32 && cout == 32) ? 4 : 2; }
 
 // ==========================================================================
-// Forward, MFMA path: CIN, COUT in {32, 64}.  Each wave owns 32-row tiles of
-// the flattened (b, r) row space (all COUT columns) and loops over them.
-// Slot groups: blockIdx.y = g handles spiral slots [g*SPG, g*SPG + SPG); with
-// SPG < 9 (layers with few rows) the partial sums go to ws[g][m][COUT] and
+// Forward, MFMA path: CIN, COUT in {32, 64}.  A wave owns 32-row tiles
+// (two 16-row groups) of the flattened (b, r) row space and all COUT
+// columns, in a persistent XCD-aware sweep.  MFMA v_mfma_f32_16x16x4_f32:
+// lane (i = l&15, kg = l>>4) holds row i's 16-B chunks kg, kg+4, ... of each
+// gathered neighbour row, so ONE gather instruction covers 16 rows x 64
+// contiguous bytes (16 cache sectors) -- the 32x32x2 lane map needed 64 and
+// made the gathers address-(TA-)bound.  K order inside a slot is permuted
+// consistently for A and B (chunk-major), exact f32 as before.
+// Slot groups: blockIdx.y = g handles slots [g*SPG, g*SPG + SPG); with
+// SPG < 9 (layers with few rows) the partials go to ws[g][m][COUT] and
 // conv_combine adds the groups (fixed order), bias and activation.
-// W slice staged in LDS as [COUT][SPG*CIN + 4] (pad: 16-lane ds_read_b128
-// groups hit distinct 16-B slots).
+// W slice staged in LDS as [COUT][SPG*CIN + 8] (pad 8: conflict-free
+// ds_read_b128 for this lane map).
 template <int CIN, int COUT, int ACT, int SPG>
 __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(
     const float* __restrict__ x, const int* __restrict__ idx, const float* __restrict__ w,
     const float* __restrict__ bias, float* __restrict__ y, float* __restrict__ ws, int vsrc,
     int rows, long total_rows) {
-  constexpr int HALF = CIN / 2;
-  constexpr int NT = COUT / 32;
+  constexpr int CH = CIN / 16;    // 16-B chunks per lane per neighbour row
+  constexpr int NCT = COUT / 16;  // 16-column output tiles
   constexpr int K = kSeq * CIN;
   constexpr int KG = SPG * CIN;
-  constexpr int KP = KG + 4;
+  constexpr int KP = KG + 8;
   extern __shared__ float lds_w[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -61,70 +80,98 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(
     st4(&lds_w[n * KP + 4 * k4], ld4(&w[(long)n * K + s0 * CIN + 4 * k4]));
   }
   __syncthreads();
-  const int i = lane & 31, h = lane >> 5;
-  float bn[NT];
+  const int r16 = lane & 15, kg = lane >> 4;
+  float bn[NCT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) bn[t] = (SPG == kSeq && bias) ? bias[t * 32 + i] : 0.f;
-  const long n_tiles = (total_rows + 31) / 32;
-  for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
+  for (int t = 0; t < NCT; ++t) bn[t] = (SPG == kSeq && bias) ? bias[t * 16 + r16] : 0.f;
+  const TileSweep sw = xcd_sweep((total_rows + 31) / 32, 4, wave);
+  for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
     const long m0 = tile * 32;
-    long m = m0 + i;
-    if (m >= total_rows) m = total_rows - 1;  // clamp loads, stores are masked
-    const int b = (int)(m / rows), r = (int)(m % rows);
-    const float* xb = x + (long)b * vsrc * CIN + h * HALF;
-    const int* ir = idx + (long)r * kSeq + s0;
-    f32x16 acc[NT];
+    const float* xb[2];
+    int src[2][SPG];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = (f32x16){0.f};
-    // software pipeline: neighbour row of slot s+1 and index of slot s+2 are
-    // in flight while slot s runs its MFMAs (loop kept rolled: a full unroll
-    // makes hipcc hoist all nine gathers and spill).
-    f32x4 a[HALF / 4], an[HALF / 4];
-    int src_n = SPG > 1 ? ir[1] : 0;
+    for (int rg = 0; rg < 2; ++rg) {
+      long m = m0 + rg * 16 + r16;
+      if (m >= total_rows) m = total_rows - 1;  // clamp loads, stores are masked
+      const int b = (int)(m / rows), r = (int)(m % rows);
+      xb[rg] = x + (long)b * vsrc * CIN + 4 * kg;
+      const int* ir = idx + (long)r * kSeq + s0;
 #pragma unroll
-    for (int q = 0; q < HALF / 4; ++q) a[q] = ld4(xb + (long)ir[0] * CIN + 4 * q);
-#pragma unroll 1
+      for (int s = 0; s < SPG; ++s) src[rg][s] = ir[s];
+    }
+    // materialise all indices here: a compiler load sunk into the slot loop
+    // would carry a waitcnt that also drains the asm prefetch
+#pragma unroll
+    for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
+      for (int s = 0; s < SPG; ++s) asm volatile("" : "+v"(src[rg][s]));
+    f32x4 acc[2][NCT];
+#pragma unroll
+    for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) acc[rg][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // Software pipeline, fully unrolled over the slots with two static
+    // register buffers: slot s+1's rows are in flight while slot s runs its
+    // MFMAs.  Gathers are inline-asm loads retired by a counted vmcnt
+    // (hipcc's own placement drained the prefetch; see gload4_async).
+    f32x4 buf[2][2][CH];
+#pragma unroll
+    for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+        gload4_async(buf[0][rg][c], xb[rg] + (long)src[rg][0] * CIN + 16 * c);
+#pragma unroll
     for (int s = 0; s < SPG; ++s) {
+      f32x4(&cur)[2][CH] = buf[s & 1];
       if (s + 1 < SPG) {
-        const int src_nn = (s + 2 < SPG) ? ir[s + 2] : 0;
 #pragma unroll
-        for (int q = 0; q < HALF / 4; ++q) an[q] = ld4(xb + (long)src_n * CIN + 4 * q);
-        src_n = src_nn;
+        for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
+          for (int c = 0; c < CH; ++c)
+            gload4_async(buf[(s + 1) & 1][rg][c], xb[rg] + (long)src[rg][s + 1] * CIN + 16 * c);
+        if (CH == 2) vm_wait4<4>(cur[0][0], cur[0][1 % CH], cur[1][0], cur[1][1 % CH]);
+        else vm_wait8<8>(cur[0][0], cur[0][1 % CH], cur[0][2 % CH], cur[0][3 % CH], cur[1][0],
+                         cur[1][1 % CH], cur[1][2 % CH], cur[1][3 % CH]);
+      } else {
+        if (CH == 2) vm_wait4<0>(cur[0][0], cur[0][1 % CH], cur[1][0], cur[1][1 % CH]);
+        else vm_wait8<0>(cur[0][0], cur[0][1 % CH], cur[0][2 % CH], cur[0][3 % CH], cur[1][0],
+                         cur[1][1 % CH], cur[1][2 % CH], cur[1][3 % CH]);
       }
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const float* wr = &lds_w[(t * 32 + i) * KP + s * CIN + h * HALF];
+      for (int t = 0; t < NCT; ++t) {
 #pragma unroll
-        for (int q = 0; q < HALF / 4; ++q) {
-          const f32x4 bw = ld4(wr + 4 * q);
-          acc[t] = mfma32(a[q].x, bw.x, acc[t]);
-          acc[t] = mfma32(a[q].y, bw.y, acc[t]);
-          acc[t] = mfma32(a[q].z, bw.z, acc[t]);
-          acc[t] = mfma32(a[q].w, bw.w, acc[t]);
+        for (int c = 0; c < CH; ++c) {
+          const f32x4 bw = ld4(&lds_w[(t * 16 + r16) * KP + s * CIN + 4 * (kg + 4 * c)]);
+#pragma unroll
+          for (int rg = 0; rg < 2; ++rg) {
+            const f32x4 av = cur[rg][c];
+            acc[rg][t] = mfma16(av.x, bw.x, acc[rg][t]);
+            acc[rg][t] = mfma16(av.y, bw.y, acc[rg][t]);
+            acc[rg][t] = mfma16(av.z, bw.z, acc[rg][t]);
+            acc[rg][t] = mfma16(av.w, bw.w, acc[rg][t]);
+          }
         }
-      }
-      if (s + 1 < SPG) {
-#pragma unroll
-        for (int q = 0; q < HALF / 4; ++q) a[q] = an[q];
       }
     }
     float* dst = (SPG == kSeq) ? y : ws + (long)g * total_rows * COUT;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int n = t * 32 + i;
+    for (int rg = 0; rg < 2; ++rg)
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        const long mo = m0 + acc_row(rr, lane);
-        if (mo < total_rows) {
-          float v = acc[t][rr];
-          if (SPG == kSeq) {
-            v += bn[t];
-            if (ACT == CFSD_ACT_ELU) v = elu_f(v);
+      for (int t = 0; t < NCT; ++t) {
+        const int n = t * 16 + r16;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const long mo = m0 + rg * 16 + 4 * kg + rr;
+          if (mo < total_rows) {
+            float v = acc[rg][t][rr];
+            if (SPG == kSeq) {
+              v += bn[t];
+              if (ACT == CFSD_ACT_ELU) v = elu_f(v);
+            }
+            dst[mo * COUT + n] = v;
           }
-          dst[mo * COUT + n] = v;
         }
       }
-    }
   }
 }
 
@@ -155,10 +202,10 @@ __global__ __launch_bounds__(256) void conv_combine(const float* __restrict__ ws
   st4(out + 4 * t, v);
 }
 
-// Forward, small input (CS <= 4 channels, e.g. the xyz input of the first
-// Enblock): one lane per (row, output channel), persistent over rows.  The
-// CS*kSeq gathered inputs of a row are the same for its COUT lanes
-// (broadcast loads); each lane keeps its weight row in registers.
+// Forward, small input (CS <= 4 channels, e.g. the xyz input conv): one
+// thread per output row computing all COUT channels.  The 9 neighbour rows
+// are CS floats each (one dwordx3 per slot); W's addresses are wave-uniform
+// compile-time offsets -> scalar loads feeding the FMAs as SGPR operands.
 template <int CS, int COUT, int ACT>
 __global__ __launch_bounds__(256) void conv_fwd_in_small(const float* __restrict__ x,
                                                          const int* __restrict__ idx,
@@ -167,34 +214,39 @@ __global__ __launch_bounds__(256) void conv_fwd_in_small(const float* __restrict
                                                          float* __restrict__ y, int vsrc,
                                                          int rows, long total_rows) {
   constexpr int K = kSeq * CS;
-  constexpr int RPW = 64 / COUT;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int o = lane % COUT, slot = lane / COUT;
-  float wr[K];
+  const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= total_rows) return;
+  const int b = (int)(m / rows), r = (int)(m % rows);
+  const float* xb = x + (long)b * vsrc * CS;
+  const int* ir = idx + (long)r * kSeq;
+  float xv[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) wr[k] = w[o * K + k];
-  const float bo = bias ? bias[o] : 0.f;
-  const long stride = (long)gridDim.x * 4 * RPW;
-  for (long m = ((long)blockIdx.x * 4 + wave) * RPW + slot; m < total_rows; m += stride) {
-    const int b = (int)(m / rows), r = (int)(m % rows);
-    const float* xb = x + (long)b * vsrc * CS;
-    const int* ir = idx + (long)r * kSeq;
-    float acc = bo;
+  for (int s = 0; s < kSeq; ++s) {
+    const float* p = xb + (long)ir[s] * CS;
 #pragma unroll
-    for (int s = 0; s < kSeq; ++s) {
-      const float* p = xb + (long)ir[s] * CS;
+    for (int c = 0; c < CS; ++c) xv[s * CS + c] = p[c];
+  }
+  float* out = y + m * COUT;
 #pragma unroll
-      for (int c = 0; c < CS; ++c) acc = fmaf(p[c], wr[s * CS + c], acc);
+  for (int o4 = 0; o4 < COUT / 4; ++o4) {
+    float acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int o = 4 * o4 + j;
+      float a = bias ? bias[o] : 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) a = fmaf(xv[k], w[o * K + k], a);
+      acc[j] = ACT == CFSD_ACT_ELU ? elu_f(a) : a;
     }
-    if (ACT == CFSD_ACT_ELU) acc = elu_f(acc);
-    y[m * COUT + o] = acc;
+    st4(out + 4 * o4, (f32x4){acc[0], acc[1], acc[2], acc[3]});
   }
 }
 
-// Forward, small output (CO <= 4 channels, e.g. the xyz output conv),
-// persistent over rows: L = CIN/4 lanes per row, each lane owns a float4 of
-// input channels of every neighbour row (one coalesced 16*L-byte read per
-// neighbour), the CO partial dots are reduced across the L lanes.
+// Forward, small output (CO <= 4 channels, e.g. the xyz output conv): one
+// thread per output row.  Per slot the thread reads its neighbour's CIN
+// floats (CIN/4 dwordx4) and does CO*CIN FMAs against W, whose wave-uniform
+// addresses become scalar loads (SGPR operands).  Low VGPR use -> high
+// occupancy to cover the gather latency.
 template <int CIN, int CO, int ACT>
 __global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restrict__ x,
                                                           const int* __restrict__ idx,
@@ -202,54 +254,36 @@ __global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restric
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ y, int vsrc,
                                                           int rows, long total_rows) {
-  constexpr int L = CIN / 4;
-  constexpr int RPW = 64 / L;
   constexpr int K = kSeq * CIN;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int q = lane % L, slot = lane / L;
-  f32x4 wr[kSeq][CO];
+  const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= total_rows) return;
+  const int b = (int)(m / rows), r = (int)(m % rows);
+  const float* xb = x + (long)b * vsrc * CIN;
+  const int* ir = idx + (long)r * kSeq;
+  int src[kSeq];
 #pragma unroll
-  for (int s = 0; s < kSeq; ++s)
+  for (int s = 0; s < kSeq; ++s) src[s] = ir[s];
+  float acc[CO];
 #pragma unroll
-    for (int o = 0; o < CO; ++o) wr[s][o] = ld4(w + (long)o * K + s * CIN + 4 * q);
-  float bo[CO];
+  for (int o = 0; o < CO; ++o) acc[o] = bias ? bias[o] : 0.f;
 #pragma unroll
-  for (int o = 0; o < CO; ++o) bo[o] = bias ? bias[o] : 0.f;
-  const long n_rows_pad = (total_rows + RPW - 1) / RPW * RPW;  // whole waves stay in the loop
-  const long stride = (long)gridDim.x * 4 * RPW;
-  for (long mm = ((long)blockIdx.x * 4 + wave) * RPW + slot; mm < n_rows_pad; mm += stride) {
-    const bool valid = mm < total_rows;
-    const long m = valid ? mm : total_rows - 1;
-    const int b = (int)(m / rows), r = (int)(m % rows);
-    const float* xb = x + (long)b * vsrc * CIN + 4 * q;
-    const int* ir = idx + (long)r * kSeq;
-    float acc[CO];
+  for (int s = 0; s < kSeq; ++s) {
+    const float* p = xb + (long)src[s] * CIN;
 #pragma unroll
-    for (int o = 0; o < CO; ++o) acc[o] = 0.f;
-#pragma unroll
-    for (int s = 0; s < kSeq; ++s) {
-      const f32x4 v = ld4(xb + (long)ir[s] * CIN);
+    for (int c4 = 0; c4 < CIN / 4; ++c4) {
+      const f32x4 v = ld4(p + 4 * c4);
 #pragma unroll
       for (int o = 0; o < CO; ++o) {
-        acc[o] = fmaf(v.x, wr[s][o].x, acc[o]);
-        acc[o] = fmaf(v.y, wr[s][o].y, acc[o]);
-        acc[o] = fmaf(v.z, wr[s][o].z, acc[o]);
-        acc[o] = fmaf(v.w, wr[s][o].w, acc[o]);
-      }
-    }
-#pragma unroll
-    for (int o = 0; o < CO; ++o)
-#pragma unroll
-      for (int d = L / 2; d >= 1; d >>= 1) acc[o] += __shfl_xor(acc[o], d);
-    if (valid && q == 0) {
-#pragma unroll
-      for (int o = 0; o < CO; ++o) {
-        float v = acc[o] + bo[o];
-        if (ACT == CFSD_ACT_ELU) v = elu_f(v);
-        y[m * CO + o] = v;
+        const float* wp = w + o * K + s * CIN + 4 * c4;
+        acc[o] = fmaf(v.x, wp[0], acc[o]);
+        acc[o] = fmaf(v.y, wp[1], acc[o]);
+        acc[o] = fmaf(v.z, wp[2], acc[o]);
+        acc[o] = fmaf(v.w, wp[3], acc[o]);
       }
     }
   }
+#pragma unroll
+  for (int o = 0; o < CO; ++o) y[m * CO + o] = ACT == CFSD_ACT_ELU ? elu_f(acc[o]) : acc[o];
 }
 
 // ==========================================================================
@@ -282,8 +316,8 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
   }
   __syncthreads();
   const int i = lane & 31, h = lane >> 5;
-  const long n_tiles = (total_rows + 31) / 32;
-  for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
+  const TileSweep sw = xcd_sweep((total_rows + 31) / 32, 4, wave);
+  for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
     const long m0 = tile * 32;
     long m = m0 + i;
     if (m >= total_rows) m = total_rows - 1;
@@ -358,11 +392,14 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
   }
 }
 
-// Backward data, small dpre (CO <= 4 channels; the xyz output conv),
-// persistent over source rows: L = CIN/4 lanes per row u, lane q owns dx
-// channels [4q, 4q+4).  W (CO x kSeq*CIN) is staged once in LDS; the first
-// two inverse entries of every slot come from inv_pair so all their dpre
-// loads are issued together; further entries (rare) are looped.
+// Backward data, small dpre (CO <= 4 channels; the xyz output conv): one
+// thread per source row (b, u) computing all CIN outputs.  The spiral
+// transpose is first folded in the CO-wide dpre space,
+//   t[s][o] = sum_{r : idx[r][s] = u} dpre[b][r][o]   (inv_pair + rare overflow),
+// then dx[c] = sum_{s,o} t[s][o] * W[o][s*CIN + c].  W's addresses are
+// wave-uniform compile-time offsets, so they are scalar loads (SGPR operands
+// of the FMAs, no LDS, no per-lane W registers).  All 9 inv_pair loads and
+// the 18 dpre row loads of a thread are independent and issued together.
 template <int CIN, int CO>
 __global__ __launch_bounds__(256) void conv_dx_out_small(const float* __restrict__ dpre,
                                                          const int* __restrict__ inv_ptr,
@@ -372,59 +409,58 @@ __global__ __launch_bounds__(256) void conv_dx_out_small(const float* __restrict
                                                          const float* __restrict__ elu_y,
                                                          float* __restrict__ dx, int vsrc,
                                                          int rows, long total_rows) {
-  constexpr int L = CIN / 4;
-  constexpr int RPW = 64 / L;
   constexpr int K = kSeq * CIN;
-  __shared__ float wl[CO * K];
-  for (int e = threadIdx.x; e < CO * K; e += blockDim.x) wl[e] = w[e];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int q = lane % L, slot = lane / L;
-  const long stride = (long)gridDim.x * 4 * RPW;
-  for (long m = ((long)blockIdx.x * 4 + wave) * RPW + slot; m < total_rows; m += stride) {
-    const int b = (int)(m / vsrc), u = (int)(m % vsrc);
-    const float* db_ = dpre + (long)b * rows * CO;
-    const int2* pu = inv_pair + (long)u * kSeq;
-    float tt[kSeq][CO];
+  const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= total_rows) return;
+  const int b = (int)(m / vsrc), u = (int)(m % vsrc);
+  const float* db_ = dpre + (long)b * rows * CO;
+  const int2* pu = inv_pair + (long)u * kSeq;
+  int2 pr[kSeq];
 #pragma unroll
-    for (int s = 0; s < kSeq; ++s) {
-      const int2 pr = pu[s];
-      const float* p0 = db_ + (long)max(pr.x, 0) * CO;
-      const float* p1 = db_ + (long)max(pr.y, 0) * CO;
-      const float f0 = pr.x >= 0 ? 1.f : 0.f, f1 = pr.y >= 0 ? 1.f : 0.f;
+  for (int s = 0; s < kSeq; ++s) pr[s] = pu[s];
+  float tt[kSeq][CO];
 #pragma unroll
-      for (int o = 0; o < CO; ++o) tt[s][o] = p0[o] * f0 + p1[o] * f1;
-    }
+  for (int s = 0; s < kSeq; ++s) {
+    const float* p0 = db_ + (long)max(pr[s].x, 0) * CO;
+    const float* p1 = db_ + (long)max(pr[s].y, 0) * CO;
+    const float f0 = pr[s].x >= 0 ? 1.f : 0.f, f1 = pr[s].y >= 0 ? 1.f : 0.f;
 #pragma unroll
-    for (int s = 0; s < kSeq; ++s) {
-      if (pu[s].y >= 0) {
-        const long key = (long)u * kSeq + s;
-        for (int e = inv_ptr[key] + 2; e < inv_ptr[key + 1]; ++e) {
-          const float* p = db_ + (long)inv_row[e] * CO;
+    for (int o = 0; o < CO; ++o) tt[s][o] = p0[o] * f0 + p1[o] * f1;
+  }
 #pragma unroll
-          for (int o = 0; o < CO; ++o) tt[s][o] += p[o];
-        }
+  for (int s = 0; s < kSeq; ++s) {
+    if (pr[s].y >= 0) {
+      const long key = (long)u * kSeq + s;
+      for (int e = inv_ptr[key] + 2; e < inv_ptr[key + 1]; ++e) {
+        const float* p = db_ + (long)inv_row[e] * CO;
+#pragma unroll
+        for (int o = 0; o < CO; ++o) tt[s][o] += p[o];
       }
     }
+  }
+  float* out = dx + m * CIN;
+  const float* ey = elu_y ? elu_y + m * CIN : nullptr;
+#pragma unroll
+  for (int c4 = 0; c4 < CIN / 4; ++c4) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < kSeq; ++s)
 #pragma unroll
       for (int o = 0; o < CO; ++o) {
-        const f32x4 wv = ld4(&wl[o * K + s * CIN + 4 * q]);
-        acc.x = fmaf(tt[s][o], wv.x, acc.x);
-        acc.y = fmaf(tt[s][o], wv.y, acc.y);
-        acc.z = fmaf(tt[s][o], wv.z, acc.z);
-        acc.w = fmaf(tt[s][o], wv.w, acc.w);
+        const float* wp = w + o * K + s * CIN + 4 * c4;
+        acc.x = fmaf(tt[s][o], wp[0], acc.x);
+        acc.y = fmaf(tt[s][o], wp[1], acc.y);
+        acc.z = fmaf(tt[s][o], wp[2], acc.z);
+        acc.w = fmaf(tt[s][o], wp[3], acc.w);
       }
-    if (elu_y) {
-      const f32x4 g = ld4(elu_y + m * CIN + 4 * q);
+    if (ey) {
+      const f32x4 g = ld4(ey + 4 * c4);
       acc.x *= elu_grad_from_out(g.x);
       acc.y *= elu_grad_from_out(g.y);
       acc.z *= elu_grad_from_out(g.z);
       acc.w *= elu_grad_from_out(g.w);
     }
-    st4(dx + m * CIN + 4 * q, acc);
+    st4(out + 4 * c4, acc);
   }
 }
 
@@ -500,9 +536,10 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
     }
   };
 
-  long tile = blockIdx.x;
-  if (tile < n_tiles) load_tile(tile);
-  for (; tile < n_tiles; tile += gridDim.x) {
+  const TileSweep sw = xcd_sweep(n_tiles, 1, 0);
+  long tile = sw.begin;
+  if (tile < sw.end) load_tile(tile);
+  for (; tile < sw.end; tile += sw.step) {
 #pragma unroll
     for (int e = 0; e < C::XPT; ++e) {
       const int f = tid + e * C::THREADS;
@@ -514,8 +551,8 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
       if (f < C::DF4) st4(&dp_lds[4 * f], ds[e]);
     }
     __syncthreads();
-    const long next = tile + gridDim.x;
-    if (next < n_tiles) load_tile(next);
+    const long next = tile + sw.step;
+    if (next < sw.end) load_tile(next);
     if (tid < COUT) {
 #pragma unroll 8
       for (int row = 0; row < 32; ++row) db_acc += dp_lds[row * COUT + tid];
@@ -541,38 +578,42 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
   if (tid < COUT) ws_db[(long)blockIdx.x * COUT + tid] = db_acc;
 }
 
-// dw[o, s*CIN + c] = sum_p slab_p[unit(s, o/32, c/32)][o%32][c%32]; 16
-// threads per output element, fixed-order xor tree (deterministic).
+// dW/db slab reduction, coalesced: a 1024-thread block owns 64 consecutive
+// slab offsets f, its 16 waves sum the slabs w, w+16, ... and the 16 partials
+// are added in fixed order (deterministic); f is then mapped to dW's layout.
 template <int CIN, int COUT>
-__global__ __launch_bounds__(256) void conv_dw_reduce(const float* __restrict__ ws,
-                                                      const float* __restrict__ ws_db,
-                                                      float* __restrict__ dw,
-                                                      float* __restrict__ db, int n_slabs) {
+__global__ __launch_bounds__(1024) void conv_dw_reduce(const float* __restrict__ ws,
+                                                       const float* __restrict__ ws_db,
+                                                       float* __restrict__ dw,
+                                                       float* __restrict__ db, int n_slabs) {
   constexpr int OT = COUT / 32, CT = CIN / 32;
   constexpr int U = DwCfg<CIN, COUT>::U;
-  constexpr long n_out = (long)COUT * kSeq * CIN;
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long e = tid >> 4;
-  const int sub = threadIdx.x & 15;
-  const bool valid = e < n_out + COUT;
-  if (!valid) e = n_out + COUT - 1;
+  constexpr int NW = U * 1024;
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int f = blockIdx.x * 64 + lane;
+  const bool valid = f < NW + COUT;
+  if (!valid) f = NW + COUT - 1;
+  const float* src = f < NW ? ws + f : ws_db + (f - NW);
+  const long stride = f < NW ? NW : COUT;
   float sum = 0.f;
-  if (e < n_out) {
-    const int o = (int)(e / (kSeq * CIN));
-    const int k = (int)(e % (kSeq * CIN));
-    const int s = k / CIN, cc = k % CIN;
-    const int un = (s * OT + o / 32) * CT + cc / 32;
-    const long off = (long)un * 1024 + (o % 32) * 32 + (cc % 32);
-    for (int p = sub; p < n_slabs; p += 16) sum += ws[(long)p * (U * 1024) + off];
-  } else {
-    const int o = (int)(e - n_out);
-    for (int p = sub; p < n_slabs; p += 16) sum += ws_db[(long)p * COUT + o];
-  }
+#pragma unroll 4
+  for (int p = wv; p < n_slabs; p += 16) sum += src[(long)p * stride];
+  part[wv][lane] = sum;
+  __syncthreads();
+  if (wv == 0 && valid) {
+    float t = part[0][lane];
 #pragma unroll
-  for (int d = 8; d >= 1; d >>= 1) sum += __shfl_xor(sum, d);
-  if (sub == 0 && valid) {
-    if (e < n_out) dw[e] = sum;
-    else db[e - n_out] = sum;
+    for (int q = 1; q < 16; ++q) t += part[q][lane];
+    if (f < NW) {
+      const int un = f >> 10, within = f & 1023;
+      const int cc = (un % CT) * 32 + (within & 31);
+      const int o = ((un / CT) % OT) * 32 + (within >> 5);
+      const int s = un / (CT * OT);
+      dw[(long)o * (kSeq * CIN) + s * CIN + cc] = t;
+    } else {
+      db[f - NW] = t;
+    }
   }
 }
 
@@ -712,21 +753,265 @@ __global__ __launch_bounds__(256) void conv_dw_out_small(const float* __restrict
   for (int e = tid; e < NEL; e += 256) ws[(long)blockIdx.x * NEL + e] = red[e];
 }
 
-__global__ __launch_bounds__(256) void slab_reduce(const float* __restrict__ ws, int n_slabs,
-                                                   int n_el, float* __restrict__ out_a, int n_a,
-                                                   float* __restrict__ out_b) {
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long e = tid >> 4;
-  const int sub = threadIdx.x & 15;
+// ==========================================================================
+// Rank-64 MFMA update used by the 3-channel weight gradients.  A wave holds
+// a 64-row tile whose per-row 27/28-vector (gathered xyz, or the spiral-
+// transposed dpre) was written transposed into wave-private LDS,
+// At[i][k] (i < 32 padded with zero rows, k = tile row), and multiplies it by
+// the tile's rows of a dense row-major matrix B (dpre, or the layer input):
+//   acc[ct] (32 x 32) += At (32 x 64) . B[row0 .. row0+64)[ct*32 .. +32).
+// v_mfma_f32_32x32x2_f32 with k-order (kk, kk+32) per step so each lane
+// reads its A values as one ds_read_b128 per 4 steps.
+constexpr int kAts = 68;  // At row stride (floats): 16-B aligned, bank-spread
+
+template <int NCT>
+__device__ __forceinline__ void rank64_mfma(const float* At, const float* __restrict__ B,
+                                            long row0, long nrows, int ldb, f32x16 (&acc)[NCT],
+                                            int lane) {
+  const int i = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int kk = 0; kk < 32; kk += 4) {
+    const f32x4 a = ld4(&At[i * kAts + 32 * h + kk]);
+    float bv[4][NCT];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      long rr = row0 + kk + j + 32 * h;
+      if (rr >= nrows) rr = nrows - 1;  // its A column is zero
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) bv[j][ct] = B[rr * ldb + ct * 32 + i];
+    }
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      acc[ct] = mfma32(a.x, bv[0][ct], acc[ct]);
+      acc[ct] = mfma32(a.y, bv[1][ct], acc[ct]);
+      acc[ct] = mfma32(a.z, bv[2][ct], acc[ct]);
+      acc[ct] = mfma32(a.w, bv[3][ct], acc[ct]);
+    }
+  }
+}
+
+// LDS writes by some lanes -> reads by other lanes of the same wave: LDS
+// executes a wave's instructions in order, so a counter wait plus a compiler
+// barrier is enough (no s_barrier; waves run independent tile counts).
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Backward weight, small input (CS <= 3; first Enblock) on MFMA:
+//   dW^T[(s,c)][o] = sum_m G[m][(s,c)] dpre[m][o],   db[o] = sum_m 1 * dpre[m][o]
+// where G is the gathered input (27 values per row); row 27 of At is the
+// all-ones row so db falls out of the same MFMAs.  Persistent waves over
+// 64-row tiles, block partials combined in fixed order -> one slab
+// [COUT*K + COUT] per block (reduced by slab_reduce).
+template <int CS, int COUT>
+__global__ __launch_bounds__(256) void conv_dw_in_mfma(const float* __restrict__ x,
+                                                       const int* __restrict__ idx,
+                                                       const float* __restrict__ dpre,
+                                                       float* __restrict__ ws, int vsrc, int rows,
+                                                       long total_rows) {
+  constexpr int K = kSeq * CS, NI = K + 1, NCT = COUT / 32, NEL = COUT * K + COUT;
+  static_assert(NI <= 32 && COUT % 32 == 0, "shape");
+  __shared__ float at_all[4 * 32 * kAts];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* At = at_all + wave * 32 * kAts;
+  for (int e = lane; e < (32 - NI) * kAts; e += 64) At[NI * kAts + e] = 0.f;
+  f32x16 acc[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[ct][r] = 0.f;
+  const long n_tiles = (total_rows + 63) / 64;
+  for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
+    const long m = tile * 64 + lane;
+    const bool valid = m < total_rows;
+    const long mm = valid ? m : total_rows - 1;
+    const int b = (int)(mm / rows), r = (int)(mm % rows);
+    const float* xb = x + (long)b * vsrc * CS;
+    const int* ir = idx + (long)r * kSeq;
+    float xv[K];
+#pragma unroll
+    for (int s = 0; s < kSeq; ++s) {
+      const float* p = xb + (long)ir[s] * CS;
+#pragma unroll
+      for (int c = 0; c < CS; ++c) xv[s * CS + c] = p[c];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) At[k * kAts + lane] = valid ? xv[k] : 0.f;
+    At[K * kAts + lane] = valid ? 1.f : 0.f;
+    wave_lds_sync();
+    rank64_mfma<NCT>(At, dpre, tile * 64, total_rows, COUT, acc, lane);
+    wave_lds_sync();
+  }
+  __syncthreads();
+  float* red = at_all;  // reuse: NEL floats
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv) {
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int i = acc_row(rr, lane), o = ct * 32 + (lane & 31);
+          if (i < NI) {
+            const int e = i < K ? o * K + i : COUT * K + o;
+            red[e] = wv == 0 ? acc[ct][rr] : red[e] + acc[ct][rr];
+          }
+        }
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < NEL; e += 256) ws[(long)blockIdx.x * NEL + e] = red[e];
+}
+
+// Backward of a small-output conv (CO*kSeq <= 32; the xyz output conv),
+// data + weight fused, in source-row space.  Per source row (b, u) a thread
+// folds the spiral transpose in the CO-wide dpre space,
+//   t[s][o] = sum_{r : idx[r][s] = u} dpre[b][r][o]       (inv_pair + overflow)
+// and then produces
+//   dx[b][u][c]  = g * sum_{s,o} t[s][o] W[o][s*CIN + c]   (VALU, W as SGPRs)
+//   dW[o][s*CIN + c] += t[s][o] x[b][u][c]                  (rank-64 MFMA per tile)
+//   db[o] += t[0][o]        (every row r appears once in slot 0's lists)
+// The dW identity is the same double sum as sum_r dpre[r] x[idx[r][s]],
+// regrouped by source row, so x is read densely instead of gathered.
+template <int CIN, int CO>
+__global__ __launch_bounds__(256) void conv_bwd_out_small(
+    const float* __restrict__ dpre, const int* __restrict__ inv_ptr,
+    const int* __restrict__ inv_row, const int2* __restrict__ inv_pair,
+    const float* __restrict__ w, const float* __restrict__ elu_y, const float* __restrict__ x,
+    float* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, long total_rows) {
+  constexpr int K = kSeq * CIN, NI = kSeq * CO, NCT = CIN / 32, NEL = CO * K + CO;
+  static_assert(NI <= 32 && CIN % 32 == 0, "shape");
+  __shared__ float at_all[4 * 32 * kAts];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* At = at_all + wave * 32 * kAts;
+  for (int e = lane; e < (32 - NI) * kAts; e += 64) At[NI * kAts + e] = 0.f;
+  f32x16 acc[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[ct][r] = 0.f;
+  float dbs[CO];
+#pragma unroll
+  for (int o = 0; o < CO; ++o) dbs[o] = 0.f;
+  const long n_tiles = (total_rows + 63) / 64;
+  for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
+    const long m = tile * 64 + lane;
+    const bool valid = m < total_rows;
+    const long mm = valid ? m : total_rows - 1;
+    const int b = (int)(mm / vsrc), u = (int)(mm % vsrc);
+    const float* db_ = dpre + (long)b * rows * CO;
+    const int2* pu = inv_pair + (long)u * kSeq;
+    int2 pr[kSeq];
+#pragma unroll
+    for (int s = 0; s < kSeq; ++s) pr[s] = pu[s];
+    float tt[kSeq][CO];
+#pragma unroll
+    for (int s = 0; s < kSeq; ++s) {
+      const float* p0 = db_ + (long)max(pr[s].x, 0) * CO;
+      const float* p1 = db_ + (long)max(pr[s].y, 0) * CO;
+      const float f0 = pr[s].x >= 0 ? 1.f : 0.f, f1 = pr[s].y >= 0 ? 1.f : 0.f;
+#pragma unroll
+      for (int o = 0; o < CO; ++o) tt[s][o] = p0[o] * f0 + p1[o] * f1;
+    }
+#pragma unroll
+    for (int s = 0; s < kSeq; ++s) {
+      if (pr[s].y >= 0) {
+        const long key = (long)u * kSeq + s;
+        for (int e = inv_ptr[key] + 2; e < inv_ptr[key + 1]; ++e) {
+          const float* p = db_ + (long)inv_row[e] * CO;
+#pragma unroll
+          for (int o = 0; o < CO; ++o) tt[s][o] += p[o];
+        }
+      }
+    }
+    if (!valid) {
+#pragma unroll
+      for (int s = 0; s < kSeq; ++s)
+#pragma unroll
+        for (int o = 0; o < CO; ++o) tt[s][o] = 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < kSeq; ++s)
+#pragma unroll
+      for (int o = 0; o < CO; ++o) At[(s * CO + o) * kAts + lane] = tt[s][o];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) dbs[o] += tt[0][o];
+    if (dx && valid) {
+      float* out = dx + mm * CIN;
+      const float* ey = elu_y ? elu_y + mm * CIN : nullptr;
+#pragma unroll
+      for (int c4 = 0; c4 < CIN / 4; ++c4) {
+        f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < kSeq; ++s)
+#pragma unroll
+          for (int o = 0; o < CO; ++o) {
+            const float* wp = w + o * K + s * CIN + 4 * c4;
+            a4.x = fmaf(tt[s][o], wp[0], a4.x);
+            a4.y = fmaf(tt[s][o], wp[1], a4.y);
+            a4.z = fmaf(tt[s][o], wp[2], a4.z);
+            a4.w = fmaf(tt[s][o], wp[3], a4.w);
+          }
+        if (ey) {
+          const f32x4 g = ld4(ey + 4 * c4);
+          a4.x *= elu_grad_from_out(g.x);
+          a4.y *= elu_grad_from_out(g.y);
+          a4.z *= elu_grad_from_out(g.z);
+          a4.w *= elu_grad_from_out(g.w);
+        }
+        st4(out + 4 * c4, a4);
+      }
+    }
+    wave_lds_sync();
+    rank64_mfma<NCT>(At, x, tile * 64, total_rows, CIN, acc, lane);
+    wave_lds_sync();
+  }
+#pragma unroll
+  for (int o = 0; o < CO; ++o)
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) dbs[o] += __shfl_xor(dbs[o], d);
+  __syncthreads();
+  float* red = at_all;
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv) {
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int i = acc_row(rr, lane), c = ct * 32 + (lane & 31);
+          if (i < NI) {
+            const int e = (i % CO) * K + (i / CO) * CIN + c;
+            red[e] = wv == 0 ? acc[ct][rr] : red[e] + acc[ct][rr];
+          }
+        }
+      if (lane == 0)
+#pragma unroll
+        for (int o = 0; o < CO; ++o) red[CO * K + o] = wv == 0 ? dbs[o] : red[CO * K + o] + dbs[o];
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < NEL; e += 256) ws[(long)blockIdx.x * NEL + e] = red[e];
+}
+
+__global__ __launch_bounds__(1024) void slab_reduce(const float* __restrict__ ws, int n_slabs,
+                                                    int n_el, float* __restrict__ out_a, int n_a,
+                                                    float* __restrict__ out_b) {
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int e = blockIdx.x * 64 + lane;
   const bool valid = e < n_el;
   if (!valid) e = n_el - 1;
   float sum = 0.f;
-  for (int p = sub; p < n_slabs; p += 16) sum += ws[(long)p * n_el + e];
+#pragma unroll 4
+  for (int p = wv; p < n_slabs; p += 16) sum += ws[(long)p * n_el + e];
+  part[wv][lane] = sum;
+  __syncthreads();
+  if (wv == 0 && valid) {
+    float t = part[0][lane];
 #pragma unroll
-  for (int d = 8; d >= 1; d >>= 1) sum += __shfl_xor(sum, d);
-  if (sub == 0 && valid) {
-    if (e < n_a) out_a[e] = sum;
-    else out_b[e - n_a] = sum;
+    for (int q = 1; q < 16; ++q) t += part[q][lane];
+    if (e < n_a) out_a[e] = t;
+    else out_b[e - n_a] = t;
   }
 }
 
@@ -763,8 +1048,16 @@ static int check_conv_args(const void* a, const void* b, const void* c, int batc
   return CFSD_OK;
 }
 
-static const long kMaxPersistentBlocks = 1024;  // 4 per CU on 256 CUs
-static const unsigned kSmallBlocks = 1024;       // persistent VALU kernels
+// Persistent VALU kernels: one resident round, never more blocks than rows/64.
+template <typename K>
+static unsigned small_grid(K kernel, long rows) {
+  const long cap = resident_blocks_of(kernel, 256, 0);
+  const long need = (rows + 63) / 64;
+  return (unsigned)(need < cap ? (need > 0 ? need : 1) : cap);
+}
+
+// One thread per row, 256-thread blocks.
+static unsigned row_grid(long rows) { return (unsigned)((rows + 255) / 256); }
 
 // Slots per group for the MFMA fwd / bwd-data kernels: few rows -> split the
 // 9 spiral slots over more waves (partials combined by conv_combine).
@@ -782,11 +1075,13 @@ static size_t slot_group_ws_floats(long m_rows, long out_cols) {
 template <int CIN, int COUT, int ACT, int SPG>
 static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const float* bias,
                            float* y, float* ws, int vsrc, int rows, long M, hipStream_t st) {
-  constexpr size_t lds = (size_t)COUT * (SPG * CIN + 4) * sizeof(float);
+  constexpr size_t lds = (size_t)COUT * (SPG * CIN + 8) * sizeof(float);
   static_assert(lds <= 80 * 1024, "W slice must fit LDS");
   const long n_tiles = (M + 31) / 32;
-  dim3 grid(persistent_blocks(n_tiles, 4, kMaxPersistentBlocks / (kSeq / SPG) + 1), kSeq / SPG);
-  hipLaunchKernelGGL((conv_fwd_mfma<CIN, COUT, ACT, SPG>), grid, dim3(256), lds, st, x, idx, w,
+  auto kern = conv_fwd_mfma<CIN, COUT, ACT, SPG>;
+  const long max_blocks = resident_blocks_of(kern, 256, lds) / (kSeq / SPG);
+  dim3 grid(balanced_blocks(n_tiles, 4, max_blocks > 0 ? max_blocks : 1), kSeq / SPG);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, x, idx, w,
                      bias, y, ws, vsrc, rows, M);
   int rc = launch_status("spiral_conv_fwd");
   if (rc || SPG == kSeq) return rc;
@@ -800,7 +1095,7 @@ template <int CIN, int COUT, int ACT>
 static int dispatch_fwd_mfma(const float* x, const int* idx, const float* w, const float* bias,
                              float* y, float* ws, size_t ws_floats, int vsrc, int rows, long M,
                              hipStream_t st) {
-  constexpr bool big = (size_t)COUT * (kSeq * CIN + 4) * sizeof(float) > 80 * 1024;
+  constexpr bool big = (size_t)COUT * (kSeq * CIN + 8) * sizeof(float) > 80 * 1024;
   int spg = ws ? pick_spg(M, ws_floats, COUT) : 9;
   if (big && spg == 9) spg = 3;  // whole W does not fit LDS
   if (spg != 9 && !ws) return set_error(CFSD_EWORKSPACE, "spiral_conv_fwd: workspace required");
@@ -840,12 +1135,15 @@ extern "C" int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const fl
 #undef FWD
 #define FWD_SMALL(KERNEL, A_, B_)                                                                \
   if (cin == A_ && cout == B_) {                                                                 \
-    if (act == CFSD_ACT_ELU)                                                                     \
-      hipLaunchKernelGGL((KERNEL<A_, B_, CFSD_ACT_ELU>), dim3(kSmallBlocks), dim3(256), 0, st, x, \
-                         idx, w, bias, y, vsrc, rows, M);                                        \
-    else                                                                                         \
-      hipLaunchKernelGGL((KERNEL<A_, B_, CFSD_ACT_NONE>), dim3(kSmallBlocks), dim3(256), 0, st,  \
-                         x, idx, w, bias, y, vsrc, rows, M);                                     \
+    if (act == CFSD_ACT_ELU) {                                                                   \
+      auto k = KERNEL<A_, B_, CFSD_ACT_ELU>;                                                     \
+      hipLaunchKernelGGL(k, dim3(row_grid(M)), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, \
+                         M);                                                                     \
+    } else {                                                                                     \
+      auto k = KERNEL<A_, B_, CFSD_ACT_NONE>;                                                    \
+      hipLaunchKernelGGL(k, dim3(row_grid(M)), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, \
+                         M);                                                                     \
+    }                                                                                            \
     return launch_status("spiral_conv_fwd_small");                                               \
   }
   FWD_SMALL(conv_fwd_in_small, 3, 16) FWD_SMALL(conv_fwd_in_small, 3, 32)
@@ -861,9 +1159,10 @@ static int launch_dx_mfma(const float* dpre, const int* inv_ptr, const int* inv_
                           float* ws, int vsrc, int rows, long M, hipStream_t st) {
   constexpr size_t lds = (size_t)SPG * CIN * (COUT + 4) * sizeof(float);
   static_assert(lds <= 80 * 1024, "W slice must fit LDS");
-  dim3 grid(persistent_blocks((M + 31) / 32, 4, kMaxPersistentBlocks / (kSeq / SPG) + 1),
-            kSeq / SPG);
-  hipLaunchKernelGGL((conv_dx_mfma<CIN, COUT, SPG>), grid, dim3(256), lds, st, dpre, inv_ptr,
+  auto kern = conv_dx_mfma<CIN, COUT, SPG>;
+  const long max_blocks = resident_blocks_of(kern, 256, lds) / (kSeq / SPG);
+  dim3 grid(balanced_blocks((M + 31) / 32, 4, max_blocks > 0 ? max_blocks : 1), kSeq / SPG);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, dpre, inv_ptr,
                      inv_row, (const int2*)inv_pair, w, elu_y, dx, ws, vsrc, rows, M);
   int rc = launch_status("spiral_conv_bwd_data");
   if (rc || SPG == kSeq) return rc;
@@ -912,7 +1211,8 @@ extern "C" int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_p
 #undef DXM
 #define DXS(CIN_, CO_)                                                                          \
   if (cin == CIN_ && cout == CO_) {                                                             \
-    hipLaunchKernelGGL((conv_dx_out_small<CIN_, CO_>), dim3(kSmallBlocks), dim3(256), 0, st,    \
+    auto k = conv_dx_out_small<CIN_, CO_>;                                                      \
+    hipLaunchKernelGGL(k, dim3(row_grid(M)), dim3(256), 0, st,                                  \
                        dpre, inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M); \
     return launch_status("spiral_conv_bwd_data_small");                                        \
   }
@@ -923,7 +1223,7 @@ extern "C" int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_p
 
 // ---- bwd weight: launch geometry shared by the workspace query and the launch
 namespace {
-enum DwKind { kDwMfma, kDwInSmall, kDwOutSmall, kDwNone };
+enum DwKind { kDwMfma, kDwInMfma, kDwInSmall, kDwOutSmall, kDwNone };
 struct DwGeom {
   DwKind kind;
   int gx;
@@ -942,6 +1242,11 @@ DwGeom dw_geom(int batch, int rows, int cin, int cout) {
     if (gx > 768) gx = 768;       // 3 blocks of 9 waves per CU
     g.gx = (int)(gx > 0 ? gx : 1);
     g.ws_floats = (size_t)g.gx * dw_units(cin, cout) * 1024 + (size_t)g.gx * cout;
+  } else if (cin <= 3 && (cout == 32 || cout == 64)) {
+    g.kind = kDwInMfma;
+    long gx = ((M + 63) / 64 + 3) / 4;  // one 64-row tile per wave per pass
+    g.gx = (int)(gx > 512 ? 512 : (gx < 1 ? 1 : gx));
+    g.ws_floats = (size_t)g.gx * ((size_t)cout * kSeq * cin + cout);
   } else if (cin <= 4 && (cout == 16 || cout == 32 || cout == 64)) {
     g.kind = kDwInSmall;
     const long per_blk = 4 * (64 / cout);
@@ -981,19 +1286,22 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
   hipStream_t st = (hipStream_t)stream;
   const long M = (long)batch * rows;
   const int n_el = cout * kSeq * cin + cout;
-  const dim3 rg((unsigned)(((long)n_el * 16 + 255) / 256));
+  const dim3 rg((unsigned)((n_el + 63) / 64));
   if (g.kind == kDwMfma) {
     float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
+    int nslab = g.gx;
 #define DWM(CIN_, COUT_)                                                                        \
   if (cin == CIN_ && cout == COUT_) {                                                           \
     using C = DwCfg<CIN_, COUT_>;                                                               \
-    hipLaunchKernelGGL((conv_dw_mfma<CIN_, COUT_>), dim3(g.gx), dim3(C::THREADS),               \
-                       C::LDS_FLOATS * sizeof(float), st, x, idx, dpre, workspace, ws_db, vsrc, \
-                       rows, M);                                                                \
+    auto k = conv_dw_mfma<CIN_, COUT_>;                                                         \
+    const int cap = resident_blocks_of(k, C::THREADS, C::LDS_FLOATS * sizeof(float));           \
+    nslab = g.gx < cap ? g.gx : cap;                                                            \
+    hipLaunchKernelGGL(k, dim3(nslab), dim3(C::THREADS), C::LDS_FLOATS * sizeof(float), st, x,  \
+                       idx, dpre, workspace, ws_db, vsrc, rows, M);                             \
     rc = launch_status("spiral_conv_bwd_weight");                                               \
     if (rc) return rc;                                                                          \
-    hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), rg, dim3(256), 0, st, workspace, ws_db,   \
-                       dw, db, g.gx);                                                           \
+    hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), rg, dim3(1024), 0, st, workspace, ws_db,  \
+                       dw, db, nslab);                                                          \
     return launch_status("spiral_conv_bwd_weight_reduce");                                      \
   }
     DWM(32, 32) DWM(32, 64) DWM(64, 32) DWM(64, 64)
@@ -1005,17 +1313,83 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
                        vsrc, rows, M);                                                            \
     rc = launch_status("spiral_conv_bwd_weight_small");                                           \
     if (rc) return rc;                                                                            \
-    hipLaunchKernelGGL(slab_reduce, rg, dim3(256), 0, st, workspace, g.gx, n_el, dw,              \
+    hipLaunchKernelGGL(slab_reduce, rg, dim3(1024), 0, st, workspace, g.gx, n_el, dw,             \
                        cout * kSeq * cin, db);                                                    \
     return launch_status("spiral_conv_bwd_weight_small_reduce");                                  \
   }
-  if (g.kind == kDwInSmall) {
+  if (g.kind == kDwInMfma) {
+    DWS(conv_dw_in_mfma, 3, 32) DWS(conv_dw_in_mfma, 3, 64)
+    DWS(conv_dw_in_mfma, 2, 32) DWS(conv_dw_in_mfma, 2, 64)
+    DWS(conv_dw_in_mfma, 1, 32) DWS(conv_dw_in_mfma, 1, 64)
+  } else if (g.kind == kDwInSmall) {
     DWS(conv_dw_in_small, 3, 16) DWS(conv_dw_in_small, 3, 32) DWS(conv_dw_in_small, 3, 64)
   } else {
     DWS(conv_dw_out_small, 16, 3) DWS(conv_dw_out_small, 32, 3) DWS(conv_dw_out_small, 64, 3)
   }
 #undef DWS
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight: unsupported channels %d -> %d", cin, cout);
+}
+
+// ---- fused backward (data + weight)
+namespace {
+bool fused_small(int cin, int cout) { return cout * kSeq <= 32 && (cin == 32 || cin == 64); }
+int fused_small_gx(long m_src) {
+  long gx = ((m_src + 63) / 64 + 3) / 4;
+  return (int)(gx > 512 ? 512 : (gx < 1 ? 1 : gx));
+}
+}  // namespace
+
+extern "C" size_t cfsd_spiral_conv_bwd_workspace(int batch, int vsrc, int rows, int seq, int cin,
+                                                 int cout) {
+  if (batch <= 0 || vsrc <= 0 || rows <= 0 || seq != kSeq || cin <= 0 || cout <= 0) return 0;
+  if (fused_small(cin, cout))
+    return (size_t)fused_small_gx((long)batch * vsrc) * ((size_t)cout * kSeq * cin + cout) *
+           sizeof(float);
+  const size_t a = cfsd_spiral_conv_workspace(batch, vsrc, rows, seq, cin, cout);
+  const size_t b = cfsd_spiral_conv_bwd_weight_workspace(batch, rows, seq, cin, cout);
+  return a > b ? a : b;
+}
+
+extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const float* dpre,
+                                    const int32_t* inv_ptr, const int32_t* inv_row,
+                                    const int32_t* inv_pair, const float* w, const float* elu_y,
+                                    float* dx, float* dw, float* db, float* workspace,
+                                    size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
+                                    int cin, int cout, void* stream) {
+  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!inv_ptr || !inv_row || !inv_pair || !w || !dw || !db || !workspace)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd: null inverse table / w / dw / db / workspace");
+  const size_t need = cfsd_spiral_conv_bwd_workspace(batch, vsrc, rows, seq, cin, cout);
+  if (workspace_bytes < need)
+    return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
+  hipStream_t st = (hipStream_t)stream;
+  if (!fused_small(cin, cout)) {
+    if (dx) {
+      rc = cfsd_spiral_conv_bwd_data(dpre, inv_ptr, inv_row, inv_pair, w, elu_y, dx, workspace,
+                                     workspace_bytes, batch, vsrc, rows, seq, cin, cout, stream);
+      if (rc) return rc;
+    }
+    return cfsd_spiral_conv_bwd_weight(x, idx, dpre, dw, db, workspace, workspace_bytes, batch,
+                                       vsrc, rows, seq, cin, cout, stream);
+  }
+  const long Ms = (long)batch * vsrc;
+  const int gx = fused_small_gx(Ms);
+  const int n_el = cout * kSeq * cin + cout;
+#define BOS(CIN_, CO_)                                                                           \
+  if (cin == CIN_ && cout == CO_) {                                                              \
+    hipLaunchKernelGGL((conv_bwd_out_small<CIN_, CO_>), dim3(gx), dim3(256), 0, st, dpre,        \
+                       inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, x, dx, workspace, vsrc, \
+                       rows, Ms);                                                                \
+    rc = launch_status("spiral_conv_bwd_small");                                                 \
+    if (rc) return rc;                                                                           \
+    hipLaunchKernelGGL(slab_reduce, dim3((unsigned)((n_el + 63) / 64)), dim3(1024), 0, st,        \
+                       workspace, gx, n_el, dw, cout * kSeq * cin, db);                          \
+    return launch_status("spiral_conv_bwd_small_reduce");                                        \
+  }
+  BOS(32, 1) BOS(32, 2) BOS(32, 3) BOS(64, 1) BOS(64, 2) BOS(64, 3)
+#undef BOS
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd: unsupported channels %d -> %d", cin, cout);
 }
 
 extern "C" int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, int batch,

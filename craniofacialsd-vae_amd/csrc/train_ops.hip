@@ -23,6 +23,30 @@ int set_error(int code, const char* fmt, ...) {
   return code;
 }
 
+int resident_blocks(const void* kernel, int block_threads, size_t dyn_lds) {
+  struct Key {
+    const void* k;
+    int t;
+    size_t l;
+    int v;
+  };
+  static thread_local Key cache[64];
+  static thread_local int n_cache = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  for (int i = 0; i < n_cache; ++i)
+    if (cache[i].k == kernel && cache[i].t == block_threads && cache[i].l == dyn_lds) return cache[i].v;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block_threads, dyn_lds) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const int v = per_cu * cus;
+  if (n_cache < 64) cache[n_cache++] = Key{kernel, block_threads, dyn_lds, v};
+  return v;
+}
+
 constexpr int kLapThreads = 256;
 
 // Block-wide sum of two values in fixed order (wave shuffle tree + LDS).

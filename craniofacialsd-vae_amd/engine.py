@@ -238,6 +238,7 @@ class SDVAEEngine:
         for (cin, cout, lv, _) in S.dec_layers():
             ws = max(ws, ops.spiral_conv_workspace(bsz, nv[lv], nv[lv], T.seq[lv], cin, cout))
         ws = max(ws, ops.spiral_conv_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
+        ws = max(ws, ops.spiral_conv_bwd_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
         b.ws = torch.empty(ws // 4 + 64, dtype=torch.float32, device=dev)
         flat_in = self.num_vert * S.out_ch[-1]
         nmu = lat * (2 if S.is_vae else 1)
@@ -342,10 +343,12 @@ class SDVAEEngine:
         ops.recon_lap_bwd(b.out, b.x, b.unit, T.lapT_csr, b.dout, 1.0, self.w_lap)
         # final SpiralConv (no activation): dpre = dout
         last_in = b.dec_out[-1]
-        ops.spiral_conv_bwd_weight(last_in, T.spiral[0], b.dout, P.gview(f"de_layers.{n + 1}.layer.weight"),
-                                   P.gview(f"de_layers.{n + 1}.layer.bias"), b.ws)
-        ops.spiral_conv_bwd_data(b.dout, T.spiral_inv[0], P.view(f"de_layers.{n + 1}.layer.weight"),
-                                 T.n_verts[0], elu_y=last_in, out=b.dpre_dec[-1], workspace=b.ws)
+        # dX and dW/db of the output conv in one source-row pass
+        ops.spiral_conv_bwd(last_in, T.spiral[0], b.dout, T.spiral_inv[0],
+                            P.view(f"de_layers.{n + 1}.layer.weight"),
+                            P.gview(f"de_layers.{n + 1}.layer.weight"),
+                            P.gview(f"de_layers.{n + 1}.layer.bias"),
+                            dx=b.dpre_dec[-1], elu_y=last_in, workspace=b.ws)
         dec = S.dec_layers()
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]

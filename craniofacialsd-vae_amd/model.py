@@ -117,14 +117,14 @@ class _SpiralConvFn(torch.autograd.Function):
         dy = dy.contiguous()
         dpre = ops.elu_bwd(dy, y) if ctx.act == ACT_ELU else dy
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = ops.spiral_conv_bwd_data(dpre, plan.inv, w, x.shape[1])
-        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+        need_w = ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2])
+        if need_w:  # fused dX + dW/db (cfsd_spiral_conv_bwd)
             dw = torch.empty_like(w)
             db = torch.empty(w.shape[0], dtype=w.dtype, device=w.device)
-            ws = torch.empty(ops.spiral_conv_bwd_weight_workspace(
-                x.shape[0], plan.rows, plan.seq, x.shape[2], w.shape[0]) // 4 + 1, device=w.device)
-            ops.spiral_conv_bwd_weight(x, plan.idx, dpre, dw, db, ws)
+            dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+            ops.spiral_conv_bwd(x, plan.idx, dpre, plan.inv, w, dw, db, dx=dx)
+        elif ctx.needs_input_grad[0]:
+            dx = ops.spiral_conv_bwd_data(dpre, plan.inv, w, x.shape[1])
         return dx, dw, (db if ctx.has_bias else None), None, None
 
 

@@ -112,6 +112,37 @@ def spiral_conv_bwd_weight(x, idx, dpre, dw, db, workspace):
          ptr(workspace), ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
 
 
+def spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout):
+    return int(_abi.lib().cfsd_spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout))
+
+
+def spiral_conv_bwd(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None):
+    """Fused dX (skipped when ``dx`` is None) + dW/db of one SpiralConv; same
+    results as spiral_conv_bwd_data followed by spiral_conv_bwd_weight."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = dpre.shape[2]
+    inv_ptr, inv_row, inv_pair = inv
+    _need(x, None, name="x")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(dpre, (bsz, rows, cout), name="dpre")
+    _need(inv_ptr, (vsrc * seq + 1,), torch.int32, "inv_ptr")
+    _need(inv_row, (rows * seq,), torch.int32, "inv_row")
+    _need(inv_pair, (vsrc * seq, 2), torch.int32, "inv_pair")
+    _need(w, (cout, seq * cin), name="w")
+    _need(dw, (cout, seq * cin), name="dw")
+    _need(db, (cout,), name="db")
+    if dx is not None:
+        _need(dx, (bsz, vsrc, cin), name="dx")
+    if elu_y is not None:
+        _need(elu_y, (bsz, vsrc, cin), name="elu_y")
+    ws, nb = _conv_ws(workspace, x.device, spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout))
+    call("cfsd_spiral_conv_bwd", ptr(x), ptr(idx), ptr(dpre), ptr(inv_ptr), ptr(inv_row),
+         ptr(inv_pair), ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb),
+         bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    return dx
+
+
 def spiral_gather(x, idx, out=None):
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape

@@ -66,8 +66,8 @@ size_t cfsd_spiral_conv_workspace(int batch, int vsrc, int rows, int seq, int ci
  * inv_ptr [vsrc*seq + 1] / inv_row [rows*seq]: CSR of the inverse spiral,
  * entry list of (u, s) = rows r with idx[r*seq+s] == u (r ascending);
  * inv_pair [vsrc*seq][2]: the first two entries of each list (-1 if absent),
- * read up front so the gathers are issued one slot ahead (may be NULL for the
- * 3-channel VALU path).  The spiral length must be 9 (all reference configs). */
+ * read up front so the gathers are issued one slot ahead (required).  The
+ * spiral length must be 9 (all reference configs). */
 int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_ptr, const int32_t* inv_row,
                               const int32_t* inv_pair, const float* w, const float* elu_y,
                               float* dx, float* workspace, size_t workspace_bytes, int batch,
@@ -81,6 +81,21 @@ int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, const float*
                                 float* db, float* workspace, size_t workspace_bytes, int batch,
                                 int vsrc, int rows, int seq, int cin, int cout, void* stream);
 size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int seq, int cin, int cout);
+
+/* Fused backward of one SpiralConv (model.py:27-41 autograd, dX and dW/db of
+ * the same layer in one call): dx exactly as cfsd_spiral_conv_bwd_data
+ * (skipped when dx == NULL, e.g. the first layer), dw/db exactly as
+ * cfsd_spiral_conv_bwd_weight.  For small-output layers (cout*seq <= 32, the
+ * xyz output conv) both come from ONE pass in source-row space: the spiral
+ * transpose is folded in the 3-wide dpre space and dW is regrouped as
+ * sum_{b,u} x[b,u,:] (x) t[b,u,s,:], so x is read densely, not gathered.
+ * workspace: cfsd_spiral_conv_bwd_workspace() bytes (shared by both stages). */
+int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const float* dpre,
+                         const int32_t* inv_ptr, const int32_t* inv_row, const int32_t* inv_pair,
+                         const float* w, const float* elu_y, float* dx, float* dw, float* db,
+                         float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows,
+                         int seq, int cin, int cout, void* stream);
+size_t cfsd_spiral_conv_bwd_workspace(int batch, int vsrc, int rows, int seq, int cin, int cout);
 
 /* Materialising spiral gather, g[b,r,s*cin+c] = x[b, idx[r,s], c]
  * (model.py:34 index_select + view).  Used as the HBM-roofline probe. */

@@ -90,10 +90,42 @@ def test_spiral_conv_bwd(otopo, dtopo, cin, cout, level, bsz, use_elu_y):
     close(db, b.grad, 1e-5, "conv db")
 
 
-def test_spiral_conv_e0_weight_grad(otopo, dtopo):
+@pytest.mark.parametrize("cin,cout,level,bsz", [(32, 3, 0, 2), (32, 3, 0, 16), (64, 3, 1, 5),
+                                                (32, 3, 3, 1), (32, 32, 1, 2), (64, 64, 2, 3)])
+@pytest.mark.parametrize("with_dx", [False, True])
+def test_spiral_conv_bwd_fused(otopo, dtopo, cin, cout, level, bsz, with_dx):
+    """cfsd_spiral_conv_bwd (dX + dW/db in one call; source-row pass for 3-ch outputs)."""
+    g = torch.Generator().manual_seed(11 + cin + cout + level + bsz)
+    sp = otopo.spirals[level]
+    v = sp.shape[0]
+    # reference in float64: dW sums up to 16*17039 products, so an fp32 oracle's
+    # own rounding would dominate the comparison
+    x = torch.randn(bsz, v, cin, generator=g).double().requires_grad_()
+    xin = O.elu(x)
+    xin_leaf = xin.detach().requires_grad_()
+    w = (torch.randn(cout, 9 * cin, generator=g) * 0.1).float().double().requires_grad_()
+    b = (torch.randn(cout, generator=g) * 0.1).double().requires_grad_()
+    y = O.spiral_conv(xin_leaf, sp, w, b)
+    dy = torch.randn(y.shape, generator=g).double()
+    y.backward(dy)
+    dx_ref = torch.autograd.grad(xin, x, xin_leaf.grad)[0]
+    dw = torch.full((cout, 9 * cin), float("nan"), device=DEV)
+    db = torch.full((cout,), float("nan"), device=DEV)
+    dx = torch.full((bsz, v, cin), float("nan"), device=DEV) if with_dx else None
+    xd = xin.detach().float().to(DEV).contiguous()
+    ops.spiral_conv_bwd(xd, dtopo.spiral[level], dy.float().to(DEV), dtopo.spiral_inv[level],
+                        w.detach().float().to(DEV), dw, db, dx=dx, elu_y=xd if with_dx else None)
+    close(dw, w.grad, 1e-5, "fused dw")
+    close(db, b.grad, 1e-5, "fused db")
+    if with_dx:
+        close(dx, dx_ref, 1e-5, "fused dx")
+
+
+@pytest.mark.parametrize("bsz", [2, 16])
+def test_spiral_conv_e0_weight_grad(otopo, dtopo, bsz):
     g = torch.Generator().manual_seed(3)
     sp = otopo.spirals[0]
-    x = torch.randn(2, sp.shape[0], 3, generator=g)
+    x = torch.randn(bsz, sp.shape[0], 3, generator=g)
     w = (torch.randn(32, 27, generator=g) * 0.1).requires_grad_()
     b = torch.zeros(32).requires_grad_()
     sel = torch.from_numpy(otopo.down[0][1])
@@ -102,7 +134,7 @@ def test_spiral_conv_e0_weight_grad(otopo, dtopo):
     y.backward(dy)
     dw = torch.empty(32, 27, device=DEV)
     db = torch.empty(32, device=DEV)
-    ws = torch.empty(ops.spiral_conv_bwd_weight_workspace(2, 4260, 9, 3, 32) // 4 + 1, device=DEV)
+    ws = torch.empty(ops.spiral_conv_bwd_weight_workspace(bsz, 4260, 9, 3, 32) // 4 + 1, device=DEV)
     ops.spiral_conv_bwd_weight(x.to(DEV), dtopo.enc_rows[0], dy.to(DEV), dw, db, ws)
     close(dw, w.grad, 1e-5, "E0 dw")
     close(db, b.grad, 1e-5, "E0 db")

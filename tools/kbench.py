@@ -1,0 +1,99 @@
+"""Micro-benchmark of individual step kernels at the C2 shapes (for rocprofv3 / PMC).
+
+python tools/kbench.py [names...]   names: fwd_d3 dx_d3 dw_d3 dout_fwd dout_dx dout_dw spmm_up0 spmm_up0T step
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT]
+import cfsd_loader  # noqa: E402
+
+cfsd_loader.load()
+from craniofacialsd_vae_amd import engine as E  # noqa: E402
+from craniofacialsd_vae_amd import ops, topology  # noqa: E402
+
+
+def main():
+    names = sys.argv[1:] or ["fwd_d3", "dx_d3", "dw_d3", "dout_fwd", "dout_dx", "dout_dw", "spmm_up0",
+                             "spmm_up0T", "e0_fwd", "e0_dw"]
+    iters = int(os.environ.get("KB_ITERS", "50"))
+    npz = dict(np.load(os.path.join(ROOT, "tests", "golden", "topology_craniofacial.npz")))
+    T = topology.DeviceTopology.from_npz(npz, device="cuda")
+    eng = E.SDVAEEngine(T, E.ModelSpec(), device="cuda")
+    b = eng.buffers(16)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for t in (b.x, b.dec_up[3], b.dec_out[3], b.dpre_dec[3], b.dout, b.dec_out[2], b.g_dec_up[3]):
+        t.copy_(torch.randn(t.shape, device="cuda", generator=g))
+    b.dec_out[3].copy_(torch.nn.functional.elu(b.dec_out[3]))
+    w3, b3 = eng._dec_w(3)
+    wout = eng.params.view("de_layers.5.layer.weight")
+    bout = eng.params.view("de_layers.5.layer.bias")
+    P = eng.params
+    cases = {
+        "fwd_d3": lambda: ops.spiral_conv_fwd(b.dec_up[3], T.spiral[0], w3, b3, 1, out=b.dec_out[3], workspace=b.ws),
+        "dx_d3": lambda: ops.spiral_conv_bwd_data(b.dpre_dec[3], T.spiral_inv[0], w3, T.n_verts[0], out=b.g_dec_up[3], workspace=b.ws),
+        "dw_d3": lambda: ops.spiral_conv_bwd_weight(b.dec_up[3], T.spiral[0], b.dpre_dec[3],
+                                                   P.gview("de_layers.4.conv.layer.weight"),
+                                                   P.gview("de_layers.4.conv.layer.bias"), b.ws),
+        "dout_fwd": lambda: ops.spiral_conv_fwd(b.dec_out[3], T.spiral[0], wout, bout, 0, out=b.out, workspace=b.ws),
+        "dout_dx": lambda: ops.spiral_conv_bwd_data(b.dout, T.spiral_inv[0], wout, T.n_verts[0], elu_y=b.dec_out[3],
+                                                    out=b.dpre_dec[3], workspace=b.ws),
+        "dout_dw": lambda: ops.spiral_conv_bwd_weight(b.dec_out[3], T.spiral[0], b.dout,
+                                                     P.gview("de_layers.5.layer.weight"),
+                                                     P.gview("de_layers.5.layer.bias"), b.ws),
+        "dout_bwd": lambda: ops.spiral_conv_bwd(b.dec_out[3], T.spiral[0], b.dout, T.spiral_inv[0], wout,
+                                                P.gview("de_layers.5.layer.weight"),
+                                                P.gview("de_layers.5.layer.bias"), dx=b.dpre_dec[3],
+                                                elu_y=b.dec_out[3], workspace=b.ws),
+        "spmm_up0": lambda: ops.spmm(T.up_csr[0], b.dec_out[2], T.n_verts[0], out=b.dec_up[3]),
+        "spmm_up0T": lambda: ops.spmm(T.upT_csr[0], b.g_dec_up[3], T.n_verts[1], elu_y=b.dec_out[2],
+                                      out=b.dpre_dec[2]),
+        "e0_fwd": lambda: ops.spiral_conv_fwd(b.x, T.enc_rows[0], *eng._enc_w(0), 1, out=b.enc_out[0], workspace=b.ws),
+        "e0_dw": lambda: ops.spiral_conv_bwd_weight(b.x, T.enc_rows[0], b.dpre_enc[0],
+                                                   P.gview("en_layers.0.conv.layer.weight"),
+                                                   P.gview("en_layers.0.conv.layer.bias"), b.ws),
+    }
+    self_idx = torch.arange(T.n_verts[0], dtype=torch.int32, device="cuda").view(-1, 1).repeat(1, 9).contiguous()
+    shift_idx = ((torch.arange(T.n_verts[0], device="cuda").view(-1, 1) + torch.arange(9, device="cuda").view(1, -1))
+                 % T.n_verts[0]).to(torch.int32).contiguous()
+    cases["fwd_d3_self"] = lambda: ops.spiral_conv_fwd(b.dec_up[3], self_idx, w3, b3, 1, out=b.dec_out[3], workspace=b.ws)
+    cases["fwd_d3_shift"] = lambda: ops.spiral_conv_fwd(b.dec_up[3], shift_idx, w3, b3, 1, out=b.dec_out[3], workspace=b.ws)
+    cases["fwd_d3_noact"] = lambda: ops.spiral_conv_fwd(b.dec_up[3], T.spiral[0], w3, b3, 0, out=b.dec_out[3], workspace=b.ws)
+    ip, ir, ipair = T.spiral_inv[0]
+    inv_noovf = (torch.zeros_like(ip), ir, ipair)
+    pair1 = ipair.clone()
+    pair1[:, 1] = -1
+    inv_nomore = (ip, ir, pair1)
+    cases["dx_d3_noovf"] = lambda: ops.spiral_conv_bwd_data(b.dpre_dec[3], inv_noovf, w3, T.n_verts[0], out=b.g_dec_up[3], workspace=b.ws)
+    cases["dx_d3_nomore"] = lambda: ops.spiral_conv_bwd_data(b.dpre_dec[3], inv_nomore, w3, T.n_verts[0], out=b.g_dec_up[3], workspace=b.ws)
+    cases["dout_bwd_noovf"] = lambda: ops.spiral_conv_bwd(b.dec_out[3], T.spiral[0], b.dout, inv_noovf, wout,
+                                                         P.gview("de_layers.5.layer.weight"),
+                                                         P.gview("de_layers.5.layer.bias"), dx=b.dpre_dec[3],
+                                                         elu_y=b.dec_out[3], workspace=b.ws)
+    cases["dout_bwd_nodx"] = lambda: ops.spiral_conv_bwd(b.dec_out[3], T.spiral[0], b.dout, T.spiral_inv[0], wout,
+                                                        P.gview("de_layers.5.layer.weight"),
+                                                        P.gview("de_layers.5.layer.bias"), workspace=b.ws)
+    if "step" in names:
+        eng.set_batch(b.x, key_index=3)
+        cases["step"] = lambda: eng.train_step_on(b)
+    for n in names:
+        fn = cases[n]
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"{n:10s} {e0.elapsed_time(e1) / iters * 1e3:9.2f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -10,7 +10,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcfsd.so")
+LIB_PATH = os.environ.get("CFSD_LIB_PATH") or os.path.join(_HERE, "libcfsd.so")
 
 _lib = None
 

@@ -20,6 +20,9 @@ inline int launch_status(const char* what) {
 }
 
 __device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
+// ELU with the hardware exp (v_exp_f32): exp(x) - 1, the form PyTorch's ELU
+// kernel evaluates; |error| <~ 1e-7 absolute.  Used in MFMA epilogues.
+__device__ __forceinline__ float elu_fast(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
 // dELU/dx written from the ELU OUTPUT y (alpha = 1): 1 for y > 0, else y + 1 = exp(x).
 __device__ __forceinline__ float elu_grad_from_out(float y) { return y > 0.f ? 1.f : y + 1.f; }
 
@@ -66,6 +69,18 @@ inline unsigned balanced_blocks(long units, int per_block, long max_blocks) {
 // waitcnt placement would drain a prefetch one slot too early.
 __device__ __forceinline__ void gload4_async(f32x4& d, const float* p) {
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+// Store hidden from hipcc's waitcnt bookkeeping (counted like the loads).
+template <int OFF>
+__device__ __forceinline__ void gstore1_async(float* p, float v) {
+  asm volatile("global_store_dword %0, %1, off offset:%2" ::"v"(p), "v"(v), "n"(OFF) : "memory");
+}
+__device__ __forceinline__ void gload1_async(int& d, const int* p) {
+  asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 template <int N>
 __device__ __forceinline__ void vm_wait4(f32x4& a, f32x4& b, f32x4& c, f32x4& d) {

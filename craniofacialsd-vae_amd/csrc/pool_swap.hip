@@ -34,13 +34,26 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   const float* xb = x + (long)b * n * c4 * 4 + 4 * q;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const int beg = row_ptr[r], end = row_ptr[r + 1];
-  for (int e = beg; e < end; ++e) {
-    const float v = val[e];
-    f32x4 xv = ld4(xb + (long)col[e] * c4 * 4);
-    acc.x = acc.x + xv.x * v;
-    acc.y = acc.y + xv.y * v;
-    acc.z = acc.z + xv.z * v;
-    acc.w = acc.w + xv.w * v;
+  // Entries in chunks of 4: the chunk's column/value and x loads are all
+  // issued before the first add (independent), the adds stay in entry order.
+  for (int e0 = beg; e0 < end; e0 += 4) {
+    float v[4];
+    f32x4 xv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = e0 + j < end ? e0 + j : end - 1;
+      v[j] = val[e];
+      xv[j] = ld4(xb + (long)col[e] * c4 * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (e0 + j < end) {
+        acc.x = acc.x + xv[j].x * v[j];
+        acc.y = acc.y + xv[j].y * v[j];
+        acc.z = acc.z + xv[j].z * v[j];
+        acc.w = acc.w + xv[j].w * v[j];
+      }
+    }
   }
   if (elu_y) {
     f32x4 g = ld4(elu_y + t * 4);

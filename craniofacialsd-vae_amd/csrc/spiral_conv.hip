@@ -242,11 +242,10 @@ __global__ __launch_bounds__(256) void conv_fwd_in_small(const float* __restrict
   }
 }
 
-// Forward, small output (CO <= 4 channels, e.g. the xyz output conv): one
-// thread per output row.  Per slot the thread reads its neighbour's CIN
-// floats (CIN/4 dwordx4) and does CO*CIN FMAs against W, whose wave-uniform
-// addresses become scalar loads (SGPR operands).  Low VGPR use -> high
-// occupancy to cover the gather latency.
+// Forward, small output (CO <= 4 channels, e.g. the xyz output conv),
+// persistent over rows: L = CIN/4 lanes per row, each lane owns a float4 of
+// input channels of every neighbour row (one coalesced 16*L-byte read per
+// neighbour), the CO partial dots are reduced across the L lanes.
 template <int CIN, int CO, int ACT>
 __global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restrict__ x,
                                                           const int* __restrict__ idx,
@@ -254,36 +253,119 @@ __global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restric
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ y, int vsrc,
                                                           int rows, long total_rows) {
+  constexpr int L = CIN / 4;
+  constexpr int RPW = 64 / L;
   constexpr int K = kSeq * CIN;
-  const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= total_rows) return;
-  const int b = (int)(m / rows), r = (int)(m % rows);
-  const float* xb = x + (long)b * vsrc * CIN;
-  const int* ir = idx + (long)r * kSeq;
-  int src[kSeq];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane % L, slot = lane / L;
+  f32x4 wr[kSeq][CO];
 #pragma unroll
-  for (int s = 0; s < kSeq; ++s) src[s] = ir[s];
-  float acc[CO];
+  for (int s = 0; s < kSeq; ++s)
 #pragma unroll
-  for (int o = 0; o < CO; ++o) acc[o] = bias ? bias[o] : 0.f;
+    for (int o = 0; o < CO; ++o) wr[s][o] = ld4(w + (long)o * K + s * CIN + 4 * q);
+  float bo[CO];
 #pragma unroll
-  for (int s = 0; s < kSeq; ++s) {
-    const float* p = xb + (long)src[s] * CIN;
+  for (int o = 0; o < CO; ++o) bo[o] = bias ? bias[o] : 0.f;
+  const long n_rows_pad = (total_rows + RPW - 1) / RPW * RPW;  // whole waves stay in the loop
+  const long stride = (long)gridDim.x * 4 * RPW;
+  for (long mm = ((long)blockIdx.x * 4 + wave) * RPW + slot; mm < n_rows_pad; mm += stride) {
+    const bool valid = mm < total_rows;
+    const long m = valid ? mm : total_rows - 1;
+    const int b = (int)(m / rows), r = (int)(m % rows);
+    const float* xb = x + (long)b * vsrc * CIN + 4 * q;
+    const int* ir = idx + (long)r * kSeq;
+    float acc[CO];
 #pragma unroll
-    for (int c4 = 0; c4 < CIN / 4; ++c4) {
-      const f32x4 v = ld4(p + 4 * c4);
+    for (int o = 0; o < CO; ++o) acc[o] = 0.f;
+#pragma unroll
+    for (int s = 0; s < kSeq; ++s) {
+      const f32x4 v = ld4(xb + (long)ir[s] * CIN);
 #pragma unroll
       for (int o = 0; o < CO; ++o) {
-        const float* wp = w + o * K + s * CIN + 4 * c4;
-        acc[o] = fmaf(v.x, wp[0], acc[o]);
-        acc[o] = fmaf(v.y, wp[1], acc[o]);
-        acc[o] = fmaf(v.z, wp[2], acc[o]);
-        acc[o] = fmaf(v.w, wp[3], acc[o]);
+        acc[o] = fmaf(v.x, wr[s][o].x, acc[o]);
+        acc[o] = fmaf(v.y, wr[s][o].y, acc[o]);
+        acc[o] = fmaf(v.z, wr[s][o].z, acc[o]);
+        acc[o] = fmaf(v.w, wr[s][o].w, acc[o]);
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < CO; ++o)
+#pragma unroll
+      for (int d = L / 2; d >= 1; d >>= 1) acc[o] += __shfl_xor(acc[o], d);
+    if (valid && q == 0) {
+#pragma unroll
+      for (int o = 0; o < CO; ++o) {
+        float v = acc[o] + bo[o];
+        if (ACT == CFSD_ACT_ELU) v = elu_f(v);
+        y[m * CO + o] = v;
       }
     }
   }
+}
+
+// Forward, small input (CS <= 3; the xyz input conv) on MFMA: a 32-row tile
+// is (32 x 27) gathered inputs times W^T (27 x COUT).  Every lane gathers its
+// row's 27 values (9 idx + 9 x CS floats, L1-shared by the two lane halves)
+// and keeps the half it feeds to v_mfma_f32_32x32x2_f32 (k-permuted: half h
+// owns k in [h*KH, h*KH + KH)); W^T lives in registers.  Output rows are
+// stored as 128-B coalesced segments.
+template <int CS, int COUT, int ACT>
+__global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict__ x,
+                                                        const int* __restrict__ idx,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bias,
+                                                        float* __restrict__ y, int vsrc, int rows,
+                                                        long total_rows) {
+  constexpr int K = kSeq * CS, KH = (K + 1) / 2, NCT = COUT / 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  float wb[NCT][KH];
+  float bn[NCT];
 #pragma unroll
-  for (int o = 0; o < CO; ++o) y[m * CO + o] = ACT == CFSD_ACT_ELU ? elu_f(acc[o]) : acc[o];
+  for (int t = 0; t < NCT; ++t) {
+    bn[t] = bias ? bias[t * 32 + i] : 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KH; ++kk) {
+      const int k = h * KH + kk;
+      wb[t][kk] = k < K ? w[(t * 32 + i) * K + k] : 0.f;
+    }
+  }
+  const long n_tiles = (total_rows + 31) / 32;
+  for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
+    long m = tile * 32 + i;
+    if (m >= total_rows) m = total_rows - 1;
+    const int b = (int)(m / rows), r = (int)(m % rows);
+    const float* xb = x + (long)b * vsrc * CS;
+    const int* ir = idx + (long)r * kSeq;
+    float g[2 * KH];
+#pragma unroll
+    for (int s = 0; s < kSeq; ++s) {
+      const float* p = xb + (long)ir[s] * CS;
+#pragma unroll
+      for (int c = 0; c < CS; ++c) g[s * CS + c] = p[c];
+    }
+#pragma unroll
+    for (int k = K; k < 2 * KH; ++k) g[k] = 0.f;
+    f32x16 acc[NCT];
+#pragma unroll
+    for (int t = 0; t < NCT; ++t) acc[t] = (f32x16){0.f};
+#pragma unroll
+    for (int kk = 0; kk < KH; ++kk) {
+      const float a = h ? g[KH + kk] : g[kk];
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) acc[t] = mfma32(a, wb[t][kk], acc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < NCT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const long mo = tile * 32 + acc_row(rr, lane);
+        if (mo < total_rows) {
+          const float v = acc[t][rr] + bn[t];
+          y[mo * COUT + t * 32 + i] = ACT == CFSD_ACT_ELU ? elu_f(v) : v;
+        }
+      }
+  }
 }
 
 // ==========================================================================
@@ -1081,8 +1163,7 @@ static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const
   auto kern = conv_fwd_mfma<CIN, COUT, ACT, SPG>;
   const long max_blocks = resident_blocks_of(kern, 256, lds) / (kSeq / SPG);
   dim3 grid(balanced_blocks(n_tiles, 4, max_blocks > 0 ? max_blocks : 1), kSeq / SPG);
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, x, idx, w,
-                     bias, y, ws, vsrc, rows, M);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, x, idx, w, bias, y, ws, vsrc, rows, M);
   int rc = launch_status("spiral_conv_fwd");
   if (rc || SPG == kSeq) return rc;
   const long n4 = M * COUT / 4;
@@ -1119,6 +1200,8 @@ extern "C" int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const fl
                                     int cin, int cout, int act, void* stream) {
   int rc = check_conv_args(x, idx, w, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
+  if ((long)batch * rows >= (1L << 31) || (long)batch * vsrc >= (1L << 31))
+    return set_error(CFSD_EINVAL, "spiral_conv_fwd: batch*rows must be < 2^31");
   if (!y) return set_error(CFSD_EINVAL, "null y");
   if (act != CFSD_ACT_NONE && act != CFSD_ACT_ELU) return set_error(CFSD_EINVAL, "bad act %d", act);
   hipStream_t st = (hipStream_t)stream;
@@ -1133,22 +1216,40 @@ extern "C" int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const fl
                                                                wsf, vsrc, rows, M, st);
   FWD(32, 32) FWD(32, 64) FWD(64, 32) FWD(64, 64)
 #undef FWD
+  if (cin <= 3 && (cout == 32 || cout == 64)) {
+    const long tiles = (M + 31) / 32;
+    const unsigned gp = (unsigned)((tiles + 3) / 4 < 2048 ? (tiles + 3) / 4 : 2048);
+#define FIN(CS_, CO_)                                                                            \
+  if (cin == CS_ && cout == CO_) {                                                               \
+    if (act == CFSD_ACT_ELU)                                                                     \
+      hipLaunchKernelGGL((conv_fwd_in_mfma<CS_, CO_, CFSD_ACT_ELU>), dim3(gp), dim3(256), 0, st,  \
+                         x, idx, w, bias, y, vsrc, rows, M);                                     \
+    else                                                                                         \
+      hipLaunchKernelGGL((conv_fwd_in_mfma<CS_, CO_, CFSD_ACT_NONE>), dim3(gp), dim3(256), 0, st, \
+                         x, idx, w, bias, y, vsrc, rows, M);                                     \
+    return launch_status("spiral_conv_fwd_in");                                                  \
+  }
+    FIN(1, 32) FIN(2, 32) FIN(3, 32) FIN(1, 64) FIN(2, 64) FIN(3, 64)
+#undef FIN
+  }
 #define FWD_SMALL(KERNEL, A_, B_)                                                                \
   if (cin == A_ && cout == B_) {                                                                 \
     if (act == CFSD_ACT_ELU) {                                                                   \
       auto k = KERNEL<A_, B_, CFSD_ACT_ELU>;                                                     \
-      hipLaunchKernelGGL(k, dim3(row_grid(M)), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, \
-                         M);                                                                     \
+      hipLaunchKernelGGL(k, dim3(GRID(k)), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M); \
     } else {                                                                                     \
       auto k = KERNEL<A_, B_, CFSD_ACT_NONE>;                                                    \
-      hipLaunchKernelGGL(k, dim3(row_grid(M)), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, \
-                         M);                                                                     \
+      hipLaunchKernelGGL(k, dim3(GRID(k)), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M); \
     }                                                                                            \
     return launch_status("spiral_conv_fwd_small");                                               \
   }
-  FWD_SMALL(conv_fwd_in_small, 3, 16) FWD_SMALL(conv_fwd_in_small, 3, 32)
-  FWD_SMALL(conv_fwd_in_small, 3, 64) FWD_SMALL(conv_fwd_out_small, 16, 3)
-  FWD_SMALL(conv_fwd_out_small, 32, 3) FWD_SMALL(conv_fwd_out_small, 64, 3)
+#define GRID(k) row_grid(M)
+  FWD_SMALL(conv_fwd_in_small, 3, 16)
+#undef GRID
+#define GRID(k) small_grid(k, M)
+  FWD_SMALL(conv_fwd_out_small, 16, 3) FWD_SMALL(conv_fwd_out_small, 32, 3)
+  FWD_SMALL(conv_fwd_out_small, 64, 3)
+#undef GRID
 #undef FWD_SMALL
   return set_error(CFSD_EINVAL, "spiral_conv_fwd: unsupported channels %d -> %d", cin, cout);
 }

@@ -81,6 +81,21 @@ def main():
     if "step" in names:
         eng.set_batch(b.x, key_index=3)
         cases["step"] = lambda: eng.train_step_on(b)
+    if os.environ.get("KB_STAMPS"):
+        for n in names:
+            b.ws.zero_()
+            cases[n]()
+            torch.cuda.synchronize()
+            st = b.ws.view(torch.int64)[: (b.ws.numel() // 2) // 8 * 8].view(-1, 8).cpu()
+            st = st[st[:, 7] == 1].double()
+            if len(st) == 0:
+                print(n, "no stamps")
+                continue
+            tiles = st[:, 5].sum()
+            print(f"{n}: waves {len(st)} tiles/wave {st[:, 5].mean():.2f} | per wave (cycles): prologue {st[:, 0].mean():.0f} "
+                  f"total {st[:, 6].mean():.0f} max {st[:, 6].max():.0f} | per tile: idx {st[:, 1].sum() / tiles:.0f} "
+                  f"slot0-wait {st[:, 2].sum() / tiles:.0f} slots {st[:, 3].sum() / tiles:.0f} epilogue {st[:, 4].sum() / tiles:.0f}")
+        return
     for n in names:
         fn = cases[n]
         for _ in range(3):

@@ -33,6 +33,7 @@ from craniofacialsd_vae_amd import ops, topology  # noqa: E402
 
 METRIC = "train meshes/sec + per-vertex L1, craniofacial SD-VAE @1/2/4/8 MI355X"
 TOPO_NPZ = os.path.join(ROOT, "tests", "golden", "topology_craniofacial.npz")
+PROFILES = os.path.join(ROOT, "profiles")
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 
@@ -154,6 +155,19 @@ def kernel_probe(runner, n_iter=20):
     return res
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the dominant kernel from the newest committed
+    PMC pass (tools/gpu_round.sh -> tools/pmc_traffic.py: FETCH_SIZE and
+    WRITE_SIZE in separate rocprofv3 runs, gfx950 FETCH_SIZE x2 correction)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(PROFILES, "*_pmc_traffic_conv_fwd_d3.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(budget_s):
     """Oracle (PyTorch-CPU restatement of the reference step) on host cores."""
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
@@ -223,6 +237,7 @@ def main():
         gather_bytes = 16 * nv * (32 + 9 * 32) * 4 + nv * 9 * 4
         t_g = probe["spiral_gather_L0"]
         cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
+        traffic, traffic_src = pmc_traffic()
         out = {
             "metric": METRIC, "value": meshes / el, "unit": "meshes/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
@@ -236,7 +251,8 @@ def main():
             "roofline": {"kernel": "cfsd conv_fwd_mfma<32,32> (decoder level 0)", "bound": "mfma",
                          "achieved": flops / t_conv / 1e12, "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": flops / t_conv / 1e12 / FP32_PEAK_TFLOPS,
-                         "traffic": None, "us_per_launch": t_conv * 1e6},
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_flop": flops, "us_per_launch": t_conv * 1e6},
             "gather_roofline": {"kernel": "cfsd spiral_gather_k (level 0, 32 ch, 16 meshes)",
                                 "bound": "hbm", "achieved": gather_bytes / t_g / 1e9,
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -15,6 +15,11 @@ namespace cfsd {
 // One thread per (b, r, 4-channel chunk).  Consecutive threads walk the
 // channel chunks of one row, so a row of C fp32 is read/written as C/4
 // 16-B accesses by C/4 adjacent lanes.
+// XCD-aware: the dispatcher places block i on XCD i % 8, so block group
+// g = blockIdx % 8 takes the g-th contiguous eighth of the (b, r, q) space
+// (two meshes of a 16-mesh batch): the rows one XCD gathers then come from
+// a ~2 x V x C x 4-byte slice that fits its 4 MB L2 instead of the whole
+// batch.  Placement changes speed only, never results.
 __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_ptr,
                                                   const int* __restrict__ col,
                                                   const float* __restrict__ val,
@@ -25,8 +30,9 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   // hipcc contracts a*b+c into fma by default; the reference rounds the
   // product and the sum separately (index_select*value, then scatter_add).
 #pragma clang fp contract(off)
-  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= total) return;
+  const long per = (total + 7) / 8;
+  const long t = (long)(blockIdx.x & 7) * per + (long)(blockIdx.x >> 3) * blockDim.x + threadIdx.x;
+  if (t >= total || t >= (long)((blockIdx.x & 7) + 1) * per) return;
   const int q = (int)(t % c4);
   const long br = t / c4;
   const int r = (int)(br % m);
@@ -34,19 +40,22 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   const float* xb = x + (long)b * n * c4 * 4 + 4 * q;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const int beg = row_ptr[r], end = row_ptr[r + 1];
-  // Entries in chunks of 4: the chunk's column/value and x loads are all
+  // Entries in chunks of 8: the chunk's column/value and x loads are all
   // issued before the first add (independent), the adds stay in entry order.
-  for (int e0 = beg; e0 < end; e0 += 4) {
-    float v[4];
-    f32x4 xv[4];
+  for (int e0 = beg; e0 < end; e0 += 8) {
+    float v[8];
+    f32x4 xv[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = e0 + j < end ? e0 + j : end - 1;
-      v[j] = val[e];
-      xv[j] = ld4(xb + (long)col[e] * c4 * 4);
+    for (int j = 0; j < 8; ++j) {  // masked, not clamped: short rows issue no extra traffic
+      v[j] = 0.f;
+      xv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (e0 + j < end) {
+        v[j] = val[e0 + j];
+        xv[j] = ld4(xb + (long)col[e0 + j] * c4 * 4);
+      }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 8; ++j) {
       if (e0 + j < end) {
         acc.x = acc.x + xv[j].x * v[j];
         acc.y = acc.y + xv[j].y * v[j];
@@ -108,7 +117,8 @@ extern "C" int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const f
   if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
     return set_error(CFSD_EINVAL, "spmm_csr: bad sizes batch=%d m=%d n=%d c=%d", batch, m, n, c);
   const long total = (long)batch * m * (c / 4);
-  hipLaunchKernelGGL(spmm_csr_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+  const long per_grp = (total + 7) / 8;  // 8 XCD groups of equal block count
+  hipLaunchKernelGGL(spmm_csr_k, dim3((unsigned)(8 * ((per_grp + 255) / 256))), dim3(256), 0,
                      (hipStream_t)stream, row_ptr, col, val, x, elu_y, y, m, n, c / 4, total);
   return launch_status("spmm_csr");
 }

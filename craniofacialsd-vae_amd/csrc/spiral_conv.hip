@@ -1075,6 +1075,178 @@ __global__ __launch_bounds__(256) void conv_bwd_out_small(
   for (int e = threadIdx.x; e < NEL; e += 256) ws[(long)blockIdx.x * NEL + e] = red[e];
 }
 
+// Same fused backward on MFMA (the kernel the step uses).  A wave owns
+// 32-source-row tiles (XCD-aware persistent sweep).  Lane (i, h) = (row,
+// half) folds only HALF of the row's spiral transpose: slots
+// s = 5h .. 5h + 4 (s < 9), i.e. t values k = s*CO + o in [h*KH, h*KH + KH),
+// KH = 5*CO, which is exactly the A operand it feeds to
+//   dx (32 x CIN) = T (32 x 2KH) . Wt (2KH x CIN),  Wt[k][c] = W[o][s*CIN + c]
+// (v_mfma_f32_32x32x2_f32, step j pairs k = j and k = KH + j; Wt in VGPRs).
+// T is also written to wave-private LDS as At[k][row] and
+//   dW^T (32 x CIN) += At (2KH x 32 rows) . x_tile (32 rows x CIN)
+// runs as 16 more MFMA steps whose K order (rows) is the accumulator row
+// order acc_row(j, lane): the x values that feed B are then the same
+// registers the dx epilogue needs for elu'(y) when elu_y == x (the model's
+// case: the output conv's input is the last Deblock's ELU output).
+constexpr int kAtS = 36;  // At row stride: conflict-free ds_read_b128 of the dW A operand
+#ifndef CFSD_BWD_OUT_OCC
+#define CFSD_BWD_OUT_OCC 1
+#endif
+template <int CIN, int CO>
+__global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
+    const float* __restrict__ dpre, const int* __restrict__ inv_ptr,
+    const int* __restrict__ inv_row, const int2* __restrict__ inv_pair,
+    const float* __restrict__ w, const float* __restrict__ elu_y, const float* __restrict__ x,
+    float* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, long total_rows) {
+  constexpr int SPH = 5, KH = SPH * CO, K = kSeq * CIN, NCT = CIN / 32, NEL = CO * K + CO;
+  static_assert(2 * KH <= 32 && CIN % 32 == 0, "shape");
+  __shared__ float at_all[4 * 32 * kAtS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 31, h = lane >> 5;
+  float* At = at_all + wave * 32 * kAtS;
+  for (int e = lane; e < (32 - 2 * KH) * kAtS; e += 64) At[2 * KH * kAtS + e] = 0.f;
+  // Wt (B operand of dx): lane (c, h) holds Wt[h*KH + j][ct*32 + c]
+  float wt[NCT][KH];
+#pragma unroll
+  for (int j = 0; j < KH; ++j) {
+    const int k = h * KH + j, sl = k / CO, o = k % CO;
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct)
+      wt[ct][j] = sl < kSeq ? w[o * K + sl * CIN + ct * 32 + li] : 0.f;
+  }
+  f32x16 dwacc[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dwacc[ct][r] = 0.f;
+  float dbs[CO];
+#pragma unroll
+  for (int o = 0; o < CO; ++o) dbs[o] = 0.f;
+  const int ey_mode = elu_y == nullptr ? 0 : (elu_y == x ? 1 : 2);
+  const long n_tiles = (total_rows + 31) / 32;
+  const TileSweep sw = xcd_sweep(n_tiles, 4, wave);
+  for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
+    const long row0 = tile * 32;
+    // half-row spiral transpose in the CO-wide dpre space
+    const long m = row0 + li;
+    const bool valid = m < total_rows;
+    const long mm = valid ? m : total_rows - 1;
+    const int b = (int)(mm / vsrc), u = (int)(mm % vsrc);
+    const float* db_ = dpre + (long)b * rows * CO;
+    int2 pr[SPH];
+#pragma unroll
+    for (int sl = 0; sl < SPH; ++sl) {
+      const int sg = h * SPH + sl;
+      pr[sl] = sg < kSeq ? inv_pair[u * kSeq + sg] : make_int2(-1, -1);
+    }
+    float tt[KH];
+#pragma unroll
+    for (int sl = 0; sl < SPH; ++sl) {
+      const int o0 = max(pr[sl].x, 0) * CO, o1 = max(pr[sl].y, 0) * CO;
+      const float f0 = pr[sl].x >= 0 ? 1.f : 0.f, f1 = pr[sl].y >= 0 ? 1.f : 0.f;
+#pragma unroll
+      for (int o = 0; o < CO; ++o) tt[sl * CO + o] = db_[o0 + o] * f0 + db_[o1 + o] * f1;
+    }
+#pragma unroll
+    for (int sl = 0; sl < SPH; ++sl) {
+      if (pr[sl].y >= 0) {
+        const int key = u * kSeq + h * SPH + sl;
+        for (int e = inv_ptr[key] + 2; e < inv_ptr[key + 1]; ++e) {
+          const int oe = inv_row[e] * CO;
+#pragma unroll
+          for (int o = 0; o < CO; ++o) tt[sl * CO + o] += db_[oe + o];
+        }
+      }
+    }
+    if (!valid) {
+#pragma unroll
+      for (int q = 0; q < KH; ++q) tt[q] = 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < KH; ++q) At[(h * KH + q) * kAtS + li] = tt[q];
+    if (h == 0) {  // slot 0 lists hold every output row once: db = sum_u t[0][o]
+#pragma unroll
+      for (int o = 0; o < CO; ++o) dbs[o] += tt[o];
+    }
+    // x tile in accumulator-row order (B operand of dW, elu' source); its
+    // loads are in flight during the dx MFMAs
+    float xv[NCT][16];
+    const float* xt = x + row0 * CIN + li;
+    const int last = (int)(total_rows - 1 - row0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int rr = min(acc_row(j, lane), last);  // clamped rows have a zero At column
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) xv[ct][j] = xt[rr * CIN + ct * 32];
+    }
+    // dx = T . Wt
+    f32x16 dxacc[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dxacc[ct][r] = 0.f;
+#pragma unroll
+      for (int j = 0; j < KH; ++j) dxacc[ct] = mfma32(tt[j], wt[ct][j], dxacc[ct]);
+    }
+    wave_lds_sync();
+    // dW^T += At . x_tile, K (rows) in accumulator-row order
+#pragma unroll
+    for (int t4 = 0; t4 < 4; ++t4) {
+      const f32x4 a = ld4(&At[li * kAtS + 8 * t4 + 4 * h]);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        dwacc[ct] = mfma32(a.x, xv[ct][4 * t4 + 0], dwacc[ct]);
+        dwacc[ct] = mfma32(a.y, xv[ct][4 * t4 + 1], dwacc[ct]);
+        dwacc[ct] = mfma32(a.z, xv[ct][4 * t4 + 2], dwacc[ct]);
+        dwacc[ct] = mfma32(a.w, xv[ct][4 * t4 + 3], dwacc[ct]);
+      }
+    }
+    if (dx) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long rr = row0 + acc_row(r, lane);
+        if (rr < total_rows) {
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) {
+            float v = dxacc[ct][r];
+            if (ey_mode == 1) v *= elu_grad_from_out(xv[ct][r]);
+            else if (ey_mode == 2) v *= elu_grad_from_out(elu_y[rr * CIN + ct * 32 + li]);
+            dx[rr * CIN + ct * 32 + li] = v;
+          }
+        }
+      }
+    }
+    wave_lds_sync();
+  }
+  // block combine (fixed wave order) -> one slab [CO*K + CO]
+#pragma unroll
+  for (int o = 0; o < CO; ++o)
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) dbs[o] += __shfl_xor(dbs[o], d);
+  __syncthreads();
+  float* red = at_all;
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv) {
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int k = acc_row(rr, lane), c = ct * 32 + li;
+          const int sl = k / CO;
+          if (sl < kSeq && k < 2 * KH) {
+            const int e = (k % CO) * K + sl * CIN + c;
+            red[e] = wv == 0 ? dwacc[ct][rr] : red[e] + dwacc[ct][rr];
+          }
+        }
+      if (lane == 0)
+#pragma unroll
+        for (int o = 0; o < CO; ++o) red[CO * K + o] = wv == 0 ? dbs[o] : red[CO * K + o] + dbs[o];
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < NEL; e += 256) ws[(long)blockIdx.x * NEL + e] = red[e];
+}
+
 __global__ __launch_bounds__(1024) void slab_reduce(const float* __restrict__ ws, int n_slabs,
                                                     int n_el, float* __restrict__ out_a, int n_a,
                                                     float* __restrict__ out_b) {
@@ -1434,9 +1606,9 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
 // ---- fused backward (data + weight)
 namespace {
 bool fused_small(int cin, int cout) { return cout * kSeq <= 32 && (cin == 32 || cin == 64); }
-int fused_small_gx(long m_src) {
-  long gx = ((m_src + 63) / 64 + 3) / 4;
-  return (int)(gx > 512 ? 512 : (gx < 1 ? 1 : gx));
+int fused_small_gx(long m_src) {  // ~2 32-row tiles per wave
+  long gx = ((m_src + 31) / 32 + 7) / 8;
+  return (int)(gx > 1024 ? 1024 : (gx < 1 ? 1 : gx));
 }
 }  // namespace
 
@@ -1479,7 +1651,7 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
   const int n_el = cout * kSeq * cin + cout;
 #define BOS(CIN_, CO_)                                                                           \
   if (cin == CIN_ && cout == CO_) {                                                              \
-    hipLaunchKernelGGL((conv_bwd_out_small<CIN_, CO_>), dim3(gx), dim3(256), 0, st, dpre,        \
+    hipLaunchKernelGGL((conv_bwd_out_mfma<CIN_, CO_>), dim3(gx), dim3(256), 0, st, dpre,         \
                        inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, x, dx, workspace, vsrc, \
                        rows, Ms);                                                                \
     rc = launch_status("spiral_conv_bwd_small");                                                 \

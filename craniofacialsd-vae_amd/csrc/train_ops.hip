@@ -139,6 +139,7 @@ __global__ __launch_bounds__(256) void latent_fwd_k(const float* __restrict__ mu
                                                     int sigmoid, float w_kl, float w_lc,
                                                     float eta1, float eta2, int bs) {
   __shared__ float zs[64 * 256];
+  __shared__ float cs[64 * 256];      // dLC/dz accumulators, column l owned by thread l
   __shared__ float dist[4 * 64 * 8];  // [kind][pair][t]
   __shared__ float2 red[4];
   const int tid = threadIdx.x;
@@ -203,8 +204,8 @@ __global__ __launch_bounds__(256) void latent_fwd_k(const float* __restrict__ mu
   if (tid < L) {
     const int l = tid;
     const bool inr = (l >= lo && l < hi);
-    float col[64];
-    for (int i = 0; i < B; ++i) col[i] = 0.f;
+    float* col = cs + l;  // col[i * L] (LDS: a private array here would live in scratch)
+    for (int i = 0; i < B; ++i) col[i * L] = 0.f;
     if (w_lc != 0.f) {
       for (int pr = 0; pr < npairs; ++pr) {
         int p = 0, rem = pr;
@@ -223,14 +224,14 @@ __global__ __launch_bounds__(256) void latent_fwd_k(const float* __restrict__ mu
           const float d1 = zs[a1 * L + l] - zs[b1 * L + l];
           const float d2 = zs[a2 * L + l] - zs[b2 * L + l];
           const float s1 = inr ? 1.f : -1.f;  // lg - dg  vs  lr - dr
-          col[a1] += s1 * k2 * d1;
-          col[b1] -= s1 * k2 * d1;
-          col[a2] -= s1 * k2 * d2;
-          col[b2] += s1 * k2 * d2;
+          col[a1 * L] += s1 * k2 * d1;
+          col[b1 * L] -= s1 * k2 * d1;
+          col[a2 * L] -= s1 * k2 * d2;
+          col[b2 * L] += s1 * k2 * d2;
         }
       }
     }
-    for (int i = 0; i < B; ++i) dlat[i * 3 * L + l] = col[i];
+    for (int i = 0; i < B; ++i) dlat[i * 3 * L + l] = col[i * L];
   }
   float2 r = block_sum2(kl_part, lc_part, red);
   if (tid == 0) {
@@ -291,139 +292,225 @@ __global__ void loss_finalize_k(const float* __restrict__ partials, int nblocks,
 // ----------------------------------------------------------- dense Linear
 // The bottleneck Linears are [16 x 4288] x [4288 x 150] (encoder, stacked
 // mu/logvar) and [16 x 75] x [75 x 4288] (decoder): tiny GEMMs whose cost is
-// parallelism and latency, not FLOPs.  Long reductions are split across
-// workgroups into a workspace and summed in a second fixed-order pass.
-constexpr int kLinKC = 256;   // k per split-K workgroup (64 lanes x 4)
-constexpr int kLinNC = 128;   // n per split-n chunk (dx of the decoder Linear)
+// parallelism and latency, not FLOPs.  Each product is ONE launch: long
+// reductions are spread over a 256-thread block and summed in fixed order
+// (deterministic), short ones run thread-per-output with the small operand
+// staged in LDS.
+// Row-group width of the block-reduction kernels (one accumulator per row).
+constexpr int kLinRG = 16;
+constexpr int kLinRedThreads = 512;   // block of the long-reduction kernels
+constexpr int kLinUnroll = 9;         // reduction terms per thread issued together
 
-// Split-K partials: block (col n, chunk ks), one wave; lane l owns k =
-// ks*256 + 4l .. +3.  ws[(ks*m + i)*n + col].
-__global__ __launch_bounds__(64) void linear_fwd_splitk(const float* __restrict__ x,
-                                                        const float* __restrict__ w,
-                                                        float* __restrict__ ws, int m, int k,
-                                                        int n) {
-  const int col = blockIdx.x, ks = blockIdx.y, lane = threadIdx.x;
-  const int k0 = ks * kLinKC + 4 * lane;
-  float wv[4];
+// Sum kLinRG per-thread values over a kLinRedThreads block in fixed order
+// (wave butterfly, then waves in index order); thread i < kLinRG gets row i.
+// `sh` is [16 waves][kLinRG] LDS.
+__device__ __forceinline__ float block_rows_sum(float (&v)[kLinRG], float* sh) {
+  constexpr int kWaves = kLinRedThreads / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) wv[q] = (k0 + q < k) ? w[(long)col * k + k0 + q] : 0.f;
-  for (int i0 = 0; i0 < m; i0 += 16) {
-    float acc[16];
+  for (int i = 0; i < kLinRG; ++i) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      acc[i] = 0.f;
-      if (i0 + i < m) {
-        const float* xr = x + (long)(i0 + i) * k;
+    for (int d = 32; d >= 1; d >>= 1) v[i] += __shfl_xor(v[i], d);
+  }
+  if (lane == 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (k0 + q < k) acc[i] = fmaf(xr[k0 + q], wv[q], acc[i]);
+    for (int i = 0; i < kLinRG; ++i) sh[wave * kLinRG + i] = v[i];
+  }
+  __syncthreads();
+  float r = 0.f;
+  if (threadIdx.x < kLinRG) {
+    r = sh[threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) r += sh[w * kLinRG + threadIdx.x];
+  }
+  __syncthreads();
+  return r;
+}
+
+// Long k (encoder Linear: [16 x 4288] x [4288 x 150]): one 512-thread block
+// per output column; each thread owns up to kLinUnroll k-terms per pass (all
+// x / W loads issued before the FMAs), rows in groups of 16, fixed-order
+// block sum.  One launch, no workspace, deterministic.
+__global__ __launch_bounds__(kLinRedThreads) void linear_fwd_kred(const float* __restrict__ x,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ bias,
+                                                                  float* __restrict__ y, int m,
+                                                                  int k, int n) {
+  __shared__ float sh[(kLinRedThreads / 64) * kLinRG];
+  const int col = blockIdx.x;
+  const float* wr = w + (long)col * k;
+  for (int i0 = 0; i0 < m; i0 += kLinRG) {
+    const int mr = min(kLinRG, m - i0);
+    float acc[kLinRG];
+#pragma unroll
+    for (int i = 0; i < kLinRG; ++i) acc[i] = 0.f;
+    for (int k0 = 0; k0 < k; k0 += kLinRedThreads * kLinUnroll) {
+      float wv[kLinUnroll];
+#pragma unroll
+      for (int u = 0; u < kLinUnroll; ++u) {
+        const int kk = k0 + u * kLinRedThreads + threadIdx.x;
+        wv[u] = kk < k ? wr[kk] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < kLinRG; ++i) {
+        const float* xr = x + (long)(i0 + min(i, mr - 1)) * k;
+        float xv[kLinUnroll];
+#pragma unroll
+        for (int u = 0; u < kLinUnroll; ++u) {
+          const int kk = k0 + u * kLinRedThreads + threadIdx.x;
+          xv[u] = kk < k ? xr[kk] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kLinUnroll; ++u) acc[i] = fmaf(xv[u], wv[u], acc[i]);
       }
     }
+    const float r = block_rows_sum(acc, sh);
+    if (threadIdx.x < mr) y[(long)(i0 + threadIdx.x) * n + col] = r + (bias ? bias[col] : 0.f);
+  }
+}
+
+// Short k (decoder Linear: [16 x 75] x [75 x 4288]): thread per (column,
+// row quad); the quad's x rows are staged in LDS (broadcast reads), the
+// thread's W row is read once for 4 outputs; y stores are coalesced.
+constexpr int kLinSmallK = 512;
+__global__ __launch_bounds__(256) void linear_fwd_nred(const float* __restrict__ x,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ bias,
+                                                       float* __restrict__ y, int m, int k,
+                                                       int n) {
+  __shared__ float xs[4 * kLinSmallK];
+  const int i0 = blockIdx.y * 4, mr = min(4, m - i0);
+  for (int e = threadIdx.x; e < mr * k; e += 256) xs[e] = x[(long)i0 * k + e];
+  __syncthreads();
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= n) return;
+  const float* wr = w + (long)col * k;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 5
+  for (int kk = 0; kk < k; ++kk) {
+    const float wv = wr[kk];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float v = acc[i];
+    for (int i = 0; i < 4; ++i) acc[i] = fmaf(xs[i * k + kk], wv, acc[i]);
+  }
+  const float bv = bias ? bias[col] : 0.f;
 #pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-      if (lane == i && i0 + i < m) ws[((long)ks * m + i0 + i) * n + col] = v;
+  for (int i = 0; i < 4; ++i)
+    if (i < mr) y[(long)(i0 + i) * n + col] = acc[i] + bv;
+}
+
+// dx, short n (encoder Linear: dx [16 x 4288] = dy [16 x 150] . W [150 x 4288]):
+// block = 64 k-columns x 4 waves; wave w sums the c-range w*n/4 .. for a row
+// quad (blockIdx.y) with dy staged in LDS and W[c][k] coalesced (all of a
+// wave's W loads in flight together); the 4 wave partials are added in order.
+constexpr int kLinDxChunk = 40;  // c terms per wave and pass
+__global__ __launch_bounds__(256) void linear_dx_nsmall(const float* __restrict__ dy,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ elu_y,
+                                                        float* __restrict__ dx, int m, int k,
+                                                        int n, int accumulate) {
+  __shared__ float ds[4 * kLinSmallK];
+  __shared__ float part[4][4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i0 = blockIdx.y * 4, mr = min(4, m - i0);
+  for (int e = threadIdx.x; e < mr * n; e += 256) ds[e] = dy[(long)i0 * n + e];
+  __syncthreads();
+  const int kk = blockIdx.x * 64 + lane;
+  const int kc = kk < k ? kk : k - 1;
+  const int per = (n + 3) / 4, c0 = wave * per, c1 = min(n, c0 + per);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int cb = c0; cb < c1; cb += kLinDxChunk) {
+    float wv[kLinDxChunk];
+#pragma unroll
+    for (int u = 0; u < kLinDxChunk; ++u) wv[u] = cb + u < c1 ? w[(long)(cb + u) * k + kc] : 0.f;
+#pragma unroll
+    for (int u = 0; u < kLinDxChunk; ++u) {
+      const int c = min(cb + u, n - 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = fmaf(ds[i * n + c], wv[u], acc[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) part[wave][i][lane] = acc[i];
+  __syncthreads();
+  if (wave < mr && kk < k) {
+    const int i = wave;
+    float v = part[0][i][lane] + part[1][i][lane] + part[2][i][lane] + part[3][i][lane];
+    const long o = (long)(i0 + i) * k + kk;
+    if (elu_y) v *= elu_grad_from_out(elu_y[o]);
+    dx[o] = accumulate ? dx[o] + v : v;
+  }
+}
+
+// dx, long n (decoder Linear: dz [16 x 75] = dh [16 x 4288] . W [4288 x 75]):
+// one 512-thread block per k column, the n reduction spread over the block
+// (kLinUnroll terms per thread in flight), fixed-order block sum.
+__global__ __launch_bounds__(kLinRedThreads) void linear_dx_nred(const float* __restrict__ dy,
+                                                                 const float* __restrict__ w,
+                                                                 const float* __restrict__ elu_y,
+                                                                 float* __restrict__ dx, int m,
+                                                                 int k, int n, int accumulate) {
+  __shared__ float sh[(kLinRedThreads / 64) * kLinRG];
+  const int kk = blockIdx.x;
+  for (int i0 = 0; i0 < m; i0 += kLinRG) {
+    const int mr = min(kLinRG, m - i0);
+    float acc[kLinRG];
+#pragma unroll
+    for (int i = 0; i < kLinRG; ++i) acc[i] = 0.f;
+    for (int c0 = 0; c0 < n; c0 += kLinRedThreads * kLinUnroll) {
+      float wv[kLinUnroll];
+#pragma unroll
+      for (int u = 0; u < kLinUnroll; ++u) {
+        const int c = c0 + u * kLinRedThreads + threadIdx.x;
+        wv[u] = c < n ? w[(long)c * k + kk] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < kLinRG; ++i) {
+        const float* dr = dy + (long)(i0 + min(i, mr - 1)) * n;
+        float dv[kLinUnroll];
+#pragma unroll
+        for (int u = 0; u < kLinUnroll; ++u) {
+          const int c = c0 + u * kLinRedThreads + threadIdx.x;
+          dv[u] = c < n ? dr[c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kLinUnroll; ++u) acc[i] = fmaf(dv[u], wv[u], acc[i]);
+      }
+    }
+    float r = block_rows_sum(acc, sh);
+    if (threadIdx.x < mr) {
+      const long o = (long)(i0 + threadIdx.x) * k + kk;
+      if (elu_y) r *= elu_grad_from_out(elu_y[o]);
+      dx[o] = accumulate ? dx[o] + r : r;
     }
   }
 }
 
-__global__ __launch_bounds__(256) void linear_fwd_reduce(const float* __restrict__ ws,
-                                                         const float* __restrict__ bias,
-                                                         float* __restrict__ y, int m, int n,
-                                                         int nks) {
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long)m * n) return;
-  float s = 0.f;
-  for (int q = 0; q < nks; ++q) s += ws[(long)q * m * n + e];
-  y[e] = s + (bias ? bias[e % n] : 0.f);
-}
-
-// Short k: one thread per (i, n); 16 consecutive threads share n (broadcast W).
-__global__ __launch_bounds__(256) void linear_fwd_smallk(const float* __restrict__ x,
-                                                         const float* __restrict__ w,
-                                                         const float* __restrict__ bias,
-                                                         float* __restrict__ y, int m, int k,
-                                                         int n) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int i = (int)(t % 16);
-  const long col = t / 16;
-  if (col >= n) return;
-  const float* wr = w + col * k;
-  for (int ii = i; ii < m; ii += 16) {
-    const float* xr = x + (long)ii * k;
-    float acc = 0.f;
-    for (int kk = 0; kk < k; ++kk) acc = fmaf(xr[kk], wr[kk], acc);
-    y[(long)ii * n + col] = acc + (bias ? bias[col] : 0.f);
-  }
-}
-
-// dx for short n (encoder Linear, n = 150): block = one wave of 64 k's for
-// row i = blockIdx.y (wave-uniform -> dy is read with scalar loads).
-__global__ __launch_bounds__(64) void linear_dx_rows(const float* __restrict__ dy,
-                                                     const float* __restrict__ w,
-                                                     const float* __restrict__ elu_y,
-                                                     float* __restrict__ dx, int m, int k, int n,
-                                                     int accumulate) {
-  const int kk = blockIdx.x * 64 + threadIdx.x;
-  const int i = blockIdx.y;
-  if (kk >= k) return;
-  const float* dyr = dy + (long)i * n;
-  float acc = 0.f;
-#pragma unroll 8
-  for (int nn = 0; nn < n; ++nn) acc = fmaf(dyr[nn], w[(long)nn * k + kk], acc);
-  const long o = (long)i * k + kk;
-  if (elu_y) acc *= elu_grad_from_out(elu_y[o]);
-  dx[o] = accumulate ? dx[o] + acc : acc;
-}
-
-// dx for long n (decoder Linear, n = 4288): split-n partials, thread per
-// (i, k) pair, ws[ns][i*k + kk].
-__global__ __launch_bounds__(256) void linear_dx_splitn(const float* __restrict__ dy,
-                                                        const float* __restrict__ w,
-                                                        float* __restrict__ ws, int m, int k,
-                                                        int n) {
-  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= (long)m * k) return;
-  const int i = (int)(p / k), kk = (int)(p % k);
-  const int n0 = blockIdx.y * kLinNC, n1 = min(n, n0 + kLinNC);
-  const float* dyr = dy + (long)i * n;
-  float acc = 0.f;
-#pragma unroll 8
-  for (int nn = n0; nn < n1; ++nn) acc = fmaf(dyr[nn], w[(long)nn * k + kk], acc);
-  ws[(long)blockIdx.y * m * k + p] = acc;
-}
-
-__global__ __launch_bounds__(256) void linear_dx_reduce(const float* __restrict__ ws,
-                                                        const float* __restrict__ elu_y,
-                                                        float* __restrict__ dx, long mk, int nns,
-                                                        int accumulate) {
-  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= mk) return;
-  float s = 0.f;
-  for (int q = 0; q < nns; ++q) s += ws[(long)q * mk + p];
-  if (elu_y) s *= elu_grad_from_out(elu_y[p]);
-  dx[p] = accumulate ? dx[p] + s : s;
-}
-
-// dw[n,k] = sum_i dy[i,n] x[i,k] (thread per element), db[n] = sum_i dy[i,n].
+// dw[n,k] = sum_i dy[i,n] x[i,k], db[n] = sum_i dy[i,n]: block row n =
+// blockIdx.y (dy[., n] wave-uniform -> scalar loads), thread per k
+// (coalesced x loads), the m terms unrolled by 16 so their loads overlap.
 __global__ __launch_bounds__(256) void linear_dw_k(const float* __restrict__ x,
                                                    const float* __restrict__ dy,
                                                    float* __restrict__ dw,
                                                    float* __restrict__ db, int m, int k, int n) {
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long nk = (long)n * k;
-  if (e < nk) {
-    const int nn = (int)(e / k), kk = (int)(e % k);
+  const int nn = blockIdx.y;
+  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (dw && kk < k) {
     float s = 0.f;
-    for (int i = 0; i < m; ++i) s = fmaf(dy[(long)i * n + nn], x[(long)i * k + kk], s);
-    if (dw) dw[e] = s;
-  } else if (e < nk + n) {
-    const int nn = (int)(e - nk);
+    int i = 0;
+    for (; i + 16 <= m; i += 16) {
+      float xv[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) xv[j] = x[(long)(i + j) * k + kk];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s = fmaf(dy[(long)(i + j) * n + nn], xv[j], s);
+    }
+    for (; i < m; ++i) s = fmaf(dy[(long)i * n + nn], x[(long)i * k + kk], s);
+    dw[(long)nn * k + kk] = s;
+  }
+  if (db && blockIdx.x == 0 && threadIdx.x == 0) {
     float s = 0.f;
     for (int i = 0; i < m; ++i) s += dy[(long)i * n + nn];
-    if (db) db[nn] = s;
+    db[nn] = s;
   }
 }
 
@@ -569,19 +656,9 @@ extern "C" int cfsd_loss_finalize(const float* partials, int nblocks, const floa
   return launch_status("loss_finalize");
 }
 
-static size_t linear_ws_floats(int m, int k, int n) {
-  size_t f = 0;
-  if (k >= 512) f = (size_t)((k + kLinKC - 1) / kLinKC) * m * n;
-  if (n > 512) {
-    const size_t g = (size_t)((n + kLinNC - 1) / kLinNC) * m * k;
-    if (g > f) f = g;
-  }
-  return f;
-}
-
 extern "C" size_t cfsd_linear_workspace(int m, int k, int n) {
   if (m <= 0 || k <= 0 || n <= 0) return 0;
-  return linear_ws_floats(m, k, n) * sizeof(float);
+  return 0;  // single-pass kernels; kept for ABI stability
 }
 
 extern "C" int cfsd_linear_fwd(const float* x, const float* w, const float* bias, float* y,
@@ -589,23 +666,17 @@ extern "C" int cfsd_linear_fwd(const float* x, const float* w, const float* bias
                                void* stream) {
   if (!x || !w || !y) return set_error(CFSD_EINVAL, "linear_fwd: null pointer");
   if (m <= 0 || k <= 0 || n <= 0) return set_error(CFSD_EINVAL, "linear_fwd: bad sizes");
+  (void)workspace;
+  (void)workspace_bytes;
   hipStream_t st = (hipStream_t)stream;
-  if (k >= 512) {
-    const int nks = (k + kLinKC - 1) / kLinKC;
-    if (!workspace || workspace_bytes < (size_t)nks * m * n * sizeof(float))
-      return set_error(CFSD_EWORKSPACE, "linear_fwd: workspace too small");
-    hipLaunchKernelGGL(linear_fwd_splitk, dim3(n, nks), dim3(64), 0, st, x, w, workspace, m, k, n);
-    int rc = launch_status("linear_fwd_splitk");
-    if (rc) return rc;
-    const long mn = (long)m * n;
-    hipLaunchKernelGGL(linear_fwd_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, st,
-                       workspace, bias, y, m, n, nks);
-    return launch_status("linear_fwd_reduce");
+  if (k > kLinSmallK) {
+    hipLaunchKernelGGL(linear_fwd_kred, dim3(n), dim3(kLinRedThreads), 0, st, x, w, bias, y, m, k,
+                       n);
+    return launch_status("linear_fwd_kred");
   }
-  const long t = (long)n * 16;
-  hipLaunchKernelGGL(linear_fwd_smallk, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, x, w,
+  hipLaunchKernelGGL(linear_fwd_nred, dim3((n + 255) / 256, (m + 3) / 4), dim3(256), 0, st, x, w,
                      bias, y, m, k, n);
-  return launch_status("linear_fwd_smallk");
+  return launch_status("linear_fwd_nred");
 }
 
 extern "C" int cfsd_linear_bwd(const float* x, const float* w, const float* dy, const float* elu_y,
@@ -614,34 +685,28 @@ extern "C" int cfsd_linear_bwd(const float* x, const float* w, const float* dy, 
                                void* stream) {
   if (!dy) return set_error(CFSD_EINVAL, "linear_bwd: null dy");
   if (m <= 0 || k <= 0 || n <= 0) return set_error(CFSD_EINVAL, "linear_bwd: bad sizes");
+  (void)workspace;
+  (void)workspace_bytes;
   hipStream_t st = (hipStream_t)stream;
   if (dx) {
     if (!w) return set_error(CFSD_EINVAL, "linear_bwd: null w");
     int rc;
-    if (n <= 512) {
-      hipLaunchKernelGGL(linear_dx_rows, dim3((k + 63) / 64, m), dim3(64), 0, st, dy, w, elu_y, dx,
-                         m, k, n, accumulate);
-      rc = launch_status("linear_dx_rows");
+    if (n <= kLinSmallK) {
+      hipLaunchKernelGGL(linear_dx_nsmall, dim3((k + 63) / 64, (m + 3) / 4), dim3(256), 0, st, dy,
+                         w, elu_y, dx, m, k, n, accumulate);
+      rc = launch_status("linear_dx_nsmall");
     } else {
-      const int nns = (n + kLinNC - 1) / kLinNC;
-      const long mk = (long)m * k;
-      if (!workspace || workspace_bytes < (size_t)nns * mk * sizeof(float))
-        return set_error(CFSD_EWORKSPACE, "linear_bwd: workspace too small");
-      hipLaunchKernelGGL(linear_dx_splitn, dim3((unsigned)((mk + 255) / 256), nns), dim3(256), 0,
-                         st, dy, w, workspace, m, k, n);
-      rc = launch_status("linear_dx_splitn");
-      if (rc) return rc;
-      hipLaunchKernelGGL(linear_dx_reduce, dim3((unsigned)((mk + 255) / 256)), dim3(256), 0, st,
-                         workspace, elu_y, dx, mk, nns, accumulate);
-      rc = launch_status("linear_dx_reduce");
+      hipLaunchKernelGGL(linear_dx_nred, dim3(k), dim3(kLinRedThreads), 0, st, dy, w, elu_y, dx, m,
+                         k, n, accumulate);
+      rc = launch_status("linear_dx_nred");
     }
     if (rc) return rc;
   }
   if (dw || db) {
     if (dw && !x) return set_error(CFSD_EINVAL, "linear_bwd: null x");
-    const long tot = (long)n * k + n;
-    hipLaunchKernelGGL(linear_dw_k, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, x, dy,
-                       dw, db, m, k, n);
+    const int bt = k >= 256 ? 256 : ((k + 63) / 64) * 64;
+    hipLaunchKernelGGL(linear_dw_k, dim3((k + bt - 1) / bt, n), dim3(bt), 0, st, x, dy, dw, db, m,
+                       k, n);
     return launch_status("linear_bwd_dw");
   }
   return CFSD_OK;

@@ -293,3 +293,99 @@ def test_train_step_deterministic(dtopo):
         outs.append((eng.params.data.cpu().clone(), eng.params.grad.cpu().clone()))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+# --------------------------------------------------------------- dense Linears
+# Both bottleneck shapes of the model (encoder [m x 4288] -> 150 stacked
+# mu/logvar, decoder 75 -> 4288) plus ragged m (not a multiple of the 4-row /
+# 16-row groups).  Torch fp32 reference, tolerance rel 1e-5 (k <= 4288 terms).
+LINEAR_CASES = [(16, 4288, 150), (16, 75, 4288), (5, 4288, 150), (3, 75, 4288), (1, 600, 7),
+                (20, 64, 33), (18, 1000, 600)]
+
+
+@pytest.mark.parametrize("m,k,n", LINEAR_CASES)
+def test_linear_fwd(m, k, n):
+    g = torch.Generator().manual_seed(m * 7 + k + n)
+    x, w, b = torch.randn(m, k, generator=g), torch.randn(n, k, generator=g) * 0.05, torch.randn(n, generator=g)
+    y = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV))
+    close(y, x.double() @ w.double().T + b.double(), 1e-5, "linear fwd")
+
+
+@pytest.mark.parametrize("m,k,n", LINEAR_CASES)
+@pytest.mark.parametrize("elu,accumulate", [(False, False), (True, False), (False, True)])
+def test_linear_bwd(m, k, n, elu, accumulate):
+    g = torch.Generator().manual_seed(m + k * 3 + n)
+    x, w = torch.randn(m, k, generator=g), torch.randn(n, k, generator=g) * 0.05
+    dy = torch.randn(m, n, generator=g)
+    ey = O.elu(torch.randn(m, k, generator=g)) if elu else None
+    dx0 = torch.randn(m, k, generator=g)
+    dx_ref = dy.double() @ w.double()
+    if elu:
+        dx_ref = dx_ref * torch.where(ey > 0, torch.ones_like(ey), ey + 1).double()
+    if accumulate:
+        dx_ref = dx_ref + dx0.double()
+    dx = dx0.clone().to(DEV) if accumulate else torch.empty(m, k, device=DEV)
+    dw, db = torch.empty(n, k, device=DEV), torch.empty(n, device=DEV)
+    ops.linear_bwd(x.to(DEV), w.to(DEV), dy.to(DEV), dx=dx, dw=dw, db=db,
+                   elu_y=ey.to(DEV) if elu else None, accumulate=accumulate)
+    close(dx, dx_ref, 1e-5, "linear dx")
+    close(dw, dy.double().T @ x.double(), 1e-5, "linear dw")
+    close(db, dy.double().sum(0), 1e-5, "linear db")
+
+
+# --------------------------------------------------------------- latent head
+@pytest.mark.parametrize("key", [0, 7, 14])
+def test_latent_head_vs_oracle(key):
+    """Reparameterisation + KL + latent consistency (fwd terms and dz/dmu/dlogvar)."""
+    g = torch.Generator().manual_seed(key)
+    L, bs = 75, 4
+    mu = torch.randn(16, L, generator=g).double().requires_grad_()
+    lv = (torch.randn(16, L, generator=g) * 0.3).double().requires_grad_()
+    eps = torch.randn(16, L, generator=g)
+    z = mu + eps.double() * torch.exp(0.5 * lv)
+    regions = O.latent_regions(15, L)
+    kl = O.kl_loss(mu, lv)
+    lc = O.latent_consistency(z, regions[key], bs)
+    (1e-4 * kl + 0.5 * lc).backward()
+    mulv = torch.cat([lv, mu], 1).detach().float().to(DEV)
+    zz, dlat, terms = torch.empty(16, L, device=DEV), torch.empty(16, 3 * L, device=DEV), torch.empty(2, device=DEV)
+    keyt = torch.full((1,), key, dtype=torch.int32, device=DEV)
+    ops.latent_fwd(mulv, eps.to(DEV), keyt, zz, dlat, terms, L, 5, True, True, False, 1e-4, 0.5, 0.5, 0.5)
+    close(zz, z.detach(), 1e-5, "z")
+    close(terms[0], kl.detach(), 1e-5, "kl")
+    close(terms[1], lc.detach(), 1e-5, "lc")
+    dmulv = torch.empty_like(mulv)
+    ops.latent_bwd(mulv, eps.to(DEV), zz, torch.zeros(16, L, device=DEV), dlat, dmulv, L, True, True, False)
+    close(dmulv[:, L:], mu.grad, 1e-5, "dmu")
+    close(dmulv[:, :L], lv.grad, 1e-5, "dlogvar")
+
+
+def test_graph_replay_matches_eager(dtopo):
+    """The hipGraph-captured resident step (device-side batch pick, key and
+    noise) gives bit-identical parameters and losses to eager launches."""
+    w = recipe.golden_weights()
+    data = torch.from_numpy(recipe.normalized_meshes(12)).to(DEV)
+    perm = torch.arange(12, dtype=torch.int32, device=DEV)
+    res = []
+    for use_graph in (False, True):
+        eng = make_engine(dtopo, w)
+        b = eng.buffers(16)
+        step = lambda: eng.resident_step(b, data, perm, 3)  # noqa: E731
+        if use_graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                step()
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+            for _ in range(3):
+                g.replay()
+        else:
+            for _ in range(4):
+                step()
+        torch.cuda.synchronize()
+        res.append((eng.params.data.cpu().clone(), b.losses.cpu().clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])

@@ -78,6 +78,18 @@ def main():
     cases["dout_bwd_nodx"] = lambda: ops.spiral_conv_bwd(b.dec_out[3], T.spiral[0], b.dout, T.spiral_inv[0], wout,
                                                         P.gview("de_layers.5.layer.weight"),
                                                         P.gview("de_layers.5.layer.bias"), workspace=b.ws)
+    W_enc, B_enc = eng._enc_lin()
+    gW_enc, gB_enc = eng._enc_lin(P.grad)
+    flat = b.enc_out[3].view(16, -1)
+    flat.copy_(torch.randn(flat.shape, device="cuda", generator=g))
+    Wd, Bd = P.view("de_layers.0.weight"), P.view("de_layers.0.bias")
+    cases["lin_enc_fwd"] = lambda: ops.linear_fwd(flat, W_enc, B_enc, out=b.mulv)
+    cases["lin_dec_fwd"] = lambda: ops.linear_fwd(b.z, Wd, Bd, out=b.h.view(16, -1))
+    cases["lin_dec_dx"] = lambda: ops.linear_bwd(b.z, Wd, b.dh.view(16, -1), dx=b.dz)
+    cases["lin_dec_dw"] = lambda: ops.linear_bwd(b.z, None, b.dh.view(16, -1), dw=P.gview("de_layers.0.weight"),
+                                                 db=P.gview("de_layers.0.bias"))
+    cases["lin_enc_dx"] = lambda: ops.linear_bwd(flat, W_enc, b.dmulv, dx=b.dpre_enc[3].view(16, -1), elu_y=flat)
+    cases["lin_enc_dw"] = lambda: ops.linear_bwd(flat, None, b.dmulv, dw=gW_enc.view(W_enc.shape), db=gB_enc)
     if "step" in names:
         eng.set_batch(b.x, key_index=3)
         cases["step"] = lambda: eng.train_step_on(b)

@@ -76,13 +76,12 @@ class Runner:
         eng, b, T = self.eng, self.b, self.topo
         ops.step_begin(eng._step_counter(b), eng.seed, eps=b.eps, key=b.key,
                        n_regions=T.n_regions, batch_idx=b.batch_idx, bs=4,
-                       n_batches=self.n_batches, perm=self.perm)
+                       n_batches=self.n_batches, perm=self.perm, adam_step=eng.params.step)
         ops.swap_features(self.data, b.batch_idx, T.region_mask, b.key, 4, out=b.x)
         eng.forward(b, train=True, acc=eng.loss_acc)
         eng.backward(b)
 
     def part_b(self):
-        self.eng.advance_step()
         self.eng.adam_step()
 
     def allreduce(self):

@@ -46,10 +46,17 @@ SIGNATURES = {
     "cfsd_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_loss_finalize": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P]),
     "cfsd_adam": (_I, [_P, _P, _P, _P, _P, _Z, _F, _F, _F, _F, _F, _P]),
-    "cfsd_step_begin": (_I, [_P, _U64, _P, _I, _P, _I, _P, _I, _I, _P, _P]),
+    "cfsd_step_begin": (_I, [_P, _U64, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P]),
+    "cfsd_dw_reduce_batch": (_I, [_P, _I, _P]),
     "cfsd_scale": (_I, [_P, _Z, _F, _P]),
     "cfsd_elu_bwd": (_I, [_P, _P, _P, _Z, _P]),
 }
+
+
+class DwSlabs(ctypes.Structure):
+    """``cfsd_dw_slabs`` (include/cfsd.h): one deferred weight-gradient slab set."""
+    _fields_ = [("workspace", _P), ("dw", _P), ("db", _P), ("batch", _I), ("vsrc", _I),
+                ("rows", _I), ("cin", _I), ("cout", _I), ("fused", _I)]
 
 
 class CfsdError(RuntimeError):

@@ -78,6 +78,17 @@ __device__ __forceinline__ void gstore1_async(float* p, float v) {
 __device__ __forceinline__ void gload1_async(int& d, const int* p) {
   asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(p) : "memory");
 }
+__device__ __forceinline__ void gload1f_async(float& d, const float* p) {
+  asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+// Retire counted loads and hand their 8 destinations back to the compiler.
+template <int N, typename T>
+__device__ __forceinline__ void vm_wait_arr8(T (&a)[8]) {
+  asm volatile("s_waitcnt vmcnt(%8)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                 "+v"(a[6]), "+v"(a[7])
+               : "n"(N));
+}
 template <int N>
 __device__ __forceinline__ void vm_wait_n() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

@@ -474,6 +474,166 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
   }
 }
 
+// ==========================================================================
+// Layers with few rows (the coarse levels: <= ~2k 32-row tiles, where the
+// persistent kernels above cannot fill 256 CUs without splitting the slots
+// over workgroups and combining partials in a second launch).  Here a wave
+// owns one 16-row x 16-column output tile and ALL 9 slots, so there is no
+// partial and no combine launch; the slots run in batches of 3 whose
+// gathers and weight loads are all in flight together (3 memory-latency
+// exposures per tile instead of 9).  v_mfma_f32_16x16x4_f32 lane map as in
+// conv_fwd_mfma (lane (i, kg) holds row i's 16-B chunks kg, kg+4, ..);
+// two accumulators (even / odd chunk) halve the dependent-MFMA chain.
+// Tasks are numbered column-tile fastest, so the waves of a workgroup
+// gather the same rows (L1 hits).
+constexpr int kLatSB = 3;  // slots per batch
+template <int CIN, int COUT, int ACT>
+__global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
+                                                    const int* __restrict__ idx,
+                                                    const float* __restrict__ w,
+                                                    const float* __restrict__ bias,
+                                                    float* __restrict__ y, int vsrc, int rows,
+                                                    long total_rows) {
+  constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN;
+  const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
+  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long n_rt = (total_rows + 15) / 16;
+  if (task >= n_rt * NCT) return;
+  const int ct = (int)(task % NCT);
+  const long rt = task / NCT;
+  long m = rt * 16 + r16;
+  if (m >= total_rows) m = total_rows - 1;  // clamp loads, stores are masked
+  const int b = (int)(m / rows), r = (int)(m % rows);
+  const float* xb = x + (long)b * vsrc * CIN + 4 * kg;
+  const int* ir = idx + (long)r * kSeq;
+  const float* wb = w + (long)(ct * 16 + r16) * K + 4 * kg;
+  int src[kSeq];
+#pragma unroll
+  for (int s = 0; s < kSeq; ++s) src[s] = ir[s];
+  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int s0 = 0; s0 < kSeq; s0 += kLatSB) {
+    f32x4 av[kLatSB][CH], bw[kLatSB][CH];
+#pragma unroll
+    for (int sl = 0; sl < kLatSB; ++sl)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        av[sl][c] = ld4(xb + (long)src[s0 + sl] * CIN + 16 * c);
+        bw[sl][c] = ld4(wb + (s0 + sl) * CIN + 16 * c);
+      }
+    // keep the batch's loads ahead of its MFMAs (hipcc otherwise interleaves
+    // them with vmcnt waits to save registers, re-exposing the latency)
+    __builtin_amdgcn_sched_group_barrier(0x020, 2 * kLatSB * CH, 0);  // VMEM reads
+    __builtin_amdgcn_sched_group_barrier(0x008, 4 * kLatSB * CH, 0);  // MFMA
+#pragma unroll
+    for (int sl = 0; sl < kLatSB; ++sl)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        f32x4& a = acc[c & 1];
+        a = mfma16(av[sl][c].x, bw[sl][c].x, a);
+        a = mfma16(av[sl][c].y, bw[sl][c].y, a);
+        a = mfma16(av[sl][c].z, bw[sl][c].z, a);
+        a = mfma16(av[sl][c].w, bw[sl][c].w, a);
+      }
+  }
+  const int n = ct * 16 + r16;
+  const float bn = bias ? bias[n] : 0.f;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const long mo = rt * 16 + 4 * kg + rr;
+    if (mo < total_rows) {
+      float v = acc[0][rr] + acc[1][rr] + bn;
+      if (ACT == CFSD_ACT_ELU) v = elu_f(v);
+      y[mo * COUT + n] = v;
+    }
+  }
+}
+
+// Backward data for layers with few source rows, same tiling as
+// conv_fwd_lat: a wave owns 16 source rows u x 16 input channels c and all
+// 9 slots.  A = T_s[u][o] (gather-sum of dpre rows through the inverse
+// spiral: the inv_pair rows of a batch of 3 slots are loaded together,
+// rare further entries added after), B = W_s^T read straight from W (4
+// strided dwords per 4-chunk of o; W is L2-resident), in flight with A.
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpre,
+                                                   const int* __restrict__ inv_ptr,
+                                                   const int* __restrict__ inv_row,
+                                                   const int2* __restrict__ inv_pair,
+                                                   const float* __restrict__ w,
+                                                   const float* __restrict__ elu_y,
+                                                   float* __restrict__ dx, int vsrc, int rows,
+                                                   long total_rows) {
+  constexpr int CH = COUT / 16, NCT = CIN / 16, K = kSeq * CIN;
+  const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
+  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long n_rt = (total_rows + 15) / 16;
+  if (task >= n_rt * NCT) return;
+  const int ct = (int)(task % NCT);
+  const long rt = task / NCT;
+  long m = rt * 16 + r16;
+  if (m >= total_rows) m = total_rows - 1;
+  const int b = (int)(m / vsrc), u = (int)(m % vsrc);
+  const float* db_ = dpre + (long)b * rows * COUT + 4 * kg;
+  const int2* pu = inv_pair + (long)u * kSeq;
+  const float* wb = w + (long)(4 * kg) * K + ct * 16 + r16;  // + o_off*K + s*CIN
+  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int s0 = 0; s0 < kSeq; s0 += kLatSB) {
+    int2 pr[kLatSB];
+#pragma unroll
+    for (int sl = 0; sl < kLatSB; ++sl) pr[sl] = pu[s0 + sl];
+    f32x4 bw[kLatSB][CH];
+#pragma unroll
+    for (int sl = 0; sl < kLatSB; ++sl)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const float* q = wb + (long)(16 * c) * K + (s0 + sl) * CIN;
+        bw[sl][c] = f32x4{q[0], q[K], q[2 * K], q[3 * K]};
+      }
+    f32x4 a[kLatSB][CH];
+#pragma unroll
+    for (int sl = 0; sl < kLatSB; ++sl) {
+      const float f0 = pr[sl].x >= 0 ? 1.f : 0.f, f1 = pr[sl].y >= 0 ? 1.f : 0.f;
+      const float* p0 = db_ + (long)max(pr[sl].x, 0) * COUT;
+      const float* p1 = db_ + (long)max(pr[sl].y, 0) * COUT;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) a[sl][c] = ld4(p0 + 16 * c) * f0 + ld4(p1 + 16 * c) * f1;
+    }
+#pragma unroll
+    for (int sl = 0; sl < kLatSB; ++sl) {
+      if (pr[sl].y >= 0) {  // rare: entries beyond the first two
+        const long key = (long)u * kSeq + s0 + sl;
+        for (int e = inv_ptr[key] + 2; e < inv_ptr[key + 1]; ++e) {
+          const float* p = db_ + (long)inv_row[e] * COUT;
+#pragma unroll
+          for (int c = 0; c < CH; ++c) a[sl][c] += ld4(p + 16 * c);
+        }
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < kLatSB; ++sl)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        f32x4& ac = acc[c & 1];
+        ac = mfma16(a[sl][c].x, bw[sl][c].x, ac);
+        ac = mfma16(a[sl][c].y, bw[sl][c].y, ac);
+        ac = mfma16(a[sl][c].z, bw[sl][c].z, ac);
+        ac = mfma16(a[sl][c].w, bw[sl][c].w, ac);
+      }
+  }
+  const int c = ct * 16 + r16;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const long mo = rt * 16 + 4 * kg + rr;
+    if (mo < total_rows) {
+      float v = acc[0][rr] + acc[1][rr];
+      if (elu_y) v *= elu_grad_from_out(elu_y[mo * CIN + c]);
+      dx[mo * CIN + c] = v;
+    }
+  }
+}
+
 // Backward data, small dpre (CO <= 4 channels; the xyz output conv): one
 // thread per source row (b, u) computing all CIN outputs.  The spiral
 // transpose is first folded in the CO-wide dpre space,
@@ -695,6 +855,151 @@ __global__ __launch_bounds__(1024) void conv_dw_reduce(const float* __restrict__
       dw[(long)o * (kSeq * CIN) + s * CIN + cc] = t;
     } else {
       db[f - NW] = t;
+    }
+  }
+}
+
+// Backward weight for layers with few rows.  conv_dw_mfma's 9/12-wave
+// workgroups each need >= 4 row tiles, which leaves most CUs idle on the
+// coarse levels; here a wave owns ONE 32x32 dW unit (s, ot, ct) and a chunk
+// of R rows (the K dimension), so units x chunks waves run at once.
+// v_mfma_f32_32x32x2_f32 straight from memory, no LDS: step j covers rows
+// (2j, 2j+1) of the chunk; A[o][k] = dpre[row_k][ot*32 + o] (a 128-B
+// coalesced dpre segment per half-wave), B[k][c] = x[b, idx[r_k][s],
+// ct*32 + c] (a 128-B gathered row segment).  8 steps per batch with all
+// loads issued first, two accumulators.  Output: slab[chunk][U][32][32] +
+// db[chunk][COUT] (units with s == 0 && ct == 0 also sum dpre) -- the
+// conv_dw_mfma slab layout, reduced by conv_dw_reduce / dw_reduce_batch.
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void conv_dw_lat(const float* __restrict__ x,
+                                                   const int* __restrict__ idx,
+                                                   const float* __restrict__ dpre,
+                                                   float* __restrict__ ws,
+                                                   float* __restrict__ ws_db, int vsrc, int rows,
+                                                   int total_rows, int rchunk, int n_chunks) {
+  constexpr int OT = COUT / 32, CT = CIN / 32, U = kSeq * OT * CT, NB = 8;
+  const int lane = threadIdx.x & 63, li = lane & 31, h = lane >> 5;
+  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= (long)n_chunks * U) return;
+  const int unit = (int)(task % U), chunk = (int)(task / U);
+  const int ct = unit % CT, ot = (unit / CT) % OT, sl = unit / (CT * OT);
+  const int r0 = chunk * rchunk, r1 = min(total_rows, r0 + rchunk);
+  // (b, r) of this lane's first row, advanced incrementally by 2 per step
+  int m = r0 + h;
+  int b = m / rows, r = m - b * rows;
+  const float* dp = dpre + ot * 32 + li;
+  const float* xs = x + ct * 32 + li;
+  f32x16 acc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
+  float dbs = 0.f;
+  const bool do_db = sl == 0 && ct == 0;
+  const int b_last = (r1 - 1) / rows, r_last = (r1 - 1) - b_last * rows;
+  static_assert(NB == 8, "vm_wait_arr8");
+  for (int m0 = r0; m0 < r1; m0 += 2 * NB) {
+    // rows past the chunk are clamped to its last row (loads stay in
+    // bounds, no branches) and weighted 0.  Counted asm loads: the 8 idx
+    // and 8 dpre loads go out together, then the 8 dependent x gathers,
+    // one wait each (hipcc's own placement serialised them).
+    int srcrow[NB], bvs[NB];
+    float okf[NB], av[NB], bv[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const bool ok = m < r1;
+      okf[j] = ok ? 1.f : 0.f;
+      bvs[j] = (ok ? b : b_last) * vsrc;
+      gload1_async(srcrow[j], idx + (ok ? r : r_last) * kSeq + sl);
+      m += 2;
+      r += 2;
+      const bool wrap = r >= rows;
+      r = wrap ? r - rows : r;
+      b = wrap ? b + 1 : b;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) gload1f_async(av[j], dp + (long)min(m0 + h + 2 * j, r1 - 1) * COUT);
+    vm_wait_arr8<NB>(srcrow);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) gload1f_async(bv[j], xs + (long)(bvs[j] + srcrow[j]) * CIN);
+    vm_wait_arr8<NB>(av);
+    vm_wait_arr8<0>(bv);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      av[j] *= okf[j];
+      acc[j & 1] = mfma32(av[j], bv[j], acc[j & 1]);
+      dbs += av[j];
+    }
+  }
+  float* slab = ws + ((long)chunk * U + unit) * 1024;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) slab[acc_row(e, lane) * 32 + li] = acc[0][e] + acc[1][e];
+  if (do_db) {
+    dbs += __shfl_xor(dbs, 32);
+    if (h == 0) ws_db[(long)chunk * COUT + ot * 32 + li] = dbs;
+  }
+}
+
+// Batched weight-gradient reduction: ONE launch reduces the deferred slab
+// sets of several layers (each left in its own workspace by a deferred
+// cfsd_spiral_conv_bwd_weight / cfsd_spiral_conv_bwd call), instead of one
+// reduce launch per layer.  Item kinds: 0 = conv_dw_mfma slabs
+// ([nslab][U*1024] + db [nslab][COUT], mapped like conv_dw_reduce), 1 =
+// plain slabs [nslab][COUT*K + COUT] (small-channel kernels, fused xyz
+// backward).  Same fixed summation order as the per-layer reduces.
+struct DwRedItem {
+  const float* ws;
+  const float* ws_db;
+  float* dw;
+  float* db;
+  int kind, cin, cout, n_slabs, n_el, blk0;
+};
+constexpr int kMaxDwRed = 16;
+struct DwRedBatch {
+  DwRedItem it[kMaxDwRed];
+  int n;
+};
+
+__global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
+  int li = 0;
+  while (li + 1 < B.n && (int)blockIdx.x >= B.it[li + 1].blk0) ++li;
+  const DwRedItem d = B.it[li];
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int f = ((int)blockIdx.x - d.blk0) * 64 + lane;
+  const bool valid = f < d.n_el;
+  if (!valid) f = d.n_el - 1;
+  const int K = kSeq * d.cin;
+  const int nw = d.n_el - d.cout;  // kind 0: dW part of a slab
+  const float* src;
+  long stride;
+  if (d.kind == 0) {
+    src = f < nw ? d.ws + f : d.ws_db + (f - nw);
+    stride = f < nw ? nw : d.cout;
+  } else {
+    src = d.ws + f;
+    stride = d.n_el;
+  }
+  float sum = 0.f;
+#pragma unroll 4
+  for (int p = wv; p < d.n_slabs; p += 16) sum += src[(long)p * stride];
+  part[wv][lane] = sum;
+  __syncthreads();
+  if (wv == 0 && valid) {
+    float t = part[0][lane];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) t += part[q][lane];
+    if (f >= nw) {
+      d.db[f - nw] = t;
+    } else if (d.kind == 0) {
+      const int CT = d.cin / 32, OT = d.cout / 32;
+      const int un = f >> 10, within = f & 1023;
+      const int cc = (un % CT) * 32 + (within & 31);
+      const int o = ((un / CT) % OT) * 32 + (within >> 5);
+      const int sl = un / (CT * OT);
+      d.dw[(long)o * K + sl * d.cin + cc] = t;
+    } else {
+      d.dw[f] = t;
     }
   }
 }
@@ -1344,10 +1649,23 @@ static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const
   return launch_status("spiral_conv_fwd_combine");
 }
 
+// Rows below which the latency-shaped kernels (conv_fwd_lat / conv_dx_lat)
+// beat the persistent ones (fewer 32-row tiles than ~8 per CU).
+#ifndef CFSD_LAT_MAX_ROWS
+#define CFSD_LAT_MAX_ROWS 65536
+#endif
+
 template <int CIN, int COUT, int ACT>
 static int dispatch_fwd_mfma(const float* x, const int* idx, const float* w, const float* bias,
                              float* y, float* ws, size_t ws_floats, int vsrc, int rows, long M,
                              hipStream_t st) {
+  // (64 -> 32 excepted: measured slower there than slot groups + combine)
+  if (M < CFSD_LAT_MAX_ROWS && !(CIN == 64 && COUT == 32)) {
+    const long tasks = (M + 15) / 16 * (COUT / 16);
+    hipLaunchKernelGGL((conv_fwd_lat<CIN, COUT, ACT>), dim3((unsigned)((tasks + 3) / 4)), dim3(256),
+                       0, st, x, idx, w, bias, y, vsrc, rows, M);
+    return launch_status("spiral_conv_fwd_lat");
+  }
   constexpr bool big = (size_t)COUT * (kSeq * CIN + 8) * sizeof(float) > 80 * 1024;
   int spg = ws ? pick_spg(M, ws_floats, COUT) : 9;
   if (big && spg == 9) spg = 3;  // whole W does not fit LDS
@@ -1450,6 +1768,12 @@ static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* in
                             const int* inv_pair, const float* w, const float* elu_y, float* dx,
                             float* ws, size_t ws_floats, int vsrc, int rows, long M,
                             hipStream_t st) {
+  if (M < CFSD_LAT_MAX_ROWS) {
+    const long tasks = (M + 15) / 16 * (CIN / 16);
+    hipLaunchKernelGGL((conv_dx_lat<CIN, COUT>), dim3((unsigned)((tasks + 3) / 4)), dim3(256), 0, st,
+                       dpre, inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M);
+    return launch_status("spiral_conv_bwd_data_lat");
+  }
   constexpr bool big = (size_t)kSeq * CIN * (COUT + 4) * sizeof(float) > 80 * 1024;
   int spg = ws ? pick_spg(M, ws_floats, CIN) : 9;
   if (big && spg == 9) spg = 3;
@@ -1496,19 +1820,43 @@ extern "C" int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_p
 
 // ---- bwd weight: launch geometry shared by the workspace query and the launch
 namespace {
-enum DwKind { kDwMfma, kDwInMfma, kDwInSmall, kDwOutSmall, kDwNone };
+enum DwKind { kDwMfma, kDwLat, kDwInMfma, kDwInSmall, kDwOutSmall, kDwNone };
 struct DwGeom {
   DwKind kind;
-  int gx;
+  int gx;  // workgroups (= slabs), or row chunks for kDwLat
   size_t ws_floats;
+  int rchunk;
 };
 
 size_t dw_units(int cin, int cout) { return (size_t)kSeq * (cout / 32) * (cin / 32); }
 
+// Workgroups (= slabs) of a conv_dw_mfma launch: the geometry's gx capped at
+// one resident round.
+int dw_mfma_slabs(int cin, int cout, int gx) {
+  int cap = gx;
+#define CAP(CIN_, COUT_)                                                                         \
+  if (cin == CIN_ && cout == COUT_) {                                                            \
+    using C = DwCfg<CIN_, COUT_>;                                                                \
+    cap = resident_blocks_of(conv_dw_mfma<CIN_, COUT_>, C::THREADS, C::LDS_FLOATS * sizeof(float)); \
+  }
+  CAP(32, 32) CAP(32, 64) CAP(64, 32) CAP(64, 64)
+#undef CAP
+  return gx < cap ? gx : cap;
+}
+
 DwGeom dw_geom(int batch, int rows, int cin, int cout) {
-  DwGeom g{kDwNone, 0, 0};
+  DwGeom g{kDwNone, 0, 0, 0};
   const long M = (long)batch * rows;
-  if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64)) {
+  if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64) && M < CFSD_LAT_MAX_ROWS) {
+    // few rows: one wave per (dW unit, row chunk); ~2k waves
+    const long U = (long)dw_units(cin, cout);
+    long R = (M * U / 2048 + 15) / 16 * 16;
+    R = R < 32 ? 32 : (R > 512 ? 512 : R);
+    g.kind = kDwLat;
+    g.rchunk = (int)R;
+    g.gx = (int)((M + R - 1) / R);
+    g.ws_floats = (size_t)g.gx * U * 1024 + (size_t)g.gx * cout;
+  } else if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64)) {
     g.kind = kDwMfma;
     const long n_tiles = (M + 31) / 32;
     long gx = (n_tiles + 3) / 4;  // >= 4 tiles per block keeps the slab traffic bounded
@@ -1549,7 +1897,10 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
                                            int seq, int cin, int cout, void* stream) {
   int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
-  if (!dw || !db || !workspace) return set_error(CFSD_EINVAL, "null dw/db/workspace");
+  if (!workspace) return set_error(CFSD_EINVAL, "null workspace");
+  if ((dw == nullptr) != (db == nullptr))
+    return set_error(CFSD_EINVAL, "dw and db must both be set (or both NULL: deferred)");
+  const bool deferred = dw == nullptr;
   DwGeom g = dw_geom(batch, rows, cin, cout);
   if (g.kind == kDwNone)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight: unsupported channels %d -> %d", cin, cout);
@@ -1560,6 +1911,23 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
   const long M = (long)batch * rows;
   const int n_el = cout * kSeq * cin + cout;
   const dim3 rg((unsigned)((n_el + 63) / 64));
+  if (g.kind == kDwLat) {
+    float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
+    const long tasks = (long)g.gx * (long)dw_units(cin, cout);
+#define DWL(CIN_, COUT_)                                                                        \
+  if (cin == CIN_ && cout == COUT_) {                                                           \
+    hipLaunchKernelGGL((conv_dw_lat<CIN_, COUT_>), dim3((unsigned)((tasks + 3) / 4)), dim3(256), \
+                       0, st, x, idx, dpre, workspace, ws_db, vsrc, rows, (int)M, g.rchunk,      \
+                       g.gx);                                                                   \
+    rc = launch_status("spiral_conv_bwd_weight_lat");                                           \
+    if (rc || deferred) return rc;                                                              \
+    hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), rg, dim3(1024), 0, st, workspace, ws_db,  \
+                       dw, db, g.gx);                                                           \
+    return launch_status("spiral_conv_bwd_weight_reduce");                                      \
+  }
+    DWL(32, 32) DWL(32, 64) DWL(64, 32) DWL(64, 64)
+#undef DWL
+  }
   if (g.kind == kDwMfma) {
     float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
     int nslab = g.gx;
@@ -1567,12 +1935,11 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
   if (cin == CIN_ && cout == COUT_) {                                                           \
     using C = DwCfg<CIN_, COUT_>;                                                               \
     auto k = conv_dw_mfma<CIN_, COUT_>;                                                         \
-    const int cap = resident_blocks_of(k, C::THREADS, C::LDS_FLOATS * sizeof(float));           \
-    nslab = g.gx < cap ? g.gx : cap;                                                            \
+    nslab = dw_mfma_slabs(cin, cout, g.gx);                                                     \
     hipLaunchKernelGGL(k, dim3(nslab), dim3(C::THREADS), C::LDS_FLOATS * sizeof(float), st, x,  \
                        idx, dpre, workspace, ws_db, vsrc, rows, M);                             \
     rc = launch_status("spiral_conv_bwd_weight");                                               \
-    if (rc) return rc;                                                                          \
+    if (rc || deferred) return rc;                                                              \
     hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), rg, dim3(1024), 0, st, workspace, ws_db,  \
                        dw, db, nslab);                                                          \
     return launch_status("spiral_conv_bwd_weight_reduce");                                      \
@@ -1585,7 +1952,7 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
     hipLaunchKernelGGL((KERNEL<A_, B_>), dim3(g.gx), dim3(256), 0, st, x, idx, dpre, workspace,   \
                        vsrc, rows, M);                                                            \
     rc = launch_status("spiral_conv_bwd_weight_small");                                           \
-    if (rc) return rc;                                                                            \
+    if (rc || deferred) return rc;                                                                \
     hipLaunchKernelGGL(slab_reduce, rg, dim3(1024), 0, st, workspace, g.gx, n_el, dw,             \
                        cout * kSeq * cin, db);                                                    \
     return launch_status("spiral_conv_bwd_weight_small_reduce");                                  \
@@ -1631,8 +1998,10 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
                                     int cin, int cout, void* stream) {
   int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
-  if (!inv_ptr || !inv_row || !inv_pair || !w || !dw || !db || !workspace)
-    return set_error(CFSD_EINVAL, "spiral_conv_bwd: null inverse table / w / dw / db / workspace");
+  if (!inv_ptr || !inv_row || !inv_pair || !w || !workspace)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd: null inverse table / w / workspace");
+  if ((dw == nullptr) != (db == nullptr))
+    return set_error(CFSD_EINVAL, "dw and db must both be set (or both NULL: deferred)");
   const size_t need = cfsd_spiral_conv_bwd_workspace(batch, vsrc, rows, seq, cin, cout);
   if (workspace_bytes < need)
     return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
@@ -1655,7 +2024,7 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
                        inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, x, dx, workspace, vsrc, \
                        rows, Ms);                                                                \
     rc = launch_status("spiral_conv_bwd_small");                                                 \
-    if (rc) return rc;                                                                           \
+    if (rc || !dw) return rc;                                                                    \
     hipLaunchKernelGGL(slab_reduce, dim3((unsigned)((n_el + 63) / 64)), dim3(1024), 0, st,        \
                        workspace, gx, n_el, dw, cout * kSeq * cin, db);                          \
     return launch_status("spiral_conv_bwd_small_reduce");                                        \
@@ -1674,4 +2043,51 @@ extern "C" int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, 
   hipLaunchKernelGGL(spiral_gather_k, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, x, idx, g, vsrc, rows, seq, cin, chunks);
   return launch_status("spiral_gather");
+}
+
+extern "C" int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* stream) {
+  if (n <= 0) return CFSD_OK;
+  if (!items) return set_error(CFSD_EINVAL, "dw_reduce_batch: null items");
+  if (n > kMaxDwRed) return set_error(CFSD_EINVAL, "dw_reduce_batch: %d items > %d", n, kMaxDwRed);
+  DwRedBatch B{};
+  B.n = n;
+  int blk = 0;
+  for (int i = 0; i < n; ++i) {
+    const cfsd_dw_slabs& q = items[i];
+    if (!q.workspace || !q.dw || !q.db) return set_error(CFSD_EINVAL, "dw_reduce_batch: item %d null", i);
+    if (q.batch <= 0 || q.rows <= 0 || q.vsrc <= 0 || q.cin <= 0 || q.cout <= 0)
+      return set_error(CFSD_EINVAL, "dw_reduce_batch: item %d bad sizes", i);
+    DwRedItem& d = B.it[i];
+    d.ws = q.workspace;
+    d.ws_db = nullptr;
+    d.dw = q.dw;
+    d.db = q.db;
+    d.cin = q.cin;
+    d.cout = q.cout;
+    const int K = kSeq * q.cin;
+    if (q.fused && fused_small(q.cin, q.cout)) {
+      d.kind = 1;
+      d.n_slabs = fused_small_gx((long)q.batch * q.vsrc);
+      d.n_el = q.cout * K + q.cout;
+    } else {
+      const DwGeom g = dw_geom(q.batch, q.rows, q.cin, q.cout);
+      if (g.kind == kDwNone)
+        return set_error(CFSD_EINVAL, "dw_reduce_batch: item %d unsupported channels", i);
+      if (g.kind == kDwMfma || g.kind == kDwLat) {
+        const int U = (int)dw_units(q.cin, q.cout);
+        d.kind = 0;
+        d.n_slabs = g.kind == kDwLat ? g.gx : dw_mfma_slabs(q.cin, q.cout, g.gx);
+        d.n_el = U * 1024 + q.cout;
+        d.ws_db = q.workspace + (size_t)g.gx * U * 1024;
+      } else {
+        d.kind = 1;
+        d.n_slabs = g.gx;
+        d.n_el = q.cout * K + q.cout;
+      }
+    }
+    d.blk0 = blk;
+    blk += (d.n_el + 63) / 64;
+  }
+  hipLaunchKernelGGL(dw_reduce_batch_k, dim3(blk), dim3(1024), 0, (hipStream_t)stream, B);
+  return launch_status("dw_reduce_batch");
 }

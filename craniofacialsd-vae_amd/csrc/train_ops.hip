@@ -547,7 +547,7 @@ __device__ __forceinline__ uint32_t mix32(uint64_t x) {
 __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
                              float* __restrict__ eps, int n_eps, int* __restrict__ key,
                              int n_regions, int* __restrict__ batch_idx, int bs, int n_batches,
-                             const int* __restrict__ perm) {
+                             const int* __restrict__ perm, int* __restrict__ adam_step) {
   __shared__ int t_sh;
   if (threadIdx.x == 0) {
     t_sh = *counter + 1;
@@ -572,7 +572,10 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) *counter = t;
+  if (threadIdx.x == 0) {
+    *counter = t;
+    if (adam_step) *adam_step += 1;
+  }
 }
 
 }  // namespace cfsd
@@ -724,12 +727,13 @@ extern "C" int cfsd_adam(float* param, const float* grad, float* m, float* v,
 
 extern "C" int cfsd_step_begin(int32_t* counter, unsigned long long seed, float* eps, int n_eps,
                                int32_t* key, int n_regions, int32_t* batch_idx, int bs,
-                               int n_batches, const int32_t* perm, void* stream) {
+                               int n_batches, const int32_t* perm, int32_t* adam_step,
+                               void* stream) {
   if (!counter) return set_error(CFSD_EINVAL, "step_begin: null counter");
   if (key && n_regions <= 0) return set_error(CFSD_EINVAL, "step_begin: n_regions");
   if (batch_idx && (bs <= 0 || bs > 256 || n_batches <= 0))
     return set_error(CFSD_EINVAL, "step_begin: bs/n_batches");
   hipLaunchKernelGGL(step_begin_k, dim3(1), dim3(256), 0, (hipStream_t)stream, counter, seed, eps,
-                     n_eps, key, n_regions, batch_idx, bs, n_batches, perm);
+                     n_eps, key, n_regions, batch_idx, bs, n_batches, perm, adam_step);
   return launch_status("step_begin");
 }

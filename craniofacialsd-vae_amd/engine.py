@@ -240,6 +240,24 @@ class SDVAEEngine:
         ws = max(ws, ops.spiral_conv_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
         ws = max(ws, ops.spiral_conv_bwd_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
         b.ws = torch.empty(ws // 4 + 64, dtype=torch.float32, device=dev)
+        # weight-gradient partials: one region per layer, all reduced by ONE
+        # cfsd_dw_reduce_batch launch at the end of the backward
+        regions = [("out", ops.spiral_conv_bwd_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0],
+                                                         S.in_ch))]
+        for i, (cin, cout, lv, _) in enumerate(S.dec_layers()):
+            regions.append((("dec", i), ops.spiral_conv_bwd_weight_workspace(bsz, nv[lv], T.seq[lv],
+                                                                             cin, cout)))
+        for (cin, cout, lv) in S.enc_layers():
+            rows = nv[lv + 1] if T.enc_select[lv] else nv[lv]
+            regions.append((("enc", lv), ops.spiral_conv_bwd_weight_workspace(bsz, rows, T.seq[lv],
+                                                                              cin, cout)))
+        total = sum((nb // 4 + 64) // 64 * 64 for _, nb in regions)
+        b.ws_dw_all = torch.empty(total, dtype=torch.float32, device=dev)
+        b.ws_dw, off = {}, 0
+        for key, nb in regions:
+            n = (nb // 4 + 64) // 64 * 64
+            b.ws_dw[key] = b.ws_dw_all[off:off + n]
+            off += n
         flat_in = self.num_vert * S.out_ch[-1]
         nmu = lat * (2 if S.is_vae else 1)
         lws = max(ops.linear_workspace(bsz, flat_in, nmu), ops.linear_workspace(bsz, lat, flat_in))
@@ -343,19 +361,24 @@ class SDVAEEngine:
         ops.recon_lap_bwd(b.out, b.x, b.unit, T.lapT_csr, b.dout, 1.0, self.w_lap)
         # final SpiralConv (no activation): dpre = dout
         last_in = b.dec_out[-1]
-        # dX and dW/db of the output conv in one source-row pass
-        ops.spiral_conv_bwd(last_in, T.spiral[0], b.dout, T.spiral_inv[0],
-                            P.view(f"de_layers.{n + 1}.layer.weight"),
-                            P.gview(f"de_layers.{n + 1}.layer.weight"),
-                            P.gview(f"de_layers.{n + 1}.layer.bias"),
-                            dx=b.dpre_dec[-1], elu_y=last_in, workspace=b.ws)
+        # dX and dW/db of the output conv in one source-row pass.  Every conv
+        # weight gradient is deferred (partials left in b.ws_dw[...]) and all
+        # of them are reduced by one launch at the end.
+        deferred = []
+
+        def defer(d, name):
+            deferred.append((d, P.gview(name + ".weight"), P.gview(name + ".bias")))
+
+        _, d = ops.spiral_conv_bwd(last_in, T.spiral[0], b.dout, T.spiral_inv[0],
+                                   P.view(f"de_layers.{n + 1}.layer.weight"), None, None,
+                                   dx=b.dpre_dec[-1], elu_y=last_in, workspace=b.ws_dw["out"])
+        defer(d, f"de_layers.{n + 1}.layer")
         dec = S.dec_layers()
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]
             w, _ = self._dec_w(i)
-            ops.spiral_conv_bwd_weight(b.dec_up[i], T.spiral[lv], b.dpre_dec[i],
-                                       P.gview(f"de_layers.{i + 1}.conv.layer.weight"),
-                                       P.gview(f"de_layers.{i + 1}.conv.layer.bias"), b.ws)
+            defer(ops.spiral_conv_bwd_weight(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
+                                             b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
             ops.spiral_conv_bwd_data(b.dpre_dec[i], T.spiral_inv[lv], w, T.n_verts[lv],
                                      out=b.g_dec_up[i], workspace=b.ws)
             if i > 0:  # through Pool(up) into the previous Deblock's ELU
@@ -386,9 +409,8 @@ class SDVAEEngine:
             w, _ = self._enc_w(lv)
             x_in = b.x if lv == 0 else b.enc_out[lv - 1]
             rows_tab = T.enc_rows[lv]
-            ops.spiral_conv_bwd_weight(x_in, rows_tab, b.dpre_enc[lv],
-                                       P.gview(f"en_layers.{lv}.conv.layer.weight"),
-                                       P.gview(f"en_layers.{lv}.conv.layer.bias"), b.ws)
+            defer(ops.spiral_conv_bwd_weight(x_in, rows_tab, b.dpre_enc[lv], None, None,
+                                             b.ws_dw[("enc", lv)]), f"en_layers.{lv}.conv.layer")
             if lv == 0:
                 break
             prev = lv - 1
@@ -401,6 +423,7 @@ class SDVAEEngine:
                                          out=b.g_pooled[prev], workspace=b.ws)
                 ops.spmm(T.downT_csr[prev], b.g_pooled[prev], T.n_verts[prev], elu_y=b.enc_full[prev],
                          out=b.dpre_enc[prev])
+        ops.dw_reduce_batch(deferred)
 
     def adam_step(self):
         P = self.params
@@ -422,13 +445,15 @@ class SDVAEEngine:
             b.eps.copy_(eps)
         return b
 
-    def train_step_on(self, b, acc=None, grad_hook=None):
-        """forward + losses + backward + (grad_hook, e.g. all-reduce) + Adam."""
+    def train_step_on(self, b, acc=None, grad_hook=None, advance=True):
+        """forward + losses + backward + (grad_hook, e.g. all-reduce) + Adam.
+        ``advance=False`` when cfsd_step_begin already advanced Adam's t."""
         self.forward(b, train=True, acc=acc)
         self.backward(b)
         if grad_hook is not None:
             grad_hook(self.params.grad)
-        self.advance_step()
+        if advance:
+            self.advance_step()
         self.adam_step()
 
     def resident_step(self, b, dataset, perm, n_batches, acc=None, grad_hook=None):
@@ -438,9 +463,9 @@ class SDVAEEngine:
         T = self.topo
         ops.step_begin(self._step_counter(b), self.seed, eps=b.eps, key=b.key,
                        n_regions=max(T.n_regions, 1), batch_idx=b.batch_idx, bs=self.swap_bs,
-                       n_batches=n_batches, perm=perm)
+                       n_batches=n_batches, perm=perm, adam_step=self.params.step)
         ops.swap_features(dataset, b.batch_idx, T.region_mask, b.key, self.swap_bs, out=b.x)
-        self.train_step_on(b, acc=acc, grad_hook=grad_hook)
+        self.train_step_on(b, acc=acc, grad_hook=grad_hook, advance=False)
 
     def _step_counter(self, b):
         if not hasattr(b, "counter"):

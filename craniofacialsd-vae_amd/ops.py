@@ -95,14 +95,18 @@ def spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout):
 
 
 def spiral_conv_bwd_weight(x, idx, dpre, dw, db, workspace):
+    """dW/db of one SpiralConv.  With ``dw is db is None`` the reduction is
+    deferred: the partials stay in ``workspace`` and a DeferredDw descriptor
+    is returned for ``dw_reduce_batch`` (which must get the real dw/db)."""
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape
     cout = dpre.shape[2]
     _need(x, None, name="x")
     _need(idx, (rows, seq), torch.int32, "idx")
     _need(dpre, (bsz, rows, cout), name="dpre")
-    _need(dw, (cout, seq * cin), name="dw")
-    _need(db, (cout,), name="db")
+    if dw is not None or db is not None:
+        _need(dw, (cout, seq * cin), name="dw")
+        _need(db, (cout,), name="db")
     _need(workspace, None, name="workspace")
     need = spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout)
     nbytes = workspace.numel() * workspace.element_size()
@@ -110,6 +114,31 @@ def spiral_conv_bwd_weight(x, idx, dpre, dw, db, workspace):
         raise ValueError(f"workspace {nbytes} < {need} bytes")
     call("cfsd_spiral_conv_bwd_weight", ptr(x), ptr(idx), ptr(dpre), ptr(dw), ptr(db),
          ptr(workspace), ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    if dw is None:
+        return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, False)
+    return None
+
+
+class DeferredDw:
+    """Slab set left by a deferred weight-gradient call (see dw_reduce_batch)."""
+
+    def __init__(self, workspace, batch, vsrc, rows, cin, cout, fused):
+        self.workspace = workspace
+        self.sizes = (batch, vsrc, rows, cin, cout, int(fused))
+
+    def desc(self, dw, db):
+        _need(dw, (self.sizes[4], 9 * self.sizes[3]), name="dw")
+        _need(db, (self.sizes[4],), name="db")
+        return _abi.DwSlabs(self.workspace.data_ptr(), dw.data_ptr(), db.data_ptr(), *self.sizes)
+
+
+def dw_reduce_batch(items):
+    """Reduce several deferred weight gradients in ONE launch.
+    ``items``: list of (DeferredDw, dw, db)."""
+    if not items:
+        return
+    arr = (_abi.DwSlabs * len(items))(*[d.desc(dw, db) for d, dw, db in items])
+    call("cfsd_dw_reduce_batch", arr, len(items), stream_ptr())
 
 
 def spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout):
@@ -130,8 +159,9 @@ def spiral_conv_bwd(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace
     _need(inv_row, (rows * seq,), torch.int32, "inv_row")
     _need(inv_pair, (vsrc * seq, 2), torch.int32, "inv_pair")
     _need(w, (cout, seq * cin), name="w")
-    _need(dw, (cout, seq * cin), name="dw")
-    _need(db, (cout,), name="db")
+    if dw is not None or db is not None:
+        _need(dw, (cout, seq * cin), name="dw")
+        _need(db, (cout,), name="db")
     if dx is not None:
         _need(dx, (bsz, vsrc, cin), name="dx")
     if elu_y is not None:
@@ -140,6 +170,8 @@ def spiral_conv_bwd(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace
     call("cfsd_spiral_conv_bwd", ptr(x), ptr(idx), ptr(dpre), ptr(inv_ptr), ptr(inv_row),
          ptr(inv_pair), ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb),
          bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    if dw is None:  # deferred weight gradient
+        return dx, DeferredDw(ws, bsz, vsrc, rows, cin, cout, True)
     return dx
 
 
@@ -312,11 +344,13 @@ def adam(param, grad, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_d
 
 
 def step_begin(counter, seed, eps=None, key=None, n_regions=0, batch_idx=None, bs=0,
-               n_batches=0, perm=None):
+               n_batches=0, perm=None, adam_step=None):
     _need(counter, (1,), torch.int32, "counter")
+    if adam_step is not None:
+        _need(adam_step, (1,), torch.int32, "adam_step")
     call("cfsd_step_begin", ptr(counter), ctypes.c_ulonglong(seed), ptr(eps),
          eps.numel() if eps is not None else 0, ptr(key), n_regions, ptr(batch_idx), bs,
-         n_batches, ptr(perm), stream_ptr())
+         n_batches, ptr(perm), ptr(adam_step), stream_ptr())
 
 
 def scale(y, alpha):

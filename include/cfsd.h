@@ -82,6 +82,20 @@ int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, const float*
                                 int vsrc, int rows, int seq, int cin, int cout, void* stream);
 size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int seq, int cin, int cout);
 
+/* Deferred weight gradients.  cfsd_spiral_conv_bwd_weight / cfsd_spiral_conv_bwd
+ * called with dw == db == NULL leave their per-workgroup partial sums in
+ * `workspace` and skip the reduction; cfsd_dw_reduce_batch then reduces up
+ * to 16 such layers (each with its own workspace) in ONE launch, with the
+ * same fixed summation order (identical results).  `fused` = the partials
+ * came from cfsd_spiral_conv_bwd on a small-output layer (cout*seq <= 32). */
+typedef struct {
+  const float* workspace;
+  float* dw;
+  float* db;
+  int batch, vsrc, rows, cin, cout, fused;
+} cfsd_dw_slabs;
+int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* stream);
+
 /* Fused backward of one SpiralConv (model.py:27-41 autograd, dX and dW/db of
  * the same layer in one call): dx exactly as cfsd_spiral_conv_bwd_data
  * (skipped when dx == NULL, e.g. the first layer), dw/db exactly as
@@ -194,10 +208,12 @@ int cfsd_adam(float* param, const float* grad, float* m, float* v, const int32_t
  * swap_batch_transform.py:26); eps[n_eps] ~ N(0,1) (replaces randn_like,
  * model.py:187); batch_idx[q] = perm[((t-1) % n_batches)*bs + q] (or the
  * identity when perm == NULL) — the shuffled, drop_last batch order of
- * MeshLoader (data_loading.py:40-42).  Any of eps/key/batch_idx may be NULL. */
+ * MeshLoader (data_loading.py:40-42); ++*adam_step (the Adam bias-correction
+ * step of this iteration, so the step needs no separate launch for it).
+ * Any of eps/key/batch_idx/adam_step may be NULL. */
 int cfsd_step_begin(int32_t* counter, unsigned long long seed, float* eps, int n_eps,
                     int32_t* key, int n_regions, int32_t* batch_idx, int bs, int n_batches,
-                    const int32_t* perm, void* stream);
+                    const int32_t* perm, int32_t* adam_step, void* stream);
 
 /* F.elu backward written from the ELU output (model.py:68,84 autograd):
  * dx = dy * (y > 0 ? 1 : y + 1).  dx may alias dy. */

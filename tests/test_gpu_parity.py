@@ -389,3 +389,40 @@ def test_graph_replay_matches_eager(dtopo):
         res.append((eng.params.data.cpu().clone(), b.losses.cpu().clone()))
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
+
+
+def test_deferred_weight_grads_batch_reduce(otopo, dtopo):
+    """Deferred dW (partials left in per-layer workspaces) reduced by ONE
+    cfsd_dw_reduce_batch launch == the per-layer reductions, bit for bit
+    (same fixed summation order); covers MFMA, 3-channel and fused kinds."""
+    g = torch.Generator().manual_seed(21)
+    cases = [(32, 32, 0, 4, otopo.spirals[0]), (64, 64, 2, 3, otopo.spirals[2]),
+             (3, 32, 1, 2, otopo.spirals[1]), (32, 3, 1, 2, otopo.spirals[1])]
+    items, refs = [], []
+    for cin, cout, level, bsz, sp in cases:
+        v = sp.shape[0]
+        x = torch.randn(bsz, v, cin, generator=g).to(DEV)
+        dpre = torch.randn(bsz, v, cout, generator=g).to(DEV)
+        nb = ops.spiral_conv_bwd_weight_workspace(bsz, v, 9, cin, cout)
+        dw, db = torch.empty(cout, 9 * cin, device=DEV), torch.empty(cout, device=DEV)
+        ops.spiral_conv_bwd_weight(x, dtopo.spiral[level], dpre, dw, db,
+                                   torch.empty(nb // 4 + 1, device=DEV))
+        refs.append((dw, db))
+        d = ops.spiral_conv_bwd_weight(x, dtopo.spiral[level], dpre, None, None,
+                                       torch.empty(nb // 4 + 1, device=DEV))
+        items.append((d, torch.full_like(dw, float("nan")), torch.full_like(db, float("nan"))))
+    # fused xyz-output backward, deferred
+    sp = otopo.spirals[0]
+    x = torch.randn(2, sp.shape[0], 32, generator=g).to(DEV)
+    dpre = torch.randn(2, sp.shape[0], 3, generator=g).to(DEV)
+    w = torch.randn(3, 288, generator=g).to(DEV)
+    dw, db = torch.empty(3, 288, device=DEV), torch.empty(3, device=DEV)
+    ops.spiral_conv_bwd(x, dtopo.spiral[0], dpre, dtopo.spiral_inv[0], w, dw, db)
+    refs.append((dw, db))
+    _, d = ops.spiral_conv_bwd(x, dtopo.spiral[0], dpre, dtopo.spiral_inv[0], w, None, None,
+                               workspace=torch.empty(ops.spiral_conv_bwd_workspace(2, sp.shape[0], sp.shape[0], 9, 32, 3) // 4 + 1, device=DEV))
+    items.append((d, torch.full_like(dw, float("nan")), torch.full_like(db, float("nan"))))
+    ops.dw_reduce_batch(items)
+    torch.cuda.synchronize()
+    for (d, dw, db), (rw, rb) in zip(items, refs):
+        assert torch.equal(dw, rw) and torch.equal(db, rb)

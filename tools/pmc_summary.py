@@ -6,7 +6,7 @@ import sys
 
 d = sys.argv[1]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
+for f in sorted(glob.glob(f"{d}/p*/**/*counter_collection.csv", recursive=True)):
     for row in csv.DictReader(open(f)):
         k = row["Kernel_Name"][:60]
         acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))

@@ -1574,22 +1574,53 @@ __global__ __launch_bounds__(1024) void slab_reduce(const float* __restrict__ ws
   }
 }
 
-// Materialising gather (HBM roofline probe): g[m, s*cin + c] = x[b, idx[r,s], c].
-// One thread per 16-B chunk of the output.
+// Materialising gather (HBM roofline probe): g[b, r, s*cin + c] = x[b, idx[r,s], c].
+// blockIdx.y = mesh b; a block covers GU*256 consecutive 16-B output chunks
+// of that mesh (thread i: chunks i, i+256, ...), so every store instruction
+// is 4 KB contiguous per wave-pair and all GU loads are in flight before the
+// first store.  Index math is 32-bit with compile-time divisors (C4 chunks
+// per neighbour row, kSeq slots): the 64-bit divisions of a flat index cost
+// more VALU time than the store stream itself.  Output stores are
+// non-temporal (write-once stream, no L2 allocation).
+constexpr int GU = 4;
+template <int C4>
 __global__ __launch_bounds__(256) void spiral_gather_k(const float* __restrict__ x,
                                                        const int* __restrict__ idx,
-                                                       float* __restrict__ g, int vsrc, int rows,
-                                                       int seq, int cin, long total_chunks) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= total_chunks) return;
-  const int c4 = cin / 4;
-  const int q = (int)(t % c4);
-  const long rs = t / c4;
-  const int s = (int)(rs % seq);
-  const long m = rs / seq;
-  const int b = (int)(m / rows), r = (int)(m % rows);
-  const float* src = x + ((long)b * vsrc + idx[(long)r * seq + s]) * cin + 4 * q;
-  st4(g + t * 4, ld4(src));
+                                                       float* __restrict__ g, int vsrc,
+                                                       int per_mesh) {
+  const int b = blockIdx.y;
+  const float* xb = x + (long)b * vsrc * (4 * C4);
+  f32x4* gb = reinterpret_cast<f32x4*>(g) + (long)b * per_mesh;
+  const int t0 = blockIdx.x * (256 * GU) + threadIdx.x;
+  int src[GU];
+#pragma unroll
+  for (int u = 0; u < GU; ++u) {
+    const int t = min(t0 + u * 256, per_mesh - 1);
+    src[u] = idx[t / C4];  // (r*kSeq + s) = t / C4: idx is [rows, kSeq] row-major
+  }
+  f32x4 v[GU];
+#pragma unroll
+  for (int u = 0; u < GU; ++u) {
+    const int t = t0 + u * 256;
+    v[u] = ld4(xb + (long)src[u] * (4 * C4) + 4 * (t % C4));
+  }
+#pragma unroll
+  for (int u = 0; u < GU; ++u) {
+    const int t = t0 + u * 256;
+    if (t < per_mesh) __builtin_nontemporal_store(v[u], gb + t);
+  }
+}
+
+// Any other channel count: one thread per chunk, runtime divisors (32-bit).
+__global__ __launch_bounds__(256) void spiral_gather_any_k(const float* __restrict__ x,
+                                                           const int* __restrict__ idx,
+                                                           float* __restrict__ g, int vsrc,
+                                                           int c4, int per_mesh) {
+  const int b = blockIdx.y;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= per_mesh) return;
+  const int src = idx[t / c4];
+  st4(g + ((long)b * per_mesh + t) * 4, ld4(x + ((long)b * vsrc + src) * (4 * c4) + 4 * (t % c4)));
 }
 
 }  // namespace cfsd
@@ -1654,13 +1685,22 @@ static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const
 #ifndef CFSD_LAT_MAX_ROWS
 #define CFSD_LAT_MAX_ROWS 65536
 #endif
+#ifndef CFSD_LAT_FWD_MAX
+#define CFSD_LAT_FWD_MAX CFSD_LAT_MAX_ROWS
+#endif
+#ifndef CFSD_LAT_DX_MAX
+#define CFSD_LAT_DX_MAX 80000  // measured: also the 68k-row D2 / E1 dx
+#endif
+#ifndef CFSD_LAT_DW_MAX
+#define CFSD_LAT_DW_MAX CFSD_LAT_MAX_ROWS
+#endif
 
 template <int CIN, int COUT, int ACT>
 static int dispatch_fwd_mfma(const float* x, const int* idx, const float* w, const float* bias,
                              float* y, float* ws, size_t ws_floats, int vsrc, int rows, long M,
                              hipStream_t st) {
   // (64 -> 32 excepted: measured slower there than slot groups + combine)
-  if (M < CFSD_LAT_MAX_ROWS && !(CIN == 64 && COUT == 32)) {
+  if (M < CFSD_LAT_FWD_MAX && !(CIN == 64 && COUT == 32)) {
     const long tasks = (M + 15) / 16 * (COUT / 16);
     hipLaunchKernelGGL((conv_fwd_lat<CIN, COUT, ACT>), dim3((unsigned)((tasks + 3) / 4)), dim3(256),
                        0, st, x, idx, w, bias, y, vsrc, rows, M);
@@ -1768,7 +1808,7 @@ static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* in
                             const int* inv_pair, const float* w, const float* elu_y, float* dx,
                             float* ws, size_t ws_floats, int vsrc, int rows, long M,
                             hipStream_t st) {
-  if (M < CFSD_LAT_MAX_ROWS) {
+  if (M < CFSD_LAT_DX_MAX) {
     const long tasks = (M + 15) / 16 * (CIN / 16);
     hipLaunchKernelGGL((conv_dx_lat<CIN, COUT>), dim3((unsigned)((tasks + 3) / 4)), dim3(256), 0, st,
                        dpre, inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M);
@@ -1847,7 +1887,7 @@ int dw_mfma_slabs(int cin, int cout, int gx) {
 DwGeom dw_geom(int batch, int rows, int cin, int cout) {
   DwGeom g{kDwNone, 0, 0, 0};
   const long M = (long)batch * rows;
-  if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64) && M < CFSD_LAT_MAX_ROWS) {
+  if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64) && M < CFSD_LAT_DW_MAX) {
     // few rows: one wave per (dW unit, row chunk); ~2k waves
     const long U = (long)dw_units(cin, cout);
     long R = (M * U / 2048 + 15) / 16 * 16;
@@ -2039,9 +2079,19 @@ extern "C" int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, 
   if (!x || !idx || !g) return set_error(CFSD_EINVAL, "spiral_gather: null pointer");
   if (batch <= 0 || vsrc <= 0 || rows <= 0 || seq <= 0 || cin <= 0 || (cin % 4))
     return set_error(CFSD_EINVAL, "spiral_gather: bad sizes");
-  const long chunks = (long)batch * rows * seq * (cin / 4);
-  hipLaunchKernelGGL(spiral_gather_k, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, x, idx, g, vsrc, rows, seq, cin, chunks);
+  const long per_mesh = (long)rows * seq * (cin / 4);
+  if (per_mesh >= (1L << 31) || batch > 65535)
+    return set_error(CFSD_EINVAL, "spiral_gather: %ld chunks per mesh / batch %d too large", per_mesh, batch);
+  const hipStream_t st = (hipStream_t)stream;
+  const int pm = (int)per_mesh;
+  if (cin == 32 || cin == 64) {
+    const dim3 grid((unsigned)((per_mesh + 256 * GU - 1) / (256 * GU)), (unsigned)batch);
+    if (cin == 32) hipLaunchKernelGGL(spiral_gather_k<8>, grid, dim3(256), 0, st, x, idx, g, vsrc, pm);
+    else hipLaunchKernelGGL(spiral_gather_k<16>, grid, dim3(256), 0, st, x, idx, g, vsrc, pm);
+  } else {
+    hipLaunchKernelGGL(spiral_gather_any_k, dim3((unsigned)((per_mesh + 255) / 256), (unsigned)batch),
+                       dim3(256), 0, st, x, idx, g, vsrc, cin / 4, pm);
+  }
   return launch_status("spiral_gather");
 }
 

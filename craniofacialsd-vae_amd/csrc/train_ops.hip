@@ -69,33 +69,64 @@ __device__ __forceinline__ float2 block_sum2(float a, float b, float2* sh) {
 }
 
 // ----------------------------------------------------------- recon + Laplacian
-// Pass 1, one thread per (b, v).  C <= 4.
+// Sparse row dot products of the Laplacian passes: entries in chunks of 8
+// whose column/value loads, then whose C-wide row loads, are issued together
+// (2 memory round trips per chunk instead of 2 per entry); past-the-end
+// entries are clamped to the row's last one and weighted 0.
+template <int C>
+__device__ __forceinline__ void lap_row_dot(int beg, int end, const int* __restrict__ col,
+                                            const float* __restrict__ val,
+                                            const float* __restrict__ xb, float (&acc)[C]) {
+  constexpr int CK = 8;
+  for (int e0 = beg; e0 < end; e0 += CK) {
+    int cc[CK];
+    float w[CK];
+#pragma unroll
+    for (int j = 0; j < CK; ++j) {
+      const int e = e0 + j < end ? e0 + j : end - 1;
+      cc[j] = col[e];
+      w[j] = e0 + j < end ? val[e] : 0.f;
+    }
+    float xv[CK][C];
+#pragma unroll
+    for (int j = 0; j < CK; ++j)
+#pragma unroll
+      for (int q = 0; q < C; ++q) xv[j][q] = xb[(long)cc[j] * C + q];
+#pragma unroll
+    for (int j = 0; j < CK; ++j)
+#pragma unroll
+      for (int q = 0; q < C; ++q) acc[q] = fmaf(w[j], xv[j][q], acc[q]);
+  }
+}
+
+// Pass 1, one thread per (b, v): squared error, L.pred row, its norm and
+// unit vector.  C <= 4.
+template <int C>
 __global__ __launch_bounds__(kLapThreads) void recon_lap_fwd_k(
     const float* __restrict__ pred, const float* __restrict__ gt, const int* __restrict__ l_ptr,
     const int* __restrict__ l_col, const float* __restrict__ l_val, float* __restrict__ unit,
-    float* __restrict__ partials, int nv, int c, long total) {
+    float* __restrict__ partials, int nv, long total) {
   __shared__ float2 sh[kLapThreads / 64];
-  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   float sq = 0.f, nrm = 0.f;
   if (t < total) {
     const int v = (int)(t % nv);
     const long b = t / nv;
-    const float* pb = pred + b * nv * c;
-    float lx[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int e = l_ptr[v]; e < l_ptr[v + 1]; ++e) {
-      const float w = l_val[e];
-      const float* p = pb + (long)l_col[e] * c;
-      for (int q = 0; q < c; ++q) lx[q] = fmaf(w, p[q], lx[q]);
-    }
+    float lx[C];
+#pragma unroll
+    for (int q = 0; q < C; ++q) lx[q] = 0.f;
+    lap_row_dot<C>(l_ptr[v], l_ptr[v + 1], l_col, l_val, pred + b * nv * C, lx);
     float n2 = 0.f;
-    for (int q = 0; q < c; ++q) {
-      float d = pred[t * c + q] - gt[t * c + q];
+#pragma unroll
+    for (int q = 0; q < C; ++q) {
+      const float d = pred[t * C + q] - gt[t * C + q];
       sq = fmaf(d, d, sq);
       n2 = fmaf(lx[q], lx[q], n2);
     }
     nrm = sqrtf(n2);
     const float inv = nrm > 0.f ? 1.f / nrm : 0.f;
-    for (int q = 0; q < c; ++q) unit[t * c + q] = lx[q] * inv;
+#pragma unroll
+    for (int q = 0; q < C; ++q) unit[t * C + q] = lx[q] * inv;
   }
   float2 r = block_sum2(sq, nrm, sh);
   if (threadIdx.x == 0) {
@@ -104,25 +135,61 @@ __global__ __launch_bounds__(kLapThreads) void recon_lap_fwd_k(
   }
 }
 
-// Pass 2, one thread per (b, u): d/dpred of w_rec*mse + w_lap*lap.
+// Loss finalisation: total = rec + w_kl*kl + w_lc*lc + w_lap*lap from the
+// recon/Laplacian block partials and the latent terms (one workgroup).
+struct LossFinalize {
+  const float* partials;
+  int nblocks;
+  const float* terms;
+  float* out;
+  float* acc;
+  float inv_n_rec, inv_lap, w_kl, w_lc, w_lap;
+};
+
+__device__ void loss_finalize_block(const LossFinalize& f, float2* sh) {
+  float a = 0.f, b = 0.f;
+  for (int i = threadIdx.x; i < f.nblocks; i += blockDim.x) {
+    a += f.partials[2 * i];
+    b += f.partials[2 * i + 1];
+  }
+  float2 r = block_sum2(a, b, sh);
+  if (threadIdx.x == 0) {
+    const float rec = r.x * f.inv_n_rec, lap = r.y * f.inv_lap;
+    const float kl = f.terms[0], lc = f.terms[1];
+    const float tot = rec + f.w_kl * kl + f.w_lc * lc + f.w_lap * lap;
+    const float v[5] = {rec, kl, lc, lap, tot};
+    for (int q = 0; q < 5; ++q) {
+      f.out[q] = v[q];
+      if (f.acc) f.acc[q] += v[q];
+    }
+    if (f.acc) f.acc[5] += 1.f;
+  }
+}
+
+// Pass 2, one thread per (b, u): d/dpred of w_rec*mse + w_lap*lap.  With
+// fin.partials set, the LAST block also finalises the losses of pass 1
+// (complete: pass 1 is the previous launch on the stream), saving a launch.
+template <int C>
 __global__ __launch_bounds__(256) void recon_lap_bwd_k(
     const float* __restrict__ pred, const float* __restrict__ gt, const float* __restrict__ unit,
     const int* __restrict__ lt_ptr, const int* __restrict__ lt_col,
-    const float* __restrict__ lt_val, float* __restrict__ dpred, int nv, int c, long total,
-    float k_rec, float k_lap) {
-  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const float* __restrict__ lt_val, float* __restrict__ dpred, int nv, long total, float k_rec,
+    float k_lap, const LossFinalize fin) {
+  if (fin.partials && blockIdx.x == gridDim.x - 1) {
+    __shared__ float2 sh[4];
+    loss_finalize_block(fin, sh);
+  }
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int u = (int)(t % nv);
   const long b = t / nv;
-  const float* ub = unit + b * nv * c;
-  float g[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int e = lt_ptr[u]; e < lt_ptr[u + 1]; ++e) {
-    const float w = lt_val[e];
-    const float* p = ub + (long)lt_col[e] * c;
-    for (int q = 0; q < c; ++q) g[q] = fmaf(w, p[q], g[q]);
-  }
-  for (int q = 0; q < c; ++q)
-    dpred[t * c + q] = k_rec * (pred[t * c + q] - gt[t * c + q]) + k_lap * g[q];
+  float g[C];
+#pragma unroll
+  for (int q = 0; q < C; ++q) g[q] = 0.f;
+  lap_row_dot<C>(lt_ptr[u], lt_ptr[u + 1], lt_col, lt_val, unit + b * nv * C, g);
+#pragma unroll
+  for (int q = 0; q < C; ++q)
+    dpred[t * C + q] = k_rec * (pred[t * C + q] - gt[t * C + q]) + k_lap * g[q];
 }
 
 // ----------------------------------------------------------- latent head
@@ -265,28 +332,9 @@ __global__ __launch_bounds__(256) void latent_bwd_k(const float* __restrict__ mu
   }
 }
 
-__global__ void loss_finalize_k(const float* __restrict__ partials, int nblocks,
-                                const float* __restrict__ terms, float* __restrict__ out,
-                                float* __restrict__ acc, float inv_n_rec, float inv_lap,
-                                float w_kl, float w_lc, float w_lap) {
+__global__ __launch_bounds__(256) void loss_finalize_k(const LossFinalize f) {
   __shared__ float2 sh[4];
-  float a = 0.f, b = 0.f;
-  for (int i = threadIdx.x; i < nblocks; i += blockDim.x) {
-    a += partials[2 * i];
-    b += partials[2 * i + 1];
-  }
-  float2 r = block_sum2(a, b, sh);
-  if (threadIdx.x == 0) {
-    const float rec = r.x * inv_n_rec, lap = r.y * inv_lap;
-    const float kl = terms[0], lc = terms[1];
-    const float tot = rec + w_kl * kl + w_lc * lc + w_lap * lap;
-    const float v[5] = {rec, kl, lc, lap, tot};
-    for (int q = 0; q < 5; ++q) {
-      out[q] = v[q];
-      if (acc) acc[q] += v[q];
-    }
-    if (acc) acc[5] += 1.f;
-  }
+  loss_finalize_block(f, sh);
 }
 
 // ----------------------------------------------------------- dense Linear
@@ -597,9 +645,15 @@ extern "C" int cfsd_recon_lap_fwd(const float* pred, const float* gt, const int3
     return set_error(CFSD_EINVAL, "recon_lap_fwd: null pointer");
   if (batch <= 0 || nv <= 0 || c <= 0 || c > 4) return set_error(CFSD_EINVAL, "recon_lap_fwd: bad sizes");
   const long total = (long)batch * nv;
-  hipLaunchKernelGGL(recon_lap_fwd_k, dim3(cfsd_recon_lap_blocks(batch, nv)), dim3(kLapThreads), 0,
-                     (hipStream_t)stream, pred, gt, l_ptr, l_col, l_val, unit_lx, partials, nv, c,
-                     total);
+  const dim3 grid(cfsd_recon_lap_blocks(batch, nv));
+  const hipStream_t st = (hipStream_t)stream;
+#define RLF(C)                                                                                  \
+  case C:                                                                                       \
+    hipLaunchKernelGGL(recon_lap_fwd_k<C>, grid, dim3(kLapThreads), 0, st, pred, gt, l_ptr, l_col, \
+                       l_val, unit_lx, partials, nv, total);                                    \
+    break;
+  switch (c) { RLF(1) RLF(2) RLF(3) RLF(4) }
+#undef RLF
   return launch_status("recon_lap_fwd");
 }
 
@@ -613,9 +667,16 @@ extern "C" int cfsd_recon_lap_bwd(const float* pred, const float* gt, const floa
   const long total = (long)batch * nv;
   const float k_rec = w_rec * 2.f / (float)(total * c);
   const float k_lap = w_lap / (float)((long)nv * batch);
-  hipLaunchKernelGGL(recon_lap_bwd_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, pred, gt, unit_lx, lt_ptr, lt_col, lt_val, dpred, nv, c,
-                     total, k_rec, k_lap);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  const hipStream_t st = (hipStream_t)stream;
+  const LossFinalize none{};  // losses finalised by cfsd_loss_finalize
+#define RLB(C)                                                                                   \
+  case C:                                                                                        \
+    hipLaunchKernelGGL(recon_lap_bwd_k<C>, grid, dim3(256), 0, st, pred, gt, unit_lx, lt_ptr,    \
+                       lt_col, lt_val, dpred, nv, total, k_rec, k_lap, none);                    \
+    break;
+  switch (c) { RLB(1) RLB(2) RLB(3) RLB(4) }
+#undef RLB
   return launch_status("recon_lap_bwd");
 }
 
@@ -654,8 +715,8 @@ extern "C" int cfsd_loss_finalize(const float* partials, int nblocks, const floa
   if (!partials || !terms || !out) return set_error(CFSD_EINVAL, "loss_finalize: null pointer");
   const float inv_n = 1.f / (float)((long)batch * nv * c);
   const float inv_lap = 1.f / (float)((long)nv * batch);
-  hipLaunchKernelGGL(loss_finalize_k, dim3(1), dim3(256), 0, (hipStream_t)stream, partials,
-                     nblocks, terms, out, acc, inv_n, inv_lap, w_kl, w_lc, w_lap);
+  const LossFinalize f{partials, nblocks, terms, out, acc, inv_n, inv_lap, w_kl, w_lc, w_lap};
+  hipLaunchKernelGGL(loss_finalize_k, dim3(1), dim3(256), 0, (hipStream_t)stream, f);
   return launch_status("loss_finalize");
 }
 

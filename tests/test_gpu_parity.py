@@ -61,6 +61,20 @@ def test_spiral_conv_fwd(otopo, dtopo, cin, cout, level, bsz, act):
     close(y, ref, 1e-5, "conv fwd")
 
 
+@pytest.mark.parametrize("cin,level,bsz", [(32, 0, 16), (64, 1, 3), (32, 3, 1), (4, 2, 2), (12, 4 - 1, 5)])
+def test_spiral_gather_bit_exact(otopo, dtopo, cin, level, bsz):
+    """Materialising gather (the HBM-roofline probe) == the reference's
+    ``x.index_select(1, indices.view(-1)).view(B, V, -1)`` (model.py:34),
+    bit-exact, including the ragged tail of the last block."""
+    g = torch.Generator().manual_seed(7 + cin + level)
+    sp = otopo.spirals[level]
+    v = sp.shape[0]
+    x = torch.randn(bsz, v, cin, generator=g)
+    ref = x.index_select(1, torch.as_tensor(sp, dtype=torch.long).reshape(-1)).view(bsz, v, -1)
+    got = ops.spiral_gather(x.to(DEV), dtopo.spiral[level])
+    assert torch.equal(got.cpu(), ref)
+
+
 @pytest.mark.parametrize("cin,cout,level,bsz", [c for c in CONV_CASES if c[0] != 3])
 @pytest.mark.parametrize("use_elu_y", [False, True])
 def test_spiral_conv_bwd(otopo, dtopo, cin, cout, level, bsz, use_elu_y):

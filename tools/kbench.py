@@ -51,6 +51,14 @@ def main():
                                                 P.gview("de_layers.5.layer.bias"), dx=b.dpre_dec[3],
                                                 elu_y=b.dec_out[3], workspace=b.ws),
         "spmm_up0": lambda: ops.spmm(T.up_csr[0], b.dec_out[2], T.n_verts[0], out=b.dec_up[3]),
+        "spmm_up1": lambda: ops.spmm(T.up_csr[1], b.dec_out[1], T.n_verts[1], out=b.dec_up[2]),
+        "spmm_up2": lambda: ops.spmm(T.up_csr[2], b.dec_out[0], T.n_verts[2], out=b.dec_up[1]),
+        "spmm_up3": lambda: ops.spmm(T.up_csr[3], b.h, T.n_verts[3], out=b.dec_up[0]),
+        "spmm_up1T": lambda: ops.spmm(T.upT_csr[1], b.g_dec_up[2], T.n_verts[2], elu_y=b.dec_out[1],
+                                      out=b.dpre_dec[1]),
+        "spmm_up2T": lambda: ops.spmm(T.upT_csr[2], b.g_dec_up[1], T.n_verts[3], elu_y=b.dec_out[0],
+                                      out=b.dpre_dec[0]),
+        "spmm_up3T": lambda: ops.spmm(T.upT_csr[3], b.g_dec_up[0], T.n_verts[4], out=b.dh),
         "spmm_up0T": lambda: ops.spmm(T.upT_csr[0], b.g_dec_up[3], T.n_verts[1], elu_y=b.dec_out[2],
                                       out=b.dpre_dec[2]),
         "e0_fwd": lambda: ops.spiral_conv_fwd(b.x, T.enc_rows[0], *eng._enc_w(0), 1, out=b.enc_out[0], workspace=b.ws),

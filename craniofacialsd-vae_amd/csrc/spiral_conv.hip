@@ -1808,7 +1808,11 @@ static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* in
                             const int* inv_pair, const float* w, const float* elu_y, float* dx,
                             float* ws, size_t ws_floats, int vsrc, int rows, long M,
                             hipStream_t st) {
-  if (M < CFSD_LAT_DX_MAX) {
+  // latency-shaped below ~64k dx rows; up to CFSD_LAT_DX_MAX when the conv
+  // was evaluated on a row subset (Enblock: ~2.25 inverse entries per dx row
+  // instead of 9) -- measured: E1 dx 32.8 vs 42 us, D2 dx (full) 49 vs 44.6 us
+  const long dpre_rows = M / vsrc * rows;
+  if (M < CFSD_LAT_MAX_ROWS || (M < CFSD_LAT_DX_MAX && 2 * dpre_rows <= M)) {
     const long tasks = (M + 15) / 16 * (CIN / 16);
     hipLaunchKernelGGL((conv_dx_lat<CIN, COUT>), dim3((unsigned)((tasks + 3) / 4)), dim3(256), 0, st,
                        dpre, inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M);

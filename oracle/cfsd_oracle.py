@@ -119,10 +119,12 @@ def encode(P, x, topo, is_vae=True):
     return mu, logvar
 
 
-def decode(P, z, topo, c_last=64):
+def decode(P, z, topo, c_last=None):
     """``Model.decode`` (``model.py:162-173``): Linear -> view [B, V4, C];
     4x (Pool up -> conv -> ELU); final SpiralConv without activation."""
     n = topo.n_levels
+    if c_last is None:
+        c_last = P["de_layers.0.weight"].shape[0] // topo.n_verts[-1]
     h = F.linear(z, P["de_layers.0.weight"], P["de_layers.0.bias"])
     h = h.view(-1, topo.n_verts[-1], c_last)
     for i in range(1, n + 1):
@@ -133,11 +135,12 @@ def decode(P, z, topo, c_last=64):
                        P[f"de_layers.{n + 1}.layer.bias"])
 
 
-def forward(P, x, topo, eps=None, train=True):
+def forward(P, x, topo, eps=None, train=True, is_vae=True):
     """``Model.forward`` + ``_reparameterize`` (``model.py:175-188``), with
-    the noise ``eps`` injected instead of ``torch.randn_like``."""
-    mu, logvar = encode(P, x, topo)
-    if train:
+    the noise ``eps`` injected instead of ``torch.randn_like``.  AE
+    (``is_vae=False``, kl_weight 0 at ``model_manager.py:67``): z = mu."""
+    mu, logvar = encode(P, x, topo, is_vae)
+    if train and is_vae:
         z = mu + eps * torch.exp(0.5 * logvar)
     else:
         z = mu
@@ -232,15 +235,19 @@ def latent_regions(n_regions, latent=75):
     return [(i * rs, (i + 1) * rs) for i in range(n_regions)]
 
 
-def losses(P, x16, topo, key_index, eps, bs=4, w=LOSS_W):
+def losses(P, x16, topo, key_index, eps, bs=4, w=LOSS_W, is_vae=True):
     """Forward + the four losses of ``_do_iteration``
-    (``model_manager.py:281-312``)."""
-    rec, z, mu, lv = forward(P, x16, topo, eps=eps, train=True)
+    (``model_manager.py:281-312``); KL only when ``w_kl > 0`` (``:285-288``),
+    latent consistency only with swapped batches (``:290-293``)."""
+    rec, z, mu, lv = forward(P, x16, topo, eps=eps, train=True, is_vae=is_vae)
     l_rec = mse_loss(rec, x16)
     l_lap = laplacian_loss(rec, topo.lap)
-    l_kl = kl_loss(mu, lv)
-    region = latent_regions(len(topo.region_keys), z.shape[1])[key_index]
-    l_lc = latent_consistency(z, region, bs)
+    l_kl = kl_loss(mu, lv) if w["kl"] > 0 else torch.tensor(0.0)
+    if w["lc"] and key_index is not None:
+        region = latent_regions(len(topo.region_keys), z.shape[1])[key_index]
+        l_lc = latent_consistency(z, region, bs)
+    else:
+        l_lc = torch.tensor(0.0)
     tot = l_rec + w["kl"] * l_kl + w["lc"] * l_lc + w["lap"] * l_lap
     return {"rec": l_rec, "kl": l_kl, "lc": l_lc, "lap": l_lap, "tot": tot,
             "out": rec, "z": z, "mu": mu, "logvar": lv}
@@ -269,13 +276,14 @@ class Adam:
             p.addcdiv_(self.m[k], denom, value=-self.lr / bc1)
 
 
-def train_step(P, opt, x4, topo, key_index, eps):
+def train_step(P, opt, x4, topo, key_index, eps, w=LOSS_W, is_vae=True):
     """One ``_do_iteration(train=True)``: swap -> forward -> losses ->
     backward -> Adam.  ``P`` holds leaf tensors (requires_grad)."""
     x16 = torch.from_numpy(swap_features(x4, topo.region_features, key_index))
     for p in P.values():
         p.grad = None
-    out = losses(P, x16, topo, key_index, torch.as_tensor(eps))
+    out = losses(P, x16, topo, key_index, None if eps is None else torch.as_tensor(eps),
+                 bs=len(x4), w=w, is_vae=is_vae)
     out["tot"].backward()
     grads = {k: p.grad.detach().clone() for k, p in P.items()}
     opt.step(P, grads)

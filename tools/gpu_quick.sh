@@ -1,6 +1,6 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r01j; rm -rf $O; mkdir -p $O
+O=gpurun_out/${TAG:-r01k}; rm -rf $O; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -60 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 timeout -k 10 300 python bench.py --no-cpu --steps 200 > $O/bench.json 2> $O/bench.err && cut -c1-200 $O/bench.json && python -c "import json; d=json.load(open('$O/bench.json')); print(d['gather_roofline'])"

@@ -373,14 +373,47 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
 // b).  For slot s the A operand is T_s[u, :] = sum_{r in inv(u,s)} dpre[r, :]
 // (gather-sum through the inverse spiral, fixed order -> deterministic); the
 // B operand is W_s^T staged in LDS as [s][c][COUT + 4].
-// inv_pair[u*S + s] = the first two rows of inv(u,s) (-1 if absent): those
-// loads are issued unconditionally one slot ahead; the rare further entries
-// (inv_ptr/inv_row from offset 2) are summed in a short loop.
+// inv_head[u*S + s] = the first four rows of inv(u,s) (-1 if absent), one
+// int4 per key, prefetched two slots ahead.  Rows 0/1 are loaded
+// unconditionally one slot ahead (clamped, weighted 0 when absent: 77 % of
+// keys have <= 1 entry, 96 % <= 2); rows 2/3 (exec-masked loads) only for
+// the lanes whose list has them; entries beyond the head (0.03 % of keys)
+// walk inv_ptr/inv_row from offset 4.  Sum order = list order.
 // Slot groups as in conv_fwd_mfma (partials -> ws, conv_combine).
+constexpr int kInvHead = CFSD_INV_HEAD;
+__device__ __forceinline__ float present(int r) { return r >= 0 ? 1.f : 0.f; }
+
+// Small-channel (CO-wide dpre rows) list folding, entries 2.. of NS keys
+// key0 + j (rows 0/1 already in t): the head's rows 2/3 as exec-masked loads,
+// then the CSR tail from offset 4 (rare).  Adds in list order.
+template <int NS, int CO>
+__device__ __forceinline__ void fold_head_tail(const int4 (&hd)[NS], long key0,
+                                               const float* __restrict__ db_,
+                                               const int* __restrict__ inv_ptr,
+                                               const int* __restrict__ inv_row,
+                                               float (&t)[NS][CO]) {
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    if (hd[j].z >= 0) {
+#pragma unroll
+      for (int o = 0; o < CO; ++o) t[j][o] += db_[hd[j].z * CO + o];
+      if (hd[j].w >= 0) {
+#pragma unroll
+        for (int o = 0; o < CO; ++o) t[j][o] += db_[hd[j].w * CO + o];
+        const long key = key0 + j;
+        for (int e = inv_ptr[key] + kInvHead; e < inv_ptr[key + 1]; ++e) {
+#pragma unroll
+          for (int o = 0; o < CO; ++o) t[j][o] += db_[inv_row[e] * CO + o];
+        }
+      }
+    }
+  }
+}
+
 template <int CIN, int COUT, int SPG>
 __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
     const float* __restrict__ dpre, const int* __restrict__ inv_ptr,
-    const int* __restrict__ inv_row, const int2* __restrict__ inv_pair,
+    const int* __restrict__ inv_row, const int4* __restrict__ inv_head,
     const float* __restrict__ w, const float* __restrict__ elu_y, float* __restrict__ dx,
     float* __restrict__ ws, int vsrc, int rows, long total_rows) {
   constexpr int HALF = COUT / 2;
@@ -405,14 +438,15 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
     if (m >= total_rows) m = total_rows - 1;
     const int b = (int)(m / vsrc), u = (int)(m % vsrc);
     const float* db_ = dpre + (long)b * rows * COUT + h * HALF;
-    const int2* pu = inv_pair + (long)u * kSeq + s0;
+    const int4* pu = inv_head + (long)u * kSeq + s0;
     f32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x16){0.f};
-    // slot pipeline: rows r0/r1 of slot s+1 and the pair of slot s+2 are in
+    // slot pipeline: rows 0/1 of slot s+1 and the head of slot s+2 are in
     // flight while slot s computes (rolled loop, see conv_fwd_mfma).
     f32x4 c0[HALF / 4], c1[HALF / 4];
-    int2 pc = pu[0], pn = SPG > 1 ? pu[1] : make_int2(-1, -1);
+    const int4 none = make_int4(-1, -1, -1, -1);
+    int4 pc = pu[0], pn = SPG > 1 ? pu[1] : none;
 #pragma unroll
     for (int q = 0; q < HALF / 4; ++q) {
       c0[q] = ld4(db_ + (long)max(pc.x, 0) * COUT + 4 * q);
@@ -421,12 +455,12 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
 #pragma unroll 1
     for (int s = 0; s < SPG; ++s) {
       f32x4 a[HALF / 4];
-      const float f0 = pc.x >= 0 ? 1.f : 0.f, f1 = pc.y >= 0 ? 1.f : 0.f;
+      const int4 cur = pc;
+      const float f0 = present(cur.x), f1 = present(cur.y);
 #pragma unroll
       for (int q = 0; q < HALF / 4; ++q) a[q] = c0[q] * f0 + c1[q] * f1;
-      const bool more = pc.y >= 0;
       if (s + 1 < SPG) {
-        const int2 pnn = (s + 2 < SPG) ? pu[s + 2] : make_int2(-1, -1);
+        const int4 pnn = (s + 2 < SPG) ? pu[s + 2] : none;
 #pragma unroll
         for (int q = 0; q < HALF / 4; ++q) {
           c0[q] = ld4(db_ + (long)max(pn.x, 0) * COUT + 4 * q);
@@ -435,13 +469,21 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
         pc = pn;
         pn = pnn;
       }
-      if (more) {  // rare: entries beyond the first two
-        const long key = (long)u * kSeq + s0 + s;
-        const int beg = inv_ptr[key] + 2, end = inv_ptr[key + 1];
-        for (int e = beg; e < end; ++e) {
-          const float* p = db_ + (long)inv_row[e] * COUT;
+      // row 2 (3.6 % of keys, ~70 % of waves): exec-masked loads straight
+      // from the head (one round trip; the CSR is walked only past row 3)
+      if (cur.z >= 0) {
 #pragma unroll
-          for (int q = 0; q < HALF / 4; ++q) a[q] += ld4(p + 4 * q);
+        for (int q = 0; q < HALF / 4; ++q) a[q] += ld4(db_ + (long)cur.z * COUT + 4 * q);
+        if (cur.w >= 0) {  // rare (0.3 % of keys): rows 3.. of the list
+          const long key = (long)u * kSeq + s0 + s;
+          const int end = inv_ptr[key + 1];
+#pragma unroll
+          for (int q = 0; q < HALF / 4; ++q) a[q] += ld4(db_ + (long)cur.w * COUT + 4 * q);
+          for (int e = inv_ptr[key] + kInvHead; e < end; ++e) {
+            const float* p = db_ + (long)inv_row[e] * COUT;
+#pragma unroll
+            for (int q = 0; q < HALF / 4; ++q) a[q] += ld4(p + 4 * q);
+          }
         }
       }
 #pragma unroll
@@ -552,14 +594,14 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
 // Backward data for layers with few source rows, same tiling as
 // conv_fwd_lat: a wave owns 16 source rows u x 16 input channels c and all
 // 9 slots.  A = T_s[u][o] (gather-sum of dpre rows through the inverse
-// spiral: the inv_pair rows of a batch of 3 slots are loaded together,
+// spiral: the inv_head rows of a batch of 3 slots are loaded together,
 // rare further entries added after), B = W_s^T read straight from W (4
 // strided dwords per 4-chunk of o; W is L2-resident), in flight with A.
 template <int CIN, int COUT>
 __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpre,
                                                    const int* __restrict__ inv_ptr,
                                                    const int* __restrict__ inv_row,
-                                                   const int2* __restrict__ inv_pair,
+                                                   const int4* __restrict__ inv_head,
                                                    const float* __restrict__ w,
                                                    const float* __restrict__ elu_y,
                                                    float* __restrict__ dx, int vsrc, int rows,
@@ -575,12 +617,12 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
   if (m >= total_rows) m = total_rows - 1;
   const int b = (int)(m / vsrc), u = (int)(m % vsrc);
   const float* db_ = dpre + (long)b * rows * COUT + 4 * kg;
-  const int2* pu = inv_pair + (long)u * kSeq;
+  const int4* pu = inv_head + (long)u * kSeq;
   const float* wb = w + (long)(4 * kg) * K + ct * 16 + r16;  // + o_off*K + s*CIN
   f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
   for (int s0 = 0; s0 < kSeq; s0 += kLatSB) {
-    int2 pr[kLatSB];
+    int4 pr[kLatSB];
 #pragma unroll
     for (int sl = 0; sl < kLatSB; ++sl) pr[sl] = pu[s0 + sl];
     f32x4 bw[kLatSB][CH];
@@ -600,14 +642,22 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
 #pragma unroll
       for (int c = 0; c < CH; ++c) a[sl][c] = ld4(p0 + 16 * c) * f0 + ld4(p1 + 16 * c) * f1;
     }
+    // rows 2 / 3 of the batch's lists: exec-masked loads straight from the
+    // head; rows 4.. walk the CSR (0.03 % of keys)
 #pragma unroll
     for (int sl = 0; sl < kLatSB; ++sl) {
-      if (pr[sl].y >= 0) {  // rare: entries beyond the first two
-        const long key = (long)u * kSeq + s0 + sl;
-        for (int e = inv_ptr[key] + 2; e < inv_ptr[key + 1]; ++e) {
-          const float* p = db_ + (long)inv_row[e] * COUT;
+      if (pr[sl].z >= 0) {
 #pragma unroll
-          for (int c = 0; c < CH; ++c) a[sl][c] += ld4(p + 16 * c);
+        for (int c = 0; c < CH; ++c) a[sl][c] += ld4(db_ + (long)pr[sl].z * COUT + 16 * c);
+        if (pr[sl].w >= 0) {
+#pragma unroll
+          for (int c = 0; c < CH; ++c) a[sl][c] += ld4(db_ + (long)pr[sl].w * COUT + 16 * c);
+          const long key = (long)u * kSeq + s0 + sl;
+          for (int e = inv_ptr[key] + kInvHead; e < inv_ptr[key + 1]; ++e) {
+            const float* p = db_ + (long)inv_row[e] * COUT;
+#pragma unroll
+            for (int c = 0; c < CH; ++c) a[sl][c] += ld4(p + 16 * c);
+          }
         }
       }
     }
@@ -637,16 +687,16 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
 // Backward data, small dpre (CO <= 4 channels; the xyz output conv): one
 // thread per source row (b, u) computing all CIN outputs.  The spiral
 // transpose is first folded in the CO-wide dpre space,
-//   t[s][o] = sum_{r : idx[r][s] = u} dpre[b][r][o]   (inv_pair + rare overflow),
+//   t[s][o] = sum_{r : idx[r][s] = u} dpre[b][r][o]   (inv_head + rare overflow),
 // then dx[c] = sum_{s,o} t[s][o] * W[o][s*CIN + c].  W's addresses are
 // wave-uniform compile-time offsets, so they are scalar loads (SGPR operands
-// of the FMAs, no LDS, no per-lane W registers).  All 9 inv_pair loads and
+// of the FMAs, no LDS, no per-lane W registers).  All 9 inv_head loads and
 // the 18 dpre row loads of a thread are independent and issued together.
 template <int CIN, int CO>
 __global__ __launch_bounds__(256) void conv_dx_out_small(const float* __restrict__ dpre,
                                                          const int* __restrict__ inv_ptr,
                                                          const int* __restrict__ inv_row,
-                                                         const int2* __restrict__ inv_pair,
+                                                         const int4* __restrict__ inv_head,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ elu_y,
                                                          float* __restrict__ dx, int vsrc,
@@ -656,8 +706,8 @@ __global__ __launch_bounds__(256) void conv_dx_out_small(const float* __restrict
   if (m >= total_rows) return;
   const int b = (int)(m / vsrc), u = (int)(m % vsrc);
   const float* db_ = dpre + (long)b * rows * CO;
-  const int2* pu = inv_pair + (long)u * kSeq;
-  int2 pr[kSeq];
+  const int4* pu = inv_head + (long)u * kSeq;
+  int4 pr[kSeq];
 #pragma unroll
   for (int s = 0; s < kSeq; ++s) pr[s] = pu[s];
   float tt[kSeq][CO];
@@ -665,21 +715,11 @@ __global__ __launch_bounds__(256) void conv_dx_out_small(const float* __restrict
   for (int s = 0; s < kSeq; ++s) {
     const float* p0 = db_ + (long)max(pr[s].x, 0) * CO;
     const float* p1 = db_ + (long)max(pr[s].y, 0) * CO;
-    const float f0 = pr[s].x >= 0 ? 1.f : 0.f, f1 = pr[s].y >= 0 ? 1.f : 0.f;
+    const float f0 = present(pr[s].x), f1 = present(pr[s].y);
 #pragma unroll
     for (int o = 0; o < CO; ++o) tt[s][o] = p0[o] * f0 + p1[o] * f1;
   }
-#pragma unroll
-  for (int s = 0; s < kSeq; ++s) {
-    if (pr[s].y >= 0) {
-      const long key = (long)u * kSeq + s;
-      for (int e = inv_ptr[key] + 2; e < inv_ptr[key + 1]; ++e) {
-        const float* p = db_ + (long)inv_row[e] * CO;
-#pragma unroll
-        for (int o = 0; o < CO; ++o) tt[s][o] += p[o];
-      }
-    }
-  }
+  fold_head_tail<kSeq, CO>(pr, (long)u * kSeq, db_, inv_ptr, inv_row, tt);
   float* out = dx + m * CIN;
   const float* ey = elu_y ? elu_y + m * CIN : nullptr;
 #pragma unroll
@@ -1253,7 +1293,7 @@ __global__ __launch_bounds__(256) void conv_dw_in_mfma(const float* __restrict__
 // Backward of a small-output conv (CO*kSeq <= 32; the xyz output conv),
 // data + weight fused, in source-row space.  Per source row (b, u) a thread
 // folds the spiral transpose in the CO-wide dpre space,
-//   t[s][o] = sum_{r : idx[r][s] = u} dpre[b][r][o]       (inv_pair + overflow)
+//   t[s][o] = sum_{r : idx[r][s] = u} dpre[b][r][o]       (inv_head + overflow)
 // and then produces
 //   dx[b][u][c]  = g * sum_{s,o} t[s][o] W[o][s*CIN + c]   (VALU, W as SGPRs)
 //   dW[o][s*CIN + c] += t[s][o] x[b][u][c]                  (rank-64 MFMA per tile)
@@ -1263,7 +1303,7 @@ __global__ __launch_bounds__(256) void conv_dw_in_mfma(const float* __restrict__
 template <int CIN, int CO>
 __global__ __launch_bounds__(256) void conv_bwd_out_small(
     const float* __restrict__ dpre, const int* __restrict__ inv_ptr,
-    const int* __restrict__ inv_row, const int2* __restrict__ inv_pair,
+    const int* __restrict__ inv_row, const int4* __restrict__ inv_head,
     const float* __restrict__ w, const float* __restrict__ elu_y, const float* __restrict__ x,
     float* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, long total_rows) {
   constexpr int K = kSeq * CIN, NI = kSeq * CO, NCT = CIN / 32, NEL = CO * K + CO;
@@ -1287,8 +1327,8 @@ __global__ __launch_bounds__(256) void conv_bwd_out_small(
     const long mm = valid ? m : total_rows - 1;
     const int b = (int)(mm / vsrc), u = (int)(mm % vsrc);
     const float* db_ = dpre + (long)b * rows * CO;
-    const int2* pu = inv_pair + (long)u * kSeq;
-    int2 pr[kSeq];
+    const int4* pu = inv_head + (long)u * kSeq;
+    int4 pr[kSeq];
 #pragma unroll
     for (int s = 0; s < kSeq; ++s) pr[s] = pu[s];
     float tt[kSeq][CO];
@@ -1296,21 +1336,11 @@ __global__ __launch_bounds__(256) void conv_bwd_out_small(
     for (int s = 0; s < kSeq; ++s) {
       const float* p0 = db_ + (long)max(pr[s].x, 0) * CO;
       const float* p1 = db_ + (long)max(pr[s].y, 0) * CO;
-      const float f0 = pr[s].x >= 0 ? 1.f : 0.f, f1 = pr[s].y >= 0 ? 1.f : 0.f;
+      const float f0 = present(pr[s].x), f1 = present(pr[s].y);
 #pragma unroll
       for (int o = 0; o < CO; ++o) tt[s][o] = p0[o] * f0 + p1[o] * f1;
     }
-#pragma unroll
-    for (int s = 0; s < kSeq; ++s) {
-      if (pr[s].y >= 0) {
-        const long key = (long)u * kSeq + s;
-        for (int e = inv_ptr[key] + 2; e < inv_ptr[key + 1]; ++e) {
-          const float* p = db_ + (long)inv_row[e] * CO;
-#pragma unroll
-          for (int o = 0; o < CO; ++o) tt[s][o] += p[o];
-        }
-      }
-    }
+    fold_head_tail<kSeq, CO>(pr, (long)u * kSeq, db_, inv_ptr, inv_row, tt);
     if (!valid) {
 #pragma unroll
       for (int s = 0; s < kSeq; ++s)
@@ -1400,7 +1430,7 @@ constexpr int kAtS = 36;  // At row stride: conflict-free ds_read_b128 of the dW
 template <int CIN, int CO>
 __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     const float* __restrict__ dpre, const int* __restrict__ inv_ptr,
-    const int* __restrict__ inv_row, const int2* __restrict__ inv_pair,
+    const int* __restrict__ inv_row, const int4* __restrict__ inv_head,
     const float* __restrict__ w, const float* __restrict__ elu_y, const float* __restrict__ x,
     float* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, long total_rows) {
   constexpr int SPH = 5, KH = SPH * CO, K = kSeq * CIN, NCT = CIN / 32, NEL = CO * K + CO;
@@ -1438,40 +1468,31 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     const long mm = valid ? m : total_rows - 1;
     const int b = (int)(mm / vsrc), u = (int)(mm % vsrc);
     const float* db_ = dpre + (long)b * rows * CO;
-    int2 pr[SPH];
+    const int4 none = make_int4(-1, -1, -1, -1);
+    int4 pr[SPH];
 #pragma unroll
     for (int sl = 0; sl < SPH; ++sl) {
       const int sg = h * SPH + sl;
-      pr[sl] = sg < kSeq ? inv_pair[u * kSeq + sg] : make_int2(-1, -1);
+      pr[sl] = sg < kSeq ? inv_head[u * kSeq + sg] : none;
     }
-    float tt[KH];
+    float tt[SPH][CO];
 #pragma unroll
     for (int sl = 0; sl < SPH; ++sl) {
       const int o0 = max(pr[sl].x, 0) * CO, o1 = max(pr[sl].y, 0) * CO;
-      const float f0 = pr[sl].x >= 0 ? 1.f : 0.f, f1 = pr[sl].y >= 0 ? 1.f : 0.f;
+      const float f0 = present(pr[sl].x), f1 = present(pr[sl].y);
 #pragma unroll
-      for (int o = 0; o < CO; ++o) tt[sl * CO + o] = db_[o0 + o] * f0 + db_[o1 + o] * f1;
+      for (int o = 0; o < CO; ++o) tt[sl][o] = db_[o0 + o] * f0 + db_[o1 + o] * f1;
     }
-#pragma unroll
-    for (int sl = 0; sl < SPH; ++sl) {
-      if (pr[sl].y >= 0) {
-        const int key = u * kSeq + h * SPH + sl;
-        for (int e = inv_ptr[key] + 2; e < inv_ptr[key + 1]; ++e) {
-          const int oe = inv_row[e] * CO;
-#pragma unroll
-          for (int o = 0; o < CO; ++o) tt[sl * CO + o] += db_[oe + o];
-        }
-      }
-    }
+    fold_head_tail<SPH, CO>(pr, (long)u * kSeq + h * SPH, db_, inv_ptr, inv_row, tt);
     if (!valid) {
 #pragma unroll
-      for (int q = 0; q < KH; ++q) tt[q] = 0.f;
+      for (int q = 0; q < KH; ++q) tt[q / CO][q % CO] = 0.f;
     }
 #pragma unroll
-    for (int q = 0; q < KH; ++q) At[(h * KH + q) * kAtS + li] = tt[q];
+    for (int q = 0; q < KH; ++q) At[(h * KH + q) * kAtS + li] = tt[q / CO][q % CO];
     if (h == 0) {  // slot 0 lists hold every output row once: db = sum_u t[0][o]
 #pragma unroll
-      for (int o = 0; o < CO; ++o) dbs[o] += tt[o];
+      for (int o = 0; o < CO; ++o) dbs[o] += tt[0][o];
     }
     // x tile in accumulator-row order (B operand of dW, elu' source); its
     // loads are in flight during the dx MFMAs
@@ -1491,7 +1512,7 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
 #pragma unroll
       for (int r = 0; r < 16; ++r) dxacc[ct][r] = 0.f;
 #pragma unroll
-      for (int j = 0; j < KH; ++j) dxacc[ct] = mfma32(tt[j], wt[ct][j], dxacc[ct]);
+      for (int j = 0; j < KH; ++j) dxacc[ct] = mfma32(tt[j / CO][j % CO], wt[ct][j], dxacc[ct]);
     }
     wave_lds_sync();
     // dW^T += At . x_tile, K (rows) in accumulator-row order
@@ -1786,7 +1807,7 @@ extern "C" int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const fl
 
 template <int CIN, int COUT, int SPG>
 static int launch_dx_mfma(const float* dpre, const int* inv_ptr, const int* inv_row,
-                          const int* inv_pair, const float* w, const float* elu_y, float* dx,
+                          const int* inv_head, const float* w, const float* elu_y, float* dx,
                           float* ws, int vsrc, int rows, long M, hipStream_t st) {
   constexpr size_t lds = (size_t)SPG * CIN * (COUT + 4) * sizeof(float);
   static_assert(lds <= 80 * 1024, "W slice must fit LDS");
@@ -1794,7 +1815,7 @@ static int launch_dx_mfma(const float* dpre, const int* inv_ptr, const int* inv_
   const long max_blocks = resident_blocks_of(kern, 256, lds) / (kSeq / SPG);
   dim3 grid(balanced_blocks((M + 31) / 32, 4, max_blocks > 0 ? max_blocks : 1), kSeq / SPG);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, dpre, inv_ptr,
-                     inv_row, (const int2*)inv_pair, w, elu_y, dx, ws, vsrc, rows, M);
+                     inv_row, (const int4*)inv_head, w, elu_y, dx, ws, vsrc, rows, M);
   int rc = launch_status("spiral_conv_bwd_data");
   if (rc || SPG == kSeq) return rc;
   const long n4 = M * CIN / 4;
@@ -1805,7 +1826,7 @@ static int launch_dx_mfma(const float* dpre, const int* inv_ptr, const int* inv_
 
 template <int CIN, int COUT>
 static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* inv_row,
-                            const int* inv_pair, const float* w, const float* elu_y, float* dx,
+                            const int* inv_head, const float* w, const float* elu_y, float* dx,
                             float* ws, size_t ws_floats, int vsrc, int rows, long M,
                             hipStream_t st) {
   // latency-shaped below ~64k dx rows; up to CFSD_LAT_DX_MAX when the conv
@@ -1815,7 +1836,7 @@ static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* in
   if (M < CFSD_LAT_MAX_ROWS || (M < CFSD_LAT_DX_MAX && 2 * dpre_rows <= M)) {
     const long tasks = (M + 15) / 16 * (CIN / 16);
     hipLaunchKernelGGL((conv_dx_lat<CIN, COUT>), dim3((unsigned)((tasks + 3) / 4)), dim3(256), 0, st,
-                       dpre, inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M);
+                       dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M);
     return launch_status("spiral_conv_bwd_data_lat");
   }
   constexpr bool big = (size_t)kSeq * CIN * (COUT + 4) * sizeof(float) > 80 * 1024;
@@ -1823,30 +1844,31 @@ static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* in
   if (big && spg == 9) spg = 3;
   if (spg != 9 && !ws) return set_error(CFSD_EWORKSPACE, "spiral_conv_bwd_data: workspace required");
   if (spg == 9)
-    return launch_dx_mfma<CIN, COUT, (big ? 3 : 9)>(dpre, inv_ptr, inv_row, inv_pair, w, elu_y, dx,
+    return launch_dx_mfma<CIN, COUT, (big ? 3 : 9)>(dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx,
                                                     ws, vsrc, rows, M, st);
   if (spg == 3)
-    return launch_dx_mfma<CIN, COUT, 3>(dpre, inv_ptr, inv_row, inv_pair, w, elu_y, dx, ws, vsrc,
+    return launch_dx_mfma<CIN, COUT, 3>(dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, ws, vsrc,
                                         rows, M, st);
-  return launch_dx_mfma<CIN, COUT, 1>(dpre, inv_ptr, inv_row, inv_pair, w, elu_y, dx, ws, vsrc,
+  return launch_dx_mfma<CIN, COUT, 1>(dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, ws, vsrc,
                                       rows, M, st);
 }
 
 extern "C" int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_ptr,
-                                         const int32_t* inv_row, const int32_t* inv_pair,
+                                         const int32_t* inv_row, const int32_t* inv_head,
                                          const float* w, const float* elu_y, float* dx,
                                          float* workspace, size_t workspace_bytes, int batch,
                                          int vsrc, int rows, int seq, int cin, int cout,
                                          void* stream) {
   int rc = check_conv_args(dpre, inv_ptr, inv_row, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
-  if (!w || !dx || !inv_pair) return set_error(CFSD_EINVAL, "null w/dx/inv_pair");
+  if (!w || !dx || !inv_head) return set_error(CFSD_EINVAL, "null w/dx/inv_head");
+  if ((uintptr_t)inv_head & 15) return set_error(CFSD_EINVAL, "inv_head must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
   const long M = (long)batch * vsrc;
   const size_t wsf = workspace ? workspace_bytes / sizeof(float) : 0;
 #define DXM(CIN_, COUT_)                                                                       \
   if (cin == CIN_ && cout == COUT_)                                                            \
-    return dispatch_dx_mfma<CIN_, COUT_>(dpre, inv_ptr, inv_row, inv_pair, w, elu_y, dx,       \
+    return dispatch_dx_mfma<CIN_, COUT_>(dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx,       \
                                          workspace, wsf, vsrc, rows, M, st);
   DXM(32, 32) DXM(32, 64) DXM(64, 32) DXM(64, 64)
 #undef DXM
@@ -1854,7 +1876,7 @@ extern "C" int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_p
   if (cin == CIN_ && cout == CO_) {                                                             \
     auto k = conv_dx_out_small<CIN_, CO_>;                                                      \
     hipLaunchKernelGGL(k, dim3(row_grid(M)), dim3(256), 0, st,                                  \
-                       dpre, inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, dx, vsrc, rows, M); \
+                       dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M); \
     return launch_status("spiral_conv_bwd_data_small");                                        \
   }
   DXS(16, 3) DXS(32, 3) DXS(64, 3)
@@ -2036,14 +2058,15 @@ extern "C" size_t cfsd_spiral_conv_bwd_workspace(int batch, int vsrc, int rows, 
 
 extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const float* dpre,
                                     const int32_t* inv_ptr, const int32_t* inv_row,
-                                    const int32_t* inv_pair, const float* w, const float* elu_y,
+                                    const int32_t* inv_head, const float* w, const float* elu_y,
                                     float* dx, float* dw, float* db, float* workspace,
                                     size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
                                     int cin, int cout, void* stream) {
   int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
-  if (!inv_ptr || !inv_row || !inv_pair || !w || !workspace)
+  if (!inv_ptr || !inv_row || !inv_head || !w || !workspace)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd: null inverse table / w / workspace");
+  if ((uintptr_t)inv_head & 15) return set_error(CFSD_EINVAL, "inv_head must be 16-B aligned");
   if ((dw == nullptr) != (db == nullptr))
     return set_error(CFSD_EINVAL, "dw and db must both be set (or both NULL: deferred)");
   const size_t need = cfsd_spiral_conv_bwd_workspace(batch, vsrc, rows, seq, cin, cout);
@@ -2052,7 +2075,7 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
   hipStream_t st = (hipStream_t)stream;
   if (!fused_small(cin, cout)) {
     if (dx) {
-      rc = cfsd_spiral_conv_bwd_data(dpre, inv_ptr, inv_row, inv_pair, w, elu_y, dx, workspace,
+      rc = cfsd_spiral_conv_bwd_data(dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, workspace,
                                      workspace_bytes, batch, vsrc, rows, seq, cin, cout, stream);
       if (rc) return rc;
     }
@@ -2065,7 +2088,7 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
 #define BOS(CIN_, CO_)                                                                           \
   if (cin == CIN_ && cout == CO_) {                                                              \
     hipLaunchKernelGGL((conv_bwd_out_mfma<CIN_, CO_>), dim3(gx), dim3(256), 0, st, dpre,         \
-                       inv_ptr, inv_row, (const int2*)inv_pair, w, elu_y, x, dx, workspace, vsrc, \
+                       inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, x, dx, workspace, vsrc, \
                        rows, Ms);                                                                \
     rc = launch_status("spiral_conv_bwd_small");                                                 \
     if (rc || !dw) return rc;                                                                    \

@@ -630,7 +630,7 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
 
 using namespace cfsd;
 
-extern "C" int cfsd_version(void) { return (1 << 16) | 0; }
+extern "C" int cfsd_version(void) { return (2 << 16) | 0; }  // 2.0: 4-wide inverse head
 extern "C" const char* cfsd_last_error_string(void) { return g_err; }
 
 extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {

@@ -11,6 +11,7 @@ import torch
 
 from . import _abi
 from ._abi import call, ptr, stream_ptr
+from .topology import INV_HEAD
 
 ACT_NONE = 0
 ACT_ELU = 1
@@ -70,21 +71,21 @@ def spiral_conv_fwd(x, idx, w, b, act=ACT_NONE, out=None, workspace=None):
 
 def spiral_conv_bwd_data(dpre, inv, w, vsrc, elu_y=None, out=None, workspace=None):
     """dx[b, u] = g * sum_{(r,s) in inv(u)} W_s^T dpre[b, r]; ``inv`` is the
-    (inv_ptr, inv_row, inv_pair) triple of ``topology.inverse_spiral``."""
+    (inv_ptr, inv_row, inv_head) triple of ``topology.inverse_spiral``."""
     bsz, rows, cout = dpre.shape
-    inv_ptr, inv_row, inv_pair = inv
+    inv_ptr, inv_row, inv_head = inv
     seq = (inv_ptr.numel() - 1) // vsrc
     cin = w.shape[1] // seq
     _need(dpre, None, name="dpre")
     _need(inv_ptr, (vsrc * seq + 1,), torch.int32, "inv_ptr")
     _need(inv_row, (rows * seq,), torch.int32, "inv_row")
-    _need(inv_pair, (vsrc * seq, 2), torch.int32, "inv_pair")
+    _need(inv_head, (vsrc * seq, INV_HEAD), torch.int32, "inv_head")
     _need(w, (cout, seq * cin), name="w")
     if elu_y is not None:
         _need(elu_y, (bsz, vsrc, cin), name="elu_y")
     dx = _out(out, (bsz, vsrc, cin), dpre)
     ws, nb = _conv_ws(workspace, dpre.device, spiral_conv_workspace(bsz, vsrc, rows, seq, cin, cout))
-    call("cfsd_spiral_conv_bwd_data", ptr(dpre), ptr(inv_ptr), ptr(inv_row), ptr(inv_pair), ptr(w),
+    call("cfsd_spiral_conv_bwd_data", ptr(dpre), ptr(inv_ptr), ptr(inv_row), ptr(inv_head), ptr(w),
          ptr(elu_y), ptr(dx), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, seq, cin, cout,
          stream_ptr())
     return dx
@@ -151,13 +152,13 @@ def spiral_conv_bwd(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape
     cout = dpre.shape[2]
-    inv_ptr, inv_row, inv_pair = inv
+    inv_ptr, inv_row, inv_head = inv
     _need(x, None, name="x")
     _need(idx, (rows, seq), torch.int32, "idx")
     _need(dpre, (bsz, rows, cout), name="dpre")
     _need(inv_ptr, (vsrc * seq + 1,), torch.int32, "inv_ptr")
     _need(inv_row, (rows * seq,), torch.int32, "inv_row")
-    _need(inv_pair, (vsrc * seq, 2), torch.int32, "inv_pair")
+    _need(inv_head, (vsrc * seq, INV_HEAD), torch.int32, "inv_head")
     _need(w, (cout, seq * cin), name="w")
     if dw is not None or db is not None:
         _need(dw, (cout, seq * cin), name="dw")
@@ -168,7 +169,7 @@ def spiral_conv_bwd(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace
         _need(elu_y, (bsz, vsrc, cin), name="elu_y")
     ws, nb = _conv_ws(workspace, x.device, spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout))
     call("cfsd_spiral_conv_bwd", ptr(x), ptr(idx), ptr(dpre), ptr(inv_ptr), ptr(inv_row),
-         ptr(inv_pair), ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb),
+         ptr(inv_head), ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb),
          bsz, vsrc, rows, seq, cin, cout, stream_ptr())
     if dw is None:  # deferred weight gradient
         return dx, DeferredDw(ws, bsz, vsrc, rows, cin, cout, True)

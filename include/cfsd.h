@@ -65,11 +65,14 @@ size_t cfsd_spiral_conv_workspace(int batch, int vsrc, int rows, int seq, int ci
  * (fuses the previous layer's ELU backward), else 1.
  * inv_ptr [vsrc*seq + 1] / inv_row [rows*seq]: CSR of the inverse spiral,
  * entry list of (u, s) = rows r with idx[r*seq+s] == u (r ascending);
- * inv_pair [vsrc*seq][2]: the first two entries of each list (-1 if absent),
- * read up front so the gathers are issued one slot ahead (required).  The
- * spiral length must be 9 (all reference configs). */
+ * inv_head [vsrc*seq][CFSD_INV_HEAD]: the first four entries of each list (-1
+ * if absent, 16-B aligned rows), read up front with one load per key so the
+ * gathers are issued without walking the CSR (required; inv_ptr/inv_row are
+ * only read for lists longer than the head).  The spiral length must be 9
+ * (all reference configs). */
+#define CFSD_INV_HEAD 4
 int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_ptr, const int32_t* inv_row,
-                              const int32_t* inv_pair, const float* w, const float* elu_y,
+                              const int32_t* inv_head, const float* w, const float* elu_y,
                               float* dx, float* workspace, size_t workspace_bytes, int batch,
                               int vsrc, int rows, int seq, int cin, int cout, void* stream);
 
@@ -105,7 +108,7 @@ int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* stream);
  * sum_{b,u} x[b,u,:] (x) t[b,u,s,:], so x is read densely, not gathered.
  * workspace: cfsd_spiral_conv_bwd_workspace() bytes (shared by both stages). */
 int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const float* dpre,
-                         const int32_t* inv_ptr, const int32_t* inv_row, const int32_t* inv_pair,
+                         const int32_t* inv_ptr, const int32_t* inv_row, const int32_t* inv_head,
                          const float* w, const float* elu_y, float* dx, float* dw, float* db,
                          float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows,
                          int seq, int cin, int cout, void* stream);

@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_reporting(lib):
-    assert lib.cfsd_version() >> 16 == 1
+    assert lib.cfsd_version() >> 16 == 2  # 2.0: 4-wide inverse-spiral head
     # argument validation happens before any HIP call: safe without a GPU
     rc = lib.cfsd_spiral_conv_fwd(None, None, None, None, None, None, 0, 1, 1, 1, 9, 32, 32, 0, None)
     assert rc == -1
@@ -51,15 +51,19 @@ def test_version_and_error_reporting(lib):
 def test_inverse_spiral_matches_bruteforce():
     rs = np.random.RandomState(0)
     idx = rs.randint(0, 50, size=(80, 9))
-    ptr, rows, pair = topology.inverse_spiral(idx, 50)
+    ptr, rows, head = topology.inverse_spiral(idx, 50)
+    assert head.shape == (50 * 9, topology.INV_HEAD)
+    longest = 0
     for u in range(50):
         for s in range(9):
             k = u * 9 + s
             got = rows[ptr[k]:ptr[k + 1]].tolist()
             exp = [r for r in range(80) if idx[r, s] == u]
             assert got == exp
-            assert pair[k, 0] == (exp[0] if exp else -1)
-            assert pair[k, 1] == (exp[1] if len(exp) > 1 else -1)
+            longest = max(longest, len(exp))
+            for j in range(topology.INV_HEAD):
+                assert head[k, j] == (exp[j] if len(exp) > j else -1)
+    assert longest > topology.INV_HEAD  # the overflow path is exercised
 
 
 def test_csr_keeps_file_order_and_transpose():

@@ -75,7 +75,7 @@ def main():
     ip, ir, ipair = T.spiral_inv[0]
     inv_noovf = (torch.zeros_like(ip), ir, ipair)
     pair1 = ipair.clone()
-    pair1[:, 1] = -1
+    pair1[:, 1:] = -1
     inv_nomore = (ip, ir, pair1)
     cases["dx_d3_noovf"] = lambda: ops.spiral_conv_bwd_data(b.dpre_dec[3], inv_noovf, w3, T.n_verts[0], out=b.g_dec_up[3], workspace=b.ws)
     cases["dx_d3_nomore"] = lambda: ops.spiral_conv_bwd_data(b.dpre_dec[3], inv_nomore, w3, T.n_verts[0], out=b.g_dec_up[3], workspace=b.ws)

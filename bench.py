@@ -167,6 +167,29 @@ def pmc_traffic():
     return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
+def c1_parity(device):
+    """The metric's second half: per-vertex L1 of C1 (encode + decode of the
+    first 8 demo meshes, eval mode, golden weights) through the HIP path
+    against the reconstructions the reference's own model.py produced
+    (tests/golden/golden_eval.npz, made by tests/golden/make_golden.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import recipe
+    npz = dict(np.load(TOPO_NPZ))
+    topo = topology.DeviceTopology.from_npz(npz, device=device)
+    eng = E.SDVAEEngine(topo, E.ModelSpec(), device=device)
+    eng.load_state_dict({k: torch.from_numpy(v) for k, v in recipe.golden_weights().items()})
+    b = eng.set_batch(torch.from_numpy(recipe.normalized_meshes(8)).to(device))
+    eng.forward(b, train=False)
+    torch.cuda.synchronize()
+    g = np.load(os.path.join(ROOT, "tests", "golden", "golden_eval.npz"))
+    d = np.abs(b.out.cpu().numpy() - g["recon"]).sum(-1)
+    return {"config": "C1: demo encode+decode, 8 meshes, eval (z = mu), golden weights",
+            "reference": "tests/golden/golden_eval.npz (reference model.py run in the build container)",
+            "max_vertex_l1": float(d.max()), "mean_vertex_l1": float(d.mean()),
+            "z_max_abs_diff": float(np.abs(b.z.cpu().numpy() - g["z"]).max()),
+            "tolerance": 1e-4, "pass": bool(d.max() <= 1e-4)}
+
+
 def cpu_baseline(budget_s):
     """Oracle (PyTorch-CPU restatement of the reference step) on host cores."""
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
@@ -235,6 +258,7 @@ def main():
         t_conv = probe["conv_fwd_D3"]
         gather_bytes = 16 * nv * (32 + 9 * 32) * 4 + nv * 9 * 4
         t_g = probe["spiral_gather_L0"]
+        parity = c1_parity(device)
         cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
         traffic, traffic_src = pmc_traffic()
         out = {
@@ -257,6 +281,7 @@ def main():
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": gather_bytes / t_g / 1e9 / HBM_PEAK_GBS,
                                 "us_per_launch": t_g * 1e6},
+            "parity": parity,
             "cpu_baseline": cpu,
             "losses_mean": (losses[:5] / max(losses[5], 1)).tolist(), "losses_finite": finite,
         }

@@ -410,16 +410,35 @@ __device__ __forceinline__ void fold_head_tail(const int4 (&hd)[NS], long key0,
   }
 }
 
+
+// dpre through a buffer descriptor: 32-bit per-lane byte offsets, and an
+// absent list row is an out-of-range offset that returns 0 with no memory
+// access.  Every row load is then ONE unconditional instruction -- no exec
+// branches, whose joins made hipcc drain the in-flight prefetch.
+constexpr int kAbsentRow = 0x7ffff000;
+__device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+#ifndef CFSD_DX_OCC
+#define CFSD_DX_OCC 3
+#endif
+constexpr int dx_occ(int cin, int cout) { return (cin == 32 && cout == 32) ? CFSD_DX_OCC : 2; }
+
 template <int CIN, int COUT, int SPG>
-__global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
+__global__ __launch_bounds__(256, dx_occ(CIN, COUT)) void conv_dx_mfma(
     const float* __restrict__ dpre, const int* __restrict__ inv_ptr,
     const int* __restrict__ inv_row, const int4* __restrict__ inv_head,
     const float* __restrict__ w, const float* __restrict__ elu_y, float* __restrict__ dx,
     float* __restrict__ ws, int vsrc, int rows, long total_rows) {
-  constexpr int HALF = COUT / 2;
+  constexpr int HALF = COUT / 2, Q = HALF / 4;
+  // K map inside a slot: lane half h, load q covers dpre channels
+  // 4*h + 8*q + [0, 4) (the two lane halves read the two 16-B halves of one
+  // 32-B segment of the row)
   constexpr int NT = CIN / 32;
   constexpr int OP = COUT + 4;
   constexpr int K = kSeq * CIN;
+  constexpr int RB = COUT * (int)sizeof(float);  // dpre row bytes
   extern __shared__ float lds_wt[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -430,6 +449,8 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
     lds_wt[k * OP + o] = w[(long)o * K + s0 * CIN + k];
   }
   __syncthreads();
+  const int nbytes = (int)(total_rows / vsrc * rows * RB);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dpre), 0, nbytes, 0x00020000);
   const int i = lane & 31, h = lane >> 5;
   const TileSweep sw = xcd_sweep((total_rows + 31) / 32, 4, wave);
   for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
@@ -437,61 +458,62 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_dx_mfma(
     long m = m0 + i;
     if (m >= total_rows) m = total_rows - 1;
     const int b = (int)(m / vsrc), u = (int)(m % vsrc);
-    const float* db_ = dpre + (long)b * rows * COUT + h * HALF;
+    const int base = b * rows * RB + 16 * h;
     const int4* pu = inv_head + (long)u * kSeq + s0;
+    auto roff = [&](int r) { return r >= 0 ? base + r * RB : kAbsentRow; };
     f32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x16){0.f};
-    // slot pipeline: rows 0/1 of slot s+1 and the head of slot s+2 are in
-    // flight while slot s computes (rolled loop, see conv_fwd_mfma).
-    f32x4 c0[HALF / 4], c1[HALF / 4];
+    // slot pipeline: list rows 0..2 of slot s+1 and the head of slot s+2
+    // are in flight while slot s computes (row 2: 3.6 % of keys but ~70 %
+    // of 32-row wave-slots).  Every load is unconditional, so hipcc's
+    // counters stay exact and the wait at the top of a slot only retires
+    // the previous slot's prefetch.
+    f32x4 c0[Q], c1[Q], c2[Q];
     const int4 none = make_int4(-1, -1, -1, -1);
     int4 pc = pu[0], pn = SPG > 1 ? pu[1] : none;
 #pragma unroll
-    for (int q = 0; q < HALF / 4; ++q) {
-      c0[q] = ld4(db_ + (long)max(pc.x, 0) * COUT + 4 * q);
-      c1[q] = ld4(db_ + (long)max(pc.y, 0) * COUT + 4 * q);
+    for (int q = 0; q < Q; ++q) {
+      c0[q] = buf_ld4(rsrc, roff(pc.x) + 32 * q);
+      c1[q] = buf_ld4(rsrc, roff(pc.y) + 32 * q);
+      c2[q] = buf_ld4(rsrc, roff(pc.z) + 32 * q);
     }
 #pragma unroll 1
     for (int s = 0; s < SPG; ++s) {
-      f32x4 a[HALF / 4];
       const int4 cur = pc;
-      const float f0 = present(cur.x), f1 = present(cur.y);
+      f32x4 a[Q];
 #pragma unroll
-      for (int q = 0; q < HALF / 4; ++q) a[q] = c0[q] * f0 + c1[q] * f1;
-      if (s + 1 < SPG) {
-        const int4 pnn = (s + 2 < SPG) ? pu[s + 2] : none;
+      for (int q = 0; q < Q; ++q) a[q] = (c0[q] + c1[q]) + c2[q];  // absent rows read as 0
+      // past the last slot the head is `none` (out-of-range loads, no
+      // traffic) rather than a branch: a branch made hipcc merge the two
+      // paths' counters into vmcnt(0), draining the prefetch every slot
+      int4 pnn = pu[min(s + 2, SPG - 1)];
+      if (s + 2 >= SPG) pnn = none;
 #pragma unroll
-        for (int q = 0; q < HALF / 4; ++q) {
-          c0[q] = ld4(db_ + (long)max(pn.x, 0) * COUT + 4 * q);
-          c1[q] = ld4(db_ + (long)max(pn.y, 0) * COUT + 4 * q);
-        }
-        pc = pn;
-        pn = pnn;
+      for (int q = 0; q < Q; ++q) {
+        c0[q] = buf_ld4(rsrc, roff(pn.x) + 32 * q);
+        c1[q] = buf_ld4(rsrc, roff(pn.y) + 32 * q);
+        c2[q] = buf_ld4(rsrc, roff(pn.z) + 32 * q);
       }
-      // row 2 (3.6 % of keys, ~70 % of waves): exec-masked loads straight
-      // from the head (one round trip; the CSR is walked only past row 3)
-      if (cur.z >= 0) {
+      pc = pn;
+      pn = pnn;
+      if (cur.w >= 0) {  // 0.3 % of keys: rows 3.. of the list
+        const long key = (long)u * kSeq + s0 + s;
+        const float* db_ = dpre + base / (int)sizeof(float);
 #pragma unroll
-        for (int q = 0; q < HALF / 4; ++q) a[q] += ld4(db_ + (long)cur.z * COUT + 4 * q);
-        if (cur.w >= 0) {  // rare (0.3 % of keys): rows 3.. of the list
-          const long key = (long)u * kSeq + s0 + s;
-          const int end = inv_ptr[key + 1];
+        for (int q = 0; q < Q; ++q) a[q] += ld4(db_ + (long)cur.w * COUT + 8 * q);
+        for (int e = inv_ptr[key] + kInvHead; e < inv_ptr[key + 1]; ++e) {
+          const float* p = db_ + (long)inv_row[e] * COUT;
 #pragma unroll
-          for (int q = 0; q < HALF / 4; ++q) a[q] += ld4(db_ + (long)cur.w * COUT + 4 * q);
-          for (int e = inv_ptr[key] + kInvHead; e < end; ++e) {
-            const float* p = db_ + (long)inv_row[e] * COUT;
-#pragma unroll
-            for (int q = 0; q < HALF / 4; ++q) a[q] += ld4(p + 4 * q);
-          }
+          for (int q = 0; q < Q; ++q) a[q] += ld4(p + 8 * q);
         }
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const float* wr = &lds_wt[(s * CIN + t * 32 + i) * OP + h * HALF];
+        const float* wr = &lds_wt[(s * CIN + t * 32 + i) * OP + 4 * h];
 #pragma unroll
-        for (int q = 0; q < HALF / 4; ++q) {
-          const f32x4 bw = ld4(wr + 4 * q);
+        for (int q = 0; q < Q; ++q) {
+          const f32x4 bw = ld4(wr + 8 * q);
           acc[t] = mfma32(a[q].x, bw.x, acc[t]);
           acc[t] = mfma32(a[q].y, bw.y, acc[t]);
           acc[t] = mfma32(a[q].z, bw.z, acc[t]);

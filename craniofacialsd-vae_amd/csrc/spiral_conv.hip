@@ -639,6 +639,10 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
   if (m >= total_rows) m = total_rows - 1;
   const int b = (int)(m / vsrc), u = (int)(m % vsrc);
   const float* db_ = dpre + (long)b * rows * COUT + 4 * kg;
+  constexpr int RB = COUT * (int)sizeof(float);
+  const int base = (b * rows * COUT + 4 * kg) * (int)sizeof(float);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dpre), 0,
+                                                      (int)(total_rows / vsrc * rows * RB), 0x00020000);
   const int4* pu = inv_head + (long)u * kSeq;
   const float* wb = w + (long)(4 * kg) * K + ct * 16 + r16;  // + o_off*K + s*CIN
   f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -655,22 +659,25 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
         const float* q = wb + (long)(16 * c) * K + (s0 + sl) * CIN;
         bw[sl][c] = f32x4{q[0], q[K], q[2 * K], q[3 * K]};
       }
+    // list rows 0..2 of the batch's keys: unconditional buffer loads, absent
+    // rows out of range (read as 0, no traffic), all in flight together
     f32x4 a[kLatSB][CH];
 #pragma unroll
     for (int sl = 0; sl < kLatSB; ++sl) {
-      const float f0 = pr[sl].x >= 0 ? 1.f : 0.f, f1 = pr[sl].y >= 0 ? 1.f : 0.f;
-      const float* p0 = db_ + (long)max(pr[sl].x, 0) * COUT;
-      const float* p1 = db_ + (long)max(pr[sl].y, 0) * COUT;
+      f32x4 r[3][CH];
+      const int hr[3] = {pr[sl].x, pr[sl].y, pr[sl].z};
 #pragma unroll
-      for (int c = 0; c < CH; ++c) a[sl][c] = ld4(p0 + 16 * c) * f0 + ld4(p1 + 16 * c) * f1;
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+          r[j][c] = buf_ld4(rsrc, hr[j] >= 0 ? base + hr[j] * RB + 64 * c : kAbsentRow);
+#pragma unroll
+      for (int c = 0; c < CH; ++c) a[sl][c] = (r[0][c] + r[1][c]) + r[2][c];
     }
-    // rows 2 / 3 of the batch's lists: exec-masked loads straight from the
-    // head; rows 4.. walk the CSR (0.03 % of keys)
+    // rows 3.. (0.3 % of keys): exec branch
 #pragma unroll
     for (int sl = 0; sl < kLatSB; ++sl) {
-      if (pr[sl].z >= 0) {
-#pragma unroll
-        for (int c = 0; c < CH; ++c) a[sl][c] += ld4(db_ + (long)pr[sl].z * COUT + 16 * c);
+      {
         if (pr[sl].w >= 0) {
 #pragma unroll
           for (int c = 0; c < CH; ++c) a[sl][c] += ld4(db_ + (long)pr[sl].w * COUT + 16 * c);
@@ -1480,6 +1487,8 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
 #pragma unroll
   for (int o = 0; o < CO; ++o) dbs[o] = 0.f;
   const int ey_mode = elu_y == nullptr ? 0 : (elu_y == x ? 1 : 2);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(dpre), 0, (int)(total_rows / vsrc * rows * CO * (long)sizeof(float)), 0x00020000);
   const long n_tiles = (total_rows + 31) / 32;
   const TileSweep sw = xcd_sweep(n_tiles, 4, wave);
   for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
@@ -1497,15 +1506,37 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
       const int sg = h * SPH + sl;
       pr[sl] = sg < kSeq ? inv_head[u * kSeq + sg] : none;
     }
+    // list rows 0..2 of the 5 keys: 45 unconditional buffer dword loads in
+    // flight together (absent rows out of range: 0, no traffic); rows 3..
+    // (0.3 % of keys) through an exec branch
     float tt[SPH][CO];
+    const int base = b * rows * CO * (int)sizeof(float);
 #pragma unroll
     for (int sl = 0; sl < SPH; ++sl) {
-      const int o0 = max(pr[sl].x, 0) * CO, o1 = max(pr[sl].y, 0) * CO;
-      const float f0 = present(pr[sl].x), f1 = present(pr[sl].y);
+      const int hr[3] = {pr[sl].x, pr[sl].y, pr[sl].z};
+      float v[3][CO];
 #pragma unroll
-      for (int o = 0; o < CO; ++o) tt[sl][o] = db_[o0 + o] * f0 + db_[o1 + o] * f1;
+      for (int j = 0; j < 3; ++j) {
+        const int off = hr[j] >= 0 ? base + hr[j] * CO * (int)sizeof(float) : kAbsentRow;
+#pragma unroll
+        for (int o = 0; o < CO; ++o)
+          v[j][o] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4 * o, 0, 0));
+      }
+#pragma unroll
+      for (int o = 0; o < CO; ++o) tt[sl][o] = (v[0][o] + v[1][o]) + v[2][o];
     }
-    fold_head_tail<SPH, CO>(pr, (long)u * kSeq + h * SPH, db_, inv_ptr, inv_row, tt);
+#pragma unroll
+    for (int sl = 0; sl < SPH; ++sl) {
+      if (pr[sl].w >= 0) {
+#pragma unroll
+        for (int o = 0; o < CO; ++o) tt[sl][o] += db_[pr[sl].w * CO + o];
+        const long key = (long)u * kSeq + h * SPH + sl;
+        for (int e = inv_ptr[key] + kInvHead; e < inv_ptr[key + 1]; ++e) {
+#pragma unroll
+          for (int o = 0; o < CO; ++o) tt[sl][o] += db_[inv_row[e] * CO + o];
+        }
+      }
+    }
     if (!valid) {
 #pragma unroll
       for (int q = 0; q < KH; ++q) tt[q / CO][q % CO] = 0.f;
@@ -1731,9 +1762,6 @@ static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const
 #ifndef CFSD_LAT_FWD_MAX
 #define CFSD_LAT_FWD_MAX CFSD_LAT_MAX_ROWS
 #endif
-#ifndef CFSD_LAT_DX_MAX
-#define CFSD_LAT_DX_MAX 80000  // measured: also the 68k-row D2 / E1 dx
-#endif
 #ifndef CFSD_LAT_DW_MAX
 #define CFSD_LAT_DW_MAX CFSD_LAT_MAX_ROWS
 #endif
@@ -1851,11 +1879,13 @@ static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* in
                             const int* inv_head, const float* w, const float* elu_y, float* dx,
                             float* ws, size_t ws_floats, int vsrc, int rows, long M,
                             hipStream_t st) {
-  // latency-shaped below ~64k dx rows; up to CFSD_LAT_DX_MAX when the conv
-  // was evaluated on a row subset (Enblock: ~2.25 inverse entries per dx row
-  // instead of 9) -- measured: E1 dx 32.8 vs 42 us, D2 dx (full) 49 vs 44.6 us
+  // latency-shaped below ~64k dx rows (the persistent kernel cannot fill the
+  // chip there without slot groups), and up to 80k rows when the conv was
+  // evaluated on a row subset (Enblock: ~2.25 list entries per dx row
+  // instead of 9; each persistent block would stage W for ~2 tiles) --
+  // measured on the 68k-row E1 dx: 33.8 us here vs 38.8 us persistent
   const long dpre_rows = M / vsrc * rows;
-  if (M < CFSD_LAT_MAX_ROWS || (M < CFSD_LAT_DX_MAX && 2 * dpre_rows <= M)) {
+  if (M < CFSD_LAT_MAX_ROWS || (M < 80000 && 2 * dpre_rows <= M)) {
     const long tasks = (M + 15) / 16 * (CIN / 16);
     hipLaunchKernelGGL((conv_dx_lat<CIN, COUT>), dim3((unsigned)((tasks + 3) / 4)), dim3(256), 0, st,
                        dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M);
@@ -1885,6 +1915,8 @@ extern "C" int cfsd_spiral_conv_bwd_data(const float* dpre, const int32_t* inv_p
   if (rc) return rc;
   if (!w || !dx || !inv_head) return set_error(CFSD_EINVAL, "null w/dx/inv_head");
   if ((uintptr_t)inv_head & 15) return set_error(CFSD_EINVAL, "inv_head must be 16-B aligned");
+  if ((long)batch * rows * cout * (long)sizeof(float) >= (1L << 31))
+    return set_error(CFSD_EINVAL, "dpre larger than 2 GiB (32-bit buffer offsets)");
   hipStream_t st = (hipStream_t)stream;
   const long M = (long)batch * vsrc;
   const size_t wsf = workspace ? workspace_bytes / sizeof(float) : 0;
@@ -2089,6 +2121,8 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
   if (!inv_ptr || !inv_row || !inv_head || !w || !workspace)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd: null inverse table / w / workspace");
   if ((uintptr_t)inv_head & 15) return set_error(CFSD_EINVAL, "inv_head must be 16-B aligned");
+  if ((long)batch * rows * cout * (long)sizeof(float) >= (1L << 31))
+    return set_error(CFSD_EINVAL, "dpre larger than 2 GiB (32-bit buffer offsets)");
   if ((dw == nullptr) != (db == nullptr))
     return set_error(CFSD_EINVAL, "dw and db must both be set (or both NULL: deferred)");
   const size_t need = cfsd_spiral_conv_bwd_workspace(batch, vsrc, rows, seq, cin, cout);

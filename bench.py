@@ -148,18 +148,25 @@ def kernel_probe(runner, n_iter=20):
     w3, bias3 = eng._dec_w(i3)
     timed("conv_fwd_D3", lambda: ops.spiral_conv_fwd(b.dec_up[i3], T.spiral[0], w3, bias3, 1,
                                                       out=b.dec_out[i3]))
+    # the D3 backward kernels exactly as the step launches them (dx with the
+    # previous Deblock's ELU folded in is the Pool transpose's input here;
+    # dW deferred: slab kernel only, reduced by the batched reduce)
+    timed("conv_dx_D3", lambda: ops.spiral_conv_bwd_data(b.dpre_dec[i3], T.spiral_inv[0], w3, T.n_verts[0],
+                                                         out=b.g_dec_up[i3], workspace=b.ws))
+    timed("conv_dw_D3", lambda: ops.spiral_conv_bwd_weight(b.dec_up[i3], T.spiral[0], b.dpre_dec[i3], None,
+                                                           None, b.ws_dw[("dec", i3)]))
     g = torch.empty(16, T.n_verts[0], 9 * 32, device=b.x.device)
     timed("spiral_gather_L0", lambda: ops.spiral_gather(b.dec_up[i3], T.spiral[0], out=g))
     del g
     return res
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the dominant kernel from the newest committed
-    PMC pass (tools/gpu_round.sh -> tools/pmc_traffic.py: FETCH_SIZE and
-    WRITE_SIZE in separate rocprofv3 runs, gfx950 FETCH_SIZE x2 correction)."""
+def pmc_traffic(key="conv_fwd_d3"):
+    """HBM bytes per launch of a D3 kernel from the newest committed PMC pass
+    (tools/gpu_round.sh -> tools/pmc_traffic.py: FETCH_SIZE and WRITE_SIZE in
+    separate rocprofv3 runs, gfx950 FETCH_SIZE x2 correction)."""
     import glob
-    files = sorted(glob.glob(os.path.join(PROFILES, "*_pmc_traffic_conv_fwd_d3.json")))
+    files = sorted(glob.glob(os.path.join(PROFILES, f"*_pmc_traffic_{key}.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -255,12 +262,24 @@ def main():
         nv = runner.topo.n_verts[0]
         # dominant kernel: fused gather+contraction of D3 (32 -> 32, 17039 rows x 16)
         flops = 2.0 * 16 * nv * 9 * 32 * 32
-        t_conv = probe["conv_fwd_D3"]
         gather_bytes = 16 * nv * (32 + 9 * 32) * 4 + nv * 9 * 4
         t_g = probe["spiral_gather_L0"]
         parity = c1_parity(device)
         cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
-        traffic, traffic_src = pmc_traffic()
+        # the three D3 (decoder level 0, 32 -> 32) conv kernels, 5.02 GFLOP
+        # each; `roofline` is the dominant one (longest launch)
+        d3 = {}
+        for name, key in (("conv_fwd_D3", "conv_fwd_d3"), ("conv_dx_D3", "conv_dx_d3"),
+                          ("conv_dw_D3", "conv_dw_d3")):
+            t = probe[name]
+            traffic, traffic_src = pmc_traffic(key)
+            d3[name] = {"us_per_launch": t * 1e6, "achieved": flops / t / 1e12,
+                        "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS, "traffic": traffic,
+                        "traffic_source": traffic_src}
+        dom = max(d3, key=lambda k: d3[k]["us_per_launch"])
+        kern_names = {"conv_fwd_D3": "conv_fwd_mfma<32,32> (decoder level 0 forward)",
+                      "conv_dx_D3": "conv_dx_mfma<32,32> (decoder level 0 data gradient)",
+                      "conv_dw_D3": "conv_dw_mfma<32,32> (decoder level 0 weight gradient)"}
         out = {
             "metric": METRIC, "value": meshes / el, "unit": "meshes/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
@@ -271,11 +290,12 @@ def main():
                        "template_vertices": nv, "levels": runner.topo.n_verts,
                        "global_batch": 16 * world, "per_gpu_batch": 16,
                        "parallelism": f"dp{world}", "graph": runner.use_graph},
-            "roofline": {"kernel": "cfsd conv_fwd_mfma<32,32> (decoder level 0)", "bound": "mfma",
-                         "achieved": flops / t_conv / 1e12, "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": flops / t_conv / 1e12 / FP32_PEAK_TFLOPS,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_flop": flops, "us_per_launch": t_conv * 1e6},
+            "roofline": {"kernel": "cfsd " + kern_names[dom], "bound": "mfma",
+                         "achieved": d3[dom]["achieved"], "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": d3[dom]["frac"],
+                         "traffic": d3[dom]["traffic"], "traffic_source": d3[dom]["traffic_source"],
+                         "algorithmic_flop": flops, "us_per_launch": d3[dom]["us_per_launch"]},
+            "d3_kernels": d3,
             "gather_roofline": {"kernel": "cfsd spiral_gather_k (level 0, 32 ch, 16 meshes)",
                                 "bound": "hbm", "achieved": gather_bytes / t_g / 1e9,
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -23,9 +23,13 @@ find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \; ||
 head -20 $OUT/kernel_stats.txt
 if [ -z "$SKIP_PMC" ]; then
   export KB_ITERS=20
-  timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc_fetch -o run -- python3 tools/kbench.py fwd_d3 > $OUT/pmc_fetch.log 2>&1
-  timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write -o run -- python3 tools/kbench.py fwd_d3 > $OUT/pmc_write.log 2>&1
-  python tools/pmc_traffic.py $OUT > $OUT/pmc_traffic.json || true
-  cat $OUT/pmc_traffic.json
+  timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc_fetch -o run -- python3 tools/kbench.py fwd_d3 dx_d3 dw_d3 > $OUT/pmc_fetch.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write -o run -- python3 tools/kbench.py fwd_d3 dx_d3 dw_d3 > $OUT/pmc_write.log 2>&1
+  python tools/pmc_traffic.py $OUT "conv_fwd_mfma<32, 32, 1, 9>" > $OUT/pmc_traffic_conv_fwd_d3.json || true
+  python tools/pmc_traffic.py $OUT "conv_dx_mfma<32, 32, 9>" > $OUT/pmc_traffic_conv_dx_d3.json || true
+  python tools/pmc_traffic.py $OUT "conv_dw_mfma<32, 32>" > $OUT/pmc_traffic_conv_dw_d3.json || true
+  cat $OUT/pmc_traffic_*.json
+  KB="fwd_d3 dx_d3 dw_d3" OUT=$OUT/pmc_sq bash tools/pmc_kernels.sh > $OUT/pmc_sq.log 2>&1 || true
+  tail -20 $OUT/pmc_sq.log
 fi
 echo ALL_DONE

@@ -78,7 +78,7 @@ class Runner:
                        n_regions=T.n_regions, batch_idx=b.batch_idx, bs=4,
                        n_batches=self.n_batches, perm=self.perm, adam_step=eng.params.step)
         ops.swap_features(self.data, b.batch_idx, T.region_mask, b.key, 4, out=b.x)
-        eng.forward(b, train=True, acc=eng.loss_acc)
+        eng.forward(b, train=True, acc=eng.loss_acc, finalize=False)
         eng.backward(b)
 
     def part_b(self):

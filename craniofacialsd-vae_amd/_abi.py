@@ -42,6 +42,8 @@ SIGNATURES = {
     "cfsd_recon_lap_blocks": (_I, [_I, _I]),
     "cfsd_recon_lap_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "cfsd_recon_lap_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P]),
+    "cfsd_recon_lap_bwd_finalize": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P, _I, _P, _P,
+                                         _P, _F, _F, _P]),
     "cfsd_latent_fwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F, _P]),
     "cfsd_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_loss_finalize": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P]),

@@ -206,58 +206,83 @@ __global__ __launch_bounds__(256) void latent_fwd_k(const float* __restrict__ mu
                                                     int sigmoid, float w_kl, float w_lc,
                                                     float eta1, float eta2, int bs) {
   __shared__ float zs[64 * 256];
-  __shared__ float cs[64 * 256];      // dLC/dz accumulators, column l owned by thread l
   __shared__ float dist[4 * 64 * 8];  // [kind][pair][t]
   __shared__ float2 red[4];
   const int tid = threadIdx.x;
   const int ldm = is_vae ? 2 * L : L;
   const int mu_off = is_vae ? L : 0;
-  // z and KL pieces
+  // z and KL pieces.  The inputs of up to 8 elements per thread are loaded
+  // before any is used (mulv was just written by the encoder Linear, possibly
+  // on another XCD: each dependent load round trip is ~1-2 us here).
   float kl_part = 0.f;
-  for (int e = tid; e < B * L; e += blockDim.x) {
-    const int i = e / L, l = e % L;
-    const float mu = mulv[i * ldm + mu_off + l];
-    float zz = mu;
-    if (is_vae) {
-      const float lv = mulv[i * ldm + l];
-      const float ex = expf(lv);
-      if (train) zz = mu + eps[e] * expf(0.5f * lv);
-      kl_part += 1.f + lv - mu * mu - ex;
-      dlat[i * 3 * L + L + l] = w_kl * mu / (float)B;
-      dlat[i * 3 * L + 2 * L + l] = w_kl * (-0.5f) * (1.f - ex) / (float)B;
-    } else {
-      if (sigmoid) zz = 1.f / (1.f + expf(-mu));
-      dlat[i * 3 * L + L + l] = 0.f;
-      dlat[i * 3 * L + 2 * L + l] = 0.f;
+  constexpr int EPT = 8;
+  for (int e0 = tid; e0 < B * L; e0 += EPT * blockDim.x) {
+    float mu_r[EPT], lv_r[EPT], ep_r[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int e = e0 + k * blockDim.x;
+      const int ec = e < B * L ? e : B * L - 1;
+      const int i = ec / L, l = ec % L;
+      mu_r[k] = mulv[i * ldm + mu_off + l];
+      lv_r[k] = is_vae ? mulv[i * ldm + l] : 0.f;
+      ep_r[k] = (is_vae && train) ? eps[ec] : 0.f;
     }
-    z[e] = zz;
-    zs[e] = zz;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int e = e0 + k * blockDim.x;
+      if (e >= B * L) break;
+      const int i = e / L, l = e % L;
+      const float mu = mu_r[k];
+      float zz = mu;
+      if (is_vae) {
+        const float lv = lv_r[k];
+        const float ex = expf(lv);
+        if (train) zz = mu + ep_r[k] * expf(0.5f * lv);
+        kl_part += 1.f + lv - mu * mu - ex;
+        dlat[i * 3 * L + L + l] = w_kl * mu / (float)B;
+        dlat[i * 3 * L + 2 * L + l] = w_kl * (-0.5f) * (1.f - ex) / (float)B;
+      } else {
+        if (sigmoid) zz = 1.f / (1.f + expf(-mu));
+        dlat[i * 3 * L + L + l] = 0.f;
+        dlat[i * 3 * L + 2 * L + l] = 0.f;
+      }
+      z[e] = zz;
+      zs[e] = zz;
+    }
   }
   __syncthreads();
-  // latent consistency distances: kinds 0=lg 1=dg 2=dr 3=lr, pairs p<q, t
+  // latent consistency distances: kinds 0=lg 1=dg 2=dr 3=lr, pairs p<q, t.
+  // Each of the 4*npairs*bs distances is summed by 8 lanes (l = j, j+8, ..)
+  // and a 3-step shuffle tree (fixed order): 75-long serial loops were the
+  // latency of this single-workgroup kernel.
   const int npairs = bs * (bs - 1) / 2;
   const int lo = region_size > 0 ? (*key) * region_size : 0;
   const int hi = lo + region_size;
   const int nd = 4 * npairs * bs;
-  for (int e = tid; e < nd && w_lc != 0.f; e += blockDim.x) {
-    const int kind = e / (npairs * bs);
-    const int pr = (e / bs) % npairs;
-    const int t = e % bs;
-    int p = 0, rem = pr;  // decode pair index in triu order
-    while (rem >= bs - 1 - p) { rem -= bs - 1 - p; ++p; }
-    const int q = p + 1 + rem;
-    int ra, rb;
-    if (kind == 0 || kind == 2) { ra = q * bs + t; rb = p * bs + t; }  // same donor t
-    else { ra = t * bs + q; rb = t * bs + p; }                          // same base t
-    const bool in_region = (kind <= 1);
+  for (int e0 = 0; e0 < nd && w_lc != 0.f; e0 += blockDim.x / 8) {
+    const int e = e0 + tid / 8, j = tid % 8;
     float d = 0.f;
-    for (int l = 0; l < L; ++l) {
-      const bool inr = (l >= lo && l < hi);
-      if (inr != in_region) continue;
-      const float df = zs[ra * L + l] - zs[rb * L + l];
-      d = fmaf(df, df, d);
+    if (e < nd) {
+      const int kind = e / (npairs * bs);
+      const int pr = (e / bs) % npairs;
+      const int t = e % bs;
+      int p = 0, rem = pr;  // decode pair index in triu order
+      while (rem >= bs - 1 - p) { rem -= bs - 1 - p; ++p; }
+      const int q = p + 1 + rem;
+      int ra, rb;
+      if (kind == 0 || kind == 2) { ra = q * bs + t; rb = p * bs + t; }  // same donor t
+      else { ra = t * bs + q; rb = t * bs + p; }                          // same base t
+      const bool in_region = (kind <= 1);
+      for (int l = j; l < L; l += 8) {
+        const bool inr = (l >= lo && l < hi);
+        const float df = inr == in_region ? zs[ra * L + l] - zs[rb * L + l] : 0.f;
+        d = fmaf(df, df, d);
+      }
     }
-    dist[e] = d;
+    d += __shfl_xor(d, 1);
+    d += __shfl_xor(d, 2);
+    d += __shfl_xor(d, 4);
+    if (e < nd && j == 0) dist[e] = d;
   }
   __syncthreads();
   const float scale = 1.f / (float)(bs * bs * bs - bs * bs);
@@ -267,38 +292,45 @@ __global__ __launch_bounds__(256) void latent_fwd_k(const float* __restrict__ mu
     const float dr = dist[2 * npairs * bs + e], lr = dist[3 * npairs * bs + e];
     lc_part += fmaxf(0.f, lr - dr + eta2) + fmaxf(0.f, lg - dg + eta1);
   }
-  // gradient of LC w.r.t. z: thread per latent dim, fixed term order
-  if (tid < L) {
-    const int l = tid;
-    const bool inr = (l >= lo && l < hi);
-    float* col = cs + l;  // col[i * L] (LDS: a private array here would live in scratch)
-    for (int i = 0; i < B; ++i) col[i * L] = 0.f;
+  // gradient of LC w.r.t. z: one thread per (row i, dim l).  Row i = (ii, jj)
+  // (base ii, donor jj) appears in the hinge terms of the pairs that contain
+  // ii (same-donor distances, t = jj) and of those that contain jj
+  // (same-base distances, t = ii); the terms are added in a fixed order.
+  const float k2 = 2.f * scale * w_lc;
+  for (int e = tid; e < B * L; e += blockDim.x) {
+    const int i = e / L, l = e % L;
+    float g = 0.f;
     if (w_lc != 0.f) {
+      const bool inr = (l >= lo && l < hi);
+      const float s1 = inr ? 1.f : -1.f;  // lg - dg  vs  lr - dr
+      const int ii = i / bs, jj = i % bs;
       for (int pr = 0; pr < npairs; ++pr) {
         int p = 0, rem = pr;
         while (rem >= bs - 1 - p) { rem -= bs - 1 - p; ++p; }
         const int q = p + 1 + rem;
-        for (int t = 0; t < bs; ++t) {
-          const int e = pr * bs + t;
-          float act;
-          if (inr) act = (dist[0 * npairs * bs + e] - dist[1 * npairs * bs + e] + eta1) > 0.f;
-          else act = (dist[3 * npairs * bs + e] - dist[2 * npairs * bs + e] + eta2) > 0.f;
-          if (act == 0.f) continue;
-          const float k2 = 2.f * scale * w_lc;
-          // same-donor distance (lg or dr): + for inr, - for the complement
-          const int a1 = q * bs + t, b1 = p * bs + t;
-          const int a2 = t * bs + q, b2 = t * bs + p;
-          const float d1 = zs[a1 * L + l] - zs[b1 * L + l];
-          const float d2 = zs[a2 * L + l] - zs[b2 * L + l];
-          const float s1 = inr ? 1.f : -1.f;  // lg - dg  vs  lr - dr
-          col[a1 * L] += s1 * k2 * d1;
-          col[b1 * L] -= s1 * k2 * d1;
-          col[a2 * L] -= s1 * k2 * d2;
-          col[b2 * L] += s1 * k2 * d2;
+        // same-donor term (t = jj): rows a1 = q*bs + t, b1 = p*bs + t
+        if (ii == q || ii == p) {
+          const int de = pr * bs + jj;
+          const bool act = inr ? (dist[0 * npairs * bs + de] - dist[1 * npairs * bs + de] + eta1) > 0.f
+                               : (dist[3 * npairs * bs + de] - dist[2 * npairs * bs + de] + eta2) > 0.f;
+          if (act) {
+            const float d1 = zs[(q * bs + jj) * L + l] - zs[(p * bs + jj) * L + l];
+            g += (ii == q ? 1.f : -1.f) * s1 * k2 * d1;
+          }
+        }
+        // same-base term (t = ii): rows a2 = t*bs + q, b2 = t*bs + p
+        if (jj == q || jj == p) {
+          const int de = pr * bs + ii;
+          const bool act = inr ? (dist[0 * npairs * bs + de] - dist[1 * npairs * bs + de] + eta1) > 0.f
+                               : (dist[3 * npairs * bs + de] - dist[2 * npairs * bs + de] + eta2) > 0.f;
+          if (act) {
+            const float d2 = zs[(ii * bs + q) * L + l] - zs[(ii * bs + p) * L + l];
+            g -= (jj == q ? 1.f : -1.f) * s1 * k2 * d2;
+          }
         }
       }
     }
-    for (int i = 0; i < B; ++i) dlat[i * 3 * L + l] = col[i * L];
+    dlat[i * 3 * L + l] = g;
   }
   float2 r = block_sum2(kl_part, lc_part, red);
   if (tid == 0) {
@@ -657,10 +689,10 @@ extern "C" int cfsd_recon_lap_fwd(const float* pred, const float* gt, const int3
   return launch_status("recon_lap_fwd");
 }
 
-extern "C" int cfsd_recon_lap_bwd(const float* pred, const float* gt, const float* unit_lx,
-                                  const int32_t* lt_ptr, const int32_t* lt_col,
-                                  const float* lt_val, float* dpred, int batch, int nv, int c,
-                                  float w_rec, float w_lap, void* stream) {
+static int recon_lap_bwd_launch(const float* pred, const float* gt, const float* unit_lx,
+                                const int32_t* lt_ptr, const int32_t* lt_col, const float* lt_val,
+                                float* dpred, int batch, int nv, int c, float w_rec, float w_lap,
+                                const LossFinalize& fin, void* stream) {
   if (!pred || !gt || !unit_lx || !lt_ptr || !lt_col || !lt_val || !dpred)
     return set_error(CFSD_EINVAL, "recon_lap_bwd: null pointer");
   if (batch <= 0 || nv <= 0 || c <= 0 || c > 4) return set_error(CFSD_EINVAL, "recon_lap_bwd: bad sizes");
@@ -669,15 +701,37 @@ extern "C" int cfsd_recon_lap_bwd(const float* pred, const float* gt, const floa
   const float k_lap = w_lap / (float)((long)nv * batch);
   const dim3 grid((unsigned)((total + 255) / 256));
   const hipStream_t st = (hipStream_t)stream;
-  const LossFinalize none{};  // losses finalised by cfsd_loss_finalize
 #define RLB(C)                                                                                   \
   case C:                                                                                        \
     hipLaunchKernelGGL(recon_lap_bwd_k<C>, grid, dim3(256), 0, st, pred, gt, unit_lx, lt_ptr,    \
-                       lt_col, lt_val, dpred, nv, total, k_rec, k_lap, none);                    \
+                       lt_col, lt_val, dpred, nv, total, k_rec, k_lap, fin);                     \
     break;
   switch (c) { RLB(1) RLB(2) RLB(3) RLB(4) }
 #undef RLB
   return launch_status("recon_lap_bwd");
+}
+
+extern "C" int cfsd_recon_lap_bwd(const float* pred, const float* gt, const float* unit_lx,
+                                  const int32_t* lt_ptr, const int32_t* lt_col,
+                                  const float* lt_val, float* dpred, int batch, int nv, int c,
+                                  float w_rec, float w_lap, void* stream) {
+  const LossFinalize none{};  // losses finalised by cfsd_loss_finalize
+  return recon_lap_bwd_launch(pred, gt, unit_lx, lt_ptr, lt_col, lt_val, dpred, batch, nv, c, w_rec,
+                              w_lap, none, stream);
+}
+
+extern "C" int cfsd_recon_lap_bwd_finalize(const float* pred, const float* gt, const float* unit_lx,
+                                           const int32_t* lt_ptr, const int32_t* lt_col,
+                                           const float* lt_val, float* dpred, int batch, int nv,
+                                           int c, float w_rec, float w_lap, const float* partials,
+                                           int nblocks, const float* terms, float* out, float* acc,
+                                           float w_kl, float w_lc, void* stream) {
+  if (!partials || !terms || !out) return set_error(CFSD_EINVAL, "recon_lap_bwd_finalize: null pointer");
+  if (batch <= 0 || nv <= 0 || c <= 0) return set_error(CFSD_EINVAL, "recon_lap_bwd_finalize: bad sizes");
+  const LossFinalize fin{partials, nblocks, terms, out, acc, 1.f / (float)((long)batch * nv * c),
+                         1.f / (float)((long)nv * batch), w_kl, w_lc, w_lap};
+  return recon_lap_bwd_launch(pred, gt, unit_lx, lt_ptr, lt_col, lt_val, dpred, batch, nv, c, w_rec,
+                              w_lap, fin, stream);
 }
 
 extern "C" int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_t* key, float* z,

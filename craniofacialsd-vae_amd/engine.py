@@ -348,24 +348,35 @@ class SDVAEEngine:
                             self.params.view(f"de_layers.{n + 1}.layer.bias"), ACT_NONE, out=b.out,
                             workspace=b.ws)
 
-    def losses_fwd(self, b, acc=None):
+    def losses_fwd(self, b, acc=None, finalize=True):
         T = self.topo
         ops.recon_lap_fwd(b.out, b.x, T.lap_csr, b.unit, b.partials)
-        ops.loss_finalize(b.partials, b.terms, b.losses, acc, b.bsz, T.n_verts[0], self.spec.in_ch,
-                          self.w_kl, self.w_lc if self._lc_on(b) else 0.0, self.w_lap)
+        if finalize:
+            ops.loss_finalize(b.partials, b.terms, b.losses, acc, b.bsz, T.n_verts[0], self.spec.in_ch,
+                              self.w_kl, self.w_lc if self._lc_on(b) else 0.0, self.w_lap)
 
-    def forward(self, b, train=True, acc=None):
+    def forward(self, b, train=True, acc=None, finalize=True):
+        """``finalize=False``: the loss reduction is left to backward(), whose
+        first launch finalises it (one launch less per train step)."""
         self.encode(b)
         self.latent(b, train)
         self.decode(b)
         if self.topo.lap_csr is not None:
-            self.losses_fwd(b, acc)
+            self.losses_fwd(b, acc, finalize)
+        b.pending_finalize = (not finalize, acc)
 
     # ----------------------------------------------------------- backward
     def backward(self, b):
         T, S, P = self.topo, self.spec, self.params
         n = S.n
-        ops.recon_lap_bwd(b.out, b.x, b.unit, T.lapT_csr, b.dout, 1.0, self.w_lap)
+        pending, acc = getattr(b, "pending_finalize", (False, None))
+        if pending:
+            ops.recon_lap_bwd_finalize(b.out, b.x, b.unit, T.lapT_csr, b.dout, 1.0, self.w_lap,
+                                       b.partials, b.terms, b.losses, acc, self.w_kl,
+                                       self.w_lc if self._lc_on(b) else 0.0)
+            b.pending_finalize = (False, None)
+        else:
+            ops.recon_lap_bwd(b.out, b.x, b.unit, T.lapT_csr, b.dout, 1.0, self.w_lap)
         # final SpiralConv (no activation): dpre = dout
         last_in = b.dec_out[-1]
         # dX and dW/db of the output conv in one source-row pass.  Every conv
@@ -481,7 +492,7 @@ class SDVAEEngine:
     def train_step_on(self, b, acc=None, grad_hook=None, advance=True):
         """forward + losses + backward + (grad_hook, e.g. all-reduce) + Adam.
         ``advance=False`` when cfsd_step_begin already advanced Adam's t."""
-        self.forward(b, train=True, acc=acc)
+        self.forward(b, train=True, acc=acc, finalize=False)
         self.backward(b)
         if grad_hook is not None:
             grad_hook(self.params.grad)

@@ -302,6 +302,22 @@ def recon_lap_bwd(pred, gt, unit, lapT_csr, dpred, w_rec, w_lap):
          stream_ptr())
 
 
+def recon_lap_bwd_finalize(pred, gt, unit, lapT_csr, dpred, w_rec, w_lap, partials, terms, out, acc,
+                           w_kl, w_lc):
+    """recon_lap_bwd + loss_finalize in one launch (the last workgroup
+    finalises the losses of the preceding recon_lap_fwd)."""
+    bsz, nv, c = pred.shape
+    _need(dpred, (bsz, nv, c), name="dpred")
+    _need(lapT_csr[0], (nv + 1,), torch.int32, "lt_ptr")
+    _need(out, (5,), name="out")
+    if acc is not None:
+        _need(acc, (6,), name="acc")
+    call("cfsd_recon_lap_bwd_finalize", ptr(pred), ptr(gt), ptr(unit), ptr(lapT_csr[0]),
+         ptr(lapT_csr[1]), ptr(lapT_csr[2]), ptr(dpred), bsz, nv, c, float(w_rec), float(w_lap),
+         ptr(partials), partials.numel() // 2, ptr(terms), ptr(out), ptr(acc), float(w_kl),
+         float(w_lc), stream_ptr())
+
+
 def latent_fwd(mulv, eps, key, z, dlat, terms, latent, region_size, train, is_vae, sigmoid,
                w_kl, w_lc, eta1, eta2):
     bsz = z.shape[0]

@@ -172,6 +172,14 @@ int cfsd_recon_lap_bwd(const float* pred, const float* gt, const float* unit_lx,
                        const int32_t* lt_ptr, const int32_t* lt_col, const float* lt_val,
                        float* dpred, int batch, int nv, int c, float w_rec, float w_lap,
                        void* stream);
+/* cfsd_recon_lap_bwd with cfsd_loss_finalize folded into its last workgroup
+ * (same arguments as both; the partials were completed by the preceding
+ * cfsd_recon_lap_fwd on the stream): one launch less per train step. */
+int cfsd_recon_lap_bwd_finalize(const float* pred, const float* gt, const float* unit_lx,
+                                const int32_t* lt_ptr, const int32_t* lt_col, const float* lt_val,
+                                float* dpred, int batch, int nv, int c, float w_rec, float w_lap,
+                                const float* partials, int nblocks, const float* terms, float* out,
+                                float* acc, float w_kl, float w_lc, void* stream);
 
 /* Latent head, forward (model.py:146-160, 184-188; model_manager.py:352-393).
  * mulv [batch, 2*latent] = [logvar | mu] when is_vae (the two encoder Linears

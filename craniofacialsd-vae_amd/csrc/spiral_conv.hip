@@ -614,12 +614,13 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
 }
 
 // Backward data for layers with few source rows, same tiling as
-// conv_fwd_lat: a wave owns 16 source rows u x 16 input channels c and all
-// 9 slots.  A = T_s[u][o] (gather-sum of dpre rows through the inverse
+// conv_fwd_lat: a wave owns 16 source rows u x CTW*16 input channels c and
+// all 9 slots (CTW = 2 for 32 input channels: the list gathers of A are
+// shared by both column tiles).  A = T_s[u][o] (gather-sum of dpre rows through the inverse
 // spiral: the inv_head rows of a batch of 3 slots are loaded together,
 // rare further entries added after), B = W_s^T read straight from W (4
 // strided dwords per 4-chunk of o; W is L2-resident), in flight with A.
-template <int CIN, int COUT>
+template <int CIN, int COUT, int CTW>
 __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpre,
                                                    const int* __restrict__ inv_ptr,
                                                    const int* __restrict__ inv_row,
@@ -628,13 +629,14 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
                                                    const float* __restrict__ elu_y,
                                                    float* __restrict__ dx, int vsrc, int rows,
                                                    long total_rows) {
-  constexpr int CH = COUT / 16, NCT = CIN / 16, K = kSeq * CIN;
+  constexpr int CH = COUT / 16, NCT = CIN / 16, K = kSeq * CIN, NTW = NCT / CTW;
+  static_assert(NCT % CTW == 0, "column tiles per wave");
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
   const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const long n_rt = (total_rows + 15) / 16;
-  if (task >= n_rt * NCT) return;
-  const int ct = (int)(task % NCT);
-  const long rt = task / NCT;
+  if (task >= n_rt * NTW) return;
+  const int ct0 = (int)(task % NTW) * CTW;
+  const long rt = task / NTW;
   long m = rt * 16 + r16;
   if (m >= total_rows) m = total_rows - 1;
   const int b = (int)(m / vsrc), u = (int)(m % vsrc);
@@ -644,21 +646,25 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dpre), 0,
                                                       (int)(total_rows / vsrc * rows * RB), 0x00020000);
   const int4* pu = inv_head + (long)u * kSeq;
-  const float* wb = w + (long)(4 * kg) * K + ct * 16 + r16;  // + o_off*K + s*CIN
-  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  const float* wb = w + (long)(4 * kg) * K + ct0 * 16 + r16;  // + ct*16 + o_off*K + s*CIN
+  f32x4 acc[CTW][2];
+#pragma unroll
+  for (int t = 0; t < CTW; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s0 = 0; s0 < kSeq; s0 += kLatSB) {
     int4 pr[kLatSB];
 #pragma unroll
     for (int sl = 0; sl < kLatSB; ++sl) pr[sl] = pu[s0 + sl];
-    f32x4 bw[kLatSB][CH];
+    f32x4 bw[kLatSB][CH][CTW];
 #pragma unroll
     for (int sl = 0; sl < kLatSB; ++sl)
 #pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        const float* q = wb + (long)(16 * c) * K + (s0 + sl) * CIN;
-        bw[sl][c] = f32x4{q[0], q[K], q[2 * K], q[3 * K]};
-      }
+      for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int t = 0; t < CTW; ++t) {
+          const float* q = wb + (long)(16 * c) * K + (s0 + sl) * CIN + 16 * t;
+          bw[sl][c][t] = f32x4{q[0], q[K], q[2 * K], q[3 * K]};
+        }
     // list rows 0..2 of the batch's keys: unconditional buffer loads, absent
     // rows out of range (read as 0, no traffic), all in flight together
     f32x4 a[kLatSB][CH];
@@ -693,26 +699,30 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
 #pragma unroll
     for (int sl = 0; sl < kLatSB; ++sl)
 #pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        f32x4& ac = acc[c & 1];
-        ac = mfma16(a[sl][c].x, bw[sl][c].x, ac);
-        ac = mfma16(a[sl][c].y, bw[sl][c].y, ac);
-        ac = mfma16(a[sl][c].z, bw[sl][c].z, ac);
-        ac = mfma16(a[sl][c].w, bw[sl][c].w, ac);
-      }
-  }
-  const int c = ct * 16 + r16;
+      for (int c = 0; c < CH; ++c)
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const long mo = rt * 16 + 4 * kg + rr;
-    if (mo < total_rows) {
-      float v = acc[0][rr] + acc[1][rr];
-      if (elu_y) v *= elu_grad_from_out(elu_y[mo * CIN + c]);
-      dx[mo * CIN + c] = v;
+        for (int t = 0; t < CTW; ++t) {
+          f32x4& ac = acc[t][c & 1];
+          ac = mfma16(a[sl][c].x, bw[sl][c][t].x, ac);
+          ac = mfma16(a[sl][c].y, bw[sl][c][t].y, ac);
+          ac = mfma16(a[sl][c].z, bw[sl][c][t].z, ac);
+          ac = mfma16(a[sl][c].w, bw[sl][c][t].w, ac);
+        }
+  }
+#pragma unroll
+  for (int t = 0; t < CTW; ++t) {
+    const int c = (ct0 + t) * 16 + r16;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const long mo = rt * 16 + 4 * kg + rr;
+      if (mo < total_rows) {
+        float v = acc[t][0][rr] + acc[t][1][rr];
+        if (elu_y) v *= elu_grad_from_out(elu_y[mo * CIN + c]);
+        dx[mo * CIN + c] = v;
+      }
     }
   }
 }
-
 // Backward data, small dpre (CO <= 4 channels; the xyz output conv): one
 // thread per source row (b, u) computing all CIN outputs.  The spiral
 // transpose is first folded in the CO-wide dpre space,
@@ -830,8 +840,9 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
         const int s = f / (32 * CIN / 4);
         long m = m0 + row;
         if (m >= total_rows) m = total_rows - 1;
-        const int b = (int)(m / rows), r = (int)(m % rows);
-        const int src = idx[(long)r * kSeq + s];
+        const int mi = (int)m;  // < 2^31 rows: 32-bit division
+        const int b = mi / rows, r = mi - b * rows;
+        const int src = idx[r * kSeq + s];
         xs[e] = ld4(x + ((long)b * vsrc + src) * CIN + 4 * c4);
       }
     }
@@ -1886,8 +1897,17 @@ static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* in
   // measured on the 68k-row E1 dx: 33.8 us here vs 38.8 us persistent
   const long dpre_rows = M / vsrc * rows;
   if (M < CFSD_LAT_MAX_ROWS || (M < 80000 && 2 * dpre_rows <= M)) {
+    // 32 -> 32 with >= 32k rows: one wave covers both 16-column tiles (the
+    // list gathers are shared instead of repeated per column tile; measured
+    // E1 dx 33 -> 29 us; the fewer, fatter waves lose on the smaller levels)
+    if (CIN == 32 && COUT == 32 && M >= 32768) {
+      const long tasks = (M + 15) / 16;
+      hipLaunchKernelGGL((conv_dx_lat<CIN, COUT, CIN / 16>), dim3((unsigned)((tasks + 3) / 4)), dim3(256),
+                         0, st, dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M);
+      return launch_status("spiral_conv_bwd_data_lat");
+    }
     const long tasks = (M + 15) / 16 * (CIN / 16);
-    hipLaunchKernelGGL((conv_dx_lat<CIN, COUT>), dim3((unsigned)((tasks + 3) / 4)), dim3(256), 0, st,
+    hipLaunchKernelGGL((conv_dx_lat<CIN, COUT, 1>), dim3((unsigned)((tasks + 3) / 4)), dim3(256), 0, st,
                        dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M);
     return launch_status("spiral_conv_bwd_data_lat");
   }

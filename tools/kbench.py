@@ -86,6 +86,10 @@ def main():
     cases["dout_bwd_nodx"] = lambda: ops.spiral_conv_bwd(b.dec_out[3], T.spiral[0], b.dout, T.spiral_inv[0], wout,
                                                         P.gview("de_layers.5.layer.weight"),
                                                         P.gview("de_layers.5.layer.bias"), workspace=b.ws)
+    for lv in (1, 2, 3):  # Enblock data gradients (latency-shaped kernels)
+        cases[f"dx_e{lv}"] = (lambda lv=lv: ops.spiral_conv_bwd_data(
+            b.dpre_enc[lv], T.enc_inv[lv], eng._enc_w(lv)[0], T.n_verts[lv], elu_y=b.enc_out[lv - 1],
+            out=b.dpre_enc[lv - 1], workspace=b.ws))
     W_enc, B_enc = eng._enc_lin()
     gW_enc, gB_enc = eng._enc_lin(P.grad)
     flat = b.enc_out[3].view(16, -1)

@@ -68,10 +68,9 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
 #endif
-  const int q = (int)(t % c4);
-  const long br = t / c4;
-  const int r = (int)(br % m);
-  const int b = (int)(br / m);
+  int br, q, b, r;
+  divmod32(t, c4, br, q);
+  divmod32(br, m, b, r);
   const float* xb = x + (long)b * n * c4 * 4 + 4 * q;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const int beg = row_ptr[r], end = row_ptr[r + 1];
@@ -103,8 +102,8 @@ __global__ __launch_bounds__(256) void swap_k(const float* __restrict__ x,
                                               int bs, int nv, int c, long total) {
   long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
-  const int v = (int)(t % nv);
-  const int ob = (int)(t / nv);
+  int ob, v;
+  divmod32(t, nv, ob, v);
   const int i = ob / bs, j = ob % bs;
   const int k = *key;
   const bool take = (i != j) && mask[(long)k * nv + v];
@@ -136,6 +135,8 @@ extern "C" int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const f
   if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
     return set_error(CFSD_EINVAL, "spmm_csr: bad sizes batch=%d m=%d n=%d c=%d", batch, m, n, c);
   const long total = (long)batch * m * (c / 4);
+  if (total >= (1L << 31) || (long)batch * n >= (1L << 31))
+    return set_error(CFSD_EINVAL, "spmm_csr: batch x rows >= 2^31 (32-bit indices)");
 #if CFSD_SPMM_XCD
   const long per_grp = (total + 7) / 8;  // 8 XCD groups of equal block count
   const unsigned nblk = (unsigned)(8 * ((per_grp + 255) / 256));
@@ -155,6 +156,7 @@ extern "C" int cfsd_swap_features(const float* x, const int32_t* batch_idx,
   if (bs <= 0 || nv <= 0 || c <= 0 || n_meshes <= 0)
     return set_error(CFSD_EINVAL, "swap_features: bad sizes");
   const long total = (long)bs * bs * nv;
+  if (total >= (1L << 31)) return set_error(CFSD_EINVAL, "swap_features: bs^2 x nv >= 2^31");
   hipLaunchKernelGGL(swap_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, x, batch_idx, region_mask, key, out, bs, nv, c, total);
   return launch_status("swap_features");

@@ -93,7 +93,8 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(
     for (int rg = 0; rg < 2; ++rg) {
       long m = m0 + rg * 16 + r16;
       if (m >= total_rows) m = total_rows - 1;  // clamp loads, stores are masked
-      const int b = (int)(m / rows), r = (int)(m % rows);
+      int b, r;
+    divmod32(m, rows, b, r);
       xb[rg] = x + (long)b * vsrc * CIN + 4 * kg;
       const int* ir = idx + (long)r * kSeq + s0;
 #pragma unroll
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(256) void conv_combine(const float* __restrict__ ws
   f32x4 v = ld4(ws + 4 * t);
   for (int g = 1; g < groups; ++g) v += ld4(ws + (long)g * n4 * 4 + 4 * t);
   if (bias) {
-    const int c = (int)((4 * t) % cols);
+    const int c = (int)(4 * t) % cols;
     v.x += bias[c]; v.y += bias[c + 1]; v.z += bias[c + 2]; v.w += bias[c + 3];
   }
   if (ACT == CFSD_ACT_ELU) {
@@ -216,7 +217,8 @@ __global__ __launch_bounds__(256) void conv_fwd_in_small(const float* __restrict
   constexpr int K = kSeq * CS;
   const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= total_rows) return;
-  const int b = (int)(m / rows), r = (int)(m % rows);
+  int b, r;
+    divmod32(m, rows, b, r);
   const float* xb = x + (long)b * vsrc * CS;
   const int* ir = idx + (long)r * kSeq;
   float xv[K];
@@ -271,7 +273,8 @@ __global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restric
   for (long mm = ((long)blockIdx.x * 4 + wave) * RPW + slot; mm < n_rows_pad; mm += stride) {
     const bool valid = mm < total_rows;
     const long m = valid ? mm : total_rows - 1;
-    const int b = (int)(m / rows), r = (int)(m % rows);
+    int b, r;
+    divmod32(m, rows, b, r);
     const float* xb = x + (long)b * vsrc * CIN + 4 * q;
     const int* ir = idx + (long)r * kSeq;
     float acc[CO];
@@ -334,7 +337,8 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
   for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
     long m = tile * 32 + i;
     if (m >= total_rows) m = total_rows - 1;
-    const int b = (int)(m / rows), r = (int)(m % rows);
+    int b, r;
+    divmod32(m, rows, b, r);
     const float* xb = x + (long)b * vsrc * CS;
     const int* ir = idx + (long)r * kSeq;
     float g[2 * KH];
@@ -457,7 +461,8 @@ __global__ __launch_bounds__(256, dx_occ(CIN, COUT)) void conv_dx_mfma(
     const long m0 = tile * 32;
     long m = m0 + i;
     if (m >= total_rows) m = total_rows - 1;
-    const int b = (int)(m / vsrc), u = (int)(m % vsrc);
+    int b, u;
+    divmod32(m, vsrc, b, u);
     const int base = b * rows * RB + 16 * h;
     const int4* pu = inv_head + (long)u * kSeq + s0;
     auto roff = [&](int r) { return r >= 0 ? base + r * RB : kAbsentRow; };
@@ -567,7 +572,8 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
   const long rt = task / NCT;
   long m = rt * 16 + r16;
   if (m >= total_rows) m = total_rows - 1;  // clamp loads, stores are masked
-  const int b = (int)(m / rows), r = (int)(m % rows);
+  int b, r;
+    divmod32(m, rows, b, r);
   const float* xb = x + (long)b * vsrc * CIN + 4 * kg;
   const int* ir = idx + (long)r * kSeq;
   const float* wb = w + (long)(ct * 16 + r16) * K + 4 * kg;
@@ -639,7 +645,8 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
   const long rt = task / NTW;
   long m = rt * 16 + r16;
   if (m >= total_rows) m = total_rows - 1;
-  const int b = (int)(m / vsrc), u = (int)(m % vsrc);
+  int b, u;
+    divmod32(m, vsrc, b, u);
   const float* db_ = dpre + (long)b * rows * COUT + 4 * kg;
   constexpr int RB = COUT * (int)sizeof(float);
   const int base = (b * rows * COUT + 4 * kg) * (int)sizeof(float);
@@ -743,7 +750,8 @@ __global__ __launch_bounds__(256) void conv_dx_out_small(const float* __restrict
   constexpr int K = kSeq * CIN;
   const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= total_rows) return;
-  const int b = (int)(m / vsrc), u = (int)(m % vsrc);
+  int b, u;
+    divmod32(m, vsrc, b, u);
   const float* db_ = dpre + (long)b * rows * CO;
   const int4* pu = inv_head + (long)u * kSeq;
   int4 pr[kSeq];
@@ -1106,7 +1114,8 @@ __global__ __launch_bounds__(256) void conv_dw_in_small(const float* __restrict_
   for (int k = 0; k <= K; ++k) acc[k] = 0.f;
   const long stride = (long)gridDim.x * 4 * RPW;
   for (long m = ((long)blockIdx.x * 4 + wave) * RPW + slot; m < total_rows; m += stride) {
-    const int b = (int)(m / rows), r = (int)(m % rows);
+    int b, r;
+    divmod32(m, rows, b, r);
     const float d = dpre[m * COUT + o];
     const float* xb = x + (long)b * vsrc * CS;
 #pragma unroll
@@ -1163,7 +1172,8 @@ __global__ __launch_bounds__(256) void conv_dw_out_small(const float* __restrict
   for (int o = 0; o < CO; ++o) dbs[o] = 0.f;
   const long stride = (long)gridDim.x * 4 * RPW;
   for (long m = ((long)blockIdx.x * 4 + wave) * RPW + slot; m < total_rows; m += stride) {
-    const int b = (int)(m / rows), r = (int)(m % rows);
+    int b, r;
+    divmod32(m, rows, b, r);
     float d[CO];
 #pragma unroll
     for (int o = 0; o < CO; ++o) d[o] = dpre[m * CO + o];
@@ -1293,7 +1303,8 @@ __global__ __launch_bounds__(256) void conv_dw_in_mfma(const float* __restrict__
     const long m = tile * 64 + lane;
     const bool valid = m < total_rows;
     const long mm = valid ? m : total_rows - 1;
-    const int b = (int)(mm / rows), r = (int)(mm % rows);
+    int b, r;
+    divmod32(mm, rows, b, r);
     const float* xb = x + (long)b * vsrc * CS;
     const int* ir = idx + (long)r * kSeq;
     float xv[K];
@@ -1365,7 +1376,8 @@ __global__ __launch_bounds__(256) void conv_bwd_out_small(
     const long m = tile * 64 + lane;
     const bool valid = m < total_rows;
     const long mm = valid ? m : total_rows - 1;
-    const int b = (int)(mm / vsrc), u = (int)(mm % vsrc);
+    int b, u;
+    divmod32(mm, vsrc, b, u);
     const float* db_ = dpre + (long)b * rows * CO;
     const int4* pu = inv_head + (long)u * kSeq;
     int4 pr[kSeq];
@@ -1508,7 +1520,8 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     const long m = row0 + li;
     const bool valid = m < total_rows;
     const long mm = valid ? m : total_rows - 1;
-    const int b = (int)(mm / vsrc), u = (int)(mm % vsrc);
+    int b, u;
+    divmod32(mm, vsrc, b, u);
     const float* db_ = dpre + (long)b * rows * CO;
     const int4 none = make_int4(-1, -1, -1, -1);
     int4 pr[SPH];
@@ -1720,6 +1733,8 @@ static int check_conv_args(const void* a, const void* b, const void* c, int batc
     return set_error(CFSD_EINVAL, "non-positive size (batch=%d vsrc=%d rows=%d seq=%d cin=%d cout=%d)",
                      batch, vsrc, rows, seq, cin, cout);
   if (seq != kSeq) return set_error(CFSD_EINVAL, "spiral length %d unsupported (built for %d)", seq, kSeq);
+  if ((long)batch * (vsrc > rows ? vsrc : rows) >= (1L << 31))
+    return set_error(CFSD_EINVAL, "batch x vertices >= 2^31 (32-bit row indices)");
   return CFSD_OK;
 }
 

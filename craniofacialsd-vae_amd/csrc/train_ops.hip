@@ -110,8 +110,8 @@ __global__ __launch_bounds__(kLapThreads) void recon_lap_fwd_k(
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   float sq = 0.f, nrm = 0.f;
   if (t < total) {
-    const int v = (int)(t % nv);
-    const long b = t / nv;
+    int b, v;
+    divmod32(t, nv, b, v);
     float lx[C];
 #pragma unroll
     for (int q = 0; q < C; ++q) lx[q] = 0.f;
@@ -181,8 +181,8 @@ __global__ __launch_bounds__(256) void recon_lap_bwd_k(
   }
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
-  const int u = (int)(t % nv);
-  const long b = t / nv;
+  int b, u;
+  divmod32(t, nv, b, u);
   float g[C];
 #pragma unroll
   for (int q = 0; q < C; ++q) g[q] = 0.f;
@@ -676,6 +676,7 @@ extern "C" int cfsd_recon_lap_fwd(const float* pred, const float* gt, const int3
   if (!pred || !gt || !l_ptr || !l_col || !l_val || !unit_lx || !partials)
     return set_error(CFSD_EINVAL, "recon_lap_fwd: null pointer");
   if (batch <= 0 || nv <= 0 || c <= 0 || c > 4) return set_error(CFSD_EINVAL, "recon_lap_fwd: bad sizes");
+  if ((long)batch * nv * c >= (1L << 31)) return set_error(CFSD_EINVAL, "recon_lap_fwd: too large");
   const long total = (long)batch * nv;
   const dim3 grid(cfsd_recon_lap_blocks(batch, nv));
   const hipStream_t st = (hipStream_t)stream;
@@ -696,6 +697,7 @@ static int recon_lap_bwd_launch(const float* pred, const float* gt, const float*
   if (!pred || !gt || !unit_lx || !lt_ptr || !lt_col || !lt_val || !dpred)
     return set_error(CFSD_EINVAL, "recon_lap_bwd: null pointer");
   if (batch <= 0 || nv <= 0 || c <= 0 || c > 4) return set_error(CFSD_EINVAL, "recon_lap_bwd: bad sizes");
+  if ((long)batch * nv * c >= (1L << 31)) return set_error(CFSD_EINVAL, "recon_lap_bwd: too large");
   const long total = (long)batch * nv;
   const float k_rec = w_rec * 2.f / (float)(total * c);
   const float k_lap = w_lap / (float)((long)nv * batch);

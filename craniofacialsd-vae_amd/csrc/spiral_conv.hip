@@ -44,6 +44,17 @@ __device__ __forceinline__ TileSweep xcd_sweep(long n_tiles, int lanes_per_block
   return t;
 }
 
+// Non-persistent grids: renumber workgroups so that XCD x (hardware
+// dispatch is round-robin, x = blockIdx % 8) owns a CONTIGUOUS 1/8 of the
+// block range -- its meshes' rows then stay in its own L2.  Bijective for any
+// gridDim.
+__device__ __forceinline__ int xcd_block() {
+  const int nb = gridDim.x, bid = blockIdx.x;
+  if (nb < 8) return bid;
+  const int g = bid & 7, lb = bid >> 3, q = nb >> 3, rem = nb & 7;
+  return g * q + min(g, rem) + lb;
+}
+
 // Occupancy target per channel shape (min waves per SIMD -> VGPR budget).
 constexpr int mfma_occ(int cin, int cout) { return (cin == 32 && cout == 32) ? 4 : 2; }
 
@@ -249,7 +260,7 @@ __global__ __launch_bounds__(256) void conv_fwd_in_small(const float* __restrict
 // input channels of every neighbour row (one coalesced 16*L-byte read per
 // neighbour), the CO partial dots are reduced across the L lanes.
 template <int CIN, int CO, int ACT>
-__global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restrict__ x,
+__global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(const float* __restrict__ x,
                                                           const int* __restrict__ idx,
                                                           const float* __restrict__ w,
                                                           const float* __restrict__ bias,
@@ -260,17 +271,20 @@ __global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restric
   constexpr int K = kSeq * CIN;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane % L, slot = lane / L;
-  f32x4 wr[kSeq][CO];
-#pragma unroll
-  for (int s = 0; s < kSeq; ++s)
-#pragma unroll
-    for (int o = 0; o < CO; ++o) wr[s][o] = ld4(w + (long)o * K + s * CIN + 4 * q);
+  // Weights live in LDS (CO*K floats), not registers: 27 float4 of weights per
+  // lane capped occupancy at 3 waves/SIMD and this kernel is gather-latency bound.
+  __shared__ f32x4 lw[CO * K / 4];
+  for (int i = threadIdx.x; i < CO * K / 4; i += blockDim.x) lw[i] = ld4(w + 4 * i);
+  __syncthreads();
   float bo[CO];
 #pragma unroll
   for (int o = 0; o < CO; ++o) bo[o] = bias ? bias[o] : 0.f;
-  const long n_rows_pad = (total_rows + RPW - 1) / RPW * RPW;  // whole waves stay in the loop
-  const long stride = (long)gridDim.x * 4 * RPW;
-  for (long mm = ((long)blockIdx.x * 4 + wave) * RPW + slot; mm < n_rows_pad; mm += stride) {
+  // XCD-aware sweep over RPW-row groups: each XCD walks a contiguous 1/8 of
+  // the rows (two meshes at batch 16), so the neighbour rows a mesh gathers 9x
+  // stay in that XCD's L2 instead of every L2 seeing every mesh
+  const TileSweep sw = xcd_sweep((total_rows + RPW - 1) / RPW, 4, wave);
+  for (long grp = sw.begin; grp < sw.end; grp += sw.step) {  // whole waves stay in the loop
+    const long mm = grp * RPW + slot;
     const bool valid = mm < total_rows;
     const long m = valid ? mm : total_rows - 1;
     int b, r;
@@ -280,15 +294,18 @@ __global__ __launch_bounds__(256) void conv_fwd_out_small(const float* __restric
     float acc[CO];
 #pragma unroll
     for (int o = 0; o < CO; ++o) acc[o] = 0.f;
+    int wq = q;
+    asm volatile("" : "+v"(wq));  // opaque per iteration: keeps the weight reads from being hoisted into VGPRs
 #pragma unroll
     for (int s = 0; s < kSeq; ++s) {
       const f32x4 v = ld4(xb + (long)ir[s] * CIN);
 #pragma unroll
       for (int o = 0; o < CO; ++o) {
-        acc[o] = fmaf(v.x, wr[s][o].x, acc[o]);
-        acc[o] = fmaf(v.y, wr[s][o].y, acc[o]);
-        acc[o] = fmaf(v.z, wr[s][o].z, acc[o]);
-        acc[o] = fmaf(v.w, wr[s][o].w, acc[o]);
+        const f32x4 wv = lw[(o * K + s * CIN) / 4 + wq];
+        acc[o] = fmaf(v.x, wv.x, acc[o]);
+        acc[o] = fmaf(v.y, wv.y, acc[o]);
+        acc[o] = fmaf(v.z, wv.z, acc[o]);
+        acc[o] = fmaf(v.w, wv.w, acc[o]);
       }
     }
 #pragma unroll
@@ -565,7 +582,7 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
                                                     long total_rows) {
   constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN;
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
-  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long task = (long)xcd_block() * 4 + (threadIdx.x >> 6);
   const long n_rt = (total_rows + 15) / 16;
   if (task >= n_rt * NCT) return;
   const int ct = (int)(task % NCT);
@@ -638,7 +655,7 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
   constexpr int CH = COUT / 16, NCT = CIN / 16, K = kSeq * CIN, NTW = NCT / CTW;
   static_assert(NCT % CTW == 0, "column tiles per wave");
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
-  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long task = (long)xcd_block() * 4 + (threadIdx.x >> 6);
   const long n_rt = (total_rows + 15) / 16;
   if (task >= n_rt * NTW) return;
   const int ct0 = (int)(task % NTW) * CTW;
@@ -967,7 +984,7 @@ __global__ __launch_bounds__(256) void conv_dw_lat(const float* __restrict__ x,
                                                    int total_rows, int rchunk, int n_chunks) {
   constexpr int OT = COUT / 32, CT = CIN / 32, U = kSeq * OT * CT, NB = 8;
   const int lane = threadIdx.x & 63, li = lane & 31, h = lane >> 5;
-  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long task = (long)xcd_block() * 4 + (threadIdx.x >> 6);
   if (task >= (long)n_chunks * U) return;
   const int unit = (int)(task % U), chunk = (int)(task / U);
   const int ct = unit % CT, ot = (unit / CT) % OT, sl = unit / (CT * OT);
@@ -1475,6 +1492,26 @@ __global__ __launch_bounds__(256) void conv_bwd_out_small(
 // order acc_row(j, lane): the x values that feed B are then the same
 // registers the dx epilogue needs for elu'(y) when elu_y == x (the model's
 // case: the output conv's input is the last Deblock's ELU output).
+// CO (1..3) consecutive floats of one dpre row in ONE buffer load.
+template <int CO>
+__device__ __forceinline__ void load_row(__amdgpu_buffer_rsrc_t rsrc, int off, float (&v)[CO]) {
+  // (bit-cast whole vectors: a bit_cast of a vector ELEMENT lvalue miscompiles
+  // to element 0 on this clang)
+  if constexpr (CO == 3) {
+    typedef float f32x3 __attribute__((ext_vector_type(3)));
+    const f32x3 t = __builtin_bit_cast(f32x3, __builtin_amdgcn_raw_buffer_load_b96(rsrc, off, 0, 0));
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+  } else if constexpr (CO == 2) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 t = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0));
+    v[0] = t.x;
+    v[1] = t.y;
+  } else {
+    v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
+  }
+}
 constexpr int kAtS = 36;  // At row stride: conflict-free ds_read_b128 of the dW A operand
 #ifndef CFSD_BWD_OUT_OCC
 #define CFSD_BWD_OUT_OCC 1
@@ -1522,6 +1559,18 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     const long mm = valid ? m : total_rows - 1;
     int b, u;
     divmod32(mm, vsrc, b, u);
+    // x tile in accumulator-row order (B operand of dW, elu' source); issued
+    // first: independent of the inverse-spiral chain, so their latency hides
+    // behind it
+    float xv[NCT][16];
+    const float* xt = x + row0 * CIN + li;
+    const int last = (int)(total_rows - 1 - row0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int rr = min(acc_row(j, lane), last);  // clamped rows have a zero At column
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) xv[ct][j] = xt[rr * CIN + ct * 32];
+    }
     const float* db_ = dpre + (long)b * rows * CO;
     const int4 none = make_int4(-1, -1, -1, -1);
     int4 pr[SPH];
@@ -1542,9 +1591,9 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int off = hr[j] >= 0 ? base + hr[j] * CO * (int)sizeof(float) : kAbsentRow;
-#pragma unroll
-        for (int o = 0; o < CO; ++o)
-          v[j][o] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4 * o, 0, 0));
+        // one load per list row: the texture path costs a cycle per distinct
+        // cache line per instruction, so per-channel dword loads tripled it
+        load_row<CO>(rsrc, off, v[j]);
       }
 #pragma unroll
       for (int o = 0; o < CO; ++o) tt[sl][o] = (v[0][o] + v[1][o]) + v[2][o];
@@ -1570,17 +1619,6 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     if (h == 0) {  // slot 0 lists hold every output row once: db = sum_u t[0][o]
 #pragma unroll
       for (int o = 0; o < CO; ++o) dbs[o] += tt[0][o];
-    }
-    // x tile in accumulator-row order (B operand of dW, elu' source); its
-    // loads are in flight during the dx MFMAs
-    float xv[NCT][16];
-    const float* xt = x + row0 * CIN + li;
-    const int last = (int)(total_rows - 1 - row0);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int rr = min(acc_row(j, lane), last);  // clamped rows have a zero At column
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) xv[ct][j] = xt[rr * CIN + ct * 32];
     }
     // dx = T . Wt
     f32x16 dxacc[NCT];

@@ -77,6 +77,10 @@ def main():
     pair1 = ipair.clone()
     pair1[:, 1:] = -1
     inv_nomore = (ip, ir, pair1)
+    pair3 = ipair.clone()
+    pair3[:, 3] = -1
+    inv_now = (ip, ir, pair3)  # timing only: no rows 3.. (no exec branch)
+    cases["dx_d3_now"] = lambda: ops.spiral_conv_bwd_data(b.dpre_dec[3], inv_now, w3, T.n_verts[0], out=b.g_dec_up[3], workspace=b.ws)
     cases["dx_d3_noovf"] = lambda: ops.spiral_conv_bwd_data(b.dpre_dec[3], inv_noovf, w3, T.n_verts[0], out=b.g_dec_up[3], workspace=b.ws)
     cases["dx_d3_nomore"] = lambda: ops.spiral_conv_bwd_data(b.dpre_dec[3], inv_nomore, w3, T.n_verts[0], out=b.g_dec_up[3], workspace=b.ws)
     cases["dout_bwd_noovf"] = lambda: ops.spiral_conv_bwd(b.dec_out[3], T.spiral[0], b.dout, inv_noovf, wout,

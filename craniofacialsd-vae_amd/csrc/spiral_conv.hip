@@ -48,12 +48,12 @@ __device__ __forceinline__ TileSweep xcd_sweep(long n_tiles, int lanes_per_block
 // dispatch is round-robin, x = blockIdx % 8) owns a CONTIGUOUS 1/8 of the
 // block range -- its meshes' rows then stay in its own L2.  Bijective for any
 // gridDim.
-__device__ __forceinline__ int xcd_block() {
-  const int nb = gridDim.x, bid = blockIdx.x;
+__device__ __forceinline__ int xcd_block_of(int bid, int nb) {
   if (nb < 8) return bid;
   const int g = bid & 7, lb = bid >> 3, q = nb >> 3, rem = nb & 7;
   return g * q + min(g, rem) + lb;
 }
+__device__ __forceinline__ int xcd_block() { return xcd_block_of(blockIdx.x, gridDim.x); }
 
 // Occupancy target per channel shape (min waves per SIMD -> VGPR budget).
 constexpr int mfma_occ(int cin, int cout) { return (cin == 32 && cout == 32) ? 4 : 2; }
@@ -643,19 +643,21 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
 // spiral: the inv_head rows of a batch of 3 slots are loaded together,
 // rare further entries added after), B = W_s^T read straight from W (4
 // strided dwords per 4-chunk of o; W is L2-resident), in flight with A.
+// (body shared by the conv_dx_lat kernel and the dx half of
+// conv_bwd_lat_pair; vb / vnb = this workgroup's number / count in its grid)
 template <int CIN, int COUT, int CTW>
-__global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpre,
-                                                   const int* __restrict__ inv_ptr,
-                                                   const int* __restrict__ inv_row,
-                                                   const int4* __restrict__ inv_head,
-                                                   const float* __restrict__ w,
-                                                   const float* __restrict__ elu_y,
-                                                   float* __restrict__ dx, int vsrc, int rows,
-                                                   long total_rows) {
+__device__ __forceinline__ void conv_dx_lat_body(int vb, int vnb, const float* __restrict__ dpre,
+                                                 const int* __restrict__ inv_ptr,
+                                                 const int* __restrict__ inv_row,
+                                                 const int4* __restrict__ inv_head,
+                                                 const float* __restrict__ w,
+                                                 const float* __restrict__ elu_y,
+                                                 float* __restrict__ dx, int vsrc, int rows,
+                                                 long total_rows) {
   constexpr int CH = COUT / 16, NCT = CIN / 16, K = kSeq * CIN, NTW = NCT / CTW;
   static_assert(NCT % CTW == 0, "column tiles per wave");
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
-  const long task = (long)xcd_block() * 4 + (threadIdx.x >> 6);
+  const long task = (long)xcd_block_of(vb, vnb) * 4 + (threadIdx.x >> 6);
   const long n_rt = (total_rows + 15) / 16;
   if (task >= n_rt * NTW) return;
   const int ct0 = (int)(task % NTW) * CTW;
@@ -746,6 +748,18 @@ __global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpr
       }
     }
   }
+}
+template <int CIN, int COUT, int CTW>
+__global__ __launch_bounds__(256) void conv_dx_lat(const float* __restrict__ dpre,
+                                                   const int* __restrict__ inv_ptr,
+                                                   const int* __restrict__ inv_row,
+                                                   const int4* __restrict__ inv_head,
+                                                   const float* __restrict__ w,
+                                                   const float* __restrict__ elu_y,
+                                                   float* __restrict__ dx, int vsrc, int rows,
+                                                   long total_rows) {
+  conv_dx_lat_body<CIN, COUT, CTW>(blockIdx.x, gridDim.x, dpre, inv_ptr, inv_row, inv_head, w,
+                                   elu_y, dx, vsrc, rows, total_rows);
 }
 // Backward data, small dpre (CO <= 4 channels; the xyz output conv): one
 // thread per source row (b, u) computing all CIN outputs.  The spiral
@@ -976,15 +990,15 @@ __global__ __launch_bounds__(1024) void conv_dw_reduce(const float* __restrict__
 // db[chunk][COUT] (units with s == 0 && ct == 0 also sum dpre) -- the
 // conv_dw_mfma slab layout, reduced by conv_dw_reduce / dw_reduce_batch.
 template <int CIN, int COUT>
-__global__ __launch_bounds__(256) void conv_dw_lat(const float* __restrict__ x,
-                                                   const int* __restrict__ idx,
-                                                   const float* __restrict__ dpre,
-                                                   float* __restrict__ ws,
-                                                   float* __restrict__ ws_db, int vsrc, int rows,
-                                                   int total_rows, int rchunk, int n_chunks) {
+__device__ __forceinline__ void conv_dw_lat_body(int vb, int vnb, const float* __restrict__ x,
+                                                 const int* __restrict__ idx,
+                                                 const float* __restrict__ dpre,
+                                                 float* __restrict__ ws,
+                                                 float* __restrict__ ws_db, int vsrc, int rows,
+                                                 int total_rows, int rchunk, int n_chunks) {
   constexpr int OT = COUT / 32, CT = CIN / 32, U = kSeq * OT * CT, NB = 8;
   const int lane = threadIdx.x & 63, li = lane & 31, h = lane >> 5;
-  const long task = (long)xcd_block() * 4 + (threadIdx.x >> 6);
+  const long task = (long)xcd_block_of(vb, vnb) * 4 + (threadIdx.x >> 6);
   if (task >= (long)n_chunks * U) return;
   const int unit = (int)(task % U), chunk = (int)(task / U);
   const int ct = unit % CT, ot = (unit / CT) % OT, sl = unit / (CT * OT);
@@ -1043,6 +1057,63 @@ __global__ __launch_bounds__(256) void conv_dw_lat(const float* __restrict__ x,
     dbs += __shfl_xor(dbs, 32);
     if (h == 0) ws_db[(long)chunk * COUT + ot * 32 + li] = dbs;
   }
+}
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void conv_dw_lat(const float* __restrict__ x,
+                                                   const int* __restrict__ idx,
+                                                   const float* __restrict__ dpre,
+                                                   float* __restrict__ ws,
+                                                   float* __restrict__ ws_db, int vsrc, int rows,
+                                                   int total_rows, int rchunk, int n_chunks) {
+  conv_dw_lat_body<CIN, COUT>(blockIdx.x, gridDim.x, x, idx, dpre, ws, ws_db, vsrc, rows,
+                              total_rows, rchunk, n_chunks);
+}
+
+// Both gradients of one coarse-level conv in ONE launch (horizontal fusion):
+// the dx and dW workgroups are independent and each set alone fills only part
+// of the chip with latency-bound waves, so interleaving them (alternate
+// workgroups while both sets last) overlaps their memory latencies instead of
+// running two half-empty launches back to back.  Each half computes exactly
+// what conv_dx_lat / conv_dw_lat compute.
+struct DxLatArgs {
+  const float* dpre;
+  const int* inv_ptr;
+  const int* inv_row;
+  const int4* inv_head;
+  const float* w;
+  const float* elu_y;
+  float* dx;
+  int vsrc, rows;
+  long total_rows;
+  int nb;
+};
+struct DwLatArgs {
+  const float* x;
+  const int* idx;
+  const float* dpre;
+  float* ws;
+  float* ws_db;
+  int vsrc, rows, total_rows, rchunk, n_chunks;
+  int nb;
+};
+template <int CIN, int COUT, int CTW>
+__global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, const DwLatArgs d) {
+  const int bid = blockIdx.x, both = 2 * min(a.nb, d.nb);
+  bool is_dx;
+  int vb;
+  if (bid < both) {
+    is_dx = (bid & 1) == 0;
+    vb = bid >> 1;
+  } else {
+    is_dx = a.nb > d.nb;
+    vb = bid - both + both / 2;
+  }
+  if (is_dx)
+    conv_dx_lat_body<CIN, COUT, CTW>(vb, a.nb, a.dpre, a.inv_ptr, a.inv_row, a.inv_head, a.w,
+                                     a.elu_y, a.dx, a.vsrc, a.rows, a.total_rows);
+  else
+    conv_dw_lat_body<CIN, COUT>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows,
+                                d.total_rows, d.rchunk, d.n_chunks);
 }
 
 // Batched weight-gradient reduction: ONE launch reduces the deferred slab
@@ -1938,22 +2009,28 @@ static int launch_dx_mfma(const float* dpre, const int* inv_ptr, const int* inv_
   return launch_status("spiral_conv_bwd_data_combine");
 }
 
+// latency-shaped dx below ~64k dx rows (the persistent kernel cannot fill
+// the chip there without slot groups), and up to 80k rows when the conv was
+// evaluated on a row subset (Enblock: ~2.25 list entries per dx row instead
+// of 9; each persistent block would stage W for ~2 tiles) -- measured on the
+// 68k-row E1 dx: 33.8 us latency-shaped vs 38.8 us persistent
+static bool dx_is_lat(long m_dx, long dpre_rows) {
+  return m_dx < CFSD_LAT_MAX_ROWS || (m_dx < 80000 && 2 * dpre_rows <= m_dx);
+}
+// 32 -> 32 with >= 32k rows: one wave covers both 16-column tiles (the list
+// gathers are shared instead of repeated per column tile; measured E1 dx
+// 33 -> 29 us; the fewer, fatter waves lose on the smaller levels)
+static int dx_lat_ctw(int cin, int cout, long m_dx) {
+  return (cin == 32 && cout == 32 && m_dx >= 32768) ? 2 : 1;
+}
+
 template <int CIN, int COUT>
 static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* inv_row,
                             const int* inv_head, const float* w, const float* elu_y, float* dx,
                             float* ws, size_t ws_floats, int vsrc, int rows, long M,
                             hipStream_t st) {
-  // latency-shaped below ~64k dx rows (the persistent kernel cannot fill the
-  // chip there without slot groups), and up to 80k rows when the conv was
-  // evaluated on a row subset (Enblock: ~2.25 list entries per dx row
-  // instead of 9; each persistent block would stage W for ~2 tiles) --
-  // measured on the 68k-row E1 dx: 33.8 us here vs 38.8 us persistent
-  const long dpre_rows = M / vsrc * rows;
-  if (M < CFSD_LAT_MAX_ROWS || (M < 80000 && 2 * dpre_rows <= M)) {
-    // 32 -> 32 with >= 32k rows: one wave covers both 16-column tiles (the
-    // list gathers are shared instead of repeated per column tile; measured
-    // E1 dx 33 -> 29 us; the fewer, fatter waves lose on the smaller levels)
-    if (CIN == 32 && COUT == 32 && M >= 32768) {
+  if (dx_is_lat(M, M / vsrc * rows)) {
+    if (dx_lat_ctw(CIN, COUT, M) == 2) {
       const long tasks = (M + 15) / 16;
       hipLaunchKernelGGL((conv_dx_lat<CIN, COUT, CIN / 16>), dim3((unsigned)((tasks + 3) / 4)), dim3(256),
                          0, st, dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M);
@@ -2172,6 +2249,24 @@ int fused_small_gx(long m_src) {  // ~2 32-row tiles per wave
 }
 }  // namespace
 
+namespace {
+// Paired only for 32-wide dpre rows: the 64-wide dx body needs ~256 VGPRs,
+// which would cap the dW workgroups sharing the kernel at 1 wave per SIMD
+// (measured: dec 64->64 and E3 32->64 got 1-3 us slower paired, 64->32 and
+// E2 32->32 3-5 us faster).
+bool bwd_paired(int batch, int vsrc, int rows, int cin, int cout) {
+  if (!((cin == 32 || cin == 64) && cout == 32)) return false;
+  return dx_is_lat((long)batch * vsrc, (long)batch * rows) &&
+         dw_geom(batch, rows, cin, cout).kind == kDwLat;
+}
+}  // namespace
+
+extern "C" int cfsd_spiral_conv_bwd_paired(int batch, int vsrc, int rows, int seq, int cin,
+                                           int cout) {
+  if (batch <= 0 || vsrc <= 0 || rows <= 0 || seq != kSeq) return 0;
+  return bwd_paired(batch, vsrc, rows, cin, cout) ? 1 : 0;
+}
+
 extern "C" size_t cfsd_spiral_conv_bwd_workspace(int batch, int vsrc, int rows, int seq, int cin,
                                                  int cout) {
   if (batch <= 0 || vsrc <= 0 || rows <= 0 || seq != kSeq || cin <= 0 || cout <= 0) return 0;
@@ -2202,6 +2297,31 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
   if (workspace_bytes < need)
     return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
   hipStream_t st = (hipStream_t)stream;
+  if (dx && bwd_paired(batch, vsrc, rows, cin, cout)) {
+    const DwGeom g = dw_geom(batch, rows, cin, cout);
+    const long M = (long)batch * vsrc;
+    const long dw_tasks = (long)g.gx * dw_units(cin, cout);
+    float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
+    DxLatArgs a{dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M, 0};
+    DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, batch * rows, g.rchunk, g.gx,
+                (int)((dw_tasks + 3) / 4)};
+    const int ctw = dx_lat_ctw(cin, cout, M);
+    a.nb = (int)(((M + 15) / 16 * (cin / 16 / ctw) + 3) / 4);
+    const dim3 grid((unsigned)(a.nb + d.nb));
+    const int n_el = cout * kSeq * cin + cout;
+#define PAIR(CIN_, COUT_, CTW_)                                                                 \
+  if (cin == CIN_ && cout == COUT_ && ctw == CTW_) {                                            \
+    hipLaunchKernelGGL((conv_bwd_lat_pair<CIN_, COUT_, CTW_>), grid, dim3(256), 0, st, a, d);    \
+    rc = launch_status("spiral_conv_bwd_lat_pair");                                             \
+    if (rc || !dw) return rc;                                                                   \
+    hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), dim3((unsigned)((n_el + 63) / 64)),        \
+                       dim3(1024), 0, st, workspace, ws_db, dw, db, g.gx);                      \
+    return launch_status("spiral_conv_bwd_weight_reduce");                                      \
+  }
+    PAIR(32, 32, 1) PAIR(32, 32, 2) PAIR(64, 32, 1)
+#undef PAIR
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd: unsupported channels %d -> %d", cin, cout);
+  }
   if (!fused_small(cin, cout)) {
     if (dx) {
       rc = cfsd_spiral_conv_bwd_data(dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, workspace,

@@ -249,15 +249,23 @@ class SDVAEEngine:
         b.ws = torch.empty(ws // 4 + 64, dtype=torch.float32, device=dev)
         # weight-gradient partials: one region per layer, all reduced by ONE
         # cfsd_dw_reduce_batch launch at the end of the backward
+        # (coarse layers whose dx and dW run as one paired launch keep the
+        # paired call's workspace: dW slabs in the same region)
         regions = [("out", ops.spiral_conv_bwd_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0],
                                                          S.in_ch))]
+        b.paired = {}
+
+        def dw_region(key, vsrc, rows, seq, cin, cout, has_dx):
+            b.paired[key] = has_dx and ops.spiral_conv_bwd_paired(bsz, vsrc, rows, seq, cin, cout)
+            nb = (ops.spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout) if b.paired[key]
+                  else ops.spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout))
+            regions.append((key, nb))
+
         for i, (cin, cout, lv, _) in enumerate(S.dec_layers()):
-            regions.append((("dec", i), ops.spiral_conv_bwd_weight_workspace(bsz, nv[lv], T.seq[lv],
-                                                                             cin, cout)))
+            dw_region(("dec", i), nv[lv], nv[lv], T.seq[lv], cin, cout, True)
         for (cin, cout, lv) in S.enc_layers():
             rows = nv[lv + 1] if T.enc_select[lv] else nv[lv]
-            regions.append((("enc", lv), ops.spiral_conv_bwd_weight_workspace(bsz, rows, T.seq[lv],
-                                                                              cin, cout)))
+            dw_region(("enc", lv), nv[lv], rows, T.seq[lv], cin, cout, lv > 0)
         total = sum((nb // 4 + 64) // 64 * 64 for _, nb in regions)
         b.ws_dw_all = torch.empty(total, dtype=torch.float32, device=dev)
         b.ws_dw, off = {}, 0
@@ -412,10 +420,15 @@ class SDVAEEngine:
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]
             w, _ = self._dec_w(i)
-            defer(weight_grad(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
-                              b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
-            ops.spiral_conv_bwd_data(b.dpre_dec[i], T.spiral_inv[lv], w, T.n_verts[lv],
-                                     out=b.g_dec_up[i], workspace=b.ws)
+            if b.paired[("dec", i)]:  # dx + dW slabs in one launch
+                _, d = ops.spiral_conv_bwd(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_inv[lv],
+                                           w, None, None, dx=b.g_dec_up[i], workspace=b.ws_dw[("dec", i)])
+                defer(d, f"de_layers.{i + 1}.conv.layer")
+            else:
+                defer(weight_grad(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
+                                  b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
+                ops.spiral_conv_bwd_data(b.dpre_dec[i], T.spiral_inv[lv], w, T.n_verts[lv],
+                                         out=b.g_dec_up[i], workspace=b.ws)
             if i > 0:  # through Pool(up) into the previous Deblock's ELU
                 ops.spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], elu_y=b.dec_out[i - 1],
                          out=b.dpre_dec[i - 1])
@@ -444,11 +457,22 @@ class SDVAEEngine:
             w, _ = self._enc_w(lv)
             x_in = b.x if lv == 0 else b.enc_out[lv - 1]
             rows_tab = T.enc_rows[lv]
+            prev = lv - 1
+            if b.paired[("enc", lv)]:  # dx + dW slabs in one launch
+                sel = T.enc_select[prev]
+                _, d = ops.spiral_conv_bwd(x_in, rows_tab, b.dpre_enc[lv], T.enc_inv[lv], w, None, None,
+                                           dx=b.dpre_enc[prev] if sel else b.g_pooled[prev],
+                                           elu_y=b.enc_out[prev] if sel else None,
+                                           workspace=b.ws_dw[("enc", lv)])
+                defer(d, f"en_layers.{lv}.conv.layer")
+                if not sel:
+                    ops.spmm(T.downT_csr[prev], b.g_pooled[prev], T.n_verts[prev],
+                             elu_y=b.enc_full[prev], out=b.dpre_enc[prev])
+                continue
             defer(weight_grad(x_in, rows_tab, b.dpre_enc[lv], None, None,
                               b.ws_dw[("enc", lv)]), f"en_layers.{lv}.conv.layer")
             if lv == 0:
                 break
-            prev = lv - 1
             if T.enc_select[prev]:
                 # input of this conv IS the ELU output of the previous Enblock
                 ops.spiral_conv_bwd_data(b.dpre_enc[lv], T.enc_inv[lv], w, T.n_verts[lv],

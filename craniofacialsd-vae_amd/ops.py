@@ -146,6 +146,11 @@ def spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout):
     return int(_abi.lib().cfsd_spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout))
 
 
+def spiral_conv_bwd_paired(bsz, vsrc, rows, seq, cin, cout):
+    """True when spiral_conv_bwd (with dx) runs dx and dW as one paired launch."""
+    return bool(_abi.lib().cfsd_spiral_conv_bwd_paired(bsz, vsrc, rows, seq, cin, cout))
+
+
 def spiral_conv_bwd(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None):
     """Fused dX (skipped when ``dx`` is None) + dW/db of one SpiralConv; same
     results as spiral_conv_bwd_data followed by spiral_conv_bwd_weight."""

@@ -106,6 +106,9 @@ int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* stream);
  * xyz output conv) both come from ONE pass in source-row space: the spiral
  * transpose is folded in the 3-wide dpre space and dW is regrouped as
  * sum_{b,u} x[b,u,:] (x) t[b,u,s,:], so x is read densely, not gathered.
+ * For coarse layers where cfsd_spiral_conv_bwd_paired() is 1, dx and the dW
+ * slabs come from ONE launch whose workgroups interleave the two (same
+ * results as the separate calls).
  * workspace: cfsd_spiral_conv_bwd_workspace() bytes (shared by both stages). */
 int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const float* dpre,
                          const int32_t* inv_ptr, const int32_t* inv_row, const int32_t* inv_head,
@@ -113,6 +116,9 @@ int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const float* dpre,
                          float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows,
                          int seq, int cin, int cout, void* stream);
 size_t cfsd_spiral_conv_bwd_workspace(int batch, int vsrc, int rows, int seq, int cin, int cout);
+/* 1 when cfsd_spiral_conv_bwd with dx != NULL runs dx and dW as one paired
+ * launch for this shape (no reference counterpart: a scheduling query). */
+int cfsd_spiral_conv_bwd_paired(int batch, int vsrc, int rows, int seq, int cin, int cout);
 
 /* Materialising spiral gather, g[b,r,s*cin+c] = x[b, idx[r,s], c]
  * (model.py:34 index_select + view).  Used as the HBM-roofline probe. */

@@ -43,9 +43,11 @@ def dtopo(topo_npz):
 CONV_CASES = [(3, 32, 3, 3), (32, 32, 3, 3), (32, 64, 3, 3), (64, 32, 2, 3), (64, 64, 2, 3),
               (32, 3, 1, 2), (32, 32, 1, 2), (3, 32, 0, 2), (32, 3, 0, 2), (32, 32, 0, 2),
               (32, 32, 0, 4), (64, 32, 0, 4), (32, 64, 1, 16), (64, 64, 1, 16)]
+# forward-only: the VALU 3-channel output kernel at its other input widths
+FWD_ONLY_CASES = [(16, 3, 2, 2), (64, 3, 1, 2), (32, 3, 0, 16)]
 
 
-@pytest.mark.parametrize("cin,cout,level,bsz", CONV_CASES)
+@pytest.mark.parametrize("cin,cout,level,bsz", CONV_CASES + FWD_ONLY_CASES)
 @pytest.mark.parametrize("act", [0, 1])
 def test_spiral_conv_fwd(otopo, dtopo, cin, cout, level, bsz, act):
     g = torch.Generator().manual_seed(cin * 100 + cout + level)
@@ -105,7 +107,9 @@ def test_spiral_conv_bwd(otopo, dtopo, cin, cout, level, bsz, use_elu_y):
 
 
 @pytest.mark.parametrize("cin,cout,level,bsz", [(32, 3, 0, 2), (32, 3, 0, 16), (64, 3, 1, 5),
-                                                (32, 3, 3, 1), (32, 32, 1, 2), (64, 64, 2, 3)])
+                                                (32, 3, 3, 1), (32, 32, 1, 2), (64, 64, 2, 3),
+                                                (32, 1, 1, 2), (32, 2, 0, 2), (64, 1, 2, 3),
+                                                (64, 2, 1, 2)])
 @pytest.mark.parametrize("with_dx", [False, True])
 def test_spiral_conv_bwd_fused(otopo, dtopo, cin, cout, level, bsz, with_dx):
     """cfsd_spiral_conv_bwd (dX + dW/db in one call; source-row pass for 3-ch outputs)."""
@@ -133,6 +137,45 @@ def test_spiral_conv_bwd_fused(otopo, dtopo, cin, cout, level, bsz, with_dx):
     close(db, b.grad, 1e-5, "fused db")
     if with_dx:
         close(dx, dx_ref, 1e-5, "fused dx")
+
+
+# (table, level, cin, cout, batch): decoder tables and the Enblock row-subset
+# tables (E1 at batch 16 is the 2-column-tile dx shape)
+PAIR_CASES = [("dec", 1, 32, 32, 2), ("dec", 2, 64, 32, 3), ("dec", 3, 64, 32, 16), ("dec", 2, 64, 32, 16),
+              ("enc", 1, 32, 32, 16), ("enc", 2, 32, 32, 16), ("enc", 3, 32, 32, 16), ("enc", 1, 32, 32, 3)]
+
+
+@pytest.mark.parametrize("table,level,cin,cout,bsz", PAIR_CASES)
+def test_spiral_conv_bwd_paired_bit_exact(dtopo, table, level, cin, cout, bsz):
+    """The paired dx+dW launch (coarse layers) == the separate dx and dW
+    kernels, bit for bit, deferred slabs included."""
+    idx = dtopo.spiral[level] if table == "dec" else dtopo.enc_rows[level]
+    inv = dtopo.spiral_inv[level] if table == "dec" else dtopo.enc_inv[level]
+    vsrc, rows = dtopo.n_verts[level], idx.shape[0]
+    assert ops.spiral_conv_bwd_paired(bsz, vsrc, rows, 9, cin, cout)
+    g = torch.Generator(device=DEV).manual_seed(level * 10 + cin + cout + bsz)
+    x = torch.randn(bsz, vsrc, cin, device=DEV, generator=g)
+    y = torch.nn.functional.elu(x)
+    dpre = torch.randn(bsz, rows, cout, device=DEV, generator=g)
+    w = torch.randn(cout, 9 * cin, device=DEV, generator=g) * 0.1
+    ws_sz = ops.spiral_conv_bwd_workspace(bsz, vsrc, rows, 9, cin, cout)
+    ws = torch.zeros(ws_sz // 4 + 1, device=DEV)
+    dx_p = torch.full((bsz, vsrc, cin), float("nan"), device=DEV)
+    dw_p, db_p = torch.empty(cout, 9 * cin, device=DEV), torch.empty(cout, device=DEV)
+    ops.spiral_conv_bwd(y, idx, dpre, inv, w, dw_p, db_p, dx=dx_p, elu_y=y, workspace=ws)
+    dx_s = ops.spiral_conv_bwd_data(dpre, inv, w, vsrc, elu_y=y)
+    dw_s, db_s = torch.empty_like(dw_p), torch.empty_like(db_p)
+    ws2 = torch.zeros(ops.spiral_conv_bwd_weight_workspace(bsz, rows, 9, cin, cout) // 4 + 1, device=DEV)
+    ops.spiral_conv_bwd_weight(y, idx, dpre, dw_s, db_s, ws2)
+    assert torch.equal(dx_p, dx_s)
+    assert torch.equal(dw_p, dw_s) and torch.equal(db_p, db_s)
+    # deferred: slabs reduced by the batched reduce
+    ws.zero_()
+    dx_d = torch.empty_like(dx_p)
+    _, d = ops.spiral_conv_bwd(y, idx, dpre, inv, w, None, None, dx=dx_d, elu_y=y, workspace=ws)
+    dw_d, db_d = torch.empty_like(dw_p), torch.empty_like(db_p)
+    ops.dw_reduce_batch([(d, dw_d, db_d)])
+    assert torch.equal(dx_d, dx_s) and torch.equal(dw_d, dw_s) and torch.equal(db_d, db_s)
 
 
 @pytest.mark.parametrize("bsz", [2, 16])

@@ -1156,9 +1156,22 @@ __global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
     src = d.ws + f;
     stride = d.n_el;
   }
+  // slabs p = wv, wv + 16, ... summed in that order; 16 loads in flight per
+  // batch (the level-0 items have ~768 slabs: 48 per wave, which as a
+  // 4-unrolled chain was 12 memory latencies back to back)
   float sum = 0.f;
-#pragma unroll 4
-  for (int p = wv; p < d.n_slabs; p += 16) sum += src[(long)p * stride];
+  int p = wv;
+#ifndef CFSD_RED_BATCH
+#define CFSD_RED_BATCH 1
+#endif
+  for (; CFSD_RED_BATCH && p + 16 * 15 < d.n_slabs; p += 16 * 16) {
+    float t[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = src[(long)(p + 16 * j) * stride];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sum += t[j];
+  }
+  for (; p < d.n_slabs; p += 16) sum += src[(long)p * stride];
   part[wv][lane] = sum;
   __syncthreads();
   if (wv == 0 && valid) {

@@ -483,3 +483,24 @@ def test_deferred_weight_grads_batch_reduce(otopo, dtopo):
     torch.cuda.synchronize()
     for (d, dw, db), (rw, rb) in zip(items, refs):
         assert torch.equal(dw, rw) and torch.equal(db, rb)
+
+
+@pytest.mark.parametrize("n,wd", [(1, 0.0), (4099, 0.0), (1082403, 0.0), (1027, 1e-2)])
+def test_adam_matches_torch(n, wd):
+    """cfsd_adam == torch.optim.Adam (the reference's optimiser,
+    model_manager.py: torch.optim.Adam(lr, weight_decay)), 3 steps, vectorised
+    body + n % 4 tail."""
+    g = torch.Generator().manual_seed(n)
+    p0 = torch.randn(n, generator=g)
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.Adam([ref], lr=1e-3, weight_decay=wd, foreach=False)
+    p, m, v = p0.to(DEV), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for _ in range(3):
+        gr = torch.randn(n, generator=g)
+        ref.grad = gr.clone()
+        opt.step()
+        step += 1
+        ops.adam(p, gr.to(DEV), m, v, step, 1e-3, weight_decay=wd)
+    close(p, ref.detach(), 1e-6, "adam param")
+    close(m, opt.state[ref]["exp_avg"], 1e-6, "adam m")

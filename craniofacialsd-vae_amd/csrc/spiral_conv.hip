@@ -573,65 +573,75 @@ __global__ __launch_bounds__(256, dx_occ(CIN, COUT)) void conv_dx_mfma(
 // Tasks are numbered column-tile fastest, so the waves of a workgroup
 // gather the same rows (L1 hits).
 constexpr int kLatSB = 3;  // slots per batch
-template <int CIN, int COUT, int ACT>
+template <int CIN, int COUT, int ACT, int CTW>
 __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
                                                     const int* __restrict__ idx,
                                                     const float* __restrict__ w,
                                                     const float* __restrict__ bias,
                                                     float* __restrict__ y, int vsrc, int rows,
                                                     long total_rows) {
-  constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN;
+  // CTW column tiles per wave share the wave's A gathers
+  constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN, NTW = NCT / CTW;
+  static_assert(NCT % CTW == 0, "column tiles per wave");
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
   const long task = (long)xcd_block() * 4 + (threadIdx.x >> 6);
   const long n_rt = (total_rows + 15) / 16;
-  if (task >= n_rt * NCT) return;
-  const int ct = (int)(task % NCT);
-  const long rt = task / NCT;
+  if (task >= n_rt * NTW) return;
+  const int ct0 = (int)(task % NTW) * CTW;
+  const long rt = task / NTW;
   long m = rt * 16 + r16;
   if (m >= total_rows) m = total_rows - 1;  // clamp loads, stores are masked
   int b, r;
-    divmod32(m, rows, b, r);
+  divmod32(m, rows, b, r);
   const float* xb = x + (long)b * vsrc * CIN + 4 * kg;
   const int* ir = idx + (long)r * kSeq;
-  const float* wb = w + (long)(ct * 16 + r16) * K + 4 * kg;
+  const float* wb = w + (long)(ct0 * 16 + r16) * K + 4 * kg;  // + t*16*K
   int src[kSeq];
 #pragma unroll
   for (int s = 0; s < kSeq; ++s) src[s] = ir[s];
-  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  f32x4 acc[CTW][2];
+#pragma unroll
+  for (int t = 0; t < CTW; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s0 = 0; s0 < kSeq; s0 += kLatSB) {
-    f32x4 av[kLatSB][CH], bw[kLatSB][CH];
+    f32x4 av[kLatSB][CH], bw[kLatSB][CH][CTW];
 #pragma unroll
     for (int sl = 0; sl < kLatSB; ++sl)
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
         av[sl][c] = ld4(xb + (long)src[s0 + sl] * CIN + 16 * c);
-        bw[sl][c] = ld4(wb + (s0 + sl) * CIN + 16 * c);
+#pragma unroll
+        for (int t = 0; t < CTW; ++t) bw[sl][c][t] = ld4(wb + (long)t * 16 * K + (s0 + sl) * CIN + 16 * c);
       }
     // keep the batch's loads ahead of its MFMAs (hipcc otherwise interleaves
     // them with vmcnt waits to save registers, re-exposing the latency)
-    __builtin_amdgcn_sched_group_barrier(0x020, 2 * kLatSB * CH, 0);  // VMEM reads
-    __builtin_amdgcn_sched_group_barrier(0x008, 4 * kLatSB * CH, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x020, (1 + CTW) * kLatSB * CH, 0);  // VMEM reads
+    __builtin_amdgcn_sched_group_barrier(0x008, 4 * CTW * kLatSB * CH, 0);    // MFMA
 #pragma unroll
     for (int sl = 0; sl < kLatSB; ++sl)
 #pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        f32x4& a = acc[c & 1];
-        a = mfma16(av[sl][c].x, bw[sl][c].x, a);
-        a = mfma16(av[sl][c].y, bw[sl][c].y, a);
-        a = mfma16(av[sl][c].z, bw[sl][c].z, a);
-        a = mfma16(av[sl][c].w, bw[sl][c].w, a);
-      }
-  }
-  const int n = ct * 16 + r16;
-  const float bn = bias ? bias[n] : 0.f;
+      for (int c = 0; c < CH; ++c)
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const long mo = rt * 16 + 4 * kg + rr;
-    if (mo < total_rows) {
-      float v = acc[0][rr] + acc[1][rr] + bn;
-      if (ACT == CFSD_ACT_ELU) v = elu_f(v);
-      y[mo * COUT + n] = v;
+        for (int t = 0; t < CTW; ++t) {
+          f32x4& a = acc[t][c & 1];
+          a = mfma16(av[sl][c].x, bw[sl][c][t].x, a);
+          a = mfma16(av[sl][c].y, bw[sl][c][t].y, a);
+          a = mfma16(av[sl][c].z, bw[sl][c][t].z, a);
+          a = mfma16(av[sl][c].w, bw[sl][c][t].w, a);
+        }
+  }
+#pragma unroll
+  for (int t = 0; t < CTW; ++t) {
+    const int n = (ct0 + t) * 16 + r16;
+    const float bn = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const long mo = rt * 16 + 4 * kg + rr;
+      if (mo < total_rows) {
+        float v = acc[t][0][rr] + acc[t][1][rr] + bn;
+        if (ACT == CFSD_ACT_ELU) v = elu_f(v);
+        y[mo * COUT + n] = v;
+      }
     }
   }
 }
@@ -1920,9 +1930,16 @@ static int dispatch_fwd_mfma(const float* x, const int* idx, const float* w, con
                              hipStream_t st) {
   // (64 -> 32 excepted: measured slower there than slot groups + combine)
   if (M < CFSD_LAT_FWD_MAX && !(CIN == 64 && COUT == 32)) {
-    const long tasks = (M + 15) / 16 * (COUT / 16);
-    hipLaunchKernelGGL((conv_fwd_lat<CIN, COUT, ACT>), dim3((unsigned)((tasks + 3) / 4)), dim3(256),
-                       0, st, x, idx, w, bias, y, vsrc, rows, M);
+#ifndef CFSD_FWD_LAT_CTW
+#define CFSD_FWD_LAT_CTW 1
+#endif
+    // one wave per column tile: sharing the A gathers across both 32 -> 32
+    // column tiles (CTW 2) measured slower here (E1 16.8 vs 16.1 us, E2 11.0
+    // vs 7.8 us, same-box A/B) -- unlike the dx, whose A is a list gather-sum
+    constexpr int ctw = (CIN == 32 && COUT == 32) ? CFSD_FWD_LAT_CTW : 1;
+    const long tasks = (M + 15) / 16 * (COUT / 16 / ctw);
+    hipLaunchKernelGGL((conv_fwd_lat<CIN, COUT, ACT, ctw>), dim3((unsigned)((tasks + 3) / 4)),
+                       dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M);
     return launch_status("spiral_conv_fwd_lat");
   }
   constexpr bool big = (size_t)COUT * (kSeq * CIN + 8) * sizeof(float) > 80 * 1024;

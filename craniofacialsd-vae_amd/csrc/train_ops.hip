@@ -377,31 +377,39 @@ __global__ __launch_bounds__(256) void loss_finalize_k(const LossFinalize f) {
 // (deterministic), short ones run thread-per-output with the small operand
 // staged in LDS.
 // Row-group width of the block-reduction kernels (one accumulator per row).
-constexpr int kLinRG = 16;
+// Rows per block (blockIdx.y = row group).  The forward's 150 column blocks
+// leave most CUs idle: 4-row groups quadruple its blocks (9.8 -> 6.7 us,
+// same-box A/B); the decoder dx is bound by its strided W column reads, which
+// every row group would repeat (16: 10.7 us, 4: 10.7-11.7, 2: 15, 1: 23.6).
+// Each row's sum order is the same for any group width.
+constexpr int kLinRGFwd = 4;
+constexpr int kLinRGDx = 16;
+constexpr int kLinRG = kLinRGDx > kLinRGFwd ? kLinRGDx : kLinRGFwd;  // LDS sizing
 constexpr int kLinRedThreads = 512;   // block of the long-reduction kernels
 constexpr int kLinUnroll = 9;         // reduction terms per thread issued together
 
 // Sum kLinRG per-thread values over a kLinRedThreads block in fixed order
 // (wave butterfly, then waves in index order); thread i < kLinRG gets row i.
 // `sh` is [16 waves][kLinRG] LDS.
-__device__ __forceinline__ float block_rows_sum(float (&v)[kLinRG], float* sh) {
+template <int RG>
+__device__ __forceinline__ float block_rows_sum(float (&v)[RG], float* sh) {
   constexpr int kWaves = kLinRedThreads / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int i = 0; i < kLinRG; ++i) {
+  for (int i = 0; i < RG; ++i) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v[i] += __shfl_xor(v[i], d);
   }
   if (lane == 0) {
 #pragma unroll
-    for (int i = 0; i < kLinRG; ++i) sh[wave * kLinRG + i] = v[i];
+    for (int i = 0; i < RG; ++i) sh[wave * RG + i] = v[i];
   }
   __syncthreads();
   float r = 0.f;
-  if (threadIdx.x < kLinRG) {
+  if (threadIdx.x < RG) {
     r = sh[threadIdx.x];
 #pragma unroll
-    for (int w = 1; w < kWaves; ++w) r += sh[w * kLinRG + threadIdx.x];
+    for (int w = 1; w < kWaves; ++w) r += sh[w * RG + threadIdx.x];
   }
   __syncthreads();
   return r;
@@ -419,11 +427,11 @@ __global__ __launch_bounds__(kLinRedThreads) void linear_fwd_kred(const float* _
   __shared__ float sh[(kLinRedThreads / 64) * kLinRG];
   const int col = blockIdx.x;
   const float* wr = w + (long)col * k;
-  for (int i0 = 0; i0 < m; i0 += kLinRG) {
-    const int mr = min(kLinRG, m - i0);
-    float acc[kLinRG];
+  for (int i0 = blockIdx.y * kLinRGFwd; i0 < m; i0 += kLinRGFwd * gridDim.y) {
+    const int mr = min(kLinRGFwd, m - i0);
+    float acc[kLinRGFwd];
 #pragma unroll
-    for (int i = 0; i < kLinRG; ++i) acc[i] = 0.f;
+    for (int i = 0; i < kLinRGFwd; ++i) acc[i] = 0.f;
     for (int k0 = 0; k0 < k; k0 += kLinRedThreads * kLinUnroll) {
       float wv[kLinUnroll];
 #pragma unroll
@@ -432,7 +440,7 @@ __global__ __launch_bounds__(kLinRedThreads) void linear_fwd_kred(const float* _
         wv[u] = kk < k ? wr[kk] : 0.f;
       }
 #pragma unroll
-      for (int i = 0; i < kLinRG; ++i) {
+      for (int i = 0; i < kLinRGFwd; ++i) {
         const float* xr = x + (long)(i0 + min(i, mr - 1)) * k;
         float xv[kLinUnroll];
 #pragma unroll
@@ -444,7 +452,7 @@ __global__ __launch_bounds__(kLinRedThreads) void linear_fwd_kred(const float* _
         for (int u = 0; u < kLinUnroll; ++u) acc[i] = fmaf(xv[u], wv[u], acc[i]);
       }
     }
-    const float r = block_rows_sum(acc, sh);
+    const float r = block_rows_sum<kLinRGFwd>(acc, sh);
     if (threadIdx.x < mr) y[(long)(i0 + threadIdx.x) * n + col] = r + (bias ? bias[col] : 0.f);
   }
 }
@@ -531,11 +539,11 @@ __global__ __launch_bounds__(kLinRedThreads) void linear_dx_nred(const float* __
                                                                  int k, int n, int accumulate) {
   __shared__ float sh[(kLinRedThreads / 64) * kLinRG];
   const int kk = blockIdx.x;
-  for (int i0 = 0; i0 < m; i0 += kLinRG) {
-    const int mr = min(kLinRG, m - i0);
-    float acc[kLinRG];
+  for (int i0 = blockIdx.y * kLinRGDx; i0 < m; i0 += kLinRGDx * gridDim.y) {
+    const int mr = min(kLinRGDx, m - i0);
+    float acc[kLinRGDx];
 #pragma unroll
-    for (int i = 0; i < kLinRG; ++i) acc[i] = 0.f;
+    for (int i = 0; i < kLinRGDx; ++i) acc[i] = 0.f;
     for (int c0 = 0; c0 < n; c0 += kLinRedThreads * kLinUnroll) {
       float wv[kLinUnroll];
 #pragma unroll
@@ -544,7 +552,7 @@ __global__ __launch_bounds__(kLinRedThreads) void linear_dx_nred(const float* __
         wv[u] = c < n ? w[(long)c * k + kk] : 0.f;
       }
 #pragma unroll
-      for (int i = 0; i < kLinRG; ++i) {
+      for (int i = 0; i < kLinRGDx; ++i) {
         const float* dr = dy + (long)(i0 + min(i, mr - 1)) * n;
         float dv[kLinUnroll];
 #pragma unroll
@@ -556,7 +564,7 @@ __global__ __launch_bounds__(kLinRedThreads) void linear_dx_nred(const float* __
         for (int u = 0; u < kLinUnroll; ++u) acc[i] = fmaf(dv[u], wv[u], acc[i]);
       }
     }
-    float r = block_rows_sum(acc, sh);
+    float r = block_rows_sum<kLinRGDx>(acc, sh);
     if (threadIdx.x < mr) {
       const long o = (long)(i0 + threadIdx.x) * k + kk;
       if (elu_y) r *= elu_grad_from_out(elu_y[o]);
@@ -809,7 +817,7 @@ extern "C" int cfsd_linear_fwd(const float* x, const float* w, const float* bias
   (void)workspace_bytes;
   hipStream_t st = (hipStream_t)stream;
   if (k > kLinSmallK) {
-    hipLaunchKernelGGL(linear_fwd_kred, dim3(n), dim3(kLinRedThreads), 0, st, x, w, bias, y, m, k,
+    hipLaunchKernelGGL(linear_fwd_kred, dim3(n, (m + kLinRGFwd - 1) / kLinRGFwd), dim3(kLinRedThreads), 0, st, x, w, bias, y, m, k,
                        n);
     return launch_status("linear_fwd_kred");
   }
@@ -835,7 +843,7 @@ extern "C" int cfsd_linear_bwd(const float* x, const float* w, const float* dy, 
                          w, elu_y, dx, m, k, n, accumulate);
       rc = launch_status("linear_dx_nsmall");
     } else {
-      hipLaunchKernelGGL(linear_dx_nred, dim3(k), dim3(kLinRedThreads), 0, st, dy, w, elu_y, dx, m,
+      hipLaunchKernelGGL(linear_dx_nred, dim3(k, (m + kLinRGDx - 1) / kLinRGDx), dim3(kLinRedThreads), 0, st, dy, w, elu_y, dx, m,
                          k, n, accumulate);
       rc = launch_status("linear_dx_nred");
     }

@@ -53,6 +53,7 @@ SIGNATURES = {
     "cfsd_dw_reduce_batch": (_I, [_P, _I, _P]),
     "cfsd_scale": (_I, [_P, _Z, _F, _P]),
     "cfsd_elu_bwd": (_I, [_P, _P, _P, _Z, _P]),
+    "cfsd_vertex_errors": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P]),
 }
 
 

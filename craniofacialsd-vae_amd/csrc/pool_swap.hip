@@ -124,9 +124,76 @@ __global__ void elu_bwd_k(const float* __restrict__ dy, const float* __restrict_
   if (t < n) dx[t] = dy[t] * elu_grad_from_out(y[t]);
 }
 
+// Per-vertex reconstruction errors (model_manager.py:395-400, test.py:81-84,
+// 280-301).  One thread per vertex row of 3 channels: optional
+// un-normalisation (x*std + mean, rounded separately as torch does), then
+// err = sqrt(((d0^2 + d1^2) + d2^2)) * to_mm and l1 = |d0| + |d1| + |d2|.
+__global__ void vertex_errors_k(const float* __restrict__ out, const float* __restrict__ gt,
+                                const float* __restrict__ mean, const float* __restrict__ std,
+                                float* __restrict__ err, float* __restrict__ l1, int nv,
+                                long total, float to_mm) {
+#pragma clang fp contract(off)
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int v = (int)t % nv;  // total * 3 < 2^31 (checked at the ABI)
+  float a[3], g[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    a[q] = out[t * 3 + q];
+    g[q] = gt[t * 3 + q];
+  }
+  if (mean) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const float s = std[v * 3 + q], m = mean[v * 3 + q];
+      a[q] = a[q] * s + m;
+      g[q] = g[q] * s + m;
+    }
+  }
+  const float d0 = a[0] - g[0], d1 = a[1] - g[1], d2 = a[2] - g[2];
+  if (err) err[t] = sqrtf(d0 * d0 + d1 * d1 + d2 * d2) * to_mm;
+  if (l1) l1[t] = fabsf(d0) + fabsf(d1) + fabsf(d2);
+}
+
+// Per-mesh mean of the vertex errors (test.py:297 torch.mean(errors, dim=1)):
+// one 256-thread workgroup per mesh, strided partial sums reduced in a fixed
+// tree (deterministic; summation order differs from torch's CPU reduction).
+__global__ void __launch_bounds__(256) row_mean_k(const float* __restrict__ err,
+                                                  float* __restrict__ mesh_mean, int nv) {
+  __shared__ float part[256];
+  const float* row = err + (long)blockIdx.x * nv;
+  float acc = 0.f;
+  for (int v = threadIdx.x; v < nv; v += 256) acc += row[v];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) mesh_mean[blockIdx.x] = part[0] / (float)nv;
+}
+
 }  // namespace cfsd
 
 using namespace cfsd;
+
+extern "C" int cfsd_vertex_errors(const float* out, const float* gt, const float* mean,
+                                  const float* std, float* err, float* l1, float* mesh_mean,
+                                  int batch, int nv, float to_mm, void* stream) {
+  if (!out || !gt) return set_error(CFSD_EINVAL, "vertex_errors: null pointer");
+  if (!mean != !std) return set_error(CFSD_EINVAL, "vertex_errors: mean and std go together");
+  if (mesh_mean && !err) return set_error(CFSD_EINVAL, "vertex_errors: mesh_mean needs err");
+  if (batch <= 0 || nv <= 0) return set_error(CFSD_EINVAL, "vertex_errors: bad sizes");
+  const long total = (long)batch * nv;
+  if (total * 3 >= (1L << 31)) return set_error(CFSD_EINVAL, "vertex_errors: batch x nv too large");
+  if (!err && !l1) return CFSD_OK;
+  hipLaunchKernelGGL(vertex_errors_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, out, gt, mean, std, err, l1, nv, total, to_mm);
+  if (mesh_mean)
+    hipLaunchKernelGGL(row_mean_k, dim3((unsigned)batch), dim3(256), 0, (hipStream_t)stream, err,
+                       mesh_mean, nv);
+  return launch_status("vertex_errors");
+}
 
 extern "C" int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const float* val,
                              const float* x, const float* elu_y, float* y, int batch, int m,

@@ -378,3 +378,40 @@ def step_begin(counter, seed, eps=None, key=None, n_regions=0, batch_idx=None, b
 def scale(y, alpha):
     _need(y, None, name="y")
     call("cfsd_scale", ptr(y), ctypes.c_size_t(y.numel()), float(alpha), stream_ptr())
+
+
+# ------------------------------------------------------------------ evaluation
+def vertex_errors(out, gt, to_mm=89.11, mean=None, std=None, want_l1=False, want_mesh_mean=False):
+    """``ModelManager.compute_vertex_errors`` (``model_manager.py:395-400``) on
+    device: ``sqrt(sum_c (out - gt)^2) * to_mm`` per vertex, ``[B, V]``.
+
+    ``mean``/``std`` ``[V, 3]`` un-normalise both inputs first
+    (``Tester._unnormalize_verts``, ``test.py:81-84``).  ``want_l1`` also
+    returns the per-vertex L1 ``sum_c |out - gt|``; ``want_mesh_mean`` the
+    per-mesh mean used by ``Tester.reconstruction_errors`` (``test.py:297``).
+    Returns ``err`` or a tuple ``(err, l1?, mesh_mean?)``."""
+    _need(out, None, name="out")
+    if out.dim() != 3 or out.shape[-1] != 3:
+        raise ValueError(f"out: shape {tuple(out.shape)}, expected [B, V, 3]")
+    bsz, nv = int(out.shape[0]), int(out.shape[1])
+    _need(gt, tuple(out.shape), name="gt")
+    if (mean is None) != (std is None):
+        raise ValueError("mean and std go together")
+    if mean is not None:
+        _need(mean, (nv, 3), name="mean")
+        _need(std, (nv, 3), name="std")
+    err = torch.empty((bsz, nv), dtype=torch.float32, device=out.device)
+    l1 = torch.empty_like(err) if want_l1 else None
+    mm = torch.empty((bsz,), dtype=torch.float32, device=out.device) if want_mesh_mean else None
+    call("cfsd_vertex_errors", ptr(out), ptr(gt), ptr(mean), ptr(std), ptr(err), ptr(l1),
+         ptr(mm), bsz, nv, float(to_mm), stream_ptr())
+    if not (want_l1 or want_mesh_mean):
+        return err
+    return (err,) + ((l1,) if want_l1 else ()) + ((mm,) if want_mesh_mean else ())
+
+
+def reconstruction_error_stats(mesh_means):
+    """The summary of ``Tester.reconstruction_errors`` (``test.py:298-301``)
+    over the concatenated per-mesh means (device tensor, torch reductions)."""
+    return {"mean": torch.mean(mesh_means).item(), "median": torch.median(mesh_means).item(),
+            "max": torch.max(mesh_means).item(), "std": torch.std(mesh_means).item()}

@@ -239,6 +239,18 @@ int cfsd_elu_bwd(const float* dy, const float* y, float* dx, size_t n, void* str
 /* Element-wise y *= alpha (gradient averaging after an all-reduce). */
 int cfsd_scale(float* y, size_t n, float alpha, void* stream);
 
+/* ---------------------------------------------------------------- evaluation
+ * Replaces ModelManager.compute_vertex_errors (model_manager.py:395-400) and
+ * the per-mesh reduction of Tester.reconstruction_errors (test.py:280-301):
+ * out, gt [batch, nv, 3]; mean/std [nv, 3] (both NULL = no un-normalisation,
+ * else u = x*std + mean as Tester._unnormalize_verts, test.py:81-84);
+ *   err[b, v]  = sqrt(sum_c (u_out - u_gt)^2) * to_mm        (may be NULL)
+ *   l1[b, v]   = sum_c |u_out - u_gt|  (the per-vertex L1 parity metric; may be NULL)
+ *   mesh_mean[b] = mean_v err[b, v]  (fixed-order reduction; needs err; may be NULL). */
+int cfsd_vertex_errors(const float* out, const float* gt, const float* mean, const float* std,
+                       float* err, float* l1, float* mesh_mean, int batch, int nv, float to_mm,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

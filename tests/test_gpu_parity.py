@@ -504,3 +504,56 @@ def test_adam_matches_torch(n, wd):
         ops.adam(p, gr.to(DEV), m, v, step, 1e-3, weight_decay=wd)
     close(p, ref.detach(), 1e-6, "adam param")
     close(m, opt.state[ref]["exp_avg"], 1e-6, "adam m")
+
+
+# --------------------------------------------------------------- evaluation (a17, f4)
+@pytest.mark.parametrize("bsz,nv,normalise", [(1, 67, False), (3, 1065, True), (16, 17039, False)])
+def test_vertex_errors_vs_oracle(bsz, nv, normalise):
+    """cfsd_vertex_errors vs ``compute_vertex_errors`` (model_manager.py:395-400,
+    oracle.vertex_errors) and the per-mesh mean of test.py:297.  Tolerance:
+    rel. 1e-6 per vertex (same fp32 operation order, contraction off), 1e-6 for
+    the mesh mean (fixed-order tree vs torch's CPU reduction)."""
+    g = torch.Generator().manual_seed(bsz * 7 + nv)
+    out = torch.randn(bsz, nv, 3, generator=g)
+    gt = torch.randn(bsz, nv, 3, generator=g)
+    mean = torch.randn(nv, 3, generator=g) if normalise else None
+    std = torch.rand(nv, 3, generator=g) + 0.5 if normalise else None
+    ro, rg = (out * std + mean, gt * std + mean) if normalise else (out, gt)
+    ref = O.vertex_errors(ro, rg, to_mm=89.11)
+    dev = (lambda t: None if t is None else t.to(DEV))
+    err, l1, mm = ops.vertex_errors(out.to(DEV), gt.to(DEV), to_mm=89.11, mean=dev(mean),
+                                    std=dev(std), want_l1=True, want_mesh_mean=True)
+    torch.cuda.synchronize()
+    close(err, ref, rel=1e-6, what="vertex err (mm)")
+    close(l1, (ro - rg).abs().sum(-1), rel=1e-6, what="per-vertex L1")
+    close(mm, torch.mean(ref, dim=1), rel=1e-6, what="per-mesh mean")
+
+
+def test_reconstruction_errors_c1(dtopo):
+    """Tester.reconstruction_errors (test.py:280-301) on the C1 demo batch:
+    device recon + un-normalised device errors vs the oracle's errors of the
+    reference's golden reconstruction (mm, 1e-2 mm absolute: the recon itself
+    differs by <= 1e-4 normalised units per vertex)."""
+    m = np.load(f"{recipe.HERE}/demo_meshes.npz")
+    g = np.load(f"{recipe.HERE}/golden_eval.npz")
+    eng = make_engine(dtopo, recipe.golden_weights())
+    x = torch.from_numpy(recipe.normalized_meshes(8)).to(DEV)
+    b = eng.set_batch(x)
+    eng.forward(b, train=False)
+    mean = torch.from_numpy(m["norm_mean"]).float().contiguous()
+    std = torch.from_numpy(m["norm_std"]).float().contiguous()
+    err, l1, mm = ops.vertex_errors(b.out.contiguous(), x, mean=mean.to(DEV), std=std.to(DEV),
+                                    want_l1=True, want_mesh_mean=True)
+    stats = ops.reconstruction_error_stats(mm)
+    xr = torch.from_numpy(recipe.normalized_meshes(8))
+    rec = torch.from_numpy(g["recon"])
+    ref = O.vertex_errors(rec * std + mean, xr * std + mean)
+    ref_mm = torch.mean(ref, dim=1)
+    assert np.abs(err.cpu().numpy() - ref.numpy()).max() <= 1e-2
+    assert abs(stats["mean"] - torch.mean(ref_mm).item()) <= 1e-3
+    assert abs(stats["max"] - torch.max(ref_mm).item()) <= 1e-3
+    assert abs(stats["median"] - torch.median(ref_mm).item()) <= 1e-3
+    assert np.isfinite(stats["std"])
+    # the same kernel's L1 term on normalised units against the golden recon
+    _, l1n = ops.vertex_errors(b.out.contiguous(), rec.to(DEV), want_l1=True)
+    assert l1n.max().item() <= 1e-4

@@ -188,6 +188,101 @@ class SDVAEEngine:
     def grads(self):
         return {k: self.params.gview(k) for k, _ in self.params.specs}
 
+    # ----------------------------------------------------------- evaluation
+    def encode_all(self, meshes, batch_size=16):
+        """``ModelManager.encode_all`` / ``encode`` (``model_manager.py:244-246,
+        402-426``): eval-mode latents (mu; sigmoid(mu) for a pre_z_sigmoid AE)
+        of device meshes ``[N, V, 3]`` (already un-swapped), in batches
+        (ragged tail allowed).  Returns a device tensor ``[N, latent]``."""
+        out = []
+        for s in range(0, meshes.shape[0], batch_size):
+            b = self.set_batch(meshes[s:s + batch_size])
+            self.encode(b)
+            self.latent(b, train=False)
+            out.append(b.z.clone())
+        return torch.cat(out, dim=0)
+
+    @staticmethod
+    def latent_stats(latents):
+        """``Tester.compute_latent_stats`` (``test.py:95-117``) of device
+        latents: per-dimension means / stds / mins / maxs (torch reductions)."""
+        return {"means": torch.mean(latents, dim=0), "stds": torch.std(latents, dim=0),
+                "mins": torch.min(latents, dim=0)[0], "maxs": torch.max(latents, dim=0)[0]}
+
+    # ----------------------------------------------------------- checkpoints
+    def optimizer_state_dict(self):
+        """The ``torch.optim.Adam.state_dict()`` the reference's optimiser
+        (``model_manager.py:69-72``, over ``Model.parameters()``) would hold
+        after the same steps: parameter ids in ``named_parameters`` order,
+        per-parameter ``step`` / ``exp_avg`` / ``exp_avg_sq`` (CPU tensors)."""
+        P, order = self.params, self.spec.reference_order(self.num_vert, self.topo.seq)
+        t = int(P.step.item())
+        group = dict(torch.optim.Adam([torch.zeros(1)], lr=self.lr,
+                                      weight_decay=self.weight_decay).state_dict()["param_groups"][0])
+        group["params"] = list(range(len(order)))
+        state = {}
+        if t > 0:
+            for i, k in enumerate(order):
+                state[i] = {"step": torch.tensor(float(t)),
+                            "exp_avg": P.view(k, P.exp_avg).detach().cpu().clone(),
+                            "exp_avg_sq": P.view(k, P.exp_avg_sq).detach().cpu().clone()}
+        return {"state": state, "param_groups": [group]}
+
+    def load_optimizer_state_dict(self, sd):
+        """Inverse of :meth:`optimizer_state_dict` (accepts a reference
+        ``optimizer.pt`` payload); all parameters must share one ``step``."""
+        P, order = self.params, self.spec.reference_order(self.num_vert, self.topo.seq)
+        groups = sd["param_groups"]
+        ids = [i for g in groups for i in g["params"]]
+        if len(ids) != len(order):
+            raise ValueError(f"optimizer state has {len(ids)} parameters, model {len(order)}")
+        self.lr = float(groups[0]["lr"])
+        self.weight_decay = float(groups[0]["weight_decay"])
+        steps = set()
+        for i, k in zip(ids, order):
+            st = sd["state"].get(i)
+            if st is None:
+                P.view(k, P.exp_avg).zero_()
+                P.view(k, P.exp_avg_sq).zero_()
+                steps.add(0)
+                continue
+            _, shape = P.offsets[k]
+            for key, buf in (("exp_avg", P.exp_avg), ("exp_avg_sq", P.exp_avg_sq)):
+                if tuple(st[key].shape) != tuple(shape):
+                    raise ValueError(f"{k}.{key}: shape {tuple(st[key].shape)} != {shape}")
+                P.view(k, buf).copy_(st[key].to(self.device, torch.float32))
+            steps.add(int(float(st["step"])))
+        if len(steps) != 1:
+            raise ValueError(f"parameters at different Adam steps {sorted(steps)}")
+        P.step.fill_(steps.pop())
+
+    def save_weights(self, checkpoint_dir, epoch):
+        """``ModelManager.save_weights`` (``model_manager.py:682-688``):
+        ``model_%08d.pt`` = {'model': state_dict} (reference keys) and
+        ``optimizer.pt`` = {'optimizer': Adam state_dict}."""
+        import os
+        net_name = os.path.join(checkpoint_dir, "model_%08d.pt" % (epoch + 1))
+        torch.save({"model": {k: v.cpu() for k, v in self.state_dict().items()}}, net_name)
+        torch.save({"optimizer": self.optimizer_state_dict()},
+                   os.path.join(checkpoint_dir, "optimizer.pt"))
+        return net_name
+
+    def resume(self, checkpoint_dir):
+        """``ModelManager.resume`` (``model_manager.py:690-706``, last model by
+        ``utils.get_model_list`` ``utils.py:180-190``); loads with
+        ``weights_only=True``.  Returns the epoch count."""
+        import os
+        names = sorted(f for f in os.listdir(checkpoint_dir)
+                       if os.path.isfile(os.path.join(checkpoint_dir, f)) and "model" in f and ".pt" in f)
+        if not names:
+            raise FileNotFoundError(f"no model checkpoint in {checkpoint_dir}")
+        last = os.path.join(checkpoint_dir, names[-1])
+        self.load_state_dict(torch.load(last, map_location="cpu", weights_only=True)["model"])
+        opt = torch.load(os.path.join(checkpoint_dir, "optimizer.pt"), map_location="cpu",
+                         weights_only=True)
+        self.load_optimizer_state_dict(opt["optimizer"])
+        return int(last[-11:-3])
+
     # ----------------------------------------------------------- buffers
     def buffers(self, bsz):
         if bsz in self._bufs:

@@ -557,3 +557,67 @@ def test_reconstruction_errors_c1(dtopo):
     # the same kernel's L1 term on normalised units against the golden recon
     _, l1n = ops.vertex_errors(b.out.contiguous(), rec.to(DEV), want_l1=True)
     assert l1n.max().item() <= 1e-4
+
+
+def _golden_step(eng, dtopo, data, step):
+    b = eng.buffers(16)
+    b.key.fill_(recipe.train_key_index(step))
+    b.eps.copy_(torch.from_numpy(recipe.train_eps(step)))
+    b.batch_idx.copy_(torch.arange(4 * step, 4 * step + 4, dtype=torch.int32))
+    ops.swap_features(data, b.batch_idx, dtopo.region_mask, b.key, 4, out=b.x)
+    eng.train_step_on(b)
+    torch.cuda.synchronize()
+
+
+def test_checkpoint_resume_and_torch_adam_interop(dtopo, tmp_path):
+    """f4: save_weights / resume (model_manager.py:682-706).  (1) A resumed
+    engine continues bit-identically to the uninterrupted one.  (2) The saved
+    optimizer.pt loads into torch.optim.Adam over the reference parameter order
+    (model_manager.py:69-72) and its next step, given the device gradient,
+    matches the device Adam (1e-6)."""
+    w = recipe.golden_weights()
+    data = torch.from_numpy(recipe.normalized_meshes(12)).to(DEV)
+    a = make_engine(dtopo, w)
+    for s in range(2):
+        _golden_step(a, dtopo, data, s)
+    name = a.save_weights(str(tmp_path), epoch=1)
+    assert name.endswith("model_00000002.pt")
+    b = make_engine(dtopo, w)
+    b.params.data.zero_()
+    assert b.resume(str(tmp_path)) == 2
+    for buf in ("data", "exp_avg", "exp_avg_sq", "step"):
+        assert torch.equal(getattr(a.params, buf), getattr(b.params, buf)), buf
+    # torch Adam from the checkpoint, reference parameter order
+    ck = torch.load(tmp_path / "model_00000002.pt", weights_only=True)["model"]
+    ref = [ck[k].clone().requires_grad_() for k in ck]
+    opt = torch.optim.Adam(ref, lr=1e-4, weight_decay=0.0, foreach=False)
+    opt.load_state_dict(torch.load(tmp_path / "optimizer.pt", weights_only=True)["optimizer"])
+    _golden_step(a, dtopo, data, 2)
+    _golden_step(b, dtopo, data, 2)
+    assert torch.equal(a.params.data, b.params.data)
+    grads = a.grads()
+    for p, k in zip(ref, ck):
+        p.grad = grads[k].detach().cpu().clone()
+    opt.step()
+    sd = a.state_dict()
+    for p, k in zip(ref, ck):
+        close(sd[k], p.detach(), 1e-6, f"adam after resume {k}")
+
+
+def test_encode_all_and_latent_stats_c1(dtopo):
+    """f4: encode_all in ragged batches (3, 3, 2) of the C1 meshes vs the
+    reference's golden mu (model_manager.py:244-246, 1e-4) and
+    compute_latent_stats (test.py:95-117) vs the same statistics of the golden
+    latents (1e-4)."""
+    g = np.load(f"{recipe.HERE}/golden_eval.npz")
+    eng = make_engine(dtopo, recipe.golden_weights())
+    x = torch.from_numpy(recipe.normalized_meshes(8)).to(DEV)
+    z = eng.encode_all(x, batch_size=3)
+    torch.cuda.synchronize()
+    assert tuple(z.shape) == (8, 75)
+    assert np.abs(z.cpu().numpy() - g["mu"]).max() <= 1e-4
+    st = eng.latent_stats(z)
+    ref = torch.from_numpy(g["mu"])
+    for k, v in {"means": ref.mean(0), "stds": ref.std(0), "mins": ref.min(0)[0],
+                 "maxs": ref.max(0)[0]}.items():
+        assert np.abs(st[k].cpu().numpy() - v.numpy()).max() <= 1e-4, k

@@ -117,3 +117,35 @@ def test_engine_parameter_layout():
     assert names[i + 1] == "en_layers.5.weight"
     assert names[i + 2: i + 4] == ["en_layers.4.bias", "en_layers.5.bias"]
     assert sum(int(np.prod(s)) for _, s in specs) == 1081881
+
+
+def test_checkpoint_format_round_trip(topo_npz, tmp_path):
+    """f4 host side: save_weights / resume (model_manager.py:682-706) on an
+    engine held in host memory (no kernel runs): reference file names and
+    payload keys, bit-identical round trip, and the optimizer.pt payload is
+    accepted by torch.optim.Adam over the reference parameter order."""
+    import torch
+    from craniofacialsd_vae_amd import engine as E
+    topo = topology.DeviceTopology.from_npz(topo_npz, device="cpu")
+    a = E.SDVAEEngine(topo, E.ModelSpec(), device="cpu")
+    g = torch.Generator().manual_seed(0)
+    a.params.exp_avg.normal_(generator=g)
+    a.params.exp_avg_sq.uniform_(generator=g)
+    a.params.step.fill_(7)
+    assert a.save_weights(str(tmp_path), 4).endswith("model_00000005.pt")
+    assert sorted(os.listdir(tmp_path)) == ["model_00000005.pt", "optimizer.pt"]
+    b = E.SDVAEEngine(topo, E.ModelSpec(), device="cpu")
+    assert b.resume(str(tmp_path)) == 5
+    for buf in ("data", "exp_avg", "exp_avg_sq", "step"):
+        assert torch.equal(getattr(a.params, buf), getattr(b.params, buf)), buf
+    ck = torch.load(tmp_path / "model_00000005.pt", weights_only=True)["model"]
+    assert list(ck) == list(a.state_dict())
+    opt = torch.optim.Adam([v.clone().requires_grad_() for v in ck.values()], lr=1e-4)
+    opt.load_state_dict(torch.load(tmp_path / "optimizer.pt", weights_only=True)["optimizer"])
+    assert len(opt.state) == len(ck)
+    st = opt.state_dict()["state"][3]
+    assert float(st["step"]) == 7.0
+    bad = a.optimizer_state_dict()
+    bad["state"][0]["step"] = torch.tensor(3.0)
+    with pytest.raises(ValueError):
+        b.load_optimizer_state_dict(bad)

@@ -233,9 +233,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs for the N>1 path on a one-GPU box (default off: RCCL,
+    # one GPU per rank): CFSD_DIST_BACKEND=gloo CFSD_SHARE_DEVICE=1.
+    backend = os.environ.get("CFSD_DIST_BACKEND", "nccl")
+    if os.environ.get("CFSD_SHARE_DEVICE"):
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     runner = Runner(world, rank, device, args.dataset, not args.no_graph)
@@ -293,7 +301,8 @@ def main():
                                    "MSE+Laplacian+KL+latent-consistency, bwd, Adam)",
                        "template_vertices": nv, "levels": runner.topo.n_verts,
                        "global_batch": 16 * world, "per_gpu_batch": 16,
-                       "parallelism": f"dp{world}", "graph": runner.use_graph},
+                       "parallelism": f"dp{world}", "graph": runner.use_graph,
+                       "collective": None if world == 1 else ("rccl all_reduce" if backend == "nccl" else backend)},
             "roofline": {"kernel": "cfsd " + kern_names[dom], "bound": "mfma",
                          "achieved": d3[dom]["achieved"], "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": d3[dom]["frac"],

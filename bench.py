@@ -277,7 +277,7 @@ def main():
         gather_bytes = 16 * nv * (32 + 9 * 32) * 4 + nv * 9 * 4
         t_g = probe["spiral_gather_L0"]
         parity = c1_parity(device)
-        cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
+        cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args.cpu_seconds)  # N=1 only
         # the three D3 (decoder level 0, 32 -> 32) conv kernels, 5.02 GFLOP
         # each; `roofline` is the dominant one (longest launch)
         d3 = {}

@@ -15,6 +15,16 @@ namespace cfsd {
 #ifndef CFSD_SPMM_XCD
 #define CFSD_SPMM_XCD 1
 #endif
+// Non-temporal output stores: the up-sampling SpMM gets ~0.8 us faster but
+// the D3 conv reading its output ~0.5-1 us slower (same-box A/B): off.
+#ifndef CFSD_SPMM_NT
+#define CFSD_SPMM_NT 0
+#endif
+// Exact 3-entry chunk for the 3-tap up-sampling rows (no clamped 4th load):
+// up0 16.4 -> 15.2 us, up1 11.2 -> 10.6 us (same-box A/B); same add order.
+#ifndef CFSD_SPMM_K3
+#define CFSD_SPMM_K3 1
+#endif
 
 template <int CK>
 __device__ __forceinline__ void spmm_row_chunks(int beg, int end, const int* __restrict__ col,
@@ -80,6 +90,10 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   // rows (its transpose: ~12) 8-entry chunks; past-the-end entries are
   // clamped to the row's last one (an L1 hit, not added) -- measured faster
   // than exec-masked loads.
+#if CFSD_SPMM_K3
+  if (end - beg == 3) spmm_row_chunks<3>(beg, end, col, val, xb, c4, acc);
+  else
+#endif
   if (end - beg <= 4) spmm_row_chunks<4>(beg, end, col, val, xb, c4, acc);
   else spmm_row_chunks<8>(beg, end, col, val, xb, c4, acc);
   if (elu_y) {
@@ -89,7 +103,11 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
     acc.z *= elu_grad_from_out(g.z);
     acc.w *= elu_grad_from_out(g.w);
   }
+#if CFSD_SPMM_NT
+  __builtin_nontemporal_store(acc, reinterpret_cast<f32x4*>(y + t * 4));
+#else
   st4(y + t * 4, acc);
+#endif
 }
 
 // out[(i*bs + j), v, :] = x[mesh(i or j), v, :]; one thread per (out mesh,

@@ -196,7 +196,13 @@ __global__ __launch_bounds__(256) void recon_lap_bwd_k(
 // Single workgroup.  mulv [B, 2L] = [logvar | mu] (rows of the stacked
 // encoder Linear), z [B, L].  dlat [B, 3L] = {w_lc*dLC/dz | w_kl*dKL/dmu | w_kl*dKL/dlogvar}.
 // terms[2] = {kl, lc}.
-__global__ __launch_bounds__(256) void latent_fwd_k(const float* __restrict__ mulv,
+// 16 waves: the LC distance and gradient phases are chains of dependent LDS
+// reads that one wave per SIMD cannot hide (256: 16.0 us, 512: 11.4,
+// 1024: 9.8, same-box A/B in the step).
+#ifndef CFSD_LAT_THREADS
+#define CFSD_LAT_THREADS 1024
+#endif
+__global__ __launch_bounds__(CFSD_LAT_THREADS) void latent_fwd_k(const float* __restrict__ mulv,
                                                     const float* __restrict__ eps,
                                                     const int* __restrict__ key,
                                                     float* __restrict__ z,
@@ -207,7 +213,7 @@ __global__ __launch_bounds__(256) void latent_fwd_k(const float* __restrict__ mu
                                                     float eta1, float eta2, int bs) {
   __shared__ float zs[64 * 256];
   __shared__ float dist[4 * 64 * 8];  // [kind][pair][t]
-  __shared__ float2 red[4];
+  __shared__ float2 red[CFSD_LAT_THREADS / 64];
   const int tid = threadIdx.x;
   const int ldm = is_vae ? 2 * L : L;
   const int mu_off = is_vae ? L : 0;
@@ -775,7 +781,7 @@ extern "C" int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_
   if (w_lc == 0.f) bs = 1;
   if (batch > 64 || latent > 256 || batch * latent > 64 * 256)
     return set_error(CFSD_EINVAL, "latent_fwd: batch %d / latent %d too large", batch, latent);
-  hipLaunchKernelGGL(latent_fwd_k, dim3(1), dim3(256), 0, (hipStream_t)stream, mulv, eps, key, z,
+  hipLaunchKernelGGL(latent_fwd_k, dim3(1), dim3(CFSD_LAT_THREADS), 0, (hipStream_t)stream, mulv, eps, key, z,
                      dlat, terms, batch, latent, region_size, train, is_vae, sigmoid, w_kl, w_lc,
                      eta1, eta2, bs);
   return launch_status("latent_fwd");

@@ -4,18 +4,21 @@ Workload (BASELINE.json config 2, ``configurations/craniofacial.yaml``): the
 real craniofacial template hierarchy (17039/4260/1065/267/67 vertices,
 spiral length 9, channels [32, 32, 32, 64], latent 75, VAE), batch_size 4
 swapped to 16 meshes per GPU per step, fp32.  A step is the full reference
-``_do_iteration``: device-side batch pick + swap key + VAE noise, feature
-swap, forward, MSE + Laplacian + KL + latent-consistency losses, backward,
-(RCCL all-reduce of the flat gradient when N > 1), Adam.  The dataset is
+``_do_iteration``: device-side epoch-shuffled batch pick + swap key + VAE
+noise, feature swap, forward, MSE + Laplacian + KL + latent-consistency
+losses, backward, (RCCL all-reduce of the flat gradient when N > 1, in two
+buckets overlapped with the encoder backward), Adam.  The dataset is
 synthetic N(0, 1) meshes resident in HBM (no checkpoint/dataset egress).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+                       [--topology craniofacial|synth5k]
 (for N > 1 launch with torch.distributed.run, one rank per GPU).
 Rank 0 prints one JSON line.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -28,75 +31,92 @@ sys.path.insert(0, ROOT)
 import cfsd_loader  # noqa: E402
 
 cfsd_loader.load()
+from craniofacialsd_vae_amd import _abi, ops, topology  # noqa: E402
+from craniofacialsd_vae_amd import dist as cdist  # noqa: E402
 from craniofacialsd_vae_amd import engine as E  # noqa: E402
-from craniofacialsd_vae_amd import ops, topology  # noqa: E402
 
 METRIC = "train meshes/sec + per-vertex L1, craniofacial SD-VAE @1/2/4/8 MI355X"
 TOPO_NPZ = os.path.join(ROOT, "tests", "golden", "topology_craniofacial.npz")
 PROFILES = os.path.join(ROOT, "profiles")
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--dataset", type=int, default=256, help="resident synthetic meshes per rank")
+    p.add_argument("--topology", default="craniofacial", choices=["craniofacial", "synth5k"])
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
-    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget")
+    p.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU-baseline sample budget")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the secondary measurements (synthetic ~5k line, kernel trace)")
     return p.parse_args()
 
 
+def load_topology(name, device):
+    if name == "craniofacial":
+        return topology.DeviceTopology.from_npz(dict(np.load(TOPO_NPZ)), device=device)
+    from craniofacialsd_vae_amd import precompute
+    return precompute.synthetic_hierarchy(device=device)
+
+
 class Runner:
-    def __init__(self, world, rank, device, n_meshes, use_graph):
-        npz = dict(np.load(TOPO_NPZ))
-        self.topo = topology.DeviceTopology.from_npz(npz, device=device)
-        self.eng = E.SDVAEEngine(self.topo, E.ModelSpec(), lr=1e-4, swap_bs=4, seed=1234 + rank,
-                                 device=device)
-        g = torch.Generator(device="cpu").manual_seed(0)
+    def __init__(self, world, rank, device, n_meshes, use_graph, topo_name="craniofacial"):
+        self.topo = load_topology(topo_name, device)
+        self.topo_name = topo_name
+        self.eng = E.SDVAEEngine(self.topo, E.ModelSpec(latent_size=75), lr=1e-4, swap_bs=4,
+                                 seed=1234 + rank, device=device)
         self.eng.reset_parameters()  # same init on every rank (broadcast below)
         self.world, self.rank = world, rank
         nv = self.topo.n_verts[0]
         gen = torch.Generator(device=device).manual_seed(1234 + rank)
-        self.data = torch.randn(n_meshes, nv, 3, device=device, generator=gen)
-        self.n_batches = n_meshes // 4
-        perm = torch.randperm(n_meshes, generator=g)[: self.n_batches * 4]
-        self.perm = perm.to(torch.int32).to(device)
+        self.data = E.ResidentData(torch.randn(n_meshes, nv, 3, device=device, generator=gen), bs=4,
+                                   shuffle=True)
         self.b = self.eng.buffers(16)
+        self.avg = cdist.GradientAverager(world)
         if world > 1:
-            dist.broadcast(self.eng.params.data, 0)
+            cdist.broadcast_parameters(self.eng.params.data, 0)
         self.use_graph = use_graph
-        self.graph_fwdbwd = self.graph_adam = None
+        self.graphs = None
 
-    # --- the step, split where the collective goes
+    # --- the step, split where the collective buckets go
     def part_a(self):
-        eng, b, T = self.eng, self.b, self.topo
-        ops.step_begin(eng._step_counter(b), eng.seed, eps=b.eps, key=b.key,
-                       n_regions=T.n_regions, batch_idx=b.batch_idx, bs=4,
-                       n_batches=self.n_batches, perm=self.perm, adam_step=eng.params.step)
-        ops.swap_features(self.data, b.batch_idx, T.region_mask, b.key, 4, out=b.x)
+        """step_begin + swap + forward + backward up to the encoder Linear."""
+        eng, b, T, d = self.eng, self.b, self.topo, self.data
+        ops.step_begin(eng.counter, eng.seed, eps=b.eps, key=b.key, n_regions=T.n_regions,
+                       batch_idx=b.batch_idx, bs=4, n_batches=d.n_batches, perm=d.rows,
+                       n_items=d.n_items, shuffle=d.shuffle, adam_step=eng.params.step)
+        ops.swap_features(d.meshes, b.batch_idx, T.region_mask, b.key, 4, out=b.x)
         eng.forward(b, train=True, acc=eng.loss_acc, finalize=False)
-        eng.backward(b)
+        eng.backward_head(b, split=self.world > 1)
 
     def part_b(self):
+        self.eng.backward_tail(self.b)
+
+    def part_c(self):
         self.eng.adam_step()
 
-    def allreduce(self):
+    def eager_step(self):
+        self.part_a()
         if self.world > 1:
-            dist.all_reduce(self.eng.params.grad)
-            ops.scale(self.eng.params.grad, 1.0 / self.world)
+            self.avg.bucket_ready(self.eng.params.grad[self.eng.enc_conv_numel():])
+        self.part_b()
+        if self.world > 1:
+            self.avg.bucket_ready(self.eng.params.grad[:self.eng.enc_conv_numel()])
+            self.avg.finish(self.eng.params.grad)
+        self.part_c()
 
     def capture(self):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                self.part_a()
-                self.allreduce()
-                self.part_b()
+                self.eager_step()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         if self.world == 1:
@@ -104,25 +124,120 @@ class Runner:
             with torch.cuda.graph(g):
                 self.part_a()
                 self.part_b()
-            self.graph_fwdbwd, self.graph_adam = g, None
+                self.part_c()
+            self.graphs = [g]
         else:
-            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga):
-                self.part_a()
-            with torch.cuda.graph(gb):
-                self.part_b()
-            self.graph_fwdbwd, self.graph_adam = ga, gb
+            self.graphs = [torch.cuda.CUDAGraph() for _ in range(3)]
+            for g, fn in zip(self.graphs, (self.part_a, self.part_b, self.part_c)):
+                with torch.cuda.graph(g):
+                    fn()
 
     def step(self):
-        if self.graph_fwdbwd is not None:
-            self.graph_fwdbwd.replay()
-            if self.graph_adam is not None:
-                self.allreduce()
-                self.graph_adam.replay()
-        else:
-            self.part_a()
-            self.allreduce()
-            self.part_b()
+        if self.graphs is None:
+            return self.eager_step()
+        if self.world == 1:
+            self.graphs[0].replay()
+            return
+        ga, gb, gc = self.graphs
+        grad = self.eng.params.grad
+        ga.replay()
+        self.avg.bucket_ready(grad[self.eng.enc_conv_numel():])  # overlaps with gb
+        gb.replay()
+        self.avg.bucket_ready(grad[:self.eng.enc_conv_numel()])
+        self.avg.finish(grad)
+        gc.replay()
+
+
+# ------------------------------------------------------------------ roofline
+def launch_cost(name, a):
+    """(flop, algorithmic HBM bytes, peak TFLOP/s) of one libcfsd launch from
+    its ABI arguments (include/cfsd.h); (0, 0, None) for bookkeeping launches
+    that do no work the algorithm requires (step counter, latent head,
+    loss finalisation, slab reduction, gradient scaling)."""
+    f4 = 4
+    if name == "cfsd_spiral_conv_fwd":
+        B, vs, rows, S, ci, co = a[7:13]
+        return 2.0 * B * rows * S * ci * co, f4 * (B * vs * ci + B * rows * co + co * S * ci) + 4 * rows * S, FP32_PEAK_TFLOPS
+    if name == "cfsd_spiral_conv_bwd_data":
+        B, vs, rows, S, ci, co = a[9:15]
+        elu = a[5] is not None
+        return (2.0 * B * rows * S * ci * co,
+                f4 * (B * rows * co + B * vs * ci * (2 if elu else 1) + co * S * ci) + 16 * vs * S, FP32_PEAK_TFLOPS)
+    if name == "cfsd_spiral_conv_bwd_weight":
+        B, vs, rows, S, ci, co = a[7:13]
+        return 2.0 * B * rows * S * ci * co, f4 * (B * vs * ci + B * rows * co + co * S * ci) + 4 * rows * S, FP32_PEAK_TFLOPS
+    if name == "cfsd_spiral_conv_bwd":
+        B, vs, rows, S, ci, co = a[13:19]
+        dx, elu = a[8] is not None, a[7] is not None
+        fl = 2.0 * B * rows * S * ci * co * (2 if dx else 1)
+        by = f4 * (B * vs * ci + B * rows * co + co * S * ci) + 4 * rows * S
+        if dx:
+            by += f4 * B * vs * ci * (2 if elu else 1) + 16 * vs * S
+        return fl, by, FP32_PEAK_TFLOPS
+    if name == "cfsd_spmm_csr":
+        B, m, n, c = a[6:10]
+        elu = a[4] is not None
+        return 0.0, f4 * B * c * (n + m * (2 if elu else 1)), None
+    if name == "cfsd_swap_features":
+        bs, nv, c = a[5:8]
+        return 0.0, f4 * (bs * nv * c + bs * bs * nv * c) + nv, None
+    if name == "cfsd_recon_lap_fwd":
+        B, nv, c = a[7:10]
+        return 0.0, f4 * 3 * B * nv * c, None
+    if name in ("cfsd_recon_lap_bwd", "cfsd_recon_lap_bwd_finalize"):
+        B, nv, c = a[7:10]
+        return 0.0, f4 * 4 * B * nv * c, None
+    if name == "cfsd_linear_fwd":
+        m, k, n = a[6:9]
+        return 2.0 * m * k * n, f4 * (m * k + n * k + m * n), FP32_PEAK_TFLOPS
+    if name == "cfsd_linear_bwd":
+        m, k, n = a[9:12]
+        dx, dw, elu = a[4] is not None, a[5] is not None, a[3] is not None
+        fl = 2.0 * m * k * n * (int(dx) + int(dw))
+        by = f4 * (m * n + n * k + m * k * (int(dx) + int(dw) + int(elu)) + n * k * int(dw))
+        return fl, by, FP32_PEAK_TFLOPS
+    if name == "cfsd_adam":
+        n = a[5].value if hasattr(a[5], "value") else a[5]
+        return 0.0, 7.0 * f4 * n, None
+    return 0.0, 0.0, None
+
+
+def step_roofline(runner, ms_per_step):
+    """Time-weighted roofline of one training step: every launch of an eager
+    step is timed with a HIP event pair on its stream (queued behind a sleep
+    kernel so the device runs them back-to-back, as in the graph), priced at
+    its roofline time max(flop/peak, bytes/8 TB/s) from the work the algorithm
+    requires (Enblock row subset applied), and the sum of those ideal times
+    is divided by the measured time."""
+    torch.cuda.synchronize()
+    torch.cuda._sleep(50_000_000)
+    with _abi.trace_launches() as rec:
+        runner.eager_step()
+    torch.cuda.synchronize()
+    rows, t_sum, ideal_sum, flop_sum, byte_sum = [], 0.0, 0.0, 0.0, 0.0
+    for name, args, e0, e1 in rec:
+        t = e0.elapsed_time(e1) * 1e-3
+        fl, by, peak = launch_cost(name, args)
+        ideal = max(fl / (peak * 1e12) if peak else 0.0, by / (HBM_PEAK_GBS * 1e9))
+        rows.append((name, t, fl, by, ideal))
+        t_sum += t
+        ideal_sum += ideal
+        flop_sum += fl
+        byte_sum += by
+    top = sorted(rows, key=lambda r: -r[1])[:8]
+    return {
+        "launches": len(rows), "kernel_time_us": t_sum * 1e6,
+        "required_gflop_per_step": flop_sum / 1e9, "algorithmic_mb_per_step": byte_sum / 1e6,
+        "ideal_time_us": ideal_sum * 1e6,
+        "frac_of_kernel_time": ideal_sum / t_sum if t_sum else None,
+        "frac_of_step_time": ideal_sum / (ms_per_step * 1e-3),
+        "achieved_tflops_step": flop_sum / (ms_per_step * 1e-3) / 1e12,
+        "note": "frac = sum over launches of max(flop/peak, bytes/HBM) / measured time; "
+                "bookkeeping launches (latent head, loss finalise, dW slab reduce, step_begin) "
+                "count as time with no required work",
+        "top_launches": [{"name": n, "us": t * 1e6, "frac": (i / t if t else None)}
+                         for n, t, _, _, i in top],
+    }
 
 
 def kernel_probe(runner, n_iter=20):
@@ -148,9 +263,8 @@ def kernel_probe(runner, n_iter=20):
     w3, bias3 = eng._dec_w(i3)
     timed("conv_fwd_D3", lambda: ops.spiral_conv_fwd(b.dec_up[i3], T.spiral[0], w3, bias3, 1,
                                                       out=b.dec_out[i3]))
-    # the D3 backward kernels exactly as the step launches them (dx with the
-    # previous Deblock's ELU folded in is the Pool transpose's input here;
-    # dW deferred: slab kernel only, reduced by the batched reduce)
+    # the D3 backward kernels exactly as the step launches them (dW deferred:
+    # slab kernel only, reduced by the batched reduce)
     timed("conv_dx_D3", lambda: ops.spiral_conv_bwd_data(b.dpre_dec[i3], T.spiral_inv[0], w3, T.n_verts[0],
                                                          out=b.g_dec_up[i3], workspace=b.ws))
     timed("conv_dw_D3", lambda: ops.spiral_conv_bwd_weight(b.dec_up[i3], T.spiral[0], b.dpre_dec[i3], None,
@@ -162,16 +276,21 @@ def kernel_probe(runner, n_iter=20):
 
 
 def pmc_traffic(key="conv_fwd_d3"):
-    """HBM bytes per launch of a D3 kernel from the newest committed PMC pass
-    (tools/gpu_round.sh -> tools/pmc_traffic.py: FETCH_SIZE and WRITE_SIZE in
-    separate rocprofv3 runs, gfx950 FETCH_SIZE x2 correction)."""
+    """HBM bytes per launch of a D3 kernel from the newest PMC pass under
+    profiles/ (tools/pmc_traffic.py: FETCH_SIZE and WRITE_SIZE in separate
+    rocprofv3 runs, gfx950 FETCH_SIZE x2 correction).  Newest = the largest
+    "created" stamp written by the tool (files without one rank by mtime)."""
     import glob
-    files = sorted(glob.glob(os.path.join(PROFILES, f"*_pmc_traffic_{key}.json")))
-    if not files:
+    best = None
+    for f in glob.glob(os.path.join(PROFILES, f"*_pmc_traffic_{key}.json")):
+        with open(f) as fh:
+            d = json.load(fh)
+        rank = (d.get("created", 0), os.path.getmtime(f))
+        if best is None or rank > best[0]:
+            best = (rank, d, f)
+    if best is None:
         return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+    return best[1].get("hbm_bytes_per_launch"), os.path.relpath(best[2], ROOT)
 
 
 def c1_parity(device):
@@ -201,31 +320,82 @@ def c1_parity(device):
             "tolerance": 1e-4, "pass": bool(d.max() <= 1e-4)}
 
 
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for ln in out.splitlines():
+            if ln.startswith("Model name:"):
+                return ln.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(budget_s):
-    """Oracle (PyTorch-CPU restatement of the reference step) on host cores."""
+    """Oracle (PyTorch-CPU restatement of the reference step, the same ATen
+    ops) on the host: with every host CPU (os.cpu_count() threads), with the
+    CPUs this process may run on (sched affinity) when that differs, and with
+    one thread.  ``value`` = the fastest multi-thread run."""
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     from oracle import cfsd_oracle as O
-    npz = dict(np.load(TOPO_NPZ))
-    T = O.Topology(npz)
     import recipe
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    T = O.Topology(dict(np.load(TOPO_NPZ)))
     P = O.make_params(recipe.golden_weights())
     opt = O.Adam(P)
     rs = np.random.RandomState(0)
     x4 = rs.randn(4, T.n_verts[0], 3).astype(np.float32)
     eps = rs.randn(16, 75).astype(np.float32)
-    O.train_step(P, opt, x4, T, 0, eps)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        O.train_step(P, opt, x4, T, n % 15, eps)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 50:
-            break
-    return {"value": 16 * n / el, "unit": "meshes/s", "cores": threads, "kind": "port",
-            "sample": f"{n} full train steps (16 swapped meshes each, fp32, oracle/cfsd_oracle.py "
-                      f"torch-CPU restatement) in {el:.1f} s"}
+    host = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = host
+    multi = sorted({host, aff}, reverse=True)
+    plan = [(t, budget_s * 0.6 / len(multi)) for t in multi] + [(1, budget_s * 0.4)]
+    runs = []
+    for threads, budget in plan:
+        torch.set_num_threads(threads)
+        O.train_step(P, opt, x4, T, 0, eps)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            O.train_step(P, opt, x4, T, n % 15, eps)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget or n >= 200:
+                break
+        runs.append({"threads": threads, "steps": n, "seconds": el, "meshes_per_s": 16 * n / el})
+    best = max(runs[:-1], key=lambda r: r["meshes_per_s"])
+    return {"value": best["meshes_per_s"], "unit": "meshes/s", "cores": best["threads"], "kind": "port",
+            "sample": f"{best['steps']} full train steps (16 swapped meshes each, fp32, "
+                      f"oracle/cfsd_oracle.py torch-CPU restatement) in {best['seconds']:.1f} s",
+            "one_thread": runs[-1]["meshes_per_s"], "host_cpus": host, "affinity_cpus": aff,
+            "cpu_model": cpu_model(), "runs": runs}
+
+
+def synth5k_line(device, steps=500, warmup=20):
+    """Secondary throughput line (north_star's "~5k verts, 4 levels"): the
+    same step on a synthetic 5120/1280/320/80/20 hierarchy built by the
+    product's own topology precompute (craniofacialsd_vae_amd.precompute)."""
+    r = Runner(1, 0, device, 256, True, "synth5k")
+    r.capture()
+    for _ in range(warmup):
+        r.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r.step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"workload": "synthetic 4-level hierarchy, same model/step, 16 meshes/GPU, fp32",
+            "levels": r.topo.n_verts, "value": 16 * steps / el, "unit": "meshes/s",
+            "ms_per_step": el / steps * 1e3, "steps": steps}
 
 
 def main():
@@ -246,7 +416,7 @@ def main():
             dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    runner = Runner(world, rank, device, args.dataset, not args.no_graph)
+    runner = Runner(world, rank, device, args.dataset, not args.no_graph, args.topology)
     if runner.use_graph:
         runner.capture()
     for _ in range(args.warmup):
@@ -262,29 +432,34 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = cdist.max_over_ranks(el, device)
     meshes = 16 * world * args.steps
+    ms_per_step = el / args.steps * 1e3
     losses = runner.eng.loss_acc.cpu().numpy()
     finite = bool(np.isfinite(losses).all())
     probe = kernel_probe(runner)
+    steprf = None if args.no_extras else step_roofline(runner, ms_per_step)
     if rank == 0:
         nv = runner.topo.n_verts[0]
-        # dominant kernel: fused gather+contraction of D3 (32 -> 32, 17039 rows x 16)
+        # dominant kernel: fused gather+contraction of D3 (32 -> 32, nv rows x 16)
         flops = 2.0 * 16 * nv * 9 * 32 * 32
         gather_bytes = 16 * nv * (32 + 9 * 32) * 4 + nv * 9 * 4
         t_g = probe["spiral_gather_L0"]
         parity = c1_parity(device)
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args.cpu_seconds)  # N=1 only
+        s5k = None
+        if not (args.no_extras or world > 1 or args.topology != "craniofacial"):
+            try:
+                s5k = synth5k_line(device)
+            except (ImportError, AttributeError) as e:  # precompute not available
+                s5k = {"error": str(e)}
         # the three D3 (decoder level 0, 32 -> 32) conv kernels, 5.02 GFLOP
         # each; `roofline` is the dominant one (longest launch)
         d3 = {}
         for name, key in (("conv_fwd_D3", "conv_fwd_d3"), ("conv_dx_D3", "conv_dx_d3"),
                           ("conv_dw_D3", "conv_dw_d3")):
             t = probe[name]
-            traffic, traffic_src = pmc_traffic(key)
+            traffic, traffic_src = pmc_traffic(key) if args.topology == "craniofacial" else (None, None)
             d3[name] = {"us_per_launch": t * 1e6, "achieved": flops / t / 1e12,
                         "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS, "traffic": traffic,
                         "traffic_source": traffic_src}
@@ -294,26 +469,29 @@ def main():
                       "conv_dw_D3": "conv_dw_mfma<32,32> (decoder level 0 weight gradient)"}
         out = {
             "metric": METRIC, "value": meshes / el, "unit": "meshes/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic N(0,1) meshes resident in HBM, random-init weights",
             "config": {"workload": "craniofacial.yaml SD-VAE train step (swap bs 4->16, fwd, "
                                    "MSE+Laplacian+KL+latent-consistency, bwd, Adam)",
-                       "template_vertices": nv, "levels": runner.topo.n_verts,
+                       "topology": args.topology, "template_vertices": nv, "levels": runner.topo.n_verts,
                        "global_batch": 16 * world, "per_gpu_batch": 16,
                        "parallelism": f"dp{world}", "graph": runner.use_graph,
-                       "collective": None if world == 1 else ("rccl all_reduce" if backend == "nccl" else backend)},
+                       "collective": None if world == 1 else
+                       (("rccl" if backend == "nccl" else backend) + " all_reduce, 2 buckets overlapped")},
             "roofline": {"kernel": "cfsd " + kern_names[dom], "bound": "mfma",
                          "achieved": d3[dom]["achieved"], "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": d3[dom]["frac"],
                          "traffic": d3[dom]["traffic"], "traffic_source": d3[dom]["traffic_source"],
                          "algorithmic_flop": flops, "us_per_launch": d3[dom]["us_per_launch"]},
             "d3_kernels": d3,
+            "step_roofline": steprf,
             "gather_roofline": {"kernel": "cfsd spiral_gather_k (level 0, 32 ch, 16 meshes)",
                                 "bound": "hbm", "achieved": gather_bytes / t_g / 1e9,
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": gather_bytes / t_g / 1e9 / HBM_PEAK_GBS,
                                 "us_per_launch": t_g * 1e6},
+            "synthetic_5k": s5k,
             "parity": parity,
             "cpu_baseline": cpu,
             "losses_mean": (losses[:5] / max(losses[5], 1)).tolist(), "losses_finite": finite,

@@ -36,7 +36,8 @@ SIGNATURES = {
     "cfsd_spiral_conv_bwd_paired": (_I, [_I, _I, _I, _I, _I, _I]),
     "cfsd_spiral_gather": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spmm_csr": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
-    "cfsd_swap_features": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "cfsd_swap_features": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "cfsd_normalize": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     "cfsd_linear_workspace": (_Z, [_I, _I, _I]),
     "cfsd_linear_fwd": (_I, [_P, _P, _P, _P, _P, _Z, _I, _I, _I, _P]),
     "cfsd_linear_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _P]),
@@ -49,7 +50,7 @@ SIGNATURES = {
     "cfsd_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_loss_finalize": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P]),
     "cfsd_adam": (_I, [_P, _P, _P, _P, _P, _Z, _F, _F, _F, _F, _F, _P]),
-    "cfsd_step_begin": (_I, [_P, _U64, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P]),
+    "cfsd_step_begin": (_I, [_P, _U64, _P, _I, _P, _I, _P, _I, _I, _P, _I, _I, _P, _P]),
     "cfsd_dw_reduce_batch": (_I, [_P, _I, _P]),
     "cfsd_scale": (_I, [_P, _Z, _F, _P]),
     "cfsd_elu_bwd": (_I, [_P, _P, _P, _Z, _P]),
@@ -109,5 +110,32 @@ def stream_ptr(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+_trace = None  # list of (name, args, start_event, end_event) while tracing
+
+
+class trace_launches:
+    """Context manager recording every libcfsd launch with a HIP event pair on
+    the launch stream (per-kernel device time of an eager step; measurement
+    only -- the product path never enables it)."""
+
+    def __enter__(self):
+        global _trace
+        self.records = []
+        _trace = self.records
+        return self.records
+
+    def __exit__(self, *exc):
+        global _trace
+        _trace = None
+        return False
+
+
 def call(name, *args):
+    if _trace is None:
+        check(getattr(lib(), name)(*args), name)
+        return
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     check(getattr(lib(), name)(*args), name)
+    e1.record()
+    _trace.append((name, args, e0, e1))

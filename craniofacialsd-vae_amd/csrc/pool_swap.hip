@@ -12,19 +12,6 @@
 
 namespace cfsd {
 
-#ifndef CFSD_SPMM_XCD
-#define CFSD_SPMM_XCD 1
-#endif
-// Non-temporal output stores: the up-sampling SpMM gets ~0.8 us faster but
-// the D3 conv reading its output ~0.5-1 us slower (same-box A/B): off.
-#ifndef CFSD_SPMM_NT
-#define CFSD_SPMM_NT 0
-#endif
-// Exact 3-entry chunk for the 3-tap up-sampling rows (no clamped 4th load):
-// up0 16.4 -> 15.2 us, up1 11.2 -> 10.6 us (same-box A/B); same add order.
-#ifndef CFSD_SPMM_K3
-#define CFSD_SPMM_K3 1
-#endif
 
 template <int CK>
 __device__ __forceinline__ void spmm_row_chunks(int beg, int end, const int* __restrict__ col,
@@ -70,14 +57,9 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   // hipcc contracts a*b+c into fma by default; the reference rounds the
   // product and the sum separately (index_select*value, then scatter_add).
 #pragma clang fp contract(off)
-#if CFSD_SPMM_XCD
   const long per = (total + 7) / 8;
   const long t = (long)(blockIdx.x & 7) * per + (long)(blockIdx.x >> 3) * blockDim.x + threadIdx.x;
   if (t >= total || t >= (long)((blockIdx.x & 7) + 1) * per) return;
-#else
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= total) return;
-#endif
   int br, q, b, r;
   divmod32(t, c4, br, q);
   divmod32(br, m, b, r);
@@ -89,12 +71,10 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   // Short rows (up-sampling: 3 barycentric taps) use 4-entry chunks, long
   // rows (its transpose: ~12) 8-entry chunks; past-the-end entries are
   // clamped to the row's last one (an L1 hit, not added) -- measured faster
-  // than exec-masked loads.
-#if CFSD_SPMM_K3
+  // than exec-masked loads.  The 3-tap rows get an exact 3-entry chunk
+  // (no clamped 4th load: up0 16.4 -> 15.2 us, same add order).
   if (end - beg == 3) spmm_row_chunks<3>(beg, end, col, val, xb, c4, acc);
-  else
-#endif
-  if (end - beg <= 4) spmm_row_chunks<4>(beg, end, col, val, xb, c4, acc);
+  else if (end - beg <= 4) spmm_row_chunks<4>(beg, end, col, val, xb, c4, acc);
   else spmm_row_chunks<8>(beg, end, col, val, xb, c4, acc);
   if (elu_y) {
     f32x4 g = ld4(elu_y + t * 4);
@@ -103,32 +83,48 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
     acc.z *= elu_grad_from_out(g.z);
     acc.w *= elu_grad_from_out(g.w);
   }
-#if CFSD_SPMM_NT
-  __builtin_nontemporal_store(acc, reinterpret_cast<f32x4*>(y + t * 4));
-#else
+  // (non-temporal stores measured: this kernel ~0.8 us faster, the conv
+  // reading y 0.5-1 us slower -> plain stores)
   st4(y + t * 4, acc);
-#endif
 }
 
 // out[(i*bs + j), v, :] = x[mesh(i or j), v, :]; one thread per (out mesh,
 // vertex); c <= 4 channels per vertex (xyz) are copied as scalars, larger c
-// in 16-B chunks.
+// in 16-B chunks.  Device-side indices are range-guarded so a bad value can
+// never fault the GPU: a key outside [0, n_regions) swaps nothing (every
+// output mesh is its base mesh) and a mesh index outside [0, n_meshes) is
+// clamped into it (the host validates both before they reach the device).
 __global__ __launch_bounds__(256) void swap_k(const float* __restrict__ x,
                                               const int* __restrict__ batch_idx,
                                               const unsigned char* __restrict__ mask,
                                               const int* __restrict__ key, float* __restrict__ out,
-                                              int bs, int nv, int c, long total) {
+                                              int bs, int nv, int c, int n_meshes, int n_regions,
+                                              long total) {
   long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   int ob, v;
   divmod32(t, nv, ob, v);
   const int i = ob / bs, j = ob % bs;
   const int k = *key;
-  const bool take = (i != j) && mask[(long)k * nv + v];
-  const long src_mesh = batch_idx[take ? j : i];
+  const bool take = (i != j) && k >= 0 && k < n_regions && mask[(long)k * nv + v];
+  const long src_mesh = min(max(batch_idx[take ? j : i], 0), n_meshes - 1);
   const float* src = x + (src_mesh * nv + v) * c;
   float* dst = out + t * c;
   for (int q = 0; q < c; ++q) dst[q] = src[q];
+}
+
+// Dataset normalisation (data_loading.py:259-260, (verts - mean) / std with
+// per-vertex [nv, c] statistics): subtraction then IEEE division, the two
+// roundings of the reference's torch ops, so the result is bit-exact.
+__global__ __launch_bounds__(256) void normalize_k(const float* __restrict__ x,
+                                                   const float* __restrict__ mean,
+                                                   const float* __restrict__ std,
+                                                   float* __restrict__ out, int per_mesh, long total) {
+#pragma clang fp contract(off)
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int e = (int)(t % per_mesh);
+  out[t] = (x[t] - mean[e]) / std[e];
 }
 
 __global__ void scale_k(float* __restrict__ y, long n, float alpha) {
@@ -222,12 +218,8 @@ extern "C" int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const f
   const long total = (long)batch * m * (c / 4);
   if (total >= (1L << 31) || (long)batch * n >= (1L << 31))
     return set_error(CFSD_EINVAL, "spmm_csr: batch x rows >= 2^31 (32-bit indices)");
-#if CFSD_SPMM_XCD
   const long per_grp = (total + 7) / 8;  // 8 XCD groups of equal block count
   const unsigned nblk = (unsigned)(8 * ((per_grp + 255) / 256));
-#else
-  const unsigned nblk = (unsigned)((total + 255) / 256);
-#endif
   hipLaunchKernelGGL(spmm_csr_k, dim3(nblk), dim3(256), 0,
                      (hipStream_t)stream, row_ptr, col, val, x, elu_y, y, m, n, c / 4, total);
   return launch_status("spmm_csr");
@@ -235,16 +227,28 @@ extern "C" int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const f
 
 extern "C" int cfsd_swap_features(const float* x, const int32_t* batch_idx,
                                   const uint8_t* region_mask, const int32_t* key, float* out,
-                                  int bs, int nv, int c, int n_meshes, void* stream) {
+                                  int bs, int nv, int c, int n_meshes, int n_regions,
+                                  void* stream) {
   if (!x || !batch_idx || !region_mask || !key || !out)
     return set_error(CFSD_EINVAL, "swap_features: null pointer");
-  if (bs <= 0 || nv <= 0 || c <= 0 || n_meshes <= 0)
+  if (bs <= 0 || nv <= 0 || c <= 0 || n_meshes <= 0 || n_regions <= 0)
     return set_error(CFSD_EINVAL, "swap_features: bad sizes");
   const long total = (long)bs * bs * nv;
   if (total >= (1L << 31)) return set_error(CFSD_EINVAL, "swap_features: bs^2 x nv >= 2^31");
   hipLaunchKernelGGL(swap_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, x, batch_idx, region_mask, key, out, bs, nv, c, total);
+                     (hipStream_t)stream, x, batch_idx, region_mask, key, out, bs, nv, c, n_meshes,
+                     n_regions, total);
   return launch_status("swap_features");
+}
+
+extern "C" int cfsd_normalize(const float* x, const float* mean, const float* std, float* out,
+                              int n_meshes, int nv, int c, void* stream) {
+  if (!x || !mean || !std || !out) return set_error(CFSD_EINVAL, "normalize: null pointer");
+  if (n_meshes <= 0 || nv <= 0 || c <= 0) return set_error(CFSD_EINVAL, "normalize: bad sizes");
+  const long total = (long)n_meshes * nv * c;
+  hipLaunchKernelGGL(normalize_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, mean, std, out, nv * c, total);
+  return launch_status("normalize");
 }
 
 extern "C" int cfsd_scale(float* y, size_t n, float alpha, void* stream) {

@@ -657,10 +657,37 @@ __device__ __forceinline__ uint32_t mix32(uint64_t x) {
   return (uint32_t)x;
 }
 
+// Keyed permutation of [0, n): a 4-round Feistel network on the smallest
+// even-bit power-of-two domain >= n, cycle-walked back into [0, n) (the
+// orbit of an in-domain value re-enters the domain, so the walk ends).
+// Replaces the host RandomSampler's torch.randperm of MeshLoader
+// (data_loading.py:40-48, shuffle=True): every epoch gets a fresh order from
+// (seed, epoch), drawn on the device so a graph replay needs no host input.
+// Restated by oracle/cfsd_oracle.py:epoch_permutation (tests).
+__device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint32_t n, uint64_t key) {
+  int bits = 2;
+  while ((1u << bits) < n) bits += 2;
+  const int h = bits / 2;
+  const uint32_t mask = (1u << h) - 1u;
+  do {
+    uint32_t l = x >> h, r = x & mask;
+#pragma unroll
+    for (int round = 0; round < 4; ++round) {
+      const uint32_t f = mix32(key + 0x9E3779B97F4A7C15ULL * (uint64_t)(round + 1) + r) & mask;
+      const uint32_t nl = r;
+      r = l ^ f;
+      l = nl;
+    }
+    x = (l << h) | r;
+  } while (x >= n);
+  return x;
+}
+
 __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
                              float* __restrict__ eps, int n_eps, int* __restrict__ key,
                              int n_regions, int* __restrict__ batch_idx, int bs, int n_batches,
-                             const int* __restrict__ perm, int* __restrict__ adam_step) {
+                             const int* __restrict__ perm, int n_items, int shuffle,
+                             int* __restrict__ adam_step) {
   __shared__ int t_sh;
   if (threadIdx.x == 0) {
     t_sh = *counter + 1;
@@ -672,8 +699,12 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
     if (key) *key = (int)(mix32(base ^ 0xABCDEFULL) % (uint32_t)n_regions);
   }
   if (batch_idx && (int)threadIdx.x < bs) {
-    const int bt = (t - 1) % n_batches;
-    const int slot = bt * bs + threadIdx.x;
+    const int bt = (t - 1) % n_batches, epoch = (t - 1) / n_batches;
+    int slot = bt * bs + threadIdx.x;
+    if (shuffle) {
+      const uint64_t ek = (seed ^ 0x5DEECE66DULL) * 0xD6E8FEB86659FD93ULL + (uint64_t)epoch;
+      slot = (int)feistel_perm((uint32_t)slot, (uint32_t)n_items, ek);
+    }
     batch_idx[threadIdx.x] = perm ? perm[slot] : slot;
   }
   if (eps) {
@@ -695,7 +726,7 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
 
 using namespace cfsd;
 
-extern "C" int cfsd_version(void) { return (2 << 16) | 0; }  // 2.0: 4-wide inverse head
+extern "C" int cfsd_version(void) { return (3 << 16) | 0; }  // 3.0: per-epoch shuffle, bf16 path
 extern "C" const char* cfsd_last_error_string(void) { return g_err; }
 
 extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {
@@ -879,13 +910,16 @@ extern "C" int cfsd_adam(float* param, const float* grad, float* m, float* v,
 
 extern "C" int cfsd_step_begin(int32_t* counter, unsigned long long seed, float* eps, int n_eps,
                                int32_t* key, int n_regions, int32_t* batch_idx, int bs,
-                               int n_batches, const int32_t* perm, int32_t* adam_step,
-                               void* stream) {
+                               int n_batches, const int32_t* perm, int n_items, int shuffle,
+                               int32_t* adam_step, void* stream) {
   if (!counter) return set_error(CFSD_EINVAL, "step_begin: null counter");
   if (key && n_regions <= 0) return set_error(CFSD_EINVAL, "step_begin: n_regions");
-  if (batch_idx && (bs <= 0 || bs > 256 || n_batches <= 0))
-    return set_error(CFSD_EINVAL, "step_begin: bs/n_batches");
+  if (batch_idx) {
+    if (bs <= 0 || bs > 256 || n_batches <= 0) return set_error(CFSD_EINVAL, "step_begin: bs/n_batches");
+    if (n_items < (long)n_batches * bs)
+      return set_error(CFSD_EINVAL, "step_begin: n_items %d < n_batches %d x bs %d", n_items, n_batches, bs);
+  }
   hipLaunchKernelGGL(step_begin_k, dim3(1), dim3(256), 0, (hipStream_t)stream, counter, seed, eps,
-                     n_eps, key, n_regions, batch_idx, bs, n_batches, perm, adam_step);
+                     n_eps, key, n_regions, batch_idx, bs, n_batches, perm, n_items, shuffle, adam_step);
   return launch_status("step_begin");
 }

@@ -41,8 +41,15 @@ def broadcast_parameters(flat, src=0):
 
 
 class GradientAverager:
-    """All-reduce(SUM) of the flat gradient bucket, then x 1/world.
+    """All-reduce(SUM) of the flat gradient, then x 1/world.
 
+    Two ways to use it (both give the same numbers):
+    * ``avg(grad)``: one blocking all-reduce of the whole bucket;
+    * bucketed, overlapped with the backward (``SDVAEEngine.train_step_on``
+      does this when handed an averager): ``bucket_ready(view)`` starts an
+      asynchronous all-reduce of one contiguous slice as soon as the backward
+      has finalised it (RCCL runs on its own stream, ordered after the work
+      already queued), ``finish(grad)`` joins them and scales.
     ``scale`` is the in-place scaling routine: libcfsd's ``cfsd_scale`` for
     device buffers (default), or any callable ``(tensor, alpha)``."""
 
@@ -53,12 +60,26 @@ class GradientAverager:
             from . import ops
             scale = ops.scale
         self.scale = scale
+        self._works = []
 
     def __call__(self, grad):
         if self.world <= 1:
             return grad
         dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=self.group)
         self.scale(grad, 1.0 / self.world)
+        return grad
+
+    def bucket_ready(self, view):
+        if self.world > 1:
+            self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
+                                               async_op=True))
+
+    def finish(self, grad):
+        works, self._works = self._works, []
+        for w in works:
+            w.wait()
+        if self.world > 1:
+            self.scale(grad, 1.0 / self.world)
         return grad
 
 

@@ -144,6 +144,9 @@ class SDVAEEngine:
         self.seed = int(seed)
         if topo.n_levels != self.spec.n:
             raise ValueError(f"topology has {topo.n_levels} levels, model {self.spec.n}")
+        if topo.lap_csr is None:
+            raise ValueError("SDVAEEngine needs the template's Laplacian (utils.load_template, "
+                             "utils.py:88-89): the training losses are MSE + Laplacian (+ KL, LC)")
         self.num_vert = topo.n_verts[-1]
         self.params = FlatParams(self.spec.param_specs(self.num_vert, topo.seq), self.device)
         n_reg = topo.n_regions if topo.n_regions else 1
@@ -153,13 +156,10 @@ class SDVAEEngine:
         self.reset_parameters()
         self._bufs = {}
         self.loss_acc = torch.zeros(6, dtype=torch.float32, device=self.device)
-        # weight gradients on a side stream, overlapped with the dx chain.
-        # Off: measured slower on MI355X (16.3k vs 17.5k meshes/s) -- the
-        # persistent level-0 kernels are sized for the whole chip and slow
-        # down ~2x when sharing it, and every fork/join costs 6-17 us of
-        # dependency latency inside the graph.
-        self.overlap_dw = False
-        self._side = None
+        self.betas, self.adam_eps = (0.9, 0.999), 1e-8
+        # device step counter: drives the VAE noise, swap key and batch order
+        # of cfsd_step_begin (one per engine, re-seeded by resume())
+        self.counter = torch.zeros(1, dtype=torch.int32, device=self.device)
 
     # ----------------------------------------------------------- parameters
     def reset_parameters(self, generator=None):
@@ -238,6 +238,10 @@ class SDVAEEngine:
             raise ValueError(f"optimizer state has {len(ids)} parameters, model {len(order)}")
         self.lr = float(groups[0]["lr"])
         self.weight_decay = float(groups[0]["weight_decay"])
+        self.betas = tuple(float(b) for b in groups[0].get("betas", (0.9, 0.999)))
+        self.adam_eps = float(groups[0].get("eps", 1e-8))
+        if groups[0].get("amsgrad", False) or groups[0].get("maximize", False):
+            raise ValueError("amsgrad / maximize Adam variants are not supported")
         steps = set()
         for i, k in zip(ids, order):
             st = sd["state"].get(i)
@@ -255,6 +259,8 @@ class SDVAEEngine:
         if len(steps) != 1:
             raise ValueError(f"parameters at different Adam steps {sorted(steps)}")
         P.step.fill_(steps.pop())
+        # the noise / swap-key / batch stream continues where it stopped
+        self.counter.copy_(P.step)
 
     def save_weights(self, checkpoint_dir, epoch):
         """``ModelManager.save_weights`` (``model_manager.py:682-688``):
@@ -303,7 +309,8 @@ class SDVAEEngine:
         nmulv = 2 * lat if S.is_vae else lat
         b.mulv, b.z = f(bsz, nmulv), f(bsz, lat)
         b.dlat, b.terms = f(bsz, 3 * lat), f(2)
-        b.eps = f(bsz, lat)
+        b.eps = torch.zeros(bsz, lat, dtype=torch.float32, device=dev)
+        b.eps_fixed = False  # True: injected by inject()/set_batch(eps=...)
         b.key = torch.zeros(1, dtype=torch.int32, device=dev)
         b.h = f(bsz, self.num_vert, S.out_ch[-1])
         b.dec_up, b.dec_out = [], []
@@ -469,7 +476,30 @@ class SDVAEEngine:
         b.pending_finalize = (not finalize, acc)
 
     # ----------------------------------------------------------- backward
-    def backward(self, b):
+    def enc_conv_numel(self):
+        """Length of the flat-buffer prefix holding the encoder conv
+        parameters (the last gradients the backward produces)."""
+        return self.params.offsets[f"en_layers.{self.spec.n}.weight"][0]
+
+    def backward(self, b, bucket_hook=None):
+        """Hand-derived backward of forward() (the reference's
+        ``loss_tot.backward()``).  With ``bucket_hook`` the gradient becomes
+        final in two contiguous buckets and the hook is called on each as soon
+        as it is (data-parallel all-reduce overlapped with the rest of the
+        backward): first everything from the encoder Linear on (decoder,
+        bottleneck: ~96 % of the parameters), after the encoder-Linear
+        backward; then the encoder convs at the end."""
+        self.backward_head(b, split=bucket_hook is not None)
+        if bucket_hook is not None:
+            bucket_hook(self.params.grad[self.enc_conv_numel():])
+        self.backward_tail(b)
+        if bucket_hook is not None:
+            bucket_hook(self.params.grad[:self.enc_conv_numel()])
+
+    def backward_head(self, b, split=False):
+        """Losses -> decoder -> latent head -> encoder Linear.  ``split``:
+        reduce the decoder conv weight gradients here (their bucket is then
+        final) instead of in backward_tail's single batched reduce."""
         T, S, P = self.topo, self.spec, self.params
         n = S.n
         pending, acc = getattr(b, "pending_finalize", (False, None))
@@ -485,27 +515,16 @@ class SDVAEEngine:
         # dX and dW/db of the output conv in one source-row pass.  Every conv
         # weight gradient is deferred (partials left in b.ws_dw[...]) and all
         # of them are reduced by one launch at the end.
+        # (weight gradients on a side stream overlapping the dx chain were
+        # measured slower on MI355X, 16.3k vs 17.5k meshes/s: the persistent
+        # level-0 kernels slow ~2x when sharing the chip and every fork/join
+        # costs 6-17 us inside the graph -> one stream)
         deferred = []
-        main = torch.cuda.current_stream(self.device)
-        side = self._side_stream() if self.overlap_dw else None
 
         def defer(d, name):
             deferred.append((d, P.gview(name + ".weight"), P.gview(name + ".bias")))
 
-        def weight_grad(*args):
-            """Weight-gradient slabs of one conv.  They are leaves of the
-            backward (nothing downstream reads them before the batched
-            reduce), so they run on a side stream forked here, concurrently
-            with the data-gradient chain -- the coarse-level launches fill
-            only a fraction of the 256 CUs each.  Same kernels, same
-            workspaces: results are bit-identical to the serial order."""
-            if side is None:
-                return ops.spiral_conv_bwd_weight(*args)
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                return ops.spiral_conv_bwd_weight(*args)
+        weight_grad = ops.spiral_conv_bwd_weight
 
         _, d = ops.spiral_conv_bwd(last_in, T.spiral[0], b.dout, T.spiral_inv[0],
                                    P.view(f"de_layers.{n + 1}.layer.weight"), None, None,
@@ -534,6 +553,10 @@ class SDVAEEngine:
                        dw=P.gview("de_layers.0.weight"), db=P.gview("de_layers.0.bias"),
                        workspace=b.lin_ws)
         ops.latent_bwd(b.mulv, b.eps, b.z, b.dz, b.dlat, b.dmulv, S.latent, True, S.is_vae, S.sigmoid)
+        if split:
+            ops.dw_reduce_batch(deferred)
+            deferred = []
+        b.deferred = deferred
         # stacked encoder Linear; ELU of the last Enblock folded into dx
         W, _ = self._enc_lin()
         gW, gB = self._enc_lin(P.grad)
@@ -548,7 +571,18 @@ class SDVAEEngine:
                            db=gB, workspace=b.lin_ws)
             ops.spmm(T.downT_csr[last], b.g_pooled[last], T.n_verts[last], elu_y=b.enc_full[last],
                      out=b.dpre_enc[last])
-        for (cin, cout, lv) in reversed(enc):
+
+    def backward_tail(self, b):
+        """Encoder convs (E_{n-1} .. E0), then ONE batched reduce of every
+        still-deferred conv weight gradient."""
+        T, S, P = self.topo, self.spec, self.params
+        deferred, b.deferred = b.deferred, []
+
+        def defer(d, name):
+            deferred.append((d, P.gview(name + ".weight"), P.gview(name + ".bias")))
+
+        weight_grad = ops.spiral_conv_bwd_weight
+        for (cin, cout, lv) in reversed(S.enc_layers()):
             w, _ = self._enc_w(lv)
             x_in = b.x if lv == 0 else b.enc_out[lv - 1]
             rows_tab = T.enc_rows[lv]
@@ -577,60 +611,100 @@ class SDVAEEngine:
                                          out=b.g_pooled[prev], workspace=b.ws)
                 ops.spmm(T.downT_csr[prev], b.g_pooled[prev], T.n_verts[prev], elu_y=b.enc_full[prev],
                          out=b.dpre_enc[prev])
-        if side is not None:  # join the weight-gradient stream
-            ev = torch.cuda.Event()
-            ev.record(side)
-            main.wait_event(ev)
         ops.dw_reduce_batch(deferred)
-
-    def _side_stream(self):
-        if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
-        return self._side
 
     def adam_step(self):
         P = self.params
-        ops.adam(P.data, P.grad, P.exp_avg, P.exp_avg_sq, P.step, self.lr,
-                 weight_decay=self.weight_decay)
+        ops.adam(P.data, P.grad, P.exp_avg, P.exp_avg_sq, P.step, self.lr, beta1=self.betas[0],
+                 beta2=self.betas[1], eps=self.adam_eps, weight_decay=self.weight_decay)
 
-    def advance_step(self):
-        """t += 1 on device (the Adam bias-correction step)."""
-        ops.step_begin(self.params.step, self.seed)
+    def advance_step(self, b=None):
+        """t += 1 on device (the Adam bias-correction step) and, for a VAE
+        batch whose noise was not injected, a fresh eps ~ N(0, 1) drawn on
+        the device (``torch.randn_like``, model.py:187) from the step counter."""
+        draw = b is not None and self.spec.is_vae and not b.eps_fixed
+        ops.step_begin(self.counter, self.seed, eps=b.eps if draw else None,
+                       adam_step=self.params.step)
 
     # ----------------------------------------------------------- entry points
     def set_batch(self, x, key_index=None, eps=None):
-        """Copy an already-swapped batch [B, V, C] (+ injected key / eps)."""
+        """Copy an already-swapped batch [B, V, C] (+ injected key / eps).
+        Without ``eps`` a VAE train step draws its own noise on the device."""
         b = self.buffers(x.shape[0])
         b.x.copy_(x)
+        self.inject(b, key_index, eps)
+        return b
+
+    def inject(self, b, key_index=None, eps=None):
+        """Fix the swap key and/or the VAE noise of batch buffers ``b`` (parity
+        tests inject the reference's values).  ``eps=None`` returns the batch to
+        device-drawn noise."""
         if key_index is not None:
             b.key.fill_(int(key_index))
         if eps is not None:
             b.eps.copy_(eps)
+        b.eps_fixed = eps is not None
         return b
 
     def train_step_on(self, b, acc=None, grad_hook=None, advance=True):
         """forward + losses + backward + (grad_hook, e.g. all-reduce) + Adam.
-        ``advance=False`` when cfsd_step_begin already advanced Adam's t."""
-        self.forward(b, train=True, acc=acc, finalize=False)
-        self.backward(b)
-        if grad_hook is not None:
-            grad_hook(self.params.grad)
+        ``advance=False`` when cfsd_step_begin already advanced Adam's t (and
+        drew the noise).  With ``advance`` the noise is drawn first."""
         if advance:
-            self.advance_step()
+            self.advance_step(b)
+        self.forward(b, train=True, acc=acc, finalize=False)
+        if hasattr(grad_hook, "bucket_ready"):  # dist.GradientAverager: overlapped buckets
+            self.backward(b, bucket_hook=grad_hook.bucket_ready)
+            grad_hook.finish(self.params.grad)
+        else:
+            self.backward(b)
+            if grad_hook is not None:
+                grad_hook(self.params.grad)
         self.adam_step()
 
-    def resident_step(self, b, dataset, perm, n_batches, acc=None, grad_hook=None):
-        """Full reference step from a resident dataset: device-side batch
-        pick + swap key + VAE noise (cfsd_step_begin), on-device feature swap,
-        then train_step_on.  No host input -> graph-capturable."""
+    def resident_step(self, b, data, acc=None, grad_hook=None):
+        """Full reference step from a resident dataset (:class:`ResidentData`):
+        device-side epoch-shuffled batch pick + swap key + VAE noise
+        (cfsd_step_begin), on-device feature swap, then train_step_on.  No
+        host input -> graph-capturable."""
         T = self.topo
-        ops.step_begin(self._step_counter(b), self.seed, eps=b.eps, key=b.key,
+        ops.step_begin(self.counter, self.seed, eps=b.eps if self.spec.is_vae else None, key=b.key,
                        n_regions=max(T.n_regions, 1), batch_idx=b.batch_idx, bs=self.swap_bs,
-                       n_batches=n_batches, perm=perm, adam_step=self.params.step)
-        ops.swap_features(dataset, b.batch_idx, T.region_mask, b.key, self.swap_bs, out=b.x)
+                       n_batches=data.n_batches, perm=data.rows, n_items=data.n_items,
+                       shuffle=data.shuffle, adam_step=self.params.step)
+        ops.swap_features(data.meshes, b.batch_idx, T.region_mask, b.key, self.swap_bs, out=b.x)
         self.train_step_on(b, acc=acc, grad_hook=grad_hook, advance=False)
 
-    def _step_counter(self, b):
-        if not hasattr(b, "counter"):
-            b.counter = torch.zeros(1, dtype=torch.int32, device=self.device)
-        return b.counter
+
+class ResidentData:
+    """A training set resident in HBM (the MeshInMemoryDataset + MeshLoader of
+    ``data_loading.py:23-51, 86-283``, without disk or worker processes).
+
+    ``meshes`` [N, V, 3] device fp32 (normalised on the device with
+    ``norm`` = {'mean', 'std'} [V, 3] when given, data_loading.py:259-260);
+    ``rows`` optional int32 subset of mesh indices (e.g. this rank's shard);
+    batches of ``bs`` base meshes with ``shuffle`` (a fresh device-drawn order
+    every epoch) and ``drop_last`` semantics (data_loading.py:40-48)."""
+
+    def __init__(self, meshes, bs, rows=None, shuffle=True, norm=None):
+        if not meshes.is_cuda or meshes.dim() != 3:
+            raise ValueError("meshes must be a [N, V, C] device tensor")
+        self.meshes = meshes.contiguous()
+        if norm is not None:
+            mean = norm["mean"].to(meshes.device, torch.float32).contiguous()
+            std = norm["std"].to(meshes.device, torch.float32).contiguous()
+            ops.normalize(self.meshes, mean, std, out=self.meshes)
+        n = meshes.shape[0]
+        if rows is not None:
+            rows = torch.as_tensor(rows).to(torch.int64).cpu()
+            if rows.numel() and (int(rows.min()) < 0 or int(rows.max()) >= n):
+                raise ValueError("rows index outside the dataset")
+            self.rows = rows.to(torch.int32).to(meshes.device)
+            self.n_items = int(rows.numel())
+        else:
+            self.rows, self.n_items = None, n
+        self.bs = int(bs)
+        self.n_batches = self.n_items // self.bs
+        if self.n_batches < 1:
+            raise ValueError(f"{self.n_items} meshes < one batch of {self.bs}")
+        self.shuffle = bool(shuffle)

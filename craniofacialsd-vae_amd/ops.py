@@ -209,14 +209,30 @@ def spmm(csr, x, m, elu_y=None, out=None):
 
 
 def swap_features(x_all, batch_idx, region_mask, key, bs, out=None):
+    """``SwapFeatures.__call__`` (swap_batch_transform.py:13-42) on device."""
     n_meshes, nv, c = x_all.shape
     _need(x_all, None, name="x_all")
     _need(batch_idx, (bs,), torch.int32, "batch_idx")
+    if region_mask is None or region_mask.dim() != 2:
+        raise ValueError("region_mask [n_regions, nv] is required")
     _need(region_mask, (region_mask.shape[0], nv), torch.uint8, "region_mask")
     _need(key, (1,), torch.int32, "key")
     y = _out(out, (bs * bs, nv, c), x_all)
     call("cfsd_swap_features", ptr(x_all), ptr(batch_idx), ptr(region_mask), ptr(key), ptr(y), bs,
-         nv, c, n_meshes, stream_ptr())
+         nv, c, n_meshes, int(region_mask.shape[0]), stream_ptr())
+    return y
+
+
+def normalize(x, mean, std, out=None):
+    """``(x - mean) / std`` per vertex (data_loading.py:259-260), bit-exact."""
+    _need(x, None, name="x")
+    if x.dim() != 3:
+        raise ValueError(f"x: shape {tuple(x.shape)}, expected [n_meshes, nv, c]")
+    n, nv, c = x.shape
+    _need(mean, (nv, c), name="mean")
+    _need(std, (nv, c), name="std")
+    y = _out(out, (n, nv, c), x)
+    call("cfsd_normalize", ptr(x), ptr(mean), ptr(std), ptr(y), n, nv, c, stream_ptr())
     return y
 
 
@@ -366,13 +382,32 @@ def adam(param, grad, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_d
 
 
 def step_begin(counter, seed, eps=None, key=None, n_regions=0, batch_idx=None, bs=0,
-               n_batches=0, perm=None, adam_step=None):
+               n_batches=0, perm=None, adam_step=None, n_items=None, shuffle=False):
+    """Per-step device bookkeeping (``cfsd_step_begin``): counter, swap key,
+    VAE noise, the epoch-shuffled drop_last batch and Adam's t.  ``perm``
+    (optional, int32) maps the ``n_items`` shuffled positions to dataset rows;
+    its length and range are the caller's contract (validated once by
+    ``engine.ResidentData``), not re-checked per step."""
     _need(counter, (1,), torch.int32, "counter")
     if adam_step is not None:
         _need(adam_step, (1,), torch.int32, "adam_step")
+    if eps is not None:
+        _need(eps, None, name="eps")
+    if key is not None:
+        _need(key, (1,), torch.int32, "key")
+    if batch_idx is not None:
+        _need(batch_idx, (bs,), torch.int32, "batch_idx")
+        if n_items is None:
+            n_items = perm.numel() if perm is not None else n_batches * bs
+        if perm is not None:
+            _need(perm, None, torch.int32, "perm")
+            if perm.numel() < n_items:
+                raise ValueError(f"perm has {perm.numel()} entries < n_items {n_items}")
+        if n_items < n_batches * bs:
+            raise ValueError(f"n_items {n_items} < n_batches {n_batches} x bs {bs}")
     call("cfsd_step_begin", ptr(counter), ctypes.c_ulonglong(seed), ptr(eps),
          eps.numel() if eps is not None else 0, ptr(key), n_regions, ptr(batch_idx), bs,
-         n_batches, ptr(perm), ptr(adam_step), stream_ptr())
+         n_batches, ptr(perm), int(n_items or 0), int(bool(shuffle)), ptr(adam_step), stream_ptr())
 
 
 def scale(y, alpha):

@@ -142,10 +142,18 @@ int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const float* val, 
  *   out[i*bs+j, v, :] = x[mesh[(i != j && mask[key*nv + v]) ? j : i], v, :]
  * x [n_meshes, nv, c] resident dataset, batch_idx [bs] device indices of the
  * base meshes, region_mask [n_regions, nv] (1 = feature vertex of the region),
- * key: device int32 scalar (region index).  Bit-exact copy. */
+ * key: device int32 scalar (region index).  Bit-exact copy.  Device values
+ * are range-guarded (never fault): a key outside [0, n_regions) swaps nothing,
+ * a mesh index outside [0, n_meshes) is clamped. */
 int cfsd_swap_features(const float* x, const int32_t* batch_idx, const uint8_t* region_mask,
                        const int32_t* key, float* out, int bs, int nv, int c, int n_meshes,
-                       void* stream);
+                       int n_regions, void* stream);
+
+/* Dataset normalisation, (x - mean) / std with per-vertex statistics
+ * (data_loading.py:259-260; mean/std [nv, c] from norm.pt): x, out
+ * [n_meshes, nv, c] (may alias).  Same two IEEE roundings as torch: bit-exact. */
+int cfsd_normalize(const float* x, const float* mean, const float* std, float* out, int n_meshes,
+                   int nv, int c, void* stream);
 
 /* ---------------------------------------------------------------- dense layers
  * nn.Linear of the latent bottleneck (model.py:114-124, 153-156, 167):
@@ -223,14 +231,18 @@ int cfsd_adam(float* param, const float* grad, float* m, float* v, const int32_t
 /* Per-step device bookkeeping (graph-replayable, no host input):
  * t = ++*counter; key = hash(seed, t) % n_regions (replaces random.choice,
  * swap_batch_transform.py:26); eps[n_eps] ~ N(0,1) (replaces randn_like,
- * model.py:187); batch_idx[q] = perm[((t-1) % n_batches)*bs + q] (or the
- * identity when perm == NULL) — the shuffled, drop_last batch order of
- * MeshLoader (data_loading.py:40-42); ++*adam_step (the Adam bias-correction
- * step of this iteration, so the step needs no separate launch for it).
+ * model.py:187); the batch of MeshLoader(shuffle=True, drop_last=True)
+ * (data_loading.py:40-48): with bt = (t-1) % n_batches, epoch = (t-1) / n_batches,
+ *   j_q = shuffle ? P_epoch(bt*bs + q) : bt*bs + q,   batch_idx[q] = perm ? perm[j_q] : j_q
+ * where P_epoch is a keyed permutation of [0, n_items) drawn from (seed, epoch)
+ * (a fresh order every epoch; n_batches*bs <= n_items, the tail is dropped) and
+ * perm (n_items entries, optional) maps positions to dataset rows (e.g. a
+ * rank's shard); ++*adam_step (the Adam bias-correction step of this iteration).
  * Any of eps/key/batch_idx/adam_step may be NULL. */
 int cfsd_step_begin(int32_t* counter, unsigned long long seed, float* eps, int n_eps,
                     int32_t* key, int n_regions, int32_t* batch_idx, int bs, int n_batches,
-                    const int32_t* perm, int32_t* adam_step, void* stream);
+                    const int32_t* perm, int n_items, int shuffle, int32_t* adam_step,
+                    void* stream);
 
 /* F.elu backward written from the ELU output (model.py:68,84 autograd):
  * dx = dy * (y > 0 ? 1 : y + 1).  dx may alias dy. */

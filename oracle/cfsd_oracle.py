@@ -293,3 +293,58 @@ def train_step(P, opt, x4, topo, key_index, eps, w=LOSS_W, is_vae=True):
 def make_params(weights):
     return {k: torch.tensor(np.asarray(v), dtype=torch.float32, requires_grad=True)
             for k, v in weights.items()}
+
+
+# --------------------------------------------------------------- data order
+M64 = (1 << 64) - 1
+
+
+def _mix32(x):
+    """The 64 -> 32-bit finaliser of libcfsd's step_begin_k (train_ops.hip)."""
+    x &= M64
+    x ^= x >> 33
+    x = (x * 0xff51afd7ed558ccd) & M64
+    x ^= x >> 33
+    x = (x * 0xc4ceb9fe1a85ec53) & M64
+    x ^= x >> 33
+    return x & 0xFFFFFFFF
+
+
+def epoch_permutation(seed, epoch, n):
+    """Order in which one epoch visits the n dataset positions: the keyed
+    Feistel permutation libcfsd draws on the device for MeshLoader(shuffle=True)
+    (data_loading.py:40-48; the reference's torch.randperm is a host RNG stream
+    this restatement does not reproduce -- the contract pinned here is "a
+    permutation per epoch", bit-exact to the kernel)."""
+    key = (((seed ^ 0x5DEECE66D) * 0xD6E8FEB86659FD93) + epoch) & M64
+    bits = 2
+    while (1 << bits) < n:
+        bits += 2
+    h = bits // 2
+    mask = (1 << h) - 1
+    out = np.empty(n, np.int64)
+    for i in range(n):
+        x = i
+        while True:
+            l, r = x >> h, x & mask
+            for rnd in range(4):
+                f = _mix32(key + 0x9E3779B97F4A7C15 * (rnd + 1) + r) & mask
+                l, r = r, l ^ f
+            x = (l << h) | r
+            if x < n:
+                break
+        out[i] = x
+    return out
+
+
+def epoch_batches(seed, epoch, n_items, bs, perm=None):
+    """The drop_last batches of one epoch: [n_items // bs, bs] dataset rows."""
+    order = epoch_permutation(seed, epoch, n_items)[: (n_items // bs) * bs]
+    if perm is not None:
+        order = np.asarray(perm)[order]
+    return order.reshape(-1, bs)
+
+
+def normalize(x, mean, std):
+    """data_loading.py:259-260: (verts - mean) / std (torch fp32 ops)."""
+    return (torch.as_tensor(x) - torch.as_tensor(mean)) / torch.as_tensor(std)

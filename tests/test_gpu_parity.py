@@ -314,9 +314,7 @@ def test_train_three_steps_golden(otopo, dtopo):
         key = recipe.train_key_index(step)
         eps = torch.from_numpy(recipe.train_eps(step))
         out, grads, x16 = O.train_step(P, opt, meshes[4 * step:4 * step + 4], otopo, key, eps.numpy())
-        b = eng.buffers(16)
-        b.key.fill_(key)
-        b.eps.copy_(eps)
+        b = eng.inject(eng.buffers(16), key, eps)
         b.batch_idx.copy_(torch.arange(4 * step, 4 * step + 4, dtype=torch.int32))
         ops.swap_features(data, b.batch_idx, dtopo.region_mask, b.key, 4, out=b.x)
         eng.train_step_on(b)
@@ -421,13 +419,13 @@ def test_graph_replay_matches_eager(dtopo):
     """The hipGraph-captured resident step (device-side batch pick, key and
     noise) gives bit-identical parameters and losses to eager launches."""
     w = recipe.golden_weights()
-    data = torch.from_numpy(recipe.normalized_meshes(12)).to(DEV)
-    perm = torch.arange(12, dtype=torch.int32, device=DEV)
     res = []
     for use_graph in (False, True):
+        data = E.ResidentData(torch.from_numpy(recipe.normalized_meshes(12)).to(DEV), bs=4,
+                              rows=list(range(11, -1, -1)), shuffle=True)
         eng = make_engine(dtopo, w)
         b = eng.buffers(16)
-        step = lambda: eng.resident_step(b, data, perm, 3)  # noqa: E731
+        step = lambda: eng.resident_step(b, data)  # noqa: E731
         if use_graph:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -560,9 +558,8 @@ def test_reconstruction_errors_c1(dtopo):
 
 
 def _golden_step(eng, dtopo, data, step):
-    b = eng.buffers(16)
-    b.key.fill_(recipe.train_key_index(step))
-    b.eps.copy_(torch.from_numpy(recipe.train_eps(step)))
+    b = eng.inject(eng.buffers(16), recipe.train_key_index(step),
+                   torch.from_numpy(recipe.train_eps(step)))
     b.batch_idx.copy_(torch.arange(4 * step, 4 * step + 4, dtype=torch.int32))
     ops.swap_features(data, b.batch_idx, dtopo.region_mask, b.key, 4, out=b.x)
     eng.train_step_on(b)

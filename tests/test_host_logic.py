@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_reporting(lib):
-    assert lib.cfsd_version() >> 16 == 2  # 2.0: 4-wide inverse-spiral head
+    assert lib.cfsd_version() >> 16 == 3  # 3.0: per-epoch shuffle, bf16 path
     # argument validation happens before any HIP call: safe without a GPU
     rc = lib.cfsd_spiral_conv_fwd(None, None, None, None, None, None, 0, 1, 1, 1, 9, 32, 32, 0, None)
     assert rc == -1
@@ -149,3 +149,24 @@ def test_checkpoint_format_round_trip(topo_npz, tmp_path):
     bad["state"][0]["step"] = torch.tensor(3.0)
     with pytest.raises(ValueError):
         b.load_optimizer_state_dict(bad)
+
+
+def test_epoch_permutation_is_a_permutation_per_epoch():
+    """Oracle restatement of the device epoch shuffle (cfsd_step_begin): each
+    epoch is a permutation of [0, n), epochs differ, drop_last batching."""
+    from oracle import cfsd_oracle as O
+    for n in (1, 2, 3, 7, 64, 250, 1000):
+        p0, p1 = O.epoch_permutation(9, 0, n), O.epoch_permutation(9, 1, n)
+        assert sorted(p0.tolist()) == list(range(n)) == sorted(p1.tolist())
+        if n > 3:
+            assert not np.array_equal(p0, p1)
+    b = O.epoch_batches(9, 2, 10, 4, perm=np.arange(100, 110))
+    assert b.shape == (2, 4) and len(np.unique(b)) == 8 and b.min() >= 100
+
+
+def test_engine_requires_laplacian(topo_npz):
+    from craniofacialsd_vae_amd import engine as E
+    npz = {k: v for k, v in topo_npz.items() if not k.startswith("lap_")}
+    topo = topology.DeviceTopology.from_npz(npz, device="cpu")
+    with pytest.raises(ValueError, match="Laplacian"):
+        E.SDVAEEngine(topo, E.ModelSpec(), device="cpu")

@@ -1,35 +1,22 @@
-#!/bin/bash
-# One GPU-box pass: parity tests, smoke, bench (+cpu baseline), kernel-trace stats of the bench,
-# and HBM-traffic PMC passes (FETCH_SIZE / WRITE_SIZE, one per run) on the dominant kernel.
-# usage (from gpurun): bash tools/gpu_round.sh [tag]
+# One GPU-box pass: GPU tests, default bench, rocprofv3 kernel stats + step timeline.
+# Usage (from the repo root, via gpurun): TAG=r02a bash tools/gpu_round.sh [tests|bench|prof ...]
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-TAG=${1:-r01}
-OUT=gpurun_out/$TAG
-rm -rf $OUT; mkdir -p $OUT
-if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 \
-    || { tail -60 $OUT/tests.log; exit 1; }
-  tail -3 $OUT/tests.log
-  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -30 $OUT/smoke.log; exit 1; }
-  tail -1 $OUT/smoke.log
-fi
-timeout -k 10 300 python -u bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
-cat $OUT/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --steps 30 --warmup 5 --no-cpu > $OUT/prof.log 2>&1 \
-  || { tail -30 $OUT/prof.log; exit 1; }
-python tools/prof_summary.py $(find $OUT/prof -name '*.db' | head -1) 60 > $OUT/kernel_stats.txt || true
-find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \; || true
-head -20 $OUT/kernel_stats.txt
-if [ -z "$SKIP_PMC" ]; then
-  export KB_ITERS=20
-  timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc_fetch -o run -- python3 tools/kbench.py fwd_d3 dx_d3 dw_d3 > $OUT/pmc_fetch.log 2>&1
-  timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write -o run -- python3 tools/kbench.py fwd_d3 dx_d3 dw_d3 > $OUT/pmc_write.log 2>&1
-  python tools/pmc_traffic.py $OUT "conv_fwd_mfma<32, 32, 1, 9>" > $OUT/pmc_traffic_conv_fwd_d3.json || true
-  python tools/pmc_traffic.py $OUT "conv_dx_mfma<32, 32, 9>" > $OUT/pmc_traffic_conv_dx_d3.json || true
-  python tools/pmc_traffic.py $OUT "conv_dw_mfma<32, 32>" > $OUT/pmc_traffic_conv_dw_d3.json || true
-  cat $OUT/pmc_traffic_*.json
-  KB="fwd_d3 dx_d3 dw_d3" OUT=$OUT/pmc_sq bash tools/pmc_kernels.sh > $OUT/pmc_sq.log 2>&1 || true
-  tail -20 $OUT/pmc_sq.log
-fi
-echo ALL_DONE
+O=gpurun_out/${TAG:-r02}; mkdir -p $O
+steps="${*:-tests bench prof}"
+for s in $steps; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/tests.log 2>&1 || { tail -80 $O/tests.log; exit 1; }
+      tail -3 $O/tests.log ;;
+    bench)
+      timeout -k 10 400 python bench.py ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+      cut -c1-400 $O/bench.json ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o bench -- python3 bench.py --steps 30 --warmup 5 --no-cpu --no-extras > $O/prof.log 2>&1 || { tail -30 $O/prof.log; exit 1; }
+      python tools/step_timeline.py $(find $O/prof -name '*.db' | head -1) > $O/timeline.txt; tail -60 $O/timeline.txt ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -30 $O/smoke.log; exit 1; }
+      tail -2 $O/smoke.log ;;
+  esac
+done

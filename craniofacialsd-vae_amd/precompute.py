@@ -571,3 +571,123 @@ def upsampling_matrix(fine_pos, coarse_pos, coarse_faces):
     vals = np.stack([alpha, beta, gamma], 1).reshape(-1).astype(np.float32)
     order = np.lexsort((rows, cols))
     return rows[order], cols[order], vals[order], (len(fine_pos), len(coarse_pos))
+
+
+# ============================================================== hierarchy
+def build_hierarchy(pos, faces, colors=None, sampling_factors=(4, 4, 4, 4), seq_lengths=(9, 9, 9, 9),
+                    dilations=None, sampling_type="basic"):
+    """The reference's precompute chain (``ModelManager._precompute_transformations``
+    + ``_precompute_spirals``, model_manager.py:176-230) from a template:
+    per sampling factor one quadric-edge-collapse level (0/1 down matrix) and
+    its barycentric up matrix, then spirals of every level but the coarsest.
+    Returns a dict in the ``topology_craniofacial.npz`` layout (``spiral_l``,
+    ``down_l_{row,col,val,shape}``, ``up_l_*``, ``pos_l``, ``face_l``,
+    ``region_*``, ``lap_*``) that ``DeviceTopology.from_npz`` consumes.
+
+    ``sampling_type='r_weighted'`` weights the collapse costs by 1/|region|
+    (mesh_simplification.py:50-59).  (The reference also appends each
+    region's contour to its feature list in place there, changing the swap
+    regions of a freshly precomputed template; that side effect is not
+    reproduced.)"""
+    n_lv = len(sampling_factors)
+    dilations = dilations or [1] * n_lv
+    tpl = Template(pos, faces, colors)
+    out = {"n_levels": np.int32(n_lv), "pos_0": tpl.pos, "face_0": tpl.faces.astype(np.int32)}
+    if colors is not None:
+        out["template_colors"] = np.asarray(colors, np.uint8)
+        keys = list(tpl.feat_and_cont.keys())
+        out["region_keys"] = np.asarray(keys)
+        for i, k in enumerate(keys):
+            out[f"region_{i}_feature"] = np.asarray(tpl.feat_and_cont[k]["feature"], np.int32)
+            out[f"region_{i}_contour"] = np.asarray(tpl.feat_and_cont[k]["contour"], np.int32)
+    out["lap_row"], out["lap_col"], out["lap_val"] = tpl.laplacian
+    cur_pos, cur_faces, cur_col = tpl.pos, tpl.faces, tpl.colors
+    for l, factor in enumerate(sampling_factors):
+        rw = None
+        if sampling_type != "basic":
+            if cur_col is None:
+                raise ValueError("region-weighted sampling needs vertex colours")
+            fc = feature_and_contour(cur_col, cur_faces)
+            rw = np.ones(len(cur_pos))
+            for k, f in fc.items():
+                rw[f["feature"] + f["contour"]] = 1 / (len(f["feature"]) + len(f["contour"]))
+        new_faces, kept = quadric_edge_collapse(cur_pos, cur_faces, factor, region_weights=rw)
+        m = len(kept)
+        out[f"down_{l}_row"] = np.arange(m, dtype=np.int32)
+        out[f"down_{l}_col"] = kept.astype(np.int32)
+        out[f"down_{l}_val"] = np.ones(m, np.float32)
+        out[f"down_{l}_shape"] = np.asarray([m, len(cur_pos)], np.int64)
+        new_pos = cur_pos[kept]
+        r, c, v, shape = upsampling_matrix(cur_pos, new_pos, new_faces)
+        out[f"up_{l}_row"], out[f"up_{l}_col"], out[f"up_{l}_val"] = (r.astype(np.int32), c.astype(np.int32), v)
+        out[f"up_{l}_shape"] = np.asarray(shape, np.int64)
+        out[f"spiral_{l}"] = preprocess_spiral(cur_faces, seq_lengths[l], cur_pos, dilations[l]).astype(np.int32)
+        out[f"pos_{l + 1}"], out[f"face_{l + 1}"] = new_pos, new_faces.astype(np.int32)
+        cur_pos, cur_faces = new_pos, new_faces
+        cur_col = None if cur_col is None else cur_col[kept]
+    return out
+
+
+def torus(n_major=80, n_minor=64, r_major=1.0, r_minor=0.35, bumps=0.04, seed=0):
+    """A closed, bumpy torus grid (n_major x n_minor vertices, 2 triangles per
+    cell, consistent winding) with vertex colours that cut it into
+    ``n_major // (n_major // 15)``-ish angular sectors -- a synthetic stand-in
+    for a coloured template (vertex colour = swap region, utils.py:93-135)."""
+    rs = np.random.RandomState(seed)
+    u = np.arange(n_major) * 2 * np.pi / n_major
+    v = np.arange(n_minor) * 2 * np.pi / n_minor
+    uu, vv = np.meshgrid(u, v, indexing="ij")
+    rr = r_minor * (1 + bumps * rs.randn(n_major, n_minor))
+    x = (r_major + rr * np.cos(vv)) * np.cos(uu)
+    y = (r_major + rr * np.cos(vv)) * np.sin(uu)
+    zz = rr * np.sin(vv)
+    pos = np.stack([x, y, zz], -1).reshape(-1, 3).astype(np.float32)
+    idx = np.arange(n_major * n_minor).reshape(n_major, n_minor)
+    i0 = idx
+    i1 = np.roll(idx, -1, axis=0)
+    i2 = np.roll(idx, -1, axis=1)
+    i3 = np.roll(np.roll(idx, -1, axis=0), -1, axis=1)
+    faces = np.concatenate([np.stack([i0, i1, i3], -1).reshape(-1, 3),
+                            np.stack([i0, i3, i2], -1).reshape(-1, 3)]).astype(np.int64)
+    sector = (np.arange(n_major) * 15 // n_major)
+    palette = np.stack([(37 * np.arange(15)) % 256, (91 * np.arange(15) + 40) % 256,
+                        (53 * np.arange(15) + 100) % 256, np.full(15, 255)], 1).astype(np.uint8)
+    colors = palette[np.repeat(sector, n_minor)]
+    return pos, faces, colors
+
+
+_SYNTH_CACHE = {}
+
+
+def synthetic_hierarchy(n_major=80, n_minor=64, device="cuda"):
+    """The north-star's synthetic ~5k-vertex, 4-level hierarchy (5120 / 1280 /
+    320 / 80 / 20 vertices, spiral length 9, 15 colour regions), built by this
+    module from a bumpy torus, as a ``DeviceTopology``."""
+    key = (n_major, n_minor)
+    if key not in _SYNTH_CACHE:
+        _SYNTH_CACHE[key] = build_hierarchy(*torus(n_major, n_minor))
+    return DeviceTopology.from_npz(_SYNTH_CACHE[key], device=device)
+
+
+def write_ply(path, pos, faces, colors=None):
+    """Binary little-endian PLY (float xyz [+ uchar RGBA], int32 triangles)."""
+    pos = np.asarray(pos, np.float32)
+    faces = np.asarray(faces, np.int32)
+    props = [("x", "<f4"), ("y", "<f4"), ("z", "<f4")]
+    head = ["ply", "format binary_little_endian 1.0", f"element vertex {len(pos)}",
+            "property float x", "property float y", "property float z"]
+    if colors is not None:
+        props += [("red", "u1"), ("green", "u1"), ("blue", "u1"), ("alpha", "u1")]
+        head += ["property uchar red", "property uchar green", "property uchar blue", "property uchar alpha"]
+    head += [f"element face {len(faces)}", "property list uchar int vertex_indices", "end_header"]
+    v = np.zeros(len(pos), np.dtype(props))
+    v["x"], v["y"], v["z"] = pos[:, 0], pos[:, 1], pos[:, 2]
+    if colors is not None:
+        c = np.asarray(colors, np.uint8)
+        v["red"], v["green"], v["blue"], v["alpha"] = c[:, 0], c[:, 1], c[:, 2], c[:, 3]
+    f = np.zeros(len(faces), np.dtype([("n", "u1"), ("i", "<i4", (3,))]))
+    f["n"], f["i"] = 3, faces
+    with open(path, "wb") as fh:
+        fh.write(("\n".join(head) + "\n").encode("ascii"))
+        fh.write(v.tobytes())
+        fh.write(f.tobytes())

@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--dataset", type=int, default=256, help="resident synthetic meshes per rank")
     p.add_argument("--topology", default="craniofacial", choices=["craniofacial", "synth5k"])
+    p.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                   help="fp32 (reference arithmetic) or bf16 (configs C3/C5: bf16 level-0/1 tensors on "
+                        "bf16 MFMA, fp32 accumulation and master weights)")
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
     p.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU-baseline sample budget")
     p.add_argument("--no-cpu", action="store_true")
@@ -66,11 +69,13 @@ def load_topology(name, device):
 
 
 class Runner:
-    def __init__(self, world, rank, device, n_meshes, use_graph, topo_name="craniofacial"):
+    def __init__(self, world, rank, device, n_meshes, use_graph, topo_name="craniofacial",
+                 precision="fp32"):
         self.topo = load_topology(topo_name, device)
         self.topo_name = topo_name
+        self.precision = precision
         self.eng = E.SDVAEEngine(self.topo, E.ModelSpec(latent_size=75), lr=1e-4, swap_bs=4,
-                                 seed=1234 + rank, device=device)
+                                 seed=1234 + rank, device=device, precision=precision)
         self.eng.reset_parameters()  # same init on every rank (broadcast below)
         self.world, self.rank = world, rank
         nv = self.topo.n_verts[0]
@@ -81,6 +86,7 @@ class Runner:
         self.avg = cdist.GradientAverager(world)
         if world > 1:
             cdist.broadcast_parameters(self.eng.params.data, 0)
+            self.eng.sync_shadow()
         self.use_graph = use_graph
         self.graphs = None
 
@@ -174,6 +180,33 @@ def launch_cost(name, a):
         if dx:
             by += f4 * B * vs * ci * (2 if elu else 1) + 16 * vs * S
         return fl, by, FP32_PEAK_TFLOPS
+    if name == "cfsd_spiral_conv_fwd_x":
+        sx, sy = (4 if a[1] == 0 else 2), (4 if a[7] == 0 else 2)
+        B, vs, rows, S, ci, co = a[8:14]
+        peak = BF16_PEAK_TFLOPS if (ci >= 16 and co >= 16) else FP32_PEAK_TFLOPS
+        return 2.0 * B * rows * S * ci * co, sx * B * vs * ci + sy * B * rows * co + 2 * co * S * ci + 4 * rows * S, peak
+    if name == "cfsd_spiral_conv_bwd_data_x":
+        sd = 4 if a[1] == 0 else 2
+        B, vs, rows, S, ci, co = a[8:14]
+        elu = a[6] is not None
+        return (2.0 * B * rows * S * ci * co, sd * B * rows * co + 2 * B * vs * ci * (2 if elu else 1)
+                + 2 * co * S * ci + 16 * vs * S, BF16_PEAK_TFLOPS)
+    if name == "cfsd_spiral_conv_bwd_weight_x":
+        sx, sd = (4 if a[1] == 0 else 2), (4 if a[4] == 0 else 2)
+        B, vs, rows, S, ci, co = a[9:15]
+        peak = BF16_PEAK_TFLOPS if ci >= 16 else FP32_PEAK_TFLOPS
+        return 2.0 * B * rows * S * ci * co, sx * B * vs * ci + sd * B * rows * co + 4 * co * S * ci + 4 * rows * S, peak
+    if name == "cfsd_spiral_conv_bwd_x":
+        B, vs, rows, S, ci, co = a[14:20]
+        dx, elu = a[9] is not None, a[8] is not None
+        fl = 2.0 * B * rows * S * ci * co * (2 if dx else 1)
+        by = 2 * B * vs * ci + 4 * B * rows * co + 4 * co * S * ci + (2 * B * vs * ci * (2 if elu else 1) if dx else 0)
+        return fl, by, FP32_PEAK_TFLOPS
+    if name == "cfsd_spmm_csr_x":
+        sx, sy = (4 if a[4] == 0 else 2), (4 if a[7] == 0 else 2)
+        B, m, n, c = a[8:12]
+        elu = a[5] is not None
+        return 0.0, B * c * (sx * n + sy * m * (2 if elu else 1)), None
     if name == "cfsd_spmm_csr":
         B, m, n, c = a[6:10]
         elu = a[4] is not None
@@ -261,14 +294,24 @@ def kernel_probe(runner, n_iter=20):
     dec = eng.spec.dec_layers()
     i3 = len(dec) - 1
     w3, bias3 = eng._dec_w(i3)
-    timed("conv_fwd_D3", lambda: ops.spiral_conv_fwd(b.dec_up[i3], T.spiral[0], w3, bias3, 1,
-                                                      out=b.dec_out[i3]))
-    # the D3 backward kernels exactly as the step launches them (dW deferred:
-    # slab kernel only, reduced by the batched reduce)
-    timed("conv_dx_D3", lambda: ops.spiral_conv_bwd_data(b.dpre_dec[i3], T.spiral_inv[0], w3, T.n_verts[0],
-                                                         out=b.g_dec_up[i3], workspace=b.ws))
-    timed("conv_dw_D3", lambda: ops.spiral_conv_bwd_weight(b.dec_up[i3], T.spiral[0], b.dpre_dec[i3], None,
-                                                           None, b.ws_dw[("dec", i3)]))
+    wname = f"de_layers.{i3 + 1}.conv.layer.weight"
+    if runner.precision == "bf16":
+        w16 = eng._w16(wname)
+        timed("conv_fwd_D3", lambda: ops.spiral_conv_fwd_x(b.dec_up[i3], T.spiral[0], w3, w16, bias3, 1,
+                                                            b.dec_out[i3]))
+        timed("conv_dx_D3", lambda: ops.spiral_conv_bwd_data_x(b.dpre_dec[i3], T.spiral_inv[0], w16,
+                                                               T.n_verts[0], out=b.g_dec_up[i3]))
+        timed("conv_dw_D3", lambda: ops.spiral_conv_bwd_weight_x(b.dec_up[i3], T.spiral[0], b.dpre_dec[i3],
+                                                                 None, None, b.ws_dw[("dec", i3)]))
+    else:
+        timed("conv_fwd_D3", lambda: ops.spiral_conv_fwd(b.dec_up[i3], T.spiral[0], w3, bias3, 1,
+                                                          out=b.dec_out[i3]))
+        # the D3 backward kernels exactly as the step launches them (dW
+        # deferred: slab kernel only, reduced by the batched reduce)
+        timed("conv_dx_D3", lambda: ops.spiral_conv_bwd_data(b.dpre_dec[i3], T.spiral_inv[0], w3,
+                                                             T.n_verts[0], out=b.g_dec_up[i3], workspace=b.ws))
+        timed("conv_dw_D3", lambda: ops.spiral_conv_bwd_weight(b.dec_up[i3], T.spiral[0], b.dpre_dec[i3],
+                                                               None, None, b.ws_dw[("dec", i3)]))
     g = torch.empty(16, T.n_verts[0], 9 * 32, device=b.x.device)
     timed("spiral_gather_L0", lambda: ops.spiral_gather(b.dec_up[i3], T.spiral[0], out=g))
     del g
@@ -416,7 +459,7 @@ def main():
             dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    runner = Runner(world, rank, device, args.dataset, not args.no_graph, args.topology)
+    runner = Runner(world, rank, device, args.dataset, not args.no_graph, args.topology, args.precision)
     if runner.use_graph:
         runner.capture()
     for _ in range(args.warmup):
@@ -446,44 +489,63 @@ def main():
         gather_bytes = 16 * nv * (32 + 9 * 32) * 4 + nv * 9 * 4
         t_g = probe["spiral_gather_L0"]
         parity = c1_parity(device)
+        bf = runner.precision == "bf16"
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args.cpu_seconds)  # N=1 only
         s5k = None
-        if not (args.no_extras or world > 1 or args.topology != "craniofacial"):
+        if not (args.no_extras or world > 1 or args.topology != "craniofacial" or bf):
             try:
                 s5k = synth5k_line(device)
             except (ImportError, AttributeError) as e:  # precompute not available
                 s5k = {"error": str(e)}
         # the three D3 (decoder level 0, 32 -> 32) conv kernels, 5.02 GFLOP
         # each; `roofline` is the dominant one (longest launch)
+        # the three D3 (decoder level 0, 32 -> 32) conv kernels, 5.02 GFLOP
+        # each; `roofline` is the dominant one (longest launch).  fp32: MFMA
+        # bound (AI 72 flop/B > ridge 19.7); bf16: HBM bound (AI ~140 flop/B
+        # < ridge 312), priced on algorithmic bytes (input + output once).
+        bf = runner.precision == "bf16"
+        s_act = 2 if bf else 4
+        d3_bytes = {"conv_fwd_D3": s_act * 16 * nv * 64 + nv * 36,
+                    "conv_dx_D3": s_act * 16 * nv * 64 + nv * 9 * 16,
+                    "conv_dw_D3": s_act * 16 * nv * 64 + nv * 36}
         d3 = {}
         for name, key in (("conv_fwd_D3", "conv_fwd_d3"), ("conv_dx_D3", "conv_dx_d3"),
                           ("conv_dw_D3", "conv_dw_d3")):
             t = probe[name]
+            key = key + ("_bf16" if bf else "")
             traffic, traffic_src = pmc_traffic(key) if args.topology == "craniofacial" else (None, None)
-            d3[name] = {"us_per_launch": t * 1e6, "achieved": flops / t / 1e12,
-                        "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS, "traffic": traffic,
-                        "traffic_source": traffic_src}
+            if bf:
+                d3[name] = {"us_per_launch": t * 1e6, "bound": "hbm", "achieved": d3_bytes[name] / t / 1e9,
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": d3_bytes[name] / t / 1e9 / HBM_PEAK_GBS, "tflops": flops / t / 1e12,
+                            "algorithmic_bytes": d3_bytes[name], "traffic": traffic, "traffic_source": traffic_src}
+            else:
+                d3[name] = {"us_per_launch": t * 1e6, "bound": "mfma", "achieved": flops / t / 1e12,
+                            "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                            "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS, "algorithmic_flop": flops,
+                            "traffic": traffic, "traffic_source": traffic_src}
         dom = max(d3, key=lambda k: d3[k]["us_per_launch"])
-        kern_names = {"conv_fwd_D3": "conv_fwd_mfma<32,32> (decoder level 0 forward)",
-                      "conv_dx_D3": "conv_dx_mfma<32,32> (decoder level 0 data gradient)",
-                      "conv_dw_D3": "conv_dw_mfma<32,32> (decoder level 0 weight gradient)"}
+        kern_names = ({"conv_fwd_D3": "conv_fwd_b16<32,32> (decoder level 0 forward, bf16)",
+                       "conv_dx_D3": "conv_dx_b16<32,32> (decoder level 0 data gradient, bf16)",
+                       "conv_dw_D3": "conv_dw_b16<32,32> (decoder level 0 weight gradient, bf16)"} if bf else
+                      {"conv_fwd_D3": "conv_fwd_mfma<32,32> (decoder level 0 forward)",
+                       "conv_dx_D3": "conv_dx_mfma<32,32> (decoder level 0 data gradient)",
+                       "conv_dw_D3": "conv_dw_mfma<32,32> (decoder level 0 weight gradient)"})
         out = {
             "metric": METRIC, "value": meshes / el, "unit": "meshes/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if bf else "fp32",
             "data": "synthetic N(0,1) meshes resident in HBM, random-init weights",
             "config": {"workload": "craniofacial.yaml SD-VAE train step (swap bs 4->16, fwd, "
                                    "MSE+Laplacian+KL+latent-consistency, bwd, Adam)",
+                       "precision": runner.precision,
                        "topology": args.topology, "template_vertices": nv, "levels": runner.topo.n_verts,
                        "global_batch": 16 * world, "per_gpu_batch": 16,
                        "parallelism": f"dp{world}", "graph": runner.use_graph,
                        "collective": None if world == 1 else
                        (("rccl" if backend == "nccl" else backend) + " all_reduce, 2 buckets overlapped")},
-            "roofline": {"kernel": "cfsd " + kern_names[dom], "bound": "mfma",
-                         "achieved": d3[dom]["achieved"], "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": d3[dom]["frac"],
-                         "traffic": d3[dom]["traffic"], "traffic_source": d3[dom]["traffic_source"],
-                         "algorithmic_flop": flops, "us_per_launch": d3[dom]["us_per_launch"]},
+            "roofline": dict({"kernel": "cfsd " + kern_names[dom]}, **d3[dom]),
             "d3_kernels": d3,
             "step_roofline": steprf,
             "gather_roofline": {"kernel": "cfsd spiral_gather_k (level 0, 32 ch, 16 meshes)",

@@ -49,7 +49,15 @@ SIGNATURES = {
     "cfsd_latent_fwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F, _P]),
     "cfsd_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_loss_finalize": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P]),
-    "cfsd_adam": (_I, [_P, _P, _P, _P, _P, _Z, _F, _F, _F, _F, _F, _P]),
+    "cfsd_adam": (_I, [_P, _P, _P, _P, _P, _Z, _F, _F, _F, _F, _F, _P, _P]),
+    "cfsd_spiral_conv_fwd_x": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "cfsd_spiral_conv_bwd_data_x": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "cfsd_spiral_conv_bwd_weight_x_workspace": (_Z, [_I, _I, _I, _I, _I]),
+    "cfsd_spiral_conv_bwd_weight_x": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _I, _P]),
+    "cfsd_spiral_conv_bwd_x": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I, _I,
+                                    _I, _I, _P]),
+    "cfsd_spmm_csr_x": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "cfsd_cast": (_I, [_P, _I, _P, _I, _Z, _P]),
     "cfsd_step_begin": (_I, [_P, _U64, _P, _I, _P, _I, _P, _I, _I, _P, _I, _I, _P, _P]),
     "cfsd_dw_reduce_batch": (_I, [_P, _I, _P]),
     "cfsd_scale": (_I, [_P, _Z, _F, _P]),

@@ -10,6 +10,38 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace cfsd {
 
+// XCD-aware persistent tile schedule.  Blocks b and b+8 share an XCD (and
+// its 4 MB L2) under the dispatcher's round-robin placement, so the blocks of
+// group g = b % G sweep ONE contiguous 1/G of the tile range: neighbouring
+// tiles gather neighbouring vertices, which then hit the same L2.  Placement
+// only changes speed, never results.
+struct TileSweep {
+  long begin, end, step;
+};
+__device__ __forceinline__ TileSweep xcd_sweep(long n_tiles, int lanes_per_block, int lane_id) {
+  const int nb = gridDim.x;
+  const int G = nb < 8 ? nb : 8;
+  const int grp = blockIdx.x % G, lb = blockIdx.x / G;
+  const int nb_g = (nb - grp + G - 1) / G;  // blocks in this group
+  const long per = (n_tiles + G - 1) / G;
+  TileSweep t;
+  t.begin = grp * per + (long)lb * lanes_per_block + lane_id;
+  t.end = min(n_tiles, (grp + 1) * per);
+  t.step = (long)nb_g * lanes_per_block;
+  return t;
+}
+
+// Non-persistent grids: renumber workgroups so that XCD x (hardware
+// dispatch is round-robin, x = blockIdx % 8) owns a CONTIGUOUS 1/8 of the
+// block range -- its meshes' rows then stay in its own L2.  Bijective for any
+// gridDim.
+__device__ __forceinline__ int xcd_block_of(int bid, int nb) {
+  if (nb < 8) return bid;
+  const int g = bid & 7, lb = bid >> 3, q = nb >> 3, rem = nb & 7;
+  return g * q + min(g, rem) + lb;
+}
+__device__ __forceinline__ int xcd_block() { return xcd_block_of(blockIdx.x, gridDim.x); }
+
 // Records the last error text (thread-local) and returns its code.
 int set_error(int code, const char* fmt, ...);
 
@@ -43,6 +75,50 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 }
 
 constexpr int kMaxBatch = 1 << 20;
+
+// ---------------------------------------------------------------- bf16 storage
+// Activations of the bf16 path are stored as raw bfloat16 (uint16_t, the
+// torch.bfloat16 bit layout) and always widened to fp32 for arithmetic;
+// narrowing is round-to-nearest-even (v_cvt_pk_bf16_f32), as torch's casts.
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float bf2f(uint32_t h16) { return __uint_as_float(h16 << 16); }
+__device__ __forceinline__ uint32_t f2bf(float f) {
+  return __builtin_bit_cast(unsigned short, (__bf16)f);
+}
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
+// element access of either storage type, arithmetic in fp32
+__device__ __forceinline__ float ldf(const float* p) { return *p; }
+__device__ __forceinline__ float ldf(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ void stf(float* p, float v) { *p = v; }
+__device__ __forceinline__ void stf(bf16_t* p, float v) { *p = (bf16_t)f2bf(v); }
+// 4 consecutive elements as fp32 (16-B or 8-B load)
+__device__ __forceinline__ f32x4 ld4f(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 ld4f(const bf16_t* p) {
+  const u32x2 v = *reinterpret_cast<const u32x2*>(p);
+  return (f32x4){__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                 __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u)};
+}
+__device__ __forceinline__ void st4f(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ void st4f(bf16_t* p, f32x4 v) {
+  *reinterpret_cast<u32x2*>(p) = (u32x2){pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
+}
+// 8 consecutive elements as a packed bf16 MFMA fragment (fp32 sources are
+// rounded to bf16 here)
+__device__ __forceinline__ u32x4 ld8bf(const bf16_t* p) { return *reinterpret_cast<const u32x4*>(p); }
+__device__ __forceinline__ u32x4 ld8bf(const float* p) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+  return (u32x4){pack_bf2(a.x, a.y), pack_bf2(a.z, a.w), pack_bf2(b.x, b.y), pack_bf2(b.z, b.w)};
+}
+// v_mfma_f32_16x16x32_bf16: lane l holds A[l&15][8(l>>4) + j], B[8(l>>4) + j][l&15]
+// (j = 0..7); D: col = l&15, row = 4(l>>4) + r.
+__device__ __forceinline__ f32x4 mfma_bf16(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
 
 // Flattened row / element indices are < 2^31 (checked at every entry point),
 // so per-thread index splits use 32-bit division: a 64-bit division is a

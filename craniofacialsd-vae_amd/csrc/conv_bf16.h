@@ -1,0 +1,30 @@
+// Launchers of the bf16 MFMA SpiralConv kernels (spiral_conv_bf16.hip),
+// called by the mixed-precision C ABI in spiral_conv.hip.  Activations and
+// gradients are bf16 or fp32 per operand (the bf16 path keeps the coarse
+// levels and the bottleneck in fp32), weights are the bf16 shadow of the fp32
+// master parameters, every product accumulates in fp32.
+#pragma once
+#include "cfsd_common.h"
+
+namespace cfsd {
+namespace bf {
+
+constexpr int DT_F32 = CFSD_DT_F32;
+constexpr int DT_BF16 = CFSD_DT_BF16;
+
+// y[m, :] = act(bias + W . gather(x)), x bf16, y bf16 or fp32 (y_dt).
+int launch_fwd(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, void* y,
+               int y_dt, int vsrc, int rows, long total_rows, int cin, int cout, int act,
+               hipStream_t st);
+// dx bf16 (times elu'(elu_y) when elu_y != NULL), dpre bf16 or fp32.
+int launch_dx(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_row,
+              const int* inv_head, const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int vsrc,
+              int rows, long total_src_rows, int cin, int cout, hipStream_t st);
+// dW / db partial slabs [n_slabs][cout*9*cin + cout] (plain layout), x bf16,
+// dpre bf16 or fp32.
+int dw_slabs(int batch, int rows, int cin, int cout);
+int launch_dw(const bf16_t* x, const int* idx, const void* dpre, int dpre_dt, float* ws, int vsrc,
+              int rows, long total_rows, int cin, int cout, hipStream_t st);
+
+}  // namespace bf
+}  // namespace cfsd

@@ -13,10 +13,10 @@
 namespace cfsd {
 
 
-template <int CK>
+template <int CK, typename TX>
 __device__ __forceinline__ void spmm_row_chunks(int beg, int end, const int* __restrict__ col,
                                                 const float* __restrict__ val,
-                                                const float* __restrict__ xb, int c4, f32x4& acc) {
+                                                const TX* __restrict__ xb, int c4, f32x4& acc) {
 #pragma clang fp contract(off)
   for (int e0 = beg; e0 < end; e0 += CK) {
     float v[CK];
@@ -25,7 +25,7 @@ __device__ __forceinline__ void spmm_row_chunks(int beg, int end, const int* __r
     for (int j = 0; j < CK; ++j) {
       const int e = e0 + j < end ? e0 + j : end - 1;
       v[j] = val[e];
-      xv[j] = ld4(xb + (long)col[e] * c4 * 4);
+      xv[j] = ld4f(xb + (long)col[e] * c4 * 4);
     }
 #pragma unroll
     for (int j = 0; j < CK; ++j) {
@@ -47,12 +47,14 @@ __device__ __forceinline__ void spmm_row_chunks(int beg, int end, const int* __r
 // (two meshes of a 16-mesh batch): the rows one XCD gathers then come from
 // a ~2 x V x C x 4-byte slice that fits its 4 MB L2 instead of the whole
 // batch.  Placement changes speed only, never results.
+// Storage types: x TX, y / elu_y TY (fp32 or bf16; fp32 arithmetic).
+template <typename TX, typename TY>
 __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_ptr,
                                                   const int* __restrict__ col,
                                                   const float* __restrict__ val,
-                                                  const float* __restrict__ x,
-                                                  const float* __restrict__ elu_y,
-                                                  float* __restrict__ y, int m, int n, int c4,
+                                                  const TX* __restrict__ x,
+                                                  const TY* __restrict__ elu_y,
+                                                  TY* __restrict__ y, int m, int n, int c4,
                                                   long total) {
   // hipcc contracts a*b+c into fma by default; the reference rounds the
   // product and the sum separately (index_select*value, then scatter_add).
@@ -63,7 +65,7 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   int br, q, b, r;
   divmod32(t, c4, br, q);
   divmod32(br, m, b, r);
-  const float* xb = x + (long)b * n * c4 * 4 + 4 * q;
+  const TX* xb = x + (long)b * n * c4 * 4 + 4 * q;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const int beg = row_ptr[r], end = row_ptr[r + 1];
   // Entries in chunks: the chunk's column/value and x loads are all issued
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   else if (end - beg <= 4) spmm_row_chunks<4>(beg, end, col, val, xb, c4, acc);
   else spmm_row_chunks<8>(beg, end, col, val, xb, c4, acc);
   if (elu_y) {
-    f32x4 g = ld4(elu_y + t * 4);
+    f32x4 g = ld4f(elu_y + t * 4);
     acc.x *= elu_grad_from_out(g.x);
     acc.y *= elu_grad_from_out(g.y);
     acc.z *= elu_grad_from_out(g.z);
@@ -85,7 +87,7 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   }
   // (non-temporal stores measured: this kernel ~0.8 us faster, the conv
   // reading y 0.5-1 us slower -> plain stores)
-  st4(y + t * 4, acc);
+  st4f(y + t * 4, acc);
 }
 
 // out[(i*bs + j), v, :] = x[mesh(i or j), v, :]; one thread per (out mesh,
@@ -111,6 +113,18 @@ __global__ __launch_bounds__(256) void swap_k(const float* __restrict__ x,
   const float* src = x + (src_mesh * nv + v) * c;
   float* dst = out + t * c;
   for (int q = 0; q < c; ++q) dst[q] = src[q];
+}
+
+// Storage conversion fp32 <-> bf16 (round to nearest even), 4 elements per
+// thread (n % 4 tail by the last thread).
+template <typename TS, typename TD>
+__global__ __launch_bounds__(256) void cast_k(const TS* __restrict__ src, TD* __restrict__ dst, long n) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x, n4 = n / 4;
+  if (q < n4) {
+    st4f(dst + 4 * q, ld4f(src + 4 * q));
+  } else if (q == n4) {
+    for (long i = 4 * n4; i < n; ++i) stf(dst + i, ldf(src + i));
+  }
 }
 
 // Dataset normalisation (data_loading.py:259-260, (verts - mean) / std with
@@ -209,20 +223,55 @@ extern "C" int cfsd_vertex_errors(const float* out, const float* gt, const float
   return launch_status("vertex_errors");
 }
 
-extern "C" int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const float* val,
-                             const float* x, const float* elu_y, float* y, int batch, int m,
-                             int n, int c, void* stream) {
+static int spmm_launch(const int32_t* row_ptr, const int32_t* col, const float* val, const void* x,
+                       int x_dt, const void* elu_y, void* y, int y_dt, int batch, int m, int n, int c,
+                       void* stream) {
   if (!row_ptr || !col || !val || !x || !y) return set_error(CFSD_EINVAL, "spmm_csr: null pointer");
   if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
     return set_error(CFSD_EINVAL, "spmm_csr: bad sizes batch=%d m=%d n=%d c=%d", batch, m, n, c);
+  if ((x_dt != CFSD_DT_F32 && x_dt != CFSD_DT_BF16) || (y_dt != CFSD_DT_F32 && y_dt != CFSD_DT_BF16))
+    return set_error(CFSD_EINVAL, "spmm_csr: bad dtype");
   const long total = (long)batch * m * (c / 4);
   if (total >= (1L << 31) || (long)batch * n >= (1L << 31))
     return set_error(CFSD_EINVAL, "spmm_csr: batch x rows >= 2^31 (32-bit indices)");
   const long per_grp = (total + 7) / 8;  // 8 XCD groups of equal block count
   const unsigned nblk = (unsigned)(8 * ((per_grp + 255) / 256));
-  hipLaunchKernelGGL(spmm_csr_k, dim3(nblk), dim3(256), 0,
-                     (hipStream_t)stream, row_ptr, col, val, x, elu_y, y, m, n, c / 4, total);
+  const hipStream_t st = (hipStream_t)stream;
+#define SPMM(TX, TY)                                                                             \
+  hipLaunchKernelGGL((spmm_csr_k<TX, TY>), dim3(nblk), dim3(256), 0, st, row_ptr, col, val,      \
+                     (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, total)
+  if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPMM(float, float);
+  else if (x_dt == CFSD_DT_F32) SPMM(float, bf16_t);
+  else if (y_dt == CFSD_DT_F32) SPMM(bf16_t, float);
+  else SPMM(bf16_t, bf16_t);
+#undef SPMM
   return launch_status("spmm_csr");
+}
+
+extern "C" int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const float* val,
+                             const float* x, const float* elu_y, float* y, int batch, int m,
+                             int n, int c, void* stream) {
+  return spmm_launch(row_ptr, col, val, x, CFSD_DT_F32, elu_y, y, CFSD_DT_F32, batch, m, n, c, stream);
+}
+
+extern "C" int cfsd_spmm_csr_x(const int32_t* row_ptr, const int32_t* col, const float* val,
+                               const void* x, int x_dt, const void* elu_y, void* y, int y_dt,
+                               int batch, int m, int n, int c, void* stream) {
+  return spmm_launch(row_ptr, col, val, x, x_dt, elu_y, y, y_dt, batch, m, n, c, stream);
+}
+
+extern "C" int cfsd_cast(const void* src, int src_dt, void* dst, int dst_dt, size_t n, void* stream) {
+  if (!src || !dst) return set_error(CFSD_EINVAL, "cast: null pointer");
+  if (n == 0) return CFSD_OK;
+  const dim3 grid((unsigned)((n / 4 + 1 + 255) / 256));
+  const hipStream_t st = (hipStream_t)stream;
+  if (src_dt == CFSD_DT_F32 && dst_dt == CFSD_DT_BF16)
+    hipLaunchKernelGGL((cast_k<float, bf16_t>), grid, dim3(256), 0, st, (const float*)src, (bf16_t*)dst, (long)n);
+  else if (src_dt == CFSD_DT_BF16 && dst_dt == CFSD_DT_F32)
+    hipLaunchKernelGGL((cast_k<bf16_t, float>), grid, dim3(256), 0, st, (const bf16_t*)src, (float*)dst, (long)n);
+  else
+    return set_error(CFSD_EINVAL, "cast: unsupported dtypes %d -> %d", src_dt, dst_dt);
+  return launch_status("cast");
 }
 
 extern "C" int cfsd_swap_features(const float* x, const int32_t* batch_idx,

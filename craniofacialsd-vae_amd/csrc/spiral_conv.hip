@@ -18,42 +18,11 @@
 // conv) would waste 29/32 of an MFMA tile, so those layers run on VALU
 // kernels shaped for them (lane-per-output-channel or 8-lanes-per-row).
 #include "cfsd_common.h"
+#include "conv_bf16.h"
 
 namespace cfsd {
 
 constexpr int kSeq = 9;  // spiral length of every configuration (craniofacial/body/default.yaml)
-
-// XCD-aware persistent tile schedule.  Blocks b and b+8 share an XCD (and
-// its 4 MB L2) under the dispatcher's round-robin placement, so the blocks of
-// group g = b % G sweep ONE contiguous 1/G of the tile range: neighbouring
-// tiles gather neighbouring vertices, which then hit the same L2.  Placement
-// only changes speed, never results.
-struct TileSweep {
-  long begin, end, step;
-};
-__device__ __forceinline__ TileSweep xcd_sweep(long n_tiles, int lanes_per_block, int lane_id) {
-  const int nb = gridDim.x;
-  const int G = nb < 8 ? nb : 8;
-  const int grp = blockIdx.x % G, lb = blockIdx.x / G;
-  const int nb_g = (nb - grp + G - 1) / G;  // blocks in this group
-  const long per = (n_tiles + G - 1) / G;
-  TileSweep t;
-  t.begin = grp * per + (long)lb * lanes_per_block + lane_id;
-  t.end = min(n_tiles, (grp + 1) * per);
-  t.step = (long)nb_g * lanes_per_block;
-  return t;
-}
-
-// Non-persistent grids: renumber workgroups so that XCD x (hardware
-// dispatch is round-robin, x = blockIdx % 8) owns a CONTIGUOUS 1/8 of the
-// block range -- its meshes' rows then stay in its own L2.  Bijective for any
-// gridDim.
-__device__ __forceinline__ int xcd_block_of(int bid, int nb) {
-  if (nb < 8) return bid;
-  const int g = bid & 7, lb = bid >> 3, q = nb >> 3, rem = nb & 7;
-  return g * q + min(g, rem) + lb;
-}
-__device__ __forceinline__ int xcd_block() { return xcd_block_of(blockIdx.x, gridDim.x); }
 
 // Occupancy target per channel shape (min waves per SIMD -> VGPR budget).
 constexpr int mfma_occ(int cin, int cout) { return (cin == 32 && cout == 32) ? 4 : 2; }
@@ -259,8 +228,8 @@ __global__ __launch_bounds__(256) void conv_fwd_in_small(const float* __restrict
 // persistent over rows: L = CIN/4 lanes per row, each lane owns a float4 of
 // input channels of every neighbour row (one coalesced 16*L-byte read per
 // neighbour), the CO partial dots are reduced across the L lanes.
-template <int CIN, int CO, int ACT>
-__global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(const float* __restrict__ x,
+template <int CIN, int CO, int ACT, typename TX = float>
+__global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(const TX* __restrict__ x,
                                                           const int* __restrict__ idx,
                                                           const float* __restrict__ w,
                                                           const float* __restrict__ bias,
@@ -289,7 +258,7 @@ __global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(con
     const long m = valid ? mm : total_rows - 1;
     int b, r;
     divmod32(m, rows, b, r);
-    const float* xb = x + (long)b * vsrc * CIN + 4 * q;
+    const TX* xb = x + (long)b * vsrc * CIN + 4 * q;
     const int* ir = idx + (long)r * kSeq;
     float acc[CO];
 #pragma unroll
@@ -298,7 +267,7 @@ __global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(con
     asm volatile("" : "+v"(wq));  // opaque per iteration: keeps the weight reads from being hoisted into VGPRs
 #pragma unroll
     for (int s = 0; s < kSeq; ++s) {
-      const f32x4 v = ld4(xb + (long)ir[s] * CIN);
+      const f32x4 v = ld4f(xb + (long)ir[s] * CIN);
 #pragma unroll
       for (int o = 0; o < CO; ++o) {
         const f32x4 wv = lw[(o * K + s * CIN) / 4 + wq];
@@ -329,12 +298,12 @@ __global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(con
 // and keeps the half it feeds to v_mfma_f32_32x32x2_f32 (k-permuted: half h
 // owns k in [h*KH, h*KH + KH)); W^T lives in registers.  Output rows are
 // stored as 128-B coalesced segments.
-template <int CS, int COUT, int ACT>
+template <int CS, int COUT, int ACT, typename TY = float>
 __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict__ x,
                                                         const int* __restrict__ idx,
                                                         const float* __restrict__ w,
                                                         const float* __restrict__ bias,
-                                                        float* __restrict__ y, int vsrc, int rows,
+                                                        TY* __restrict__ y, int vsrc, int rows,
                                                         long total_rows) {
   constexpr int K = kSeq * CS, KH = (K + 1) / 2, NCT = COUT / 32;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -383,7 +352,7 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
         const long mo = tile * 32 + acc_row(rr, lane);
         if (mo < total_rows) {
           const float v = acc[t][rr] + bn[t];
-          y[mo * COUT + t * 32 + i] = ACT == CFSD_ACT_ELU ? elu_f(v) : v;
+          stf(&y[mo * COUT + t * 32 + i], ACT == CFSD_ACT_ELU ? elu_f(v) : v);
         }
       }
   }
@@ -1352,8 +1321,8 @@ __global__ __launch_bounds__(256) void conv_dw_out_small(const float* __restrict
 // reads its A values as one ds_read_b128 per 4 steps.
 constexpr int kAts = 68;  // At row stride (floats): 16-B aligned, bank-spread
 
-template <int NCT>
-__device__ __forceinline__ void rank64_mfma(const float* At, const float* __restrict__ B,
+template <int NCT, typename TB>
+__device__ __forceinline__ void rank64_mfma(const float* At, const TB* __restrict__ B,
                                             long row0, long nrows, int ldb, f32x16 (&acc)[NCT],
                                             int lane) {
   const int i = lane & 31, h = lane >> 5;
@@ -1366,7 +1335,7 @@ __device__ __forceinline__ void rank64_mfma(const float* At, const float* __rest
       long rr = row0 + kk + j + 32 * h;
       if (rr >= nrows) rr = nrows - 1;  // its A column is zero
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) bv[j][ct] = B[rr * ldb + ct * 32 + i];
+      for (int ct = 0; ct < NCT; ++ct) bv[j][ct] = ldf(&B[rr * ldb + ct * 32 + i]);
     }
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
@@ -1392,10 +1361,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 // all-ones row so db falls out of the same MFMAs.  Persistent waves over
 // 64-row tiles, block partials combined in fixed order -> one slab
 // [COUT*K + COUT] per block (reduced by slab_reduce).
-template <int CS, int COUT>
+template <int CS, int COUT, typename TD = float>
 __global__ __launch_bounds__(256) void conv_dw_in_mfma(const float* __restrict__ x,
                                                        const int* __restrict__ idx,
-                                                       const float* __restrict__ dpre,
+                                                       const TD* __restrict__ dpre,
                                                        float* __restrict__ ws, int vsrc, int rows,
                                                        long total_rows) {
   constexpr int K = kSeq * CS, NI = K + 1, NCT = COUT / 32, NEL = COUT * K + COUT;
@@ -1610,12 +1579,12 @@ constexpr int kAtS = 36;  // At row stride: conflict-free ds_read_b128 of the dW
 #ifndef CFSD_BWD_OUT_OCC
 #define CFSD_BWD_OUT_OCC 1
 #endif
-template <int CIN, int CO>
+template <int CIN, int CO, typename TX = float>
 __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     const float* __restrict__ dpre, const int* __restrict__ inv_ptr,
     const int* __restrict__ inv_row, const int4* __restrict__ inv_head,
-    const float* __restrict__ w, const float* __restrict__ elu_y, const float* __restrict__ x,
-    float* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, long total_rows) {
+    const float* __restrict__ w, const TX* __restrict__ elu_y, const TX* __restrict__ x,
+    TX* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, long total_rows) {
   constexpr int SPH = 5, KH = SPH * CO, K = kSeq * CIN, NCT = CIN / 32, NEL = CO * K + CO;
   static_assert(2 * KH <= 32 && CIN % 32 == 0, "shape");
   __shared__ float at_all[4 * 32 * kAtS];
@@ -1657,13 +1626,13 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     // first: independent of the inverse-spiral chain, so their latency hides
     // behind it
     float xv[NCT][16];
-    const float* xt = x + row0 * CIN + li;
+    const TX* xt = x + row0 * CIN + li;
     const int last = (int)(total_rows - 1 - row0);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int rr = min(acc_row(j, lane), last);  // clamped rows have a zero At column
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) xv[ct][j] = xt[rr * CIN + ct * 32];
+      for (int ct = 0; ct < NCT; ++ct) xv[ct][j] = ldf(&xt[rr * CIN + ct * 32]);
     }
     const float* db_ = dpre + (long)b * rows * CO;
     const int4 none = make_int4(-1, -1, -1, -1);
@@ -1745,8 +1714,8 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
           for (int ct = 0; ct < NCT; ++ct) {
             float v = dxacc[ct][r];
             if (ey_mode == 1) v *= elu_grad_from_out(xv[ct][r]);
-            else if (ey_mode == 2) v *= elu_grad_from_out(elu_y[rr * CIN + ct * 32 + li]);
-            dx[rr * CIN + ct * 32 + li] = v;
+            else if (ey_mode == 2) v *= elu_grad_from_out(ldf(&elu_y[rr * CIN + ct * 32 + li]));
+            stf(&dx[rr * CIN + ct * 32 + li], v);
           }
         }
       }
@@ -2401,6 +2370,178 @@ extern "C" int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, 
   return launch_status("spiral_gather");
 }
 
+// ============================================================== mixed precision (bf16 path)
+// The bf16 path of the step stores the level-0/1 activations and gradients
+// in bf16 (engine precision "bf16"); these entry points take each operand's
+// storage type and route the 32/64-channel layers to the bf16 MFMA kernels
+// (spiral_conv_bf16.hip) and the xyz layers to the small-channel kernels
+// above, instantiated for bf16 operands.  Weights: `w` fp32 master (small
+// layers), `w_bf16` its bf16 shadow (MFMA layers).
+static bool mfma_shape(int cin, int cout) {
+  return (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
+}
+static bool dt_ok(int dt) { return dt == CFSD_DT_F32 || dt == CFSD_DT_BF16; }
+
+extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* idx, const float* w,
+                                      const uint16_t* w_bf16, const float* bias, void* y, int y_dt,
+                                      int batch, int vsrc, int rows, int seq, int cin, int cout,
+                                      int act, void* stream) {
+  int rc = check_conv_args(x, idx, y, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!dt_ok(x_dt) || !dt_ok(y_dt)) return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: bad dtype");
+  if (act != CFSD_ACT_NONE && act != CFSD_ACT_ELU) return set_error(CFSD_EINVAL, "bad act %d", act);
+  const hipStream_t st = (hipStream_t)stream;
+  const long M = (long)batch * rows;
+  if (mfma_shape(cin, cout) && x_dt == CFSD_DT_BF16) {
+    if (!w_bf16) return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: w_bf16 required");
+    return bf::launch_fwd((const bf16_t*)x, idx, (const bf16_t*)w_bf16, bias, y, y_dt, vsrc, rows, M, cin,
+                          cout, act, st);
+  }
+  if (!w) return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: w required");
+  if (cin <= 3 && (cout == 32 || cout == 64) && x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_BF16) {
+    const long tiles = (M + 31) / 32;
+    const unsigned gp = (unsigned)((tiles + 3) / 4 < 2048 ? (tiles + 3) / 4 : 2048);
+#define FINB(CS_, CO_)                                                                           \
+  if (cin == CS_ && cout == CO_) {                                                               \
+    if (act == CFSD_ACT_ELU)                                                                     \
+      hipLaunchKernelGGL((conv_fwd_in_mfma<CS_, CO_, CFSD_ACT_ELU, bf16_t>), dim3(gp), dim3(256), \
+                         0, st, (const float*)x, idx, w, bias, (bf16_t*)y, vsrc, rows, M);       \
+    else                                                                                         \
+      hipLaunchKernelGGL((conv_fwd_in_mfma<CS_, CO_, CFSD_ACT_NONE, bf16_t>), dim3(gp), dim3(256), \
+                         0, st, (const float*)x, idx, w, bias, (bf16_t*)y, vsrc, rows, M);       \
+    return launch_status("spiral_conv_fwd_in_bf16");                                             \
+  }
+    FINB(1, 32) FINB(2, 32) FINB(3, 32) FINB(1, 64) FINB(2, 64) FINB(3, 64)
+#undef FINB
+  }
+  if (cout <= 3 && (cin == 16 || cin == 32 || cin == 64) && x_dt == CFSD_DT_BF16 && y_dt == CFSD_DT_F32) {
+#define FOUTB(CI_, CO_)                                                                           \
+  if (cin == CI_ && cout == CO_) {                                                                \
+    if (act == CFSD_ACT_ELU) {                                                                    \
+      auto k = conv_fwd_out_small<CI_, CO_, CFSD_ACT_ELU, bf16_t>;                                \
+      hipLaunchKernelGGL(k, dim3(small_grid(k, M)), dim3(256), 0, st, (const bf16_t*)x, idx, w,   \
+                         bias, (float*)y, vsrc, rows, M);                                         \
+    } else {                                                                                      \
+      auto k = conv_fwd_out_small<CI_, CO_, CFSD_ACT_NONE, bf16_t>;                               \
+      hipLaunchKernelGGL(k, dim3(small_grid(k, M)), dim3(256), 0, st, (const bf16_t*)x, idx, w,   \
+                         bias, (float*)y, vsrc, rows, M);                                         \
+    }                                                                                             \
+    return launch_status("spiral_conv_fwd_out_bf16");                                             \
+  }
+    FOUTB(16, 3) FOUTB(32, 3) FOUTB(64, 3) FOUTB(32, 1) FOUTB(32, 2)
+#undef FOUTB
+  }
+  return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: unsupported %d -> %d with dtypes %d -> %d", cin, cout,
+                   x_dt, y_dt);
+}
+
+extern "C" int cfsd_spiral_conv_bwd_data_x(const void* dpre, int dpre_dt, const int32_t* inv_ptr,
+                                           const int32_t* inv_row, const int32_t* inv_head,
+                                           const uint16_t* w_bf16, const uint16_t* elu_y,
+                                           uint16_t* dx, int batch, int vsrc, int rows, int seq,
+                                           int cin, int cout, void* stream) {
+  int rc = check_conv_args(dpre, inv_ptr, inv_row, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!w_bf16 || !dx || !inv_head) return set_error(CFSD_EINVAL, "null w_bf16/dx/inv_head");
+  if (!dt_ok(dpre_dt)) return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_x: bad dtype");
+  if ((uintptr_t)inv_head & 15) return set_error(CFSD_EINVAL, "inv_head must be 16-B aligned");
+  if ((long)batch * rows * cout * (dpre_dt == CFSD_DT_F32 ? 4L : 2L) >= (1L << 31))
+    return set_error(CFSD_EINVAL, "dpre larger than 2 GiB (32-bit buffer offsets)");
+  if (!mfma_shape(cin, cout))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_x: unsupported channels %d -> %d", cin, cout);
+  return bf::launch_dx(dpre, dpre_dt, inv_ptr, inv_row, inv_head, (const bf16_t*)w_bf16,
+                       (const bf16_t*)elu_y, (bf16_t*)dx, vsrc, rows, (long)batch * vsrc, cin, cout,
+                       (hipStream_t)stream);
+}
+
+extern "C" size_t cfsd_spiral_conv_bwd_weight_x_workspace(int batch, int rows, int seq, int cin,
+                                                          int cout) {
+  if (batch <= 0 || rows <= 0 || seq != kSeq || cin <= 0 || cout <= 0) return 0;
+  if (mfma_shape(cin, cout))
+    return (size_t)bf::dw_slabs(batch, rows, cin, cout) * ((size_t)cout * kSeq * cin + cout) * sizeof(float);
+  return cfsd_spiral_conv_bwd_weight_workspace(batch, rows, seq, cin, cout);
+}
+
+extern "C" int cfsd_spiral_conv_bwd_weight_x(const void* x, int x_dt, const int32_t* idx,
+                                             const void* dpre, int dpre_dt, float* dw, float* db,
+                                             float* workspace, size_t workspace_bytes, int batch,
+                                             int vsrc, int rows, int seq, int cin, int cout,
+                                             void* stream) {
+  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!dt_ok(x_dt) || !dt_ok(dpre_dt)) return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_x: bad dtype");
+  if (!workspace) return set_error(CFSD_EINVAL, "null workspace");
+  if ((dw == nullptr) != (db == nullptr))
+    return set_error(CFSD_EINVAL, "dw and db must both be set (or both NULL: deferred)");
+  const size_t need = cfsd_spiral_conv_bwd_weight_x_workspace(batch, rows, seq, cin, cout);
+  if (workspace_bytes < need)
+    return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
+  const hipStream_t st = (hipStream_t)stream;
+  const long M = (long)batch * rows;
+  const int n_el = cout * kSeq * cin + cout;
+  const dim3 rg((unsigned)((n_el + 63) / 64));
+  int n_slabs = 0;
+  if (mfma_shape(cin, cout) && x_dt == CFSD_DT_BF16) {
+    rc = bf::launch_dw((const bf16_t*)x, idx, dpre, dpre_dt, workspace, vsrc, rows, M, cin, cout, st);
+    n_slabs = bf::dw_slabs(batch, rows, cin, cout);
+  } else if (cin <= 3 && (cout == 32 || cout == 64) && x_dt == CFSD_DT_F32 && dpre_dt == CFSD_DT_BF16) {
+    const DwGeom g = dw_geom(batch, rows, cin, cout);
+    if (g.kind != kDwInMfma) return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_x: geometry");
+#define DWIB(CS_, CO_)                                                                             \
+  if (cin == CS_ && cout == CO_)                                                                   \
+    hipLaunchKernelGGL((conv_dw_in_mfma<CS_, CO_, bf16_t>), dim3(g.gx), dim3(256), 0, st,          \
+                       (const float*)x, idx, (const bf16_t*)dpre, workspace, vsrc, rows, M);
+    DWIB(1, 32) DWIB(2, 32) DWIB(3, 32) DWIB(1, 64) DWIB(2, 64) DWIB(3, 64)
+#undef DWIB
+    rc = launch_status("spiral_conv_bwd_weight_in_bf16");
+    n_slabs = g.gx;
+  } else {
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_x: unsupported %d -> %d with dtypes %d/%d", cin,
+                     cout, x_dt, dpre_dt);
+  }
+  if (rc || !dw) return rc;
+  hipLaunchKernelGGL(slab_reduce, rg, dim3(1024), 0, st, workspace, n_slabs, n_el, dw, cout * kSeq * cin, db);
+  return launch_status("spiral_conv_bwd_weight_x_reduce");
+}
+
+extern "C" int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* idx, const float* dpre,
+                                      const int32_t* inv_ptr, const int32_t* inv_row,
+                                      const int32_t* inv_head, const float* w, const void* elu_y,
+                                      void* dx, float* dw, float* db, float* workspace,
+                                      size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
+                                      int cin, int cout, void* stream) {
+  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (x_dt != CFSD_DT_BF16) return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: x must be bf16");
+  if (!fused_small(cin, cout))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: small-output layers only (%d -> %d)", cin, cout);
+  if (!inv_ptr || !inv_row || !inv_head || !w || !workspace)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: null inverse table / w / workspace");
+  if ((uintptr_t)inv_head & 15) return set_error(CFSD_EINVAL, "inv_head must be 16-B aligned");
+  if ((dw == nullptr) != (db == nullptr))
+    return set_error(CFSD_EINVAL, "dw and db must both be set (or both NULL: deferred)");
+  const size_t need = cfsd_spiral_conv_bwd_workspace(batch, vsrc, rows, seq, cin, cout);
+  if (workspace_bytes < need) return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
+  const hipStream_t st = (hipStream_t)stream;
+  const long Ms = (long)batch * vsrc;
+  const int gx = fused_small_gx(Ms);
+  const int n_el = cout * kSeq * cin + cout;
+#define BOSB(CIN_, CO_)                                                                          \
+  if (cin == CIN_ && cout == CO_) {                                                              \
+    hipLaunchKernelGGL((conv_bwd_out_mfma<CIN_, CO_, bf16_t>), dim3(gx), dim3(256), 0, st, dpre, \
+                       inv_ptr, inv_row, (const int4*)inv_head, w, (const bf16_t*)elu_y,          \
+                       (const bf16_t*)x, (bf16_t*)dx, workspace, vsrc, rows, Ms);                 \
+    rc = launch_status("spiral_conv_bwd_small_bf16");                                            \
+    if (rc || !dw) return rc;                                                                    \
+    hipLaunchKernelGGL(slab_reduce, dim3((unsigned)((n_el + 63) / 64)), dim3(1024), 0, st,        \
+                       workspace, gx, n_el, dw, cout * kSeq * cin, db);                          \
+    return launch_status("spiral_conv_bwd_small_reduce");                                        \
+  }
+  BOSB(32, 1) BOSB(32, 2) BOSB(32, 3) BOSB(64, 1) BOSB(64, 2) BOSB(64, 3)
+#undef BOSB
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: unsupported channels %d -> %d", cin, cout);
+}
+
 extern "C" int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* stream) {
   if (n <= 0) return CFSD_OK;
   if (!items) return set_error(CFSD_EINVAL, "dw_reduce_batch: null items");
@@ -2421,7 +2562,11 @@ extern "C" int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* str
     d.cin = q.cin;
     d.cout = q.cout;
     const int K = kSeq * q.cin;
-    if (q.fused && fused_small(q.cin, q.cout)) {
+    if (q.fused == 2 && mfma_shape(q.cin, q.cout)) {  // bf16 MFMA dW: plain slabs
+      d.kind = 1;
+      d.n_slabs = bf::dw_slabs(q.batch, q.rows, q.cin, q.cout);
+      d.n_el = q.cout * K + q.cout;
+    } else if (q.fused && fused_small(q.cin, q.cout)) {
       d.kind = 1;
       d.n_slabs = fused_small_gx((long)q.batch * q.vsrc);
       d.n_el = q.cout * K + q.cout;

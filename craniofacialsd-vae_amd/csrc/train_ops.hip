@@ -622,10 +622,13 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 // Four elements per thread in 16-B accesses (the four state arrays are
 // streamed once: 7 x 4 B per element of HBM traffic); the n % 4 tail goes to
 // the last thread.  Same per-element arithmetic as a scalar loop.
+// With `shadow` != NULL the updated parameters are also written as bf16 (the
+// weights the bf16 kernels read: fp32 master + bf16 copy in one pass).
 __global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, const float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v,
                                               const int* __restrict__ step, long n, float lr,
-                                              float b1, float b2, float eps, float wd) {
+                                              float b1, float b2, float eps, float wd,
+                                              bf16_t* __restrict__ shadow) {
   const long q = (long)blockIdx.x * blockDim.x + threadIdx.x, n4 = n / 4;
   if (q > n4) return;
   const int t = *step;
@@ -640,10 +643,14 @@ __global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, const float
 #pragma unroll
     for (int j = 0; j < 4; ++j) adam_elem(pa[j], ga[j], ma[j], va[j], b1, b2, eps, wd, step_size, sqrt_bc2);
     st4(p + 4 * q, f32x4{pa[0], pa[1], pa[2], pa[3]});
+    if (shadow) st4f(shadow + 4 * q, f32x4{pa[0], pa[1], pa[2], pa[3]});
     st4(m + 4 * q, f32x4{ma[0], ma[1], ma[2], ma[3]});
     st4(v + 4 * q, f32x4{va[0], va[1], va[2], va[3]});
   } else {
-    for (long i = 4 * n4; i < n; ++i) adam_elem(p[i], g[i], m[i], v[i], b1, b2, eps, wd, step_size, sqrt_bc2);
+    for (long i = 4 * n4; i < n; ++i) {
+      adam_elem(p[i], g[i], m[i], v[i], b1, b2, eps, wd, step_size, sqrt_bc2);
+      if (shadow) stf(shadow + i, p[i]);
+    }
   }
 }
 
@@ -898,13 +905,13 @@ extern "C" int cfsd_linear_bwd(const float* x, const float* w, const float* dy, 
 
 extern "C" int cfsd_adam(float* param, const float* grad, float* m, float* v,
                          const int32_t* step, size_t n, float lr, float beta1, float beta2,
-                         float eps, float weight_decay, void* stream) {
+                         float eps, float weight_decay, uint16_t* param_bf16, void* stream) {
   if (!param || !grad || !m || !v || !step) return set_error(CFSD_EINVAL, "adam: null pointer");
   if (n == 0) return CFSD_OK;
-  if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) & 15)
+  if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v | (uintptr_t)param_bf16 * 2) & 15)
     return set_error(CFSD_EINVAL, "adam: param/grad/m/v must be 16-B aligned");
   hipLaunchKernelGGL(adam_k, dim3((unsigned)((n / 4 + 1 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     param, grad, m, v, step, (long)n, lr, beta1, beta2, eps, weight_decay);
+                     param, grad, m, v, step, (long)n, lr, beta1, beta2, eps, weight_decay, param_bf16);
   return launch_status("adam");
 }
 

@@ -106,6 +106,7 @@ class FlatParams:
         self.exp_avg = torch.zeros(off, dtype=torch.float32, device=device)
         self.exp_avg_sq = torch.zeros(off, dtype=torch.float32, device=device)
         self.step = torch.zeros(1, dtype=torch.int32, device=device)
+        self.shadow = None  # bf16 copy of `data` (precision "bf16"), refreshed by Adam
 
     def view(self, name, buf=None):
         off, shape = self.offsets[name]
@@ -132,7 +133,16 @@ class SDVAEEngine:
     topology and any number of batch sizes (buffers cached per batch)."""
 
     def __init__(self, topo, spec=None, lr=1e-4, weight_decay=0.0, w_kl=1e-4, w_lc=0.5,
-                 w_lap=0.1, eta1=0.5, eta2=0.5, swap_bs=4, seed=0, device="cuda"):
+                 w_lap=0.1, eta1=0.5, eta2=0.5, swap_bs=4, seed=0, device="cuda", precision="fp32"):
+        """``precision``: "fp32" (the reference's arithmetic, the parity
+        configuration) or "bf16" (configs C3/C5: the level-0/1 activations
+        and gradients -- the large tensors -- stored in bf16, their convs on
+        bf16 MFMA with the bf16 shadow of the fp32 master weights, fp32
+        accumulation; coarse levels, bottleneck, losses, gradients and Adam
+        stay fp32)."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.precision = precision
         self.topo = topo
         self.spec = spec or ModelSpec()
         self.device = torch.device(device)
@@ -149,6 +159,13 @@ class SDVAEEngine:
                              "utils.py:88-89): the training losses are MSE + Laplacian (+ KL, LC)")
         self.num_vert = topo.n_verts[-1]
         self.params = FlatParams(self.spec.param_specs(self.num_vert, topo.seq), self.device)
+        # levels whose tensors are bf16 (the two finest; never the bottleneck)
+        self.lp_levels = set()
+        if precision == "bf16":
+            if not all(topo.enc_select) or self.spec.n < 3:
+                raise ValueError("bf16 precision needs 0/1 selection down-sampling and >= 3 levels")
+            self.lp_levels = {0, 1}
+            self.params.shadow = torch.zeros(self.params.numel, dtype=torch.bfloat16, device=self.device)
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -173,6 +190,12 @@ class SDVAEEngine:
                 fan_out, fan_in = shape
                 a = math.sqrt(6.0 / (fan_in + fan_out))
                 v.uniform_(-a, a, generator=generator)
+        self.sync_shadow()
+
+    def sync_shadow(self):
+        """Refresh the bf16 weight shadow from the fp32 master (bf16 mode)."""
+        if self.params.shadow is not None and self.device.type == "cuda":
+            ops.cast(self.params.data, self.params.shadow)
 
     def state_dict(self):
         n, order = self.spec.n, self.spec.reference_order(self.num_vert, self.topo.seq)
@@ -184,6 +207,7 @@ class SDVAEEngine:
             if tuple(t.shape) != tuple(shape):
                 raise ValueError(f"{name}: shape {tuple(t.shape)} != {shape}")
             self.params.view(name).copy_(t.to(self.device, torch.float32))
+        self.sync_shadow()
 
     def grads(self):
         return {k: self.params.gview(k) for k, _ in self.params.specs}
@@ -295,17 +319,23 @@ class SDVAEEngine:
             return self._bufs[bsz]
         T, S, dev = self.topo, self.spec, self.device
         f = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731
+        lp = self.lp_levels
+
+        def fl(level, *shape):  # storage of a level's activation / gradient
+            return torch.empty(shape, dtype=torch.bfloat16 if level in lp else torch.float32, device=dev)
+
         b = _Buffers()
         b.bsz = bsz
         nv = T.n_verts
         lat = S.latent
+        last_enc = S.enc_layers()[-1][2]
         b.x = f(bsz, nv[0], S.in_ch)
         b.enc_full = [None] * S.n     # full-resolution conv outputs (non-selection path)
         b.enc_out = []                # pooled Enblock outputs [B, V_{i+1}, C_i]
         for (cin, cout, lv) in S.enc_layers():
             if not T.enc_select[lv]:
                 b.enc_full[lv] = f(bsz, nv[lv], cout)
-            b.enc_out.append(f(bsz, nv[lv + 1], cout))
+            b.enc_out.append(f(bsz, nv[lv + 1], cout) if lv == last_enc else fl(lv + 1, bsz, nv[lv + 1], cout))
         nmulv = 2 * lat if S.is_vae else lat
         b.mulv, b.z = f(bsz, nmulv), f(bsz, lat)
         b.dlat, b.terms = f(bsz, 3 * lat), f(2)
@@ -315,8 +345,8 @@ class SDVAEEngine:
         b.h = f(bsz, self.num_vert, S.out_ch[-1])
         b.dec_up, b.dec_out = [], []
         for (cin, cout, lv, ui) in S.dec_layers():
-            b.dec_up.append(f(bsz, nv[lv], cin))
-            b.dec_out.append(f(bsz, nv[lv], cout))
+            b.dec_up.append(fl(lv, bsz, nv[lv], cin))
+            b.dec_out.append(fl(lv, bsz, nv[lv], cout))
         b.out = f(bsz, nv[0], S.in_ch)
         b.unit = f(bsz, nv[0], S.in_ch)
         b.partials = f(2 * ops.recon_lap_blocks(bsz, nv[0]))
@@ -328,8 +358,8 @@ class SDVAEEngine:
         b.dh = torch.empty_like(b.h)
         b.dz = f(bsz, lat)
         b.dmulv = torch.empty_like(b.mulv)
-        b.dpre_enc = [f(bsz, (nv[lv + 1] if T.enc_select[lv] else nv[lv]), cout)
-                      for (cin, cout, lv) in S.enc_layers()]
+        b.dpre_enc = [f(bsz, nv[lv + 1], cout) if (lv == last_enc or not T.enc_select[lv])
+                      else fl(lv + 1, bsz, nv[lv + 1], cout) for (cin, cout, lv) in S.enc_layers()]
         b.g_enc_in = [None] + [f(bsz, nv[lv], cin) if not T.enc_select[lv - 1] else None
                                for (cin, cout, lv) in S.enc_layers()[1:]]
         b.g_pooled = [f(bsz, nv[lv + 1], cout) if not T.enc_select[lv] else None
@@ -357,17 +387,20 @@ class SDVAEEngine:
                                                          S.in_ch))]
         b.paired = {}
 
-        def dw_region(key, vsrc, rows, seq, cin, cout, has_dx):
-            b.paired[key] = has_dx and ops.spiral_conv_bwd_paired(bsz, vsrc, rows, seq, cin, cout)
-            nb = (ops.spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout) if b.paired[key]
-                  else ops.spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout))
+        def dw_region(key, vsrc, rows, seq, cin, cout, has_dx, low):
+            b.paired[key] = (not low) and has_dx and ops.spiral_conv_bwd_paired(bsz, vsrc, rows, seq, cin, cout)
+            if low:
+                nb = ops.spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout)
+            else:
+                nb = (ops.spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout) if b.paired[key]
+                      else ops.spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout))
             regions.append((key, nb))
 
         for i, (cin, cout, lv, _) in enumerate(S.dec_layers()):
-            dw_region(("dec", i), nv[lv], nv[lv], T.seq[lv], cin, cout, True)
+            dw_region(("dec", i), nv[lv], nv[lv], T.seq[lv], cin, cout, True, lv in lp)
         for (cin, cout, lv) in S.enc_layers():
             rows = nv[lv + 1] if T.enc_select[lv] else nv[lv]
-            dw_region(("enc", lv), nv[lv], rows, T.seq[lv], cin, cout, lv > 0)
+            dw_region(("enc", lv), nv[lv], rows, T.seq[lv], cin, cout, lv > 0, lv in lp)
         total = sum((nb // 4 + 64) // 64 * 64 for _, nb in regions)
         b.ws_dw_all = torch.empty(total, dtype=torch.float32, device=dev)
         b.ws_dw, off = {}, 0
@@ -392,6 +425,26 @@ class SDVAEEngine:
     def _dec_w(self, i):  # de_layers[i + 1]
         return (self.params.view(f"de_layers.{i + 1}.conv.layer.weight"),
                 self.params.view(f"de_layers.{i + 1}.conv.layer.bias"))
+
+    def _w16(self, wname):
+        """bf16 shadow view of a conv weight (bf16 mode)."""
+        return self.params.view(wname, self.params.shadow)
+
+    def _conv_fwd(self, b, x, idx, wname, act, out):
+        """SpiralConv forward on fp32 or mixed/bf16 operands."""
+        P = self.params
+        w, bias = P.view(wname + ".weight"), P.view(wname + ".bias")
+        if x.dtype == torch.float32 and out.dtype == torch.float32:
+            ops.spiral_conv_fwd(x, idx, w, bias, act, out=out, workspace=b.ws)
+        else:
+            ops.spiral_conv_fwd_x(x, idx, w, self._w16(wname + ".weight"), bias, act, out)
+
+    @staticmethod
+    def _spmm(csr, x, m, out, elu_y=None):
+        if x.dtype == torch.float32 and out.dtype == torch.float32:
+            ops.spmm(csr, x, m, elu_y=elu_y, out=out)
+        else:
+            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out)
 
     def _lin_names(self):
         n = self.spec.n
@@ -418,8 +471,7 @@ class SDVAEEngine:
         for (cin, cout, lv) in S.enc_layers():
             w, bias = self._enc_w(lv)
             if T.enc_select[lv]:
-                ops.spiral_conv_fwd(h, T.enc_rows[lv], w, bias, ACT_ELU, out=b.enc_out[lv],
-                                    workspace=b.ws)
+                self._conv_fwd(b, h, T.enc_rows[lv], f"en_layers.{lv}.conv.layer", ACT_ELU, b.enc_out[lv])
             else:
                 ops.spiral_conv_fwd(h, T.spiral[lv], w, bias, ACT_ELU, out=b.enc_full[lv],
                                     workspace=b.ws)
@@ -448,15 +500,12 @@ class SDVAEEngine:
                        workspace=b.lin_ws)
         h = b.h
         for i, (cin, cout, lv, ui) in enumerate(S.dec_layers()):
-            ops.spmm(T.up_csr[ui], h, T.n_verts[lv], out=b.dec_up[i])
-            w, bias = self._dec_w(i)
-            ops.spiral_conv_fwd(b.dec_up[i], T.spiral[lv], w, bias, ACT_ELU, out=b.dec_out[i],
-                                workspace=b.ws)
+            self._spmm(T.up_csr[ui], h, T.n_verts[lv], out=b.dec_up[i])
+            self._conv_fwd(b, b.dec_up[i], T.spiral[lv], f"de_layers.{i + 1}.conv.layer", ACT_ELU,
+                           b.dec_out[i])
             h = b.dec_out[i]
         n = S.n
-        ops.spiral_conv_fwd(h, T.spiral[0], self.params.view(f"de_layers.{n + 1}.layer.weight"),
-                            self.params.view(f"de_layers.{n + 1}.layer.bias"), ACT_NONE, out=b.out,
-                            workspace=b.ws)
+        self._conv_fwd(b, h, T.spiral[0], f"de_layers.{n + 1}.layer", ACT_NONE, b.out)
 
     def losses_fwd(self, b, acc=None, finalize=True):
         T = self.topo
@@ -526,15 +575,22 @@ class SDVAEEngine:
 
         weight_grad = ops.spiral_conv_bwd_weight
 
-        _, d = ops.spiral_conv_bwd(last_in, T.spiral[0], b.dout, T.spiral_inv[0],
-                                   P.view(f"de_layers.{n + 1}.layer.weight"), None, None,
-                                   dx=b.dpre_dec[-1], elu_y=last_in, workspace=b.ws_dw["out"])
+        bwd_out = ops.spiral_conv_bwd_x if last_in.dtype == torch.bfloat16 else ops.spiral_conv_bwd
+        _, d = bwd_out(last_in, T.spiral[0], b.dout, T.spiral_inv[0],
+                       P.view(f"de_layers.{n + 1}.layer.weight"), None, None,
+                       dx=b.dpre_dec[-1], elu_y=last_in, workspace=b.ws_dw["out"])
         defer(d, f"de_layers.{n + 1}.layer")
         dec = S.dec_layers()
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]
             w, _ = self._dec_w(i)
-            if b.paired[("dec", i)]:  # dx + dW slabs in one launch
+            if lv in self.lp_levels:  # bf16 operands: bf16 MFMA dW slabs + dx
+                defer(ops.spiral_conv_bwd_weight_x(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
+                                                   b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
+                ops.spiral_conv_bwd_data_x(b.dpre_dec[i], T.spiral_inv[lv],
+                                           self._w16(f"de_layers.{i + 1}.conv.layer.weight"), T.n_verts[lv],
+                                           out=b.g_dec_up[i])
+            elif b.paired[("dec", i)]:  # dx + dW slabs in one launch
                 _, d = ops.spiral_conv_bwd(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_inv[lv],
                                            w, None, None, dx=b.g_dec_up[i], workspace=b.ws_dw[("dec", i)])
                 defer(d, f"de_layers.{i + 1}.conv.layer")
@@ -544,10 +600,10 @@ class SDVAEEngine:
                 ops.spiral_conv_bwd_data(b.dpre_dec[i], T.spiral_inv[lv], w, T.n_verts[lv],
                                          out=b.g_dec_up[i], workspace=b.ws)
             if i > 0:  # through Pool(up) into the previous Deblock's ELU
-                ops.spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], elu_y=b.dec_out[i - 1],
-                         out=b.dpre_dec[i - 1])
+                self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dpre_dec[i - 1],
+                           elu_y=b.dec_out[i - 1])
             else:
-                ops.spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh)
+                self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh)
         # decoder Linear
         ops.linear_bwd(b.z, P.view("de_layers.0.weight"), b.dh.view(b.bsz, -1), dx=b.dz,
                        dw=P.gview("de_layers.0.weight"), db=P.gview("de_layers.0.bias"),
@@ -587,6 +643,14 @@ class SDVAEEngine:
             x_in = b.x if lv == 0 else b.enc_out[lv - 1]
             rows_tab = T.enc_rows[lv]
             prev = lv - 1
+            if lv in self.lp_levels:  # bf16 operands (selection down-sampling)
+                defer(ops.spiral_conv_bwd_weight_x(x_in, rows_tab, b.dpre_enc[lv], None, None,
+                                                   b.ws_dw[("enc", lv)]), f"en_layers.{lv}.conv.layer")
+                if lv > 0:
+                    ops.spiral_conv_bwd_data_x(b.dpre_enc[lv], T.enc_inv[lv],
+                                               self._w16(f"en_layers.{lv}.conv.layer.weight"), T.n_verts[lv],
+                                               elu_y=b.enc_out[prev], out=b.dpre_enc[prev])
+                continue
             if b.paired[("enc", lv)]:  # dx + dW slabs in one launch
                 sel = T.enc_select[prev]
                 _, d = ops.spiral_conv_bwd(x_in, rows_tab, b.dpre_enc[lv], T.enc_inv[lv], w, None, None,
@@ -616,7 +680,7 @@ class SDVAEEngine:
     def adam_step(self):
         P = self.params
         ops.adam(P.data, P.grad, P.exp_avg, P.exp_avg_sq, P.step, self.lr, beta1=self.betas[0],
-                 beta2=self.betas[1], eps=self.adam_eps, weight_decay=self.weight_decay)
+                 beta2=self.betas[1], eps=self.adam_eps, weight_decay=self.weight_decay, shadow=P.shadow)
 
     def advance_step(self, b=None):
         """t += 1 on device (the Adam bias-correction step) and, for a VAE

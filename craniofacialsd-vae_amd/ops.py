@@ -15,6 +15,9 @@ from .topology import INV_HEAD
 
 ACT_NONE = 0
 ACT_ELU = 1
+DT_F32 = 0    # CFSD_DT_F32
+DT_BF16 = 1   # CFSD_DT_BF16
+_DTYPES = {torch.float32: DT_F32, torch.bfloat16: DT_BF16}
 
 
 def _need(t, shape, dtype=torch.float32, name="tensor"):
@@ -29,6 +32,19 @@ def _need(t, shape, dtype=torch.float32, name="tensor"):
     if shape is not None and tuple(t.shape) != tuple(shape):
         raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
     return t
+
+
+def _dt(t, name="tensor"):
+    if t.dtype not in _DTYPES:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected float32 or bfloat16")
+    return _DTYPES[t.dtype]
+
+
+def _needx(t, shape, name="tensor"):
+    """_need for a mixed-precision operand (fp32 or bf16)."""
+    if t is None:
+        raise ValueError(f"{name} is required")
+    return _need(t, shape, t.dtype if t.dtype in _DTYPES else torch.float32, name)
 
 
 def _out(out, shape, like, name="out"):
@@ -372,13 +388,19 @@ def loss_finalize(partials, terms, out, acc, bsz, nv, c, w_kl, w_lc, w_lap):
 
 
 # ------------------------------------------------------------------ optimiser
-def adam(param, grad, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):
+def adam(param, grad, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0,
+         shadow=None):
+    """Adam over the flat fp32 buffers; ``shadow`` (bf16, same length) also
+    receives the updated parameters (the bf16 path's weight copy)."""
     n = param.numel()
     for t, nm in ((param, "param"), (grad, "grad"), (m, "m"), (v, "v")):
         _need(t, (n,), name=nm)
     _need(step, (1,), torch.int32, "step")
+    if shadow is not None:
+        _need(shadow, (n,), torch.bfloat16, "shadow")
     call("cfsd_adam", ptr(param), ptr(grad), ptr(m), ptr(v), ptr(step), ctypes.c_size_t(n),
-         float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), stream_ptr())
+         float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), ptr(shadow),
+         stream_ptr())
 
 
 def step_begin(counter, seed, eps=None, key=None, n_regions=0, batch_idx=None, bs=0,
@@ -450,3 +472,124 @@ def reconstruction_error_stats(mesh_means):
     over the concatenated per-mesh means (device tensor, torch reductions)."""
     return {"mean": torch.mean(mesh_means).item(), "median": torch.median(mesh_means).item(),
             "max": torch.max(mesh_means).item(), "std": torch.std(mesh_means).item()}
+
+
+# ------------------------------------------------------------------ bf16 path
+# Mixed-precision entry points (include/cfsd.h "bf16 path"): activations /
+# gradients are float32 or bfloat16 tensors, weights are the fp32 master view
+# and its bf16 shadow view.
+def cast(src, out):
+    """fp32 <-> bf16 storage conversion (round to nearest even)."""
+    _needx(src, None, "src")
+    _needx(out, tuple(src.shape), "out")
+    call("cfsd_cast", ptr(src), _dt(src), ptr(out), _dt(out), ctypes.c_size_t(src.numel()), stream_ptr())
+    return out
+
+
+def spiral_conv_fwd_x(x, idx, w, w_bf16, b, act, out):
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = w.shape[0]
+    _needx(x, None, "x")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(w, (cout, seq * cin), name="w")
+    if w_bf16 is not None:
+        _need(w_bf16, (cout, seq * cin), torch.bfloat16, "w_bf16")
+    if b is not None:
+        _need(b, (cout,), name="bias")
+    _needx(out, (bsz, rows, cout), "out")
+    call("cfsd_spiral_conv_fwd_x", ptr(x), _dt(x), ptr(idx), ptr(w), ptr(w_bf16), ptr(b), ptr(out),
+         _dt(out), bsz, vsrc, rows, seq, cin, cout, act, stream_ptr())
+    return out
+
+
+def spiral_conv_bwd_data_x(dpre, inv, w_bf16, vsrc, elu_y=None, out=None):
+    bsz, rows, cout = dpre.shape
+    inv_ptr, inv_row, inv_head = inv
+    seq = (inv_ptr.numel() - 1) // vsrc
+    cin = w_bf16.shape[1] // seq
+    _needx(dpre, None, "dpre")
+    _need(inv_ptr, (vsrc * seq + 1,), torch.int32, "inv_ptr")
+    _need(inv_row, (rows * seq,), torch.int32, "inv_row")
+    _need(inv_head, (vsrc * seq, INV_HEAD), torch.int32, "inv_head")
+    _need(w_bf16, (cout, seq * cin), torch.bfloat16, "w_bf16")
+    if elu_y is not None:
+        _need(elu_y, (bsz, vsrc, cin), torch.bfloat16, "elu_y")
+    if out is None:
+        out = torch.empty((bsz, vsrc, cin), dtype=torch.bfloat16, device=dpre.device)
+    _need(out, (bsz, vsrc, cin), torch.bfloat16, "dx")
+    call("cfsd_spiral_conv_bwd_data_x", ptr(dpre), _dt(dpre), ptr(inv_ptr), ptr(inv_row), ptr(inv_head),
+         ptr(w_bf16), ptr(elu_y), ptr(out), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    return out
+
+
+def spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout):
+    return int(_abi.lib().cfsd_spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout))
+
+
+def spiral_conv_bwd_weight_x(x, idx, dpre, dw, db, workspace):
+    """dW/db of a bf16-path conv (x / dpre fp32 or bf16); ``dw is db is None``
+    defers the reduction (returns a DeferredDw for dw_reduce_batch)."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = dpre.shape[2]
+    _needx(x, None, "x")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _needx(dpre, (bsz, rows, cout), "dpre")
+    if dw is not None or db is not None:
+        _need(dw, (cout, seq * cin), name="dw")
+        _need(db, (cout,), name="db")
+    _need(workspace, None, name="workspace")
+    need = spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout)
+    nbytes = workspace.numel() * workspace.element_size()
+    if nbytes < need:
+        raise ValueError(f"workspace {nbytes} < {need} bytes")
+    call("cfsd_spiral_conv_bwd_weight_x", ptr(x), _dt(x), ptr(idx), ptr(dpre), _dt(dpre), ptr(dw), ptr(db),
+         ptr(workspace), ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    if dw is None:
+        mfma = cin in (32, 64) and cout in (32, 64)
+        return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2 if mfma else 0)
+    return None
+
+
+def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None):
+    """Fused dx + dW of the xyz output conv with bf16 x / elu_y / dx."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = dpre.shape[2]
+    inv_ptr, inv_row, inv_head = inv
+    _need(x, None, torch.bfloat16, "x")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(dpre, (bsz, rows, cout), name="dpre")
+    _need(inv_head, (vsrc * seq, INV_HEAD), torch.int32, "inv_head")
+    _need(w, (cout, seq * cin), name="w")
+    if dx is not None:
+        _need(dx, (bsz, vsrc, cin), torch.bfloat16, "dx")
+    if elu_y is not None:
+        _need(elu_y, (bsz, vsrc, cin), torch.bfloat16, "elu_y")
+    if dw is not None or db is not None:
+        _need(dw, (cout, seq * cin), name="dw")
+        _need(db, (cout,), name="db")
+    ws, nb = _conv_ws(workspace, x.device, spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout))
+    call("cfsd_spiral_conv_bwd_x", ptr(x), DT_BF16, ptr(idx), ptr(dpre), ptr(inv_ptr), ptr(inv_row),
+         ptr(inv_head), ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb),
+         bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    if dw is None:
+        return dx, DeferredDw(ws, bsz, vsrc, rows, cin, cout, 1)
+    return dx
+
+
+def spmm_x(csr, x, m, elu_y=None, out=None):
+    """Pool SpMM with fp32 or bf16 operands (fp32 sums, file order)."""
+    row_ptr, col, val = csr
+    bsz, n, c = x.shape
+    _needx(x, None, "x")
+    _need(row_ptr, (m + 1,), torch.int32, "row_ptr")
+    _need(col, None, torch.int32, "col")
+    _need(val, (col.numel(),), name="val")
+    _needx(out, (bsz, m, c), "out")
+    if elu_y is not None:
+        _need(elu_y, (bsz, m, c), out.dtype, "elu_y")
+    call("cfsd_spmm_csr_x", ptr(row_ptr), ptr(col), ptr(val), ptr(x), _dt(x), ptr(elu_y), ptr(out),
+         _dt(out), bsz, m, n, c, stream_ptr())
+    return out

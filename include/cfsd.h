@@ -37,6 +37,11 @@ extern "C" {
 #define CFSD_ACT_NONE 0
 #define CFSD_ACT_ELU 1
 
+/* Storage type of an activation / gradient operand of the mixed-precision
+ * (bf16) entry points: fp32, or bfloat16 as raw uint16 (torch.bfloat16 bits). */
+#define CFSD_DT_F32 0
+#define CFSD_DT_BF16 1
+
 /* ABI version: (major << 16) | minor. */
 int cfsd_version(void);
 const char* cfsd_last_error_string(void);
@@ -89,8 +94,9 @@ size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int seq, int c
  * called with dw == db == NULL leave their per-workgroup partial sums in
  * `workspace` and skip the reduction; cfsd_dw_reduce_batch then reduces up
  * to 16 such layers (each with its own workspace) in ONE launch, with the
- * same fixed summation order (identical results).  `fused` = the partials
- * came from cfsd_spiral_conv_bwd on a small-output layer (cout*seq <= 32). */
+ * same fixed summation order (identical results).  `fused` = 1: the partials
+ * came from cfsd_spiral_conv_bwd(_x) on a small-output layer (cout*seq <= 32);
+ * 2: from cfsd_spiral_conv_bwd_weight_x on a 32/64-channel layer (bf16). */
 typedef struct {
   const float* workspace;
   float* dw;
@@ -224,9 +230,12 @@ int cfsd_loss_finalize(const float* partials, int nblocks, const float* terms, f
 /* ---------------------------------------------------------------- optimiser
  * torch.optim.Adam step (model_manager.py:69-72, 316) over one flat fp32
  * parameter buffer.  `step` is a device int32 holding the 1-based step number
- * t used for the bias corrections (advanced by cfsd_step_begin). */
+ * t used for the bias corrections (advanced by cfsd_step_begin).  With
+ * param_bf16 != NULL (8-B aligned) the updated parameters are also written
+ * there as bf16 (the weight shadow the bf16 kernels read; may be NULL). */
 int cfsd_adam(float* param, const float* grad, float* m, float* v, const int32_t* step, size_t n,
-              float lr, float beta1, float beta2, float eps, float weight_decay, void* stream);
+              float lr, float beta1, float beta2, float eps, float weight_decay,
+              uint16_t* param_bf16, void* stream);
 
 /* Per-step device bookkeeping (graph-replayable, no host input):
  * t = ++*counter; key = hash(seed, t) % n_regions (replaces random.choice,
@@ -250,6 +259,49 @@ int cfsd_elu_bwd(const float* dy, const float* y, float* dx, size_t n, void* str
 
 /* Element-wise y *= alpha (gradient averaging after an all-reduce). */
 int cfsd_scale(float* y, size_t n, float alpha, void* stream);
+
+/* ---------------------------------------------------------------- bf16 path
+ * Mixed-precision variants (BASELINE.json configs C3/C5: bf16 activations and
+ * weights, fp32 accumulation, fp32 master weights + Adam).  Each activation /
+ * gradient operand carries its storage type (CFSD_DT_F32 / CFSD_DT_BF16);
+ * the engine's bf16 mode keeps the level-0/1 tensors in bf16 and the coarse
+ * levels + bottleneck in fp32.  Same arithmetic as the fp32 entry points
+ * above (model.py:27-55 and autograd), products in bf16, sums in fp32.
+ * 32/64-channel layers need x bf16 and the bf16 weight shadow `w_bf16`
+ * ([cout, seq*cin], from cfsd_adam/cfsd_cast); the xyz layers use the fp32
+ * `w` (input conv: x fp32 -> y bf16; output conv: x bf16 -> y fp32). */
+int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* idx, const float* w,
+                           const uint16_t* w_bf16, const float* bias, void* y, int y_dt, int batch,
+                           int vsrc, int rows, int seq, int cin, int cout, int act, void* stream);
+/* dx (bf16) of a 32/64-channel layer; dpre bf16 or fp32; elu_y bf16 or NULL. */
+int cfsd_spiral_conv_bwd_data_x(const void* dpre, int dpre_dt, const int32_t* inv_ptr,
+                                const int32_t* inv_row, const int32_t* inv_head,
+                                const uint16_t* w_bf16, const uint16_t* elu_y, uint16_t* dx,
+                                int batch, int vsrc, int rows, int seq, int cin, int cout,
+                                void* stream);
+/* dW/db (fp32): 32/64-channel layers (x bf16, dpre bf16/fp32) and the xyz
+ * input layer (x fp32, dpre bf16).  dw == db == NULL defers the reduction
+ * (cfsd_dw_reduce_batch item with fused = 2 for the 32/64-channel kind, 0
+ * for the input layer). */
+size_t cfsd_spiral_conv_bwd_weight_x_workspace(int batch, int rows, int seq, int cin, int cout);
+int cfsd_spiral_conv_bwd_weight_x(const void* x, int x_dt, const int32_t* idx, const void* dpre,
+                                  int dpre_dt, float* dw, float* db, float* workspace,
+                                  size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
+                                  int cin, int cout, void* stream);
+/* Fused dx + dW of the xyz output layer (cout*seq <= 32) with x, elu_y, dx
+ * bf16 and dpre fp32 (workspace: cfsd_spiral_conv_bwd_workspace; deferred
+ * items use fused = 1). */
+int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* idx, const float* dpre,
+                           const int32_t* inv_ptr, const int32_t* inv_row, const int32_t* inv_head,
+                           const float* w, const void* elu_y, void* dx, float* dw, float* db,
+                           float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows,
+                           int seq, int cin, int cout, void* stream);
+/* cfsd_spmm_csr with per-operand storage types (elu_y has y's type). */
+int cfsd_spmm_csr_x(const int32_t* row_ptr, const int32_t* col, const float* val, const void* x,
+                    int x_dt, const void* elu_y, void* y, int y_dt, int batch, int m, int n, int c,
+                    void* stream);
+/* Storage conversion fp32 <-> bf16 (round to nearest even), n elements. */
+int cfsd_cast(const void* src, int src_dt, void* dst, int dst_dt, size_t n, void* stream);
 
 /* ---------------------------------------------------------------- evaluation
  * Replaces ModelManager.compute_vertex_errors (model_manager.py:395-400) and

@@ -1,0 +1,288 @@
+"""bf16 path (BASELINE.json configs C3/C5): every bf16 kernel against the
+oracle run in float64 on the SAME bf16-rounded inputs, then the full bf16
+train step against the fp32 reference goldens.
+
+Tolerances (stated per test): a product of two bf16 values is exact in fp32
+and every sum is fp32, so fp32 outputs carry only fp32 summation error
+(rel 1e-5 of the largest magnitude); bf16 outputs add one rounding (half a
+bf16 ulp = 2^-9 relative); the dx kernel also rounds the inverse-spiral
+gather-sum A to bf16 once before the MFMA (1e-2 of the largest magnitude).
+The Pool SpMM sums fp32 products in file order exactly like the oracle, so
+its bf16 output is bit-exact to the oracle's fp32 result rounded to bf16.
+Reference: model.py:27-55 (+ autograd), model_manager.py:274-326.
+"""
+import numpy as np
+import pytest
+import torch
+
+import cfsd_loader
+import recipe
+from oracle import cfsd_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+torch.set_num_threads(1)
+
+
+@pytest.fixture(scope="module")
+def mods():
+    cfsd_loader.load()
+    from craniofacialsd_vae_amd import engine as E
+    from craniofacialsd_vae_amd import ops, topology
+    return E, ops, topology
+
+
+@pytest.fixture(scope="module")
+def dtopo(mods, topo_npz):
+    return mods[2].DeviceTopology.from_npz(topo_npz, device=DEV)
+
+
+def rb(t):
+    """bf16-rounded copy (as float64 for the reference)."""
+    return t.to(BF).double()
+
+
+def err_rel_max(got, ref):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    return float((got - ref).abs().max() / (ref.abs().max() + 1e-30))
+
+
+def gather(x, sp):
+    idx = torch.as_tensor(sp, dtype=torch.long)
+    return torch.index_select(x, 1, idx.reshape(-1)).view(x.shape[0], idx.shape[0], -1)
+
+
+# (cin, cout, level, batch) of the 32/64-channel bf16 MFMA kernels
+MFMA_CASES = [(32, 32, 0, 2), (32, 32, 1, 16), (32, 32, 3, 3), (32, 64, 2, 3), (64, 32, 2, 3),
+              (64, 64, 3, 2)]
+
+
+@pytest.mark.parametrize("cin,cout,level,bsz", MFMA_CASES)
+@pytest.mark.parametrize("act", [0, 1])
+@pytest.mark.parametrize("out_bf16", [True, False])
+def test_conv_fwd_bf16(mods, otopo, dtopo, cin, cout, level, bsz, act, out_bf16):
+    _, ops, _ = mods
+    g = torch.Generator().manual_seed(cin + cout + level + act)
+    sp = otopo.spirals[level]
+    v = sp.shape[0]
+    x = torch.randn(bsz, v, cin, generator=g)
+    w = torch.randn(cout, 9 * cin, generator=g) * 0.1
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = gather(rb(x), sp) @ rb(w).T + b.double()
+    if act:
+        ref = torch.nn.functional.elu(ref)
+    out = torch.empty(bsz, v, cout, dtype=BF if out_bf16 else torch.float32, device=DEV)
+    ops.spiral_conv_fwd_x(x.to(BF).to(DEV), dtopo.spiral[level], w.to(DEV), w.to(BF).to(DEV), b.to(DEV),
+                          act, out)
+    tol = 2.0 ** -8 if out_bf16 else 1e-5
+    assert err_rel_max(out.float(), ref) <= tol
+
+
+@pytest.mark.parametrize("table,cin,cout,level,bsz", [("dec", 32, 32, 0, 2), ("dec", 32, 32, 1, 16),
+                                                      ("enc", 32, 32, 1, 16), ("dec", 64, 32, 2, 3),
+                                                      ("dec", 32, 64, 3, 3), ("dec", 64, 64, 2, 2)])
+@pytest.mark.parametrize("dpre_f32", [False, True])
+def test_conv_bwd_bf16(mods, otopo, dtopo, table, cin, cout, level, bsz, dpre_f32):
+    """dx (bf16, with elu') and dW/db (fp32) of the bf16 MFMA kernels, on the
+    full spiral table and on the Enblock row subset (E1's shape)."""
+    _, ops, _ = mods
+    g = torch.Generator().manual_seed(5 + cin + cout + level)
+    sp = otopo.spirals[level]
+    if table == "enc":
+        sp = sp[np.asarray(otopo.down[level][1])[np.argsort(otopo.down[level][0])]]
+        idx, inv = dtopo.enc_rows[level], dtopo.enc_inv[level]
+    else:
+        idx, inv = dtopo.spiral[level], dtopo.spiral_inv[level]
+    vsrc, rows = otopo.spirals[level].shape[0], sp.shape[0]
+    y = torch.nn.functional.elu(torch.randn(bsz, vsrc, cin, generator=g))  # the conv input (an ELU output)
+    w = torch.randn(cout, 9 * cin, generator=g) * 0.1
+    dpre = torch.randn(bsz, rows, cout, generator=g)
+    yb, wb = rb(y), rb(w)
+    dpb = dpre.double() if dpre_f32 else rb(dpre)
+    xl = yb.clone().requires_grad_()
+    wl = wb.clone().requires_grad_()
+    bl = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+    (gather(xl, sp) @ wl.T + bl).backward(dpb)
+    dx_ref = xl.grad * torch.where(yb > 0, 1.0, yb + 1.0)
+    dpre_dev = (dpre if dpre_f32 else dpre.to(BF)).to(DEV)
+    y_dev = y.to(BF).to(DEV)
+    dx = ops.spiral_conv_bwd_data_x(dpre_dev, inv, w.to(BF).to(DEV), vsrc, elu_y=y_dev)
+    assert err_rel_max(dx.float(), dx_ref) <= 1e-2
+    dw = torch.empty(cout, 9 * cin, device=DEV)
+    db = torch.empty(cout, device=DEV)
+    ws = torch.empty(ops.spiral_conv_bwd_weight_x_workspace(bsz, rows, 9, cin, cout) // 4 + 1, device=DEV)
+    ops.spiral_conv_bwd_weight_x(y_dev, idx, dpre_dev, dw, db, ws)
+    assert err_rel_max(dw, wl.grad) <= 1e-4
+    assert err_rel_max(db, bl.grad) <= 1e-4
+    # deferred slabs through the batched reduce: identical
+    ws.zero_()
+    d = ops.spiral_conv_bwd_weight_x(y_dev, idx, dpre_dev, None, None, ws)
+    dw2, db2 = torch.empty_like(dw), torch.empty_like(db)
+    ops.dw_reduce_batch([(d, dw2, db2)])
+    assert torch.equal(dw2, dw) and torch.equal(db2, db)
+
+
+@pytest.mark.parametrize("level,kind,x_bf16,y_bf16", [(0, "up", True, True), (1, "up", False, True),
+                                                       (0, "upT", True, True), (1, "upT", True, False),
+                                                       (2, "down", True, True)])
+@pytest.mark.parametrize("with_elu", [False, True])
+def test_spmm_bf16_bit_exact(mods, otopo, dtopo, level, kind, x_bf16, y_bf16, with_elu):
+    _, ops, _ = mods
+    g = torch.Generator().manual_seed(level * 3 + len(kind))
+    coo = otopo.up[level] if kind != "down" else otopo.down[level]
+    m, n = coo[3]
+    if kind == "upT":
+        row, col, val, _ = coo
+        coo, (m, n) = (col, row, val, (n, m)), (n, m)
+        csr = dtopo.upT_csr[level]
+    else:
+        csr = dtopo.up_csr[level] if kind == "up" else dtopo.down_csr[level]
+    x = torch.randn(4, n, 32, generator=g)
+    if x_bf16:
+        x = x.to(BF).float()
+    ref = O.pool(x, coo)
+    ey = torch.nn.functional.elu(torch.randn(4, m, 32, generator=g))
+    if with_elu:
+        eyq = ey.to(BF).float() if y_bf16 else ey
+        ref = ref * torch.where(eyq > 0, torch.ones_like(eyq), eyq + 1.0)
+    out = torch.empty(4, m, 32, dtype=BF if y_bf16 else torch.float32, device=DEV)
+    xd = (x.to(BF) if x_bf16 else x).to(DEV)
+    eyd = (ey.to(BF) if y_bf16 else ey).to(DEV) if with_elu else None
+    ops.spmm_x(csr, xd, m, elu_y=eyd, out=out)
+    exp = ref.to(BF) if y_bf16 else ref
+    assert torch.equal(out.cpu(), exp)
+
+
+@pytest.mark.parametrize("bsz", [2, 16])
+def test_xyz_layers_bf16(mods, otopo, dtopo, bsz):
+    """The xyz layers of the bf16 step: input conv (fp32 x -> bf16 y) and
+    its dW with bf16 dpre; output conv (bf16 x -> fp32 y) and its fused
+    dx (bf16) + dW."""
+    _, ops, _ = mods
+    g = torch.Generator().manual_seed(bsz)
+    sp0 = otopo.spirals[0]
+    sel = np.asarray(otopo.down[0][1])[np.argsort(otopo.down[0][0])]
+    x = torch.randn(bsz, sp0.shape[0], 3, generator=g)
+    w0 = torch.randn(32, 27, generator=g) * 0.1
+    b0 = torch.randn(32, generator=g) * 0.1
+    ref = torch.nn.functional.elu(gather(x.double(), sp0[sel]) @ w0.double().T + b0.double())
+    y = torch.empty(bsz, len(sel), 32, dtype=BF, device=DEV)
+    ops.spiral_conv_fwd_x(x.to(DEV), dtopo.enc_rows[0], w0.to(DEV), None, b0.to(DEV), 1, y)
+    assert err_rel_max(y.float(), ref) <= 2.0 ** -8
+    dpre = torch.randn(bsz, len(sel), 32, generator=g)
+    dw, db = torch.empty(32, 27, device=DEV), torch.empty(32, device=DEV)
+    ws = torch.empty(ops.spiral_conv_bwd_weight_x_workspace(bsz, len(sel), 9, 3, 32) // 4 + 1, device=DEV)
+    ops.spiral_conv_bwd_weight_x(x.to(DEV), dtopo.enc_rows[0], dpre.to(BF).to(DEV), dw, db, ws)
+    gx = gather(x.double(), sp0[sel])
+    assert err_rel_max(dw, torch.einsum("bro,brk->ok", rb(dpre), gx)) <= 1e-5
+    assert err_rel_max(db, rb(dpre).sum((0, 1))) <= 1e-5
+    # output conv
+    h = torch.nn.functional.elu(torch.randn(bsz, sp0.shape[0], 32, generator=g))
+    w5 = torch.randn(3, 288, generator=g) * 0.1
+    b5 = torch.randn(3, generator=g) * 0.1
+    out = torch.empty(bsz, sp0.shape[0], 3, device=DEV)
+    hd = h.to(BF).to(DEV)
+    ops.spiral_conv_fwd_x(hd, dtopo.spiral[0], w5.to(DEV), None, b5.to(DEV), 0, out)
+    hl = rb(h).requires_grad_()
+    wl = w5.double().requires_grad_()
+    bl = b5.double().requires_grad_()
+    ref = gather(hl, sp0) @ wl.T + bl
+    assert err_rel_max(out, ref) <= 1e-5
+    dout = torch.randn(ref.shape, generator=g)
+    ref.backward(dout.double())
+    dx_ref = hl.grad * torch.where(rb(h) > 0, 1.0, rb(h) + 1.0)
+    dx = torch.empty(bsz, sp0.shape[0], 32, dtype=BF, device=DEV)
+    dw, db = torch.empty(3, 288, device=DEV), torch.empty(3, device=DEV)
+    ops.spiral_conv_bwd_x(hd, dtopo.spiral[0], dout.to(DEV), dtopo.spiral_inv[0], w5.to(DEV), dw, db,
+                          dx=dx, elu_y=hd)
+    assert err_rel_max(dx.float(), dx_ref) <= 2.0 ** -8
+    assert err_rel_max(dw, wl.grad) <= 1e-5
+    assert err_rel_max(db, bl.grad) <= 1e-5
+
+
+def test_adam_writes_bf16_shadow(mods):
+    _, ops, _ = mods
+    n = 1000003
+    g = torch.Generator().manual_seed(1)
+    p, gr = torch.randn(n, generator=g).to(DEV), torch.randn(n, generator=g).to(DEV)
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    step = torch.ones(1, dtype=torch.int32, device=DEV)
+    sh = torch.empty(n, dtype=BF, device=DEV)
+    ops.adam(p, gr, m, v, step, 1e-3, shadow=sh)
+    assert torch.equal(sh, p.to(BF))
+    back = torch.empty(n, device=DEV)
+    ops.cast(sh, back)
+    assert torch.equal(back, sh.float())
+
+
+# bf16 step vs the fp32 reference goldens (tests/golden/golden_train.npz).
+# Bars (bf16 storage of the level-0/1 tensors, fp32 everywhere else): losses
+# rel 2e-2, reconstruction per-vertex L1 <= 2e-2 (normalised units), every
+# gradient cosine >= 0.99 against the reference's fp32 gradient.
+def test_bf16_train_three_steps_vs_fp32_golden(mods, otopo, dtopo):
+    E, ops, _ = mods
+    g = np.load(f"{recipe.HERE}/golden_train.npz")
+    w = recipe.golden_weights()
+    eng = E.SDVAEEngine(dtopo, E.ModelSpec(), device=DEV, precision="bf16")
+    eng.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
+    P = O.make_params(w)
+    opt = O.Adam(P)
+    meshes = recipe.normalized_meshes(12)
+    data = torch.from_numpy(meshes).to(DEV)
+    report = []
+    for step in range(3):
+        key = recipe.train_key_index(step)
+        eps = torch.from_numpy(recipe.train_eps(step))
+        out, grads, _ = O.train_step(P, opt, meshes[4 * step:4 * step + 4], otopo, key, eps.numpy())
+        b = eng.inject(eng.buffers(16), key, eps)
+        b.batch_idx.copy_(torch.arange(4 * step, 4 * step + 4, dtype=torch.int32))
+        ops.swap_features(data, b.batch_idx, dtopo.region_mask, b.key, 4, out=b.x)
+        eng.train_step_on(b)
+        torch.cuda.synchronize()
+        got = b.losses.cpu().numpy()
+        rel = np.abs(got - g[f"s{step}_losses"]) / np.abs(g[f"s{step}_losses"])
+        l1 = np.abs(b.out.cpu().numpy() - out["out"].detach().numpy()).sum(-1).max()
+        cos = {}
+        for name, gd in eng.grads().items():
+            a, r = gd.detach().cpu().double().ravel(), grads[name].double().ravel()
+            cos[name] = float(a @ r / (a.norm() * r.norm() + 1e-30))
+        report.append((step, rel.max(), l1, min(cos.values())))
+        assert rel.max() <= 2e-2, f"step {step} loss rel {rel}"
+        assert l1 <= 2e-2, f"step {step} per-vertex L1 {l1}"
+        assert min(cos.values()) >= 0.99, f"step {step} grad cosine {sorted(cos.items(), key=lambda kv: kv[1])[:3]}"
+    print("bf16 vs fp32 golden (step, loss rel, max per-vertex L1, min grad cosine):", report)
+
+
+def test_bf16_graph_step_runs(mods, dtopo):
+    """The resident bf16 step captures into a hipGraph and replays with
+    identical results to eager launches."""
+    E, _, _ = mods
+    w = recipe.golden_weights()
+    res = []
+    for use_graph in (False, True):
+        data = E.ResidentData(torch.from_numpy(recipe.normalized_meshes(12)).to(DEV), bs=4, shuffle=True)
+        eng = E.SDVAEEngine(dtopo, E.ModelSpec(), device=DEV, precision="bf16")
+        eng.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
+        b = eng.buffers(16)
+        step = lambda: eng.resident_step(b, data)  # noqa: E731
+        if use_graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                step()
+            torch.cuda.current_stream().wait_stream(s)
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                step()
+            for _ in range(3):
+                gr.replay()
+        else:
+            for _ in range(4):
+                step()
+        torch.cuda.synchronize()
+        res.append((eng.params.data.cpu().clone(), b.losses.cpu().clone(), eng.params.shadow.cpu().clone()))
+        assert torch.isfinite(res[-1][1]).all()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert torch.equal(res[0][2], res[1][2])

@@ -1,0 +1,241 @@
+"""Data side of the training path: the reference's dataset / loader / feature
+swap (``data_loading.py:23-283``, ``swap_batch_transform.py:7-52``) with the
+swap on the GPU.
+
+Two ways in:
+
+* drop-in objects with the reference's interface -- :class:`Data` (the
+  attribute bag ``torch_geometric.data.Data`` is used as),
+  :class:`SwapFeatures` ``(template)(batched_data)`` and
+  :class:`MeshCollater` -- for a host DataLoader: the collated batch is moved
+  to the device once and swapped there by ``cfsd_swap_features``, and the
+  label fields (y / augmented / age / gender / swapped) are built exactly as
+  the reference builds them;
+* the resident path the training driver uses: :func:`load_mesh_dataset` reads
+  the mesh files once, splits and normalises them as the reference does, and
+  returns :class:`engine.ResidentData` sets (whole set in HBM, device-drawn
+  epoch shuffle, swap fused into the step).
+"""
+import json
+import os
+import random
+
+import numpy as np
+import torch
+from torch.utils.data.dataloader import default_collate
+
+from . import ops
+from .engine import ResidentData
+
+
+class Data:
+    """Attribute bag standing in for ``torch_geometric.data.Data`` (the
+    reference stores x / y / augmented / age / gender / swapped on it)."""
+
+    def __init__(self, **kwargs):
+        for k, v in kwargs.items():
+            setattr(self, k, v)
+
+    @property
+    def keys(self):
+        return [k for k in vars(self)]
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+    def __setitem__(self, k, v):
+        setattr(self, k, v)
+
+    def to(self, device):
+        for k in self.keys:
+            v = getattr(self, k)
+            if torch.is_tensor(v):
+                setattr(self, k, v.to(device))
+        return self
+
+
+def _region_mask(feat_and_cont, nv, device):
+    keys = list(feat_and_cont.keys())
+    mask = np.zeros((len(keys), nv), np.uint8)
+    for i, k in enumerate(keys):
+        mask[i, np.asarray(feat_and_cont[k]["feature"], np.int64)] = 1
+    return torch.from_numpy(mask).to(device)
+
+
+class SwapFeatures:
+    """``SwapFeatures`` (swap_batch_transform.py:7-42): ``bs`` meshes ->
+    ``bs**2``; output ``i*bs + j`` is mesh ``i`` with the feature vertices of
+    one random region (``random.choice`` over the template's regions, as the
+    reference) taken from mesh ``j``.  ``batched_data.x`` must be a device
+    tensor (the swap runs on the GPU, bit-exact); labels as the reference:
+    diagonal entries keep the originals, off-diagonal ones get y None,
+    augmented 1, age -1, gender 'n/a'; ``swapped`` = the region key."""
+
+    def __init__(self, template):
+        self._template = template
+        self._features_and_contours = template.feat_and_cont
+        self._zones_keys = list(template.feat_and_cont.keys())
+        self._masks = {}
+
+    def __call__(self, batched_data, key=None):
+        x = batched_data.x
+        if not x.is_cuda:
+            raise RuntimeError("SwapFeatures runs on the GPU: move the collated batch to the device first")
+        bs = x.shape[0]
+        nv = x.shape[1]
+        dev = x.device
+        if dev not in self._masks:
+            self._masks[dev] = _region_mask(self._features_and_contours, nv, dev)
+        key = random.choice(self._zones_keys) if key is None else key
+        kidx = torch.tensor([self._zones_keys.index(key)], dtype=torch.int32, device=dev)
+        new_batch = ops.swap_features(x.contiguous().float(), torch.arange(bs, dtype=torch.int32, device=dev),
+                                      self._masks[dev], kidx, bs)
+        aug = batched_data.augmented
+        age = batched_data.age
+        aug_t = torch.as_tensor(aug)
+        age_t = torch.as_tensor(age)
+        new_y = [None] * (bs ** 2)
+        new_aug = torch.ones([bs ** 2, 1], device=aug_t.device, dtype=aug_t.dtype)
+        new_gender = ["n/a"] * (bs ** 2)
+        new_age = -torch.ones([bs ** 2, 1], device=age_t.device, dtype=age_t.dtype)
+        for i in range(bs):
+            d = i * bs + i
+            new_y[d] = batched_data.y[i]
+            new_aug[d] = aug_t[i]
+            new_gender[d] = batched_data.gender[i]
+            new_age[d] = age_t[i]
+        return Data(x=new_batch, y=new_y, swapped=key, augmented=new_aug, age=new_age, gender=new_gender)
+
+
+class MeshCollater:
+    """``MeshCollater`` (data_loading.py:62-83): default-collate every field
+    of a list of :class:`Data`, move the batch to ``device`` and swap there.
+    Use it with ``num_workers=0`` (the swap needs the GPU; the reference
+    swapped on CPU in 8 worker processes)."""
+
+    def __init__(self, feature_swapper=None, device="cuda"):
+        self._swapper = feature_swapper
+        self._device = torch.device(device)
+
+    def __call__(self, data_list):
+        return self.collate(data_list)
+
+    def collate(self, data_list):
+        if not isinstance(data_list[0], Data):
+            raise TypeError(f"DataLoader found invalid type: {type(data_list[0])}. "
+                            f"Expected craniofacialsd_vae_amd.data.Data instead")
+        keys = list(set.union(*[set(d.keys) for d in data_list]))
+        batched = Data()
+        for key in keys:
+            batched[key] = default_collate([d[key] for d in data_list])
+        batched.x = batched.x.to(self._device)
+        if self._swapper is not None:
+            batched = self._swapper(batched)
+        return batched
+
+
+# ------------------------------------------------------------------ dataset files
+def read_obj_vertices(path):
+    """Vertices of an OBJ file in file order (trimesh ``process=False``)."""
+    vs = []
+    with open(path) as f:
+        for ln in f:
+            if ln.startswith("v "):
+                vs.append([float(t) for t in ln.split()[1:4]])
+    return np.asarray(vs, np.float64)
+
+
+def load_mesh(path):
+    """``MeshInMemoryDataset.load_mesh`` (data_loading.py:220-229): vertices
+    as float32."""
+    if path.endswith(".ply"):
+        from .precompute import read_ply
+        return torch.tensor(read_ply(path)[0], dtype=torch.float)
+    return torch.tensor(read_obj_vertices(path), dtype=torch.float)
+
+
+def find_filenames(root):
+    """``find_filenames(find_augmented=False)`` without a dataset summary
+    (data_loading.py:166-178): every .ply / .obj outside 'aug' folders."""
+    files = []
+    for dirpath, _, fnames in os.walk(root):
+        for f in fnames:
+            if (f.endswith(".ply") or f.endswith(".obj")) and "aug" not in dirpath:
+                files.append(f)
+    return files
+
+
+def split_data(root, split_path, stratified=False):
+    """``MeshInMemoryDataset.split_data`` (data_loading.py:180-218): reuse
+    ``data_split.json`` when present, else sort the file names and split
+    (stratified 80/10/10 by class letter with sklearn, or the reference's
+    ``i % 100`` rule: <= 5 test, <= 10 validation, else train) and write it."""
+    try:
+        with open(split_path) as fp:
+            d = json.load(fp)
+        return d["train"], d["test"], d["val"]
+    except FileNotFoundError:
+        pass
+    names = sorted(find_filenames(root))
+    if stratified:
+        from sklearn.model_selection import train_test_split
+        y = [n[0] for n in names]
+        train, test, _, test_y = train_test_split(names, y, stratify=y, test_size=0.2)
+        test, val, _, _ = train_test_split(test, test_y, stratify=test_y, test_size=0.5)
+    else:
+        train, test, val = [], [], []
+        for i, f in enumerate(names):
+            (test if i % 100 <= 5 else val if i % 100 <= 10 else train).append(f)
+    with open(split_path, "w") as fp:
+        json.dump({"train": train, "test": test, "val": val}, fp)
+    return train, test, val
+
+
+def labels_of(name):
+    """Class label from the file name (data_loading.py:265-266): first letter
+    ('b' paediatric folded into 'n'); 'aug' in the path marks augmentation."""
+    base = name.split("/")[1] if "/" in name else name
+    y = base[0]
+    return ("n" if y == "b" else y), ("aug" in name)
+
+
+def compute_mean_and_std(root, train_names, norm_path):
+    """``compute_mean_and_std`` (data_loading.py:231-252): load ``norm.pt``
+    (weights_only) or compute the per-vertex mean / std (torch, CPU) of the
+    training meshes and save it."""
+    try:
+        return torch.load(norm_path, weights_only=True)
+    except FileNotFoundError:
+        verts = torch.stack([load_mesh(os.path.join(root, n)) for n in train_names])
+        mean = torch.mean(verts, dim=0)
+        std = torch.std(verts, dim=0)
+        std = torch.where(std > 0, std, torch.tensor(1e-8))
+        norm = {"mean": mean, "std": std}
+        torch.save(norm, norm_path)
+        return norm
+
+
+def load_mesh_dataset(data_config, batch_size, device="cuda"):
+    """``get_data_loaders`` (data_loading.py:23-51) for the resident path:
+    train / validation / test :class:`engine.ResidentData` sets (meshes
+    normalised on the device with norm.pt, data_loading.py:259-260; train and
+    validation shuffled every epoch with drop_last, test in file order) plus
+    the normalisation dict and the per-set file names and labels."""
+    root = data_config["dataset_path"]
+    pre = data_config["precomputed_path"]
+    os.makedirs(pre, exist_ok=True)
+    train, test, val = split_data(root, os.path.join(pre, "data_split.json"),
+                                  data_config.get("stratified_split", False))
+    norm = compute_mean_and_std(root, train, os.path.join(pre, "norm.pt"))
+    sets = {}
+    for kind, names, shuffle in (("train", train, True), ("val", val, True), ("test", test, False)):
+        if len(names) < batch_size:
+            sets[kind] = None
+            continue
+        meshes = torch.stack([load_mesh(os.path.join(root, n)) for n in names]).to(device)
+        rd = ResidentData(meshes, bs=batch_size, shuffle=shuffle,
+                          norm=norm if data_config.get("normalize_data", True) else None)
+        rd.names = list(names)
+        rd.labels = [labels_of(n) for n in names]
+        sets[kind] = rd
+    return sets["train"], sets["val"], sets["test"], norm

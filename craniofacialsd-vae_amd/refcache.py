@@ -1,6 +1,6 @@
-"""Execution-free reader for the reference's ``spirals.pkl`` / ``transforms.pkl``.
-
-TEST INFRASTRUCTURE ONLY (runs in the build container, never on the GPU box).
+"""Execution-free reader for the reference's precomputed cache
+(``spirals.pkl`` / ``transforms.pkl`` / ``norm.pt``), so a reference
+``precomputed_path`` drops in unchanged under ``manager.ModelManager``.
 
 The reference caches its geometry precompute with plain ``pickle.dump``
 (``model_manager.py:203-205, 227-228``).  Those files are untrusted data, so we
@@ -168,3 +168,30 @@ def load(path):
         else:
             raise ValueError(f"unsupported pickle opcode {n}")
     raise ValueError("no STOP opcode")
+
+
+def load_precomputed(path):
+    """The reference's ``precomputed_path`` (model_manager.py:176-230) as a
+    dict in the ``topology_craniofacial.npz`` layout (spirals, down/up COO in
+    file order, low-resolution faces/positions), read without executing
+    anything from the files.  The template itself (regions, Laplacian) is
+    added by the caller."""
+    import os
+
+    import numpy as np
+    spirals = load(os.path.join(path, "spirals.pkl"))
+    low, down, up = load(os.path.join(path, "transforms.pkl"))
+    if not (len(spirals) == len(down) == len(up) == len(low)):
+        raise ValueError(f"{path}: spirals / transforms level counts differ")
+    out = {"n_levels": np.int32(len(spirals))}
+    for l in range(len(spirals)):
+        out[f"spiral_{l}"] = spirals[l].numpy().astype(np.int32)
+        for name, tr in (("down", down[l]), ("up", up[l])):
+            idx = tr["indices"].numpy()
+            out[f"{name}_{l}_row"] = idx[0].astype(np.int32)
+            out[f"{name}_{l}_col"] = idx[1].astype(np.int32)
+            out[f"{name}_{l}_val"] = tr["values"].numpy().astype(np.float32)
+            out[f"{name}_{l}_shape"] = np.asarray(tr["size"], np.int64)
+        out[f"pos_{l + 1}"] = low[l]["pos"].numpy().astype(np.float32)
+        out[f"face_{l + 1}"] = low[l]["face"].numpy().T.astype(np.int32)
+    return out

@@ -235,11 +235,12 @@ def latent_regions(n_regions, latent=75):
     return [(i * rs, (i + 1) * rs) for i in range(n_regions)]
 
 
-def losses(P, x16, topo, key_index, eps, bs=4, w=LOSS_W, is_vae=True):
+def losses(P, x16, topo, key_index, eps, bs=4, w=LOSS_W, is_vae=True, train=True):
     """Forward + the four losses of ``_do_iteration``
     (``model_manager.py:281-312``); KL only when ``w_kl > 0`` (``:285-288``),
-    latent consistency only with swapped batches (``:290-293``)."""
-    rec, z, mu, lv = forward(P, x16, topo, eps=eps, train=True, is_vae=is_vae)
+    latent consistency only with swapped batches (``:290-293``).
+    ``train=False``: the validation pass (eval mode, z = mu)."""
+    rec, z, mu, lv = forward(P, x16, topo, eps=eps, train=train, is_vae=is_vae)
     l_rec = mse_loss(rec, x16)
     l_lap = laplacian_loss(rec, topo.lap)
     l_kl = kl_loss(mu, lv) if w["kl"] > 0 else torch.tensor(0.0)

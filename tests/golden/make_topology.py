@@ -39,8 +39,11 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, HERE)
-import safe_unpickle  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+import cfsd_loader  # noqa: E402
+
+cfsd_loader.load()
+from craniofacialsd_vae_amd import refcache as safe_unpickle  # noqa: E402
 
 REF = os.environ.get("CFSD_REFERENCE", "/root/reference")
 DEMO = os.path.join(REF, "demo_files")

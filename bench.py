@@ -313,7 +313,8 @@ def kernel_probe(runner, n_iter=20):
         timed("conv_dw_D3", lambda: ops.spiral_conv_bwd_weight(b.dec_up[i3], T.spiral[0], b.dpre_dec[i3],
                                                                None, None, b.ws_dw[("dec", i3)]))
     g = torch.empty(16, T.n_verts[0], 9 * 32, device=b.x.device)
-    timed("spiral_gather_L0", lambda: ops.spiral_gather(b.dec_up[i3], T.spiral[0], out=g))
+    xg = b.dec_up[i3] if b.dec_up[i3].dtype == torch.float32 else b.dec_up[i3].float()
+    timed("spiral_gather_L0", lambda: ops.spiral_gather(xg, T.spiral[0], out=g))
     del g
     return res
 
@@ -381,11 +382,31 @@ def cpu_model():
     return "unknown"
 
 
+def usable_cpus():
+    """CPUs this process may actually use: the cgroup CPU quota (cpu.max)
+    when one is set, else the scheduler affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, min(aff, int(float(quota) / float(period))))
+    except (OSError, ValueError):
+        pass
+    return aff
+
+
 def cpu_baseline(budget_s):
     """Oracle (PyTorch-CPU restatement of the reference step, the same ATen
-    ops) on the host: with every host CPU (os.cpu_count() threads), with the
-    CPUs this process may run on (sched affinity) when that differs, and with
-    one thread.  ``value`` = the fastest multi-thread run."""
+    ops) on the host: with the CPUs this process may use (cgroup quota /
+    affinity; also OMP_NUM_THREADS when set) and with one thread; ``value`` =
+    the fastest.  With os.cpu_count() threads on a quota-limited box the run
+    is oversubscribed (measured on the 256-CPU GPU host with a 16-CPU share:
+    0.56 meshes/s, 28.5 s for ONE step, profiles/r02e_bench.json), so that
+    configuration is reported, not re-run by default."""
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     from oracle import cfsd_oracle as O
     import recipe
@@ -396,12 +417,14 @@ def cpu_baseline(budget_s):
     x4 = rs.randn(4, T.n_verts[0], 3).astype(np.float32)
     eps = rs.randn(16, 75).astype(np.float32)
     host = os.cpu_count() or 1
-    try:
-        aff = len(os.sched_getaffinity(0))
-    except AttributeError:
-        aff = host
-    multi = sorted({host, aff}, reverse=True)
-    plan = [(t, budget_s * 0.6 / len(multi)) for t in multi] + [(1, budget_s * 0.4)]
+    usable = usable_cpus()
+    cand = {usable}
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        cand.add(min(int(os.environ["OMP_NUM_THREADS"]), host))
+    if os.environ.get("CFSD_CPU_ALL_THREADS"):
+        cand.add(host)
+    multi = sorted(cand, reverse=True)
+    plan = [(t, budget_s * 0.65 / len(multi)) for t in multi] + [(1, budget_s * 0.35)]
     runs = []
     for threads, budget in plan:
         torch.set_num_threads(threads)
@@ -414,11 +437,11 @@ def cpu_baseline(budget_s):
             if el >= budget or n >= 200:
                 break
         runs.append({"threads": threads, "steps": n, "seconds": el, "meshes_per_s": 16 * n / el})
-    best = max(runs[:-1], key=lambda r: r["meshes_per_s"])
+    best = max(runs, key=lambda r: r["meshes_per_s"])
     return {"value": best["meshes_per_s"], "unit": "meshes/s", "cores": best["threads"], "kind": "port",
             "sample": f"{best['steps']} full train steps (16 swapped meshes each, fp32, "
                       f"oracle/cfsd_oracle.py torch-CPU restatement) in {best['seconds']:.1f} s",
-            "one_thread": runs[-1]["meshes_per_s"], "host_cpus": host, "affinity_cpus": aff,
+            "one_thread": runs[-1]["meshes_per_s"], "host_cpus": host, "usable_cpus": usable,
             "cpu_model": cpu_model(), "runs": runs}
 
 

@@ -103,15 +103,32 @@ def param_names(n_enc=4):
     return names
 
 
-def encode(P, x, topo, is_vae=True):
+def _q(t):
+    """bf16 storage of a tensor (round to nearest even), widened back."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+def _w(P, name, low):
+    """A conv weight as the bf16 path reads it: the bf16 shadow when the layer
+    runs on bf16 MFMA (``low``), else the fp32 master."""
+    return _q(P[name]) if low else P[name]
+
+
+def encode(P, x, topo, is_vae=True, lp=()):
     """``Model.encode`` (``model.py:146-160``): 4x (conv -> ELU -> Pool down),
-    vertex-major flatten, Linear mu = en_layers[-1], logvar = en_layers[-2]."""
+    vertex-major flatten, Linear mu = en_layers[-1], logvar = en_layers[-2].
+    ``lp``: levels stored in bf16 (emulates the engine's bf16 precision: those
+    activations rounded to bf16, 32/64-channel convs reading them use bf16
+    weights); empty = the reference's fp32."""
     n = topo.n_levels
     h = x
     for i in range(n):
-        h = elu(spiral_conv(h, topo.spirals[i], P[f"en_layers.{i}.conv.layer.weight"],
-                            P[f"en_layers.{i}.conv.layer.bias"]))
+        wname = f"en_layers.{i}.conv.layer.weight"
+        low = i in lp and h.shape[-1] >= 16
+        h = elu(spiral_conv(h, topo.spirals[i], _w(P, wname, low), P[f"en_layers.{i}.conv.layer.bias"]))
         h = pool(h, topo.down[i])
+        if (i + 1) in lp and i + 1 < n:
+            h = _q(h)
     last = n + 1 if is_vae else n
     flat = h.reshape(-1, P[f"en_layers.{last}.weight"].shape[1])
     mu = F.linear(flat, P[f"en_layers.{last}.weight"], P[f"en_layers.{last}.bias"])
@@ -119,32 +136,38 @@ def encode(P, x, topo, is_vae=True):
     return mu, logvar
 
 
-def decode(P, z, topo, c_last=None):
+def decode(P, z, topo, c_last=None, lp=()):
     """``Model.decode`` (``model.py:162-173``): Linear -> view [B, V4, C];
-    4x (Pool up -> conv -> ELU); final SpiralConv without activation."""
+    4x (Pool up -> conv -> ELU); final SpiralConv without activation.
+    ``lp`` as in :func:`encode`."""
     n = topo.n_levels
     if c_last is None:
         c_last = P["de_layers.0.weight"].shape[0] // topo.n_verts[-1]
     h = F.linear(z, P["de_layers.0.weight"], P["de_layers.0.bias"])
     h = h.view(-1, topo.n_verts[-1], c_last)
     for i in range(1, n + 1):
-        h = pool(h, topo.up[n - i])
-        h = elu(spiral_conv(h, topo.spirals[n - i], P[f"de_layers.{i}.conv.layer.weight"],
+        lv = n - i
+        h = pool(h, topo.up[lv])
+        if lv in lp:
+            h = _q(h)
+        h = elu(spiral_conv(h, topo.spirals[lv], _w(P, f"de_layers.{i}.conv.layer.weight", lv in lp),
                             P[f"de_layers.{i}.conv.layer.bias"]))
+        if lv in lp:
+            h = _q(h)
     return spiral_conv(h, topo.spirals[0], P[f"de_layers.{n + 1}.layer.weight"],
                        P[f"de_layers.{n + 1}.layer.bias"])
 
 
-def forward(P, x, topo, eps=None, train=True, is_vae=True):
+def forward(P, x, topo, eps=None, train=True, is_vae=True, lp=()):
     """``Model.forward`` + ``_reparameterize`` (``model.py:175-188``), with
     the noise ``eps`` injected instead of ``torch.randn_like``.  AE
     (``is_vae=False``, kl_weight 0 at ``model_manager.py:67``): z = mu."""
-    mu, logvar = encode(P, x, topo, is_vae)
+    mu, logvar = encode(P, x, topo, is_vae, lp)
     if train and is_vae:
         z = mu + eps * torch.exp(0.5 * logvar)
     else:
         z = mu
-    return decode(P, z, topo), z, mu, logvar
+    return decode(P, z, topo, lp=lp), z, mu, logvar
 
 
 # ---------------------------------------------------------------- losses
@@ -235,12 +258,13 @@ def latent_regions(n_regions, latent=75):
     return [(i * rs, (i + 1) * rs) for i in range(n_regions)]
 
 
-def losses(P, x16, topo, key_index, eps, bs=4, w=LOSS_W, is_vae=True, train=True):
+def losses(P, x16, topo, key_index, eps, bs=4, w=LOSS_W, is_vae=True, train=True, lp=()):
     """Forward + the four losses of ``_do_iteration``
     (``model_manager.py:281-312``); KL only when ``w_kl > 0`` (``:285-288``),
     latent consistency only with swapped batches (``:290-293``).
-    ``train=False``: the validation pass (eval mode, z = mu)."""
-    rec, z, mu, lv = forward(P, x16, topo, eps=eps, train=train, is_vae=is_vae)
+    ``train=False``: the validation pass (eval mode, z = mu); ``lp``: bf16
+    storage emulation (see :func:`encode`)."""
+    rec, z, mu, lv = forward(P, x16, topo, eps=eps, train=train, is_vae=is_vae, lp=lp)
     l_rec = mse_loss(rec, x16)
     l_lap = laplacian_loss(rec, topo.lap)
     l_kl = kl_loss(mu, lv) if w["kl"] > 0 else torch.tensor(0.0)

@@ -127,6 +127,24 @@ __global__ __launch_bounds__(256) void cast_k(const TS* __restrict__ src, TD* __
   }
 }
 
+// Spectral blend of the augmentation (utils.py:244-267): coefficients
+// s4[p, j, :] = s1 + v[p, j] * (s2 - s1) for j < n_blend, else s1 (the
+// reference's s3/s4 assembly; spectral_combination is the 0/1 special case of
+// v).  s1, s2, s4 [pairs, k, c]; v [pairs, k].  Same operation order as numpy.
+__global__ __launch_bounds__(256) void spectral_blend_k(const float* __restrict__ s1,
+                                                        const float* __restrict__ s2,
+                                                        const float* __restrict__ v,
+                                                        float* __restrict__ s4, int k, int c,
+                                                        int n_blend, long total) {
+#pragma clang fp contract(off)
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const long pj = t / c;
+  const int j = (int)(pj % k);
+  const float a = s1[t];
+  s4[t] = j < n_blend ? a + v[pj] * (s2[t] - a) : a;
+}
+
 // Dataset normalisation (data_loading.py:259-260, (verts - mean) / std with
 // per-vertex [nv, c] statistics): subtraction then IEEE division, the two
 // roundings of the reference's torch ops, so the result is bit-exact.
@@ -288,6 +306,16 @@ extern "C" int cfsd_swap_features(const float* x, const int32_t* batch_idx,
                      (hipStream_t)stream, x, batch_idx, region_mask, key, out, bs, nv, c, n_meshes,
                      n_regions, total);
   return launch_status("swap_features");
+}
+
+extern "C" int cfsd_spectral_blend(const float* s1, const float* s2, const float* values, float* s4,
+                                   int pairs, int k, int c, int n_blend, void* stream) {
+  if (!s1 || !s2 || !values || !s4) return set_error(CFSD_EINVAL, "spectral_blend: null pointer");
+  if (pairs <= 0 || k <= 0 || c <= 0 || n_blend < 0) return set_error(CFSD_EINVAL, "spectral_blend: bad sizes");
+  const long total = (long)pairs * k * c;
+  hipLaunchKernelGGL(spectral_blend_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, s1, s2, values, s4, k, c, n_blend, total);
+  return launch_status("spectral_blend");
 }
 
 extern "C" int cfsd_normalize(const float* x, const float* mean, const float* std, float* out,

@@ -239,6 +239,20 @@ def swap_features(x_all, batch_idx, region_mask, key, bs, out=None):
     return y
 
 
+def spectral_blend(s1, s2, values, n_blend, out=None):
+    """Augmentation coefficients s1 + v * (s2 - s1) on the first ``n_blend``
+    spectral components (utils.py:256-267); s1/s2 [pairs, k, c], values [pairs, k]."""
+    _need(s1, None, name="s1")
+    if s1.dim() != 3:
+        raise ValueError(f"s1: shape {tuple(s1.shape)}, expected [pairs, k, c]")
+    p, k, c = s1.shape
+    _need(s2, (p, k, c), name="s2")
+    _need(values, (p, k), name="values")
+    y = _out(out, (p, k, c), s1)
+    call("cfsd_spectral_blend", ptr(s1), ptr(s2), ptr(values), ptr(y), p, k, c, int(n_blend), stream_ptr())
+    return y
+
+
 def normalize(x, mean, std, out=None):
     """``(x - mean) / std`` per vertex (data_loading.py:259-260), bit-exact."""
     _need(x, None, name="x")

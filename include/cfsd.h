@@ -155,6 +155,14 @@ int cfsd_swap_features(const float* x, const int32_t* batch_idx, const uint8_t* 
                        const int32_t* key, float* out, int bs, int nv, int c, int n_meshes,
                        int n_regions, void* stream);
 
+/* Spectral augmentation blend (utils.py:244-267, data_loading.py:359-364):
+ * with s1 = U^T x1, s2 = U^T x2 [pairs, k, c] (U: the k smallest Laplacian
+ * eigenvectors), s4[p,j,:] = s1 + values[p,j]*(s2 - s1) for j < n_blend, else
+ * s1; the augmented mesh is then U s4.  values [pairs, k] (spectral_interpolation:
+ * N(0.5, 0.5) draws; spectral_combination: 0/1 selector). */
+int cfsd_spectral_blend(const float* s1, const float* s2, const float* values, float* s4, int pairs,
+                        int k, int c, int n_blend, void* stream);
+
 /* Dataset normalisation, (x - mean) / std with per-vertex statistics
  * (data_loading.py:259-260; mean/std [nv, c] from norm.pt): x, out
  * [n_meshes, nv, c] (may alias).  Same two IEEE roundings as torch: bit-exact. */

@@ -373,3 +373,16 @@ def epoch_batches(seed, epoch, n_items, bs, perm=None):
 def normalize(x, mean, std):
     """data_loading.py:259-260: (verts - mean) / std (torch fp32 ops)."""
     return (torch.as_tensor(x) - torch.as_tensor(mean)) / torch.as_tensor(std)
+
+
+# --------------------------------------------------------------- augmentation
+def spectral_interpolation(u, x1, x2, values, interp_until=30):
+    """``spectral_interpolation`` (utils.py:256-267) in float64 NumPy with the
+    random ``values`` [k] injected (the reference draws N(0.5, 0.5))."""
+    u = np.asarray(u, np.float64)
+    s1 = u.T @ np.asarray(x1, np.float64)
+    s2 = u.T @ np.asarray(x2, np.float64)
+    s3 = s1 + np.asarray(values, np.float64).reshape(-1, 1) * (s2 - s1)
+    s4 = s1.copy()
+    s4[:interp_until] = s3[:interp_until]
+    return u @ s4

@@ -996,19 +996,23 @@ __device__ __forceinline__ void conv_dw_lat_body(int vb, int vnb, const float* _
   const bool do_db = sl == 0 && ct == 0;
   const int b_last = (r1 - 1) / rows, r_last = (r1 - 1) - b_last * rows;
   static_assert(NB == 8, "vm_wait_arr8");
-  for (int m0 = r0; m0 < r1; m0 += 2 * NB) {
-    // rows past the chunk are clamped to its last row (loads stay in
-    // bounds, no branches) and weighted 0.  Counted asm loads: the 8 idx
-    // and 8 dpre loads go out together, then the 8 dependent x gathers,
-    // one wait each (hipcc's own placement serialised them).
-    int srcrow[NB], bvs[NB];
-    float okf[NB], av[NB], bv[NB];
+  // Rows past the chunk are clamped to its last row (loads stay in bounds,
+  // no branches) and weighted 0.  Pipelined one batch ahead: while batch i's
+  // 8 dependent x gathers are in flight, batch i+1's 8 idx and 8 dpre loads
+  // are issued, so a batch costs ~one memory latency instead of two.  The x
+  // gathers are counted asm loads retired by an explicit vmcnt in the same
+  // iteration (hipcc's own placement serialised them); the idx / dpre loads
+  // are ordinary loads that hipcc waits for itself -- they cross the loop
+  // back-edge, where an asm-hidden load could be copied before it landed.
+  int srcrow[NB], bvs[NB];
+  float okf[NB], av[NB];
+  auto fetch = [&](int m0_, int (&sr)[NB], int (&bs)[NB], float (&ok_)[NB], float (&a_)[NB]) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const bool ok = m < r1;
-      okf[j] = ok ? 1.f : 0.f;
-      bvs[j] = (ok ? b : b_last) * vsrc;
-      gload1_async(srcrow[j], idx + (ok ? r : r_last) * kSeq + sl);
+      ok_[j] = ok ? 1.f : 0.f;
+      bs[j] = (ok ? b : b_last) * vsrc;
+      sr[j] = idx[(ok ? r : r_last) * kSeq + sl];
       m += 2;
       r += 2;
       const bool wrap = r >= rows;
@@ -1016,17 +1020,36 @@ __device__ __forceinline__ void conv_dw_lat_body(int vb, int vnb, const float* _
       b = wrap ? b + 1 : b;
     }
 #pragma unroll
-    for (int j = 0; j < NB; ++j) gload1f_async(av[j], dp + (long)min(m0 + h + 2 * j, r1 - 1) * COUT);
-    vm_wait_arr8<NB>(srcrow);
+    for (int j = 0; j < NB; ++j) a_[j] = dp[(long)min(m0_ + h + 2 * j, r1 - 1) * COUT];
+  };
+  fetch(r0, srcrow, bvs, okf, av);
+  for (int m0 = r0; m0 < r1; m0 += 2 * NB) {
+    float bv[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) gload1f_async(bv[j], xs + (long)(bvs[j] + srcrow[j]) * CIN);
-    vm_wait_arr8<NB>(av);
-    vm_wait_arr8<0>(bv);
+    const bool more = m0 + 2 * NB < r1;  // wave-uniform
+    int srcrow_n[NB], bvs_n[NB];
+    float okf_n[NB], av_n[NB];
+    if (more) {
+      fetch(m0 + 2 * NB, srcrow_n, bvs_n, okf_n, av_n);
+      vm_wait_arr8<2 * NB>(bv);  // x gathers retired, the next batch in flight
+    } else {
+      vm_wait_arr8<0>(bv);
+    }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      av[j] *= okf[j];
-      acc[j & 1] = mfma32(av[j], bv[j], acc[j & 1]);
-      dbs += av[j];
+      const float aj = av[j] * okf[j];
+      acc[j & 1] = mfma32(aj, bv[j], acc[j & 1]);
+      dbs += aj;
+    }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        srcrow[j] = srcrow_n[j];
+        bvs[j] = bvs_n[j];
+        okf[j] = okf_n[j];
+        av[j] = av_n[j];
+      }
     }
   }
   float* slab = ws + ((long)chunk * U + unit) * 1024;
@@ -1093,6 +1116,150 @@ __global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, cons
   else
     conv_dw_lat_body<CIN, COUT>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows,
                                 d.total_rows, d.rchunk, d.n_chunks);
+}
+
+// ==========================================================================
+// Backward data of a conv evaluated on a ROW SUBSET (the Enblocks: the conv
+// runs only at the vertices the 0/1 down-sample keeps).  There a source row
+// has ~2.25 non-empty (u, s) inverse lists of its 9, so the inverse-spiral
+// formulation (A = per-slot gather-sum of dpre, MFMA over all 9 slots of
+// every source row) spends ~3/4 of its MFMA work on zero rows.  Instead the
+// reference's own two steps (autograd of model.py:40 then :34):
+//  (1) AddmmBackward at the kept rows only: dG[b,r, s*CIN+c] =
+//      sum_o dpre[b,r,o] w[o, s*CIN+c], a dense [rows, COUT] x [COUT, 9*CIN]
+//      MFMA product (conv_dg_body; it shares a launch with the dW slabs);
+//  (2) IndexSelectBackward (index_add_): dx[b,u,:] = g * sum_{p in flat(u)}
+//      dG[b, p, :] where flat(u) lists the flattened spiral positions
+//      p = r*9 + s with idx[r,s] == u in ASCENDING p -- the sequential
+//      index_add_ order of the reference (conv_dx_rowsub_gather).
+// dG row-major [batch*rows][9*CIN] fp32 in the workspace, behind the slabs.
+struct DgArgs {
+  const float* dpre;
+  const float* w;
+  float* dg;
+  int total_rows;  // batch * rows
+  int n_groups;    // column groups per 16-row tile (divides 9*CIN/16)
+  int nb;          // workgroups of this half
+};
+// LDS of a dG workgroup: W^T of its column group, [ntg*16][COUT + 4]
+template <int CIN, int COUT>
+constexpr int dg_lds_floats(int n_groups) { return kSeq * CIN / n_groups * (COUT + 4); }
+
+// v_mfma_f32_16x16x4_f32.  A workgroup owns one column group (ntg 16-wide
+// n-tiles, the same for its 4 waves) and 4 consecutive 16-row tiles, a wave
+// one tile.  Lane (i, kg) holds dpre row i's channels [kg*COUT/4, +COUT/4)
+// (MFMA step t uses o = kg*COUT/4 + t, B permuted the same way: exact f32
+// sums over o); B from the group's W^T staged in LDS as wl[n][o] (row pad 4:
+// conflict-free ds_read_b128 for 16 consecutive n).  Every dG element is
+// written exactly once.
+template <int CIN, int COUT>
+__device__ __forceinline__ void conv_dg_body(int vb, int vnb, const DgArgs& g, float* wl) {
+  constexpr int K = kSeq * CIN, NT = K / 16, KP = COUT / 4, LDW = COUT + 4;
+  const int lane = threadIdx.x & 63, j = lane & 15, kg = lane >> 4;
+  const int wgi = xcd_block_of(vb, vnb);
+  const int ntg = NT / g.n_groups, grp = wgi % g.n_groups;
+  const int rt = (wgi / g.n_groups) * 4 + (threadIdx.x >> 6);
+  const int row = min(rt * 16 + j, g.total_rows - 1);  // clamp loads, stores masked
+  f32x4 a[KP / 4];
+#pragma unroll
+  for (int q = 0; q < KP / 4; ++q) a[q] = ld4(g.dpre + (long)row * COUT + kg * KP + 4 * q);
+  // stage the group's W^T (A loads in flight); consecutive threads take
+  // consecutive o (conflict-free LDS writes)
+  const int n0 = grp * ntg * 16;
+  for (int e = threadIdx.x; e < COUT * ntg * 4; e += blockDim.x) {
+    const int o = e % COUT, n4 = (e / COUT) * 4;
+    const f32x4 v = ld4(g.w + o * K + n0 + n4);
+    wl[(n4 + 0) * LDW + o] = v.x;
+    wl[(n4 + 1) * LDW + o] = v.y;
+    wl[(n4 + 2) * LDW + o] = v.z;
+    wl[(n4 + 3) * LDW + o] = v.w;
+  }
+  __syncthreads();
+  if (rt * 16 >= g.total_rows) return;
+  const int mo0 = rt * 16 + 4 * kg;
+  for (int nt = 0; nt < ntg; ++nt) {
+    const float* bp = wl + (nt * 16 + j) * LDW + kg * KP;
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int q = 0; q < KP / 4; ++q) {
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(bp + 4 * q);
+      f32x4& ac = acc[q & 1];
+      ac = mfma16(a[q].x, bv.x, ac);
+      ac = mfma16(a[q].y, bv.y, ac);
+      ac = mfma16(a[q].z, bv.z, ac);
+      ac = mfma16(a[q].w, bv.w, ac);
+    }
+    float* out = g.dg + (long)mo0 * K + n0 + nt * 16 + j;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+      if (mo0 + rr < g.total_rows) out[(long)rr * K] = acc[0][rr] + acc[1][rr];
+  }
+}
+
+// dG workgroups and dW-slab workgroups (conv_dw_lat_body) of one Enblock conv
+// interleaved in one launch, as conv_bwd_lat_pair.
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void conv_bwd_rowsub_pair(const DgArgs a, const DwLatArgs d) {
+  extern __shared__ float wl[];
+  const int bid = blockIdx.x, both = 2 * min(a.nb, d.nb);
+  bool is_dg;
+  int vb;
+  if (bid < both) {
+    is_dg = (bid & 1) == 0;
+    vb = bid >> 1;
+  } else {
+    is_dg = a.nb > d.nb;
+    vb = bid - both + both / 2;
+  }
+  if (is_dg)
+    conv_dg_body<CIN, COUT>(vb, a.nb, a, wl);
+  else
+    conv_dw_lat_body<CIN, COUT>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows,
+                                d.total_rows, d.rchunk, d.n_chunks);
+}
+
+// (2): a thread per (source row, 16-B channel chunk); the row's flat list
+// (4*G entries, -1 padded) is read as G int4 loads (one address per row ->
+// broadcast), every dG load is an unconditional buffer load (an absent entry
+// is an out-of-range offset: 0.0, no memory access), all in flight together;
+// summed in list order; elu'(elu_y) epilogue.
+template <int CIN, int G>
+__global__ __launch_bounds__(256) void conv_dx_rowsub_gather(const float* __restrict__ dg,
+                                                             const int4* __restrict__ flat,
+                                                             const float* __restrict__ elu_y,
+                                                             float* __restrict__ dx, int vsrc,
+                                                             int rows, int total_src,
+                                                             int dg_bytes) {
+  constexpr int Q = CIN / 4;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= total_src * Q) return;
+  const int m = t / Q, q = t - m * Q;
+  const int b = m / vsrc, u = m - b * vsrc;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dg), 0, dg_bytes, 0x00020000);
+  const int base = (b * rows * kSeq * CIN + 4 * q) * (int)sizeof(float);
+  int4 e[G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) e[k] = flat[u * G + k];
+  auto off = [&](int p) { return p >= 0 ? base + p * (CIN * (int)sizeof(float)) : kAbsentRow; };
+  f32x4 v[4 * G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    v[4 * k + 0] = buf_ld4(rsrc, off(e[k].x));
+    v[4 * k + 1] = buf_ld4(rsrc, off(e[k].y));
+    v[4 * k + 2] = buf_ld4(rsrc, off(e[k].z));
+    v[4 * k + 3] = buf_ld4(rsrc, off(e[k].w));
+  }
+  f32x4 s = v[0];
+#pragma unroll
+  for (int k = 1; k < 4 * G; ++k) s += v[k];
+  if (elu_y) {
+    const f32x4 y = ld4(elu_y + (long)m * CIN + 4 * q);
+    s.x *= elu_grad_from_out(y.x);
+    s.y *= elu_grad_from_out(y.y);
+    s.z *= elu_grad_from_out(y.z);
+    s.w *= elu_grad_from_out(y.w);
+  }
+  st4(dx + (long)m * CIN + 4 * q, s);
 }
 
 // Batched weight-gradient reduction: ONE launch reduces the deferred slab
@@ -2347,6 +2514,101 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
   BOS(32, 1) BOS(32, 2) BOS(32, 3) BOS(64, 1) BOS(64, 2) BOS(64, 3)
 #undef BOS
   return set_error(CFSD_EINVAL, "spiral_conv_bwd: unsupported channels %d -> %d", cin, cout);
+}
+
+// ---- row-subset backward (dG + dW slabs, then the flat-list gather)
+namespace {
+size_t rowsub_dg_floats(int batch, int rows, int cin) {
+  return ((size_t)batch * rows * kSeq * cin + 63) / 64 * 64;
+}
+size_t rowsub_slab_floats(int batch, int rows, int cin, int cout) {
+  return (dw_geom(batch, rows, cin, cout).ws_floats + 63) / 64 * 64;
+}
+// 32 input channels (every Enblock after the first in the reference configs;
+// W^T of a 64-channel input would not leave LDS for a second workgroup)
+bool rowsub_shape(int cin, int cout) { return cin == 32 && (cout == 32 || cout == 64); }
+// column groups per 16-row tile: enough waves to cover the chip (~2k)
+int rowsub_groups(long row_tiles, int n_tiles) {
+  static const int divs[] = {1, 2, 3, 4, 6, 9, 12, 18, 36};
+  for (int d : divs)
+    if (n_tiles % d == 0 && row_tiles * d >= 1536) return d;
+  return n_tiles;
+}
+}  // namespace
+
+extern "C" size_t cfsd_spiral_conv_bwd_rowsub_workspace(int batch, int vsrc, int rows, int seq,
+                                                        int cin, int cout) {
+  if (batch <= 0 || vsrc <= 0 || rows <= 0 || seq != kSeq || !rowsub_shape(cin, cout)) return 0;
+  return (rowsub_slab_floats(batch, rows, cin, cout) + rowsub_dg_floats(batch, rows, cin)) *
+         sizeof(float);
+}
+
+extern "C" int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, const float* dpre,
+                                           const int32_t* inv_flat, int flat_width,
+                                           const float* w, const float* elu_y, float* dx,
+                                           float* dw, float* db, float* workspace,
+                                           size_t workspace_bytes, int batch, int vsrc, int rows,
+                                           int seq, int cin, int cout, void* stream) {
+  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!inv_flat || !w || !dx || !workspace)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub: null inv_flat / w / dx / workspace");
+  if (!rowsub_shape(cin, cout))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub: unsupported channels %d -> %d", cin, cout);
+  if (flat_width <= 0 || flat_width > 16 || flat_width % 4)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub: flat_width %d not in {4, 8, 12, 16}", flat_width);
+  if ((uintptr_t)inv_flat & 15) return set_error(CFSD_EINVAL, "inv_flat must be 16-B aligned");
+  if ((dw == nullptr) != (db == nullptr))
+    return set_error(CFSD_EINVAL, "dw and db must both be set (or both NULL: deferred)");
+  const size_t need = cfsd_spiral_conv_bwd_rowsub_workspace(batch, vsrc, rows, seq, cin, cout);
+  if (workspace_bytes < need)
+    return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
+  const size_t dg_el = (size_t)batch * rows * kSeq * cin;
+  if (dg_el * sizeof(float) >= (size_t)kAbsentRow)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub: dG of %zu floats exceeds 32-bit buffer offsets", dg_el);
+  hipStream_t st = (hipStream_t)stream;
+  const DwGeom g = dw_geom(batch, rows, cin, cout);
+  float* dg = workspace + rowsub_slab_floats(batch, rows, cin, cout);
+  const int total = batch * rows;
+  const int n_tiles = kSeq * cin / 16;
+  DgArgs a{dpre, w, dg, total, 0, 0};
+  a.n_groups = rowsub_groups((total + 15) / 16, n_tiles);
+  a.nb = (int)(((total + 15) / 16 + 3) / 4) * a.n_groups;
+  const bool lat = g.kind == kDwLat;
+  float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
+  DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, total, g.rchunk, g.gx, 0};
+  if (lat) d.nb = (int)(((long)g.gx * (long)dw_units(cin, cout) + 3) / 4);
+  const dim3 grid((unsigned)(a.nb + d.nb));
+  const int n_el = cout * kSeq * cin + cout;
+#define RSP(CIN_, COUT_)                                                                          \
+  if (cin == CIN_ && cout == COUT_) {                                                             \
+    hipLaunchKernelGGL((conv_bwd_rowsub_pair<CIN_, COUT_>), grid, dim3(256),                      \
+                       (dg_lds_floats<CIN_, COUT_>(a.n_groups) * sizeof(float)), st, a, d);                  \
+    rc = launch_status("spiral_conv_bwd_rowsub_pair");                                           \
+    if (!rc && lat && dw)                                                                         \
+      hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), dim3((unsigned)((n_el + 63) / 64)),       \
+                         dim3(1024), 0, st, workspace, ws_db, dw, db, g.gx);                      \
+  }
+  RSP(32, 32) RSP(32, 64)
+#undef RSP
+  if (rc || (rc = launch_status("spiral_conv_bwd_rowsub_reduce"))) return rc;
+  if (!lat) {  // many rows: the persistent dW kernel, same slab layout
+    rc = cfsd_spiral_conv_bwd_weight(x, idx, dpre, dw, db, workspace, workspace_bytes, batch, vsrc,
+                                     rows, seq, cin, cout, stream);
+    if (rc) return rc;
+  }
+  const long threads = (long)batch * vsrc * (cin / 4);
+  const dim3 gg((unsigned)((threads + 255) / 256));
+  const int G = flat_width / 4, M = batch * vsrc;
+#define RSG(CIN_, G_)                                                                             \
+  if (cin == CIN_ && G == G_) {                                                                   \
+    hipLaunchKernelGGL((conv_dx_rowsub_gather<CIN_, G_>), gg, dim3(256), 0, st, dg,               \
+                       (const int4*)inv_flat, elu_y, dx, vsrc, rows, M, (int)(dg_el * sizeof(float))); \
+    return launch_status("spiral_conv_bwd_rowsub_gather");                                       \
+  }
+  RSG(32, 1) RSG(32, 2) RSG(32, 3) RSG(32, 4)
+#undef RSG
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub: unsupported channels %d -> %d", cin, cout);
 }
 
 extern "C" int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, int batch,

@@ -387,8 +387,16 @@ class SDVAEEngine:
                                                          S.in_ch))]
         b.paired = {}
 
-        def dw_region(key, vsrc, rows, seq, cin, cout, has_dx, low):
+        b.rowsub = {}
+
+        def dw_region(key, vsrc, rows, seq, cin, cout, has_dx, low, flat=None):
             b.paired[key] = (not low) and has_dx and ops.spiral_conv_bwd_paired(bsz, vsrc, rows, seq, cin, cout)
+            # Enblock conv on a row subset: dG at the kept rows + flat-list gather
+            rs = ops.spiral_conv_bwd_rowsub_workspace(bsz, vsrc, rows, seq, cin, cout)
+            b.rowsub[key] = (not low) and has_dx and flat is not None and rs > 0
+            if b.rowsub[key]:
+                regions.append((key, rs))
+                return
             if low:
                 nb = ops.spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout)
             else:
@@ -400,7 +408,8 @@ class SDVAEEngine:
             dw_region(("dec", i), nv[lv], nv[lv], T.seq[lv], cin, cout, True, lv in lp)
         for (cin, cout, lv) in S.enc_layers():
             rows = nv[lv + 1] if T.enc_select[lv] else nv[lv]
-            dw_region(("enc", lv), nv[lv], rows, T.seq[lv], cin, cout, lv > 0, lv in lp)
+            dw_region(("enc", lv), nv[lv], rows, T.seq[lv], cin, cout, lv > 0, lv in lp,
+                      T.enc_flat[lv] if T.enc_select[lv] else None)
         total = sum((nb // 4 + 64) // 64 * 64 for _, nb in regions)
         b.ws_dw_all = torch.empty(total, dtype=torch.float32, device=dev)
         b.ws_dw, off = {}, 0
@@ -650,6 +659,17 @@ class SDVAEEngine:
                     ops.spiral_conv_bwd_data_x(b.dpre_enc[lv], T.enc_inv[lv],
                                                self._w16(f"en_layers.{lv}.conv.layer.weight"), T.n_verts[lv],
                                                elu_y=b.enc_out[prev], out=b.dpre_enc[prev])
+                continue
+            if b.rowsub[("enc", lv)]:  # dG at the kept rows (+ dW slabs), then the flat gather
+                sel = T.enc_select[prev]
+                _, d = ops.spiral_conv_bwd_rowsub(x_in, rows_tab, b.dpre_enc[lv], T.enc_flat[lv], w, None, None,
+                                                  dx=b.dpre_enc[prev] if sel else b.g_pooled[prev],
+                                                  elu_y=b.enc_out[prev] if sel else None,
+                                                  workspace=b.ws_dw[("enc", lv)])
+                defer(d, f"en_layers.{lv}.conv.layer")
+                if not sel:
+                    ops.spmm(T.downT_csr[prev], b.g_pooled[prev], T.n_verts[prev],
+                             elu_y=b.enc_full[prev], out=b.dpre_enc[prev])
                 continue
             if b.paired[("enc", lv)]:  # dx + dW slabs in one launch
                 sel = T.enc_select[prev]

@@ -197,6 +197,42 @@ def spiral_conv_bwd(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace
     return dx
 
 
+def spiral_conv_bwd_rowsub_workspace(bsz, vsrc, rows, seq, cin, cout):
+    """0 when the shape has no row-subset backward (cin != 32)."""
+    return int(_abi.lib().cfsd_spiral_conv_bwd_rowsub_workspace(bsz, vsrc, rows, seq, cin, cout))
+
+
+def spiral_conv_bwd_rowsub(x, idx, dpre, flat, w, dw, db, dx, elu_y=None, workspace=None):
+    """dX + dW/db of a conv evaluated on a row subset (an Enblock conv):
+    dG = dpre.W at the kept rows, then the ascending-order gather-sum of dG
+    through ``flat`` = ``topology.inverse_flat``'s (table, width)."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = dpre.shape[2]
+    table, width = flat
+    _need(x, None, name="x")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(dpre, (bsz, rows, cout), name="dpre")
+    _need(table, (vsrc, width), torch.int32, "inv_flat")
+    _need(w, (cout, seq * cin), name="w")
+    if dw is not None or db is not None:
+        _need(dw, (cout, seq * cin), name="dw")
+        _need(db, (cout,), name="db")
+    _need(dx, (bsz, vsrc, cin), name="dx")
+    if elu_y is not None:
+        _need(elu_y, (bsz, vsrc, cin), name="elu_y")
+    need = spiral_conv_bwd_rowsub_workspace(bsz, vsrc, rows, seq, cin, cout)
+    if need == 0:
+        raise ValueError(f"no row-subset backward for {cin} -> {cout} channels")
+    ws, nb = _conv_ws(workspace, x.device, need)
+    call("cfsd_spiral_conv_bwd_rowsub", ptr(x), ptr(idx), ptr(dpre), ptr(table), width, ptr(w),
+         ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, seq,
+         cin, cout, stream_ptr())
+    if dw is None:  # deferred weight gradient (slabs at the workspace start)
+        return dx, DeferredDw(ws, bsz, vsrc, rows, cin, cout, True)
+    return dx
+
+
 def spiral_gather(x, idx, out=None):
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape

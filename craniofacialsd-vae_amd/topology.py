@@ -76,6 +76,27 @@ def inverse_spiral(idx, vsrc):
     return _i32(ptr), _i32(rows_sorted), _i32(head)
 
 
+def inverse_flat(idx, vsrc, max_width=16):
+    """Per source vertex u, the flattened spiral positions p = r*S + s with
+    ``idx[r, s] == u`` in ascending p (the order the reference's
+    ``index_add_`` -- the autograd of ``index_select``, model.py:34 -- adds
+    them), padded with -1 to a width that is a multiple of 4.  Returns
+    ([vsrc, width] int32, width), or (None, 0) when some fan-in exceeds
+    ``max_width`` (the row-subset backward then uses the inverse CSR)."""
+    idx = np.asarray(idx, np.int64)
+    flat = idx.reshape(-1)
+    cnt = np.bincount(flat, minlength=vsrc)
+    width = max(4, int(-(-cnt.max() // 4) * 4)) if flat.size else 4
+    if width > max_width:
+        return None, 0
+    order = np.argsort(flat, kind="stable")  # p ascending inside each u
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    slot = np.arange(flat.size) - np.repeat(start, cnt)
+    out = -np.ones((vsrc, width), np.int64)
+    out[flat[order], slot] = order
+    return _i32(out), width
+
+
 def selection_rows(row, col, val, m):
     """Return the kept-vertex list if the COO transform is a 0/1 row
     selection (exactly one entry of value 1.0 per row), else None."""
@@ -131,6 +152,7 @@ class DeviceTopology:
         self.enc_rows = []      # per Enblock: evaluated spiral table (subset or full)
         self.enc_inv = []
         self.enc_select = []    # True when Pool(down) folds into the row subset
+        self.enc_flat = []      # per Enblock on a row subset: (inverse_flat table, width)
         self.down_csr, self.downT_csr = [], []
         self.up_csr, self.upT_csr = [], []
         self.np_spirals = [np.asarray(s, np.int64) for s in spirals]
@@ -148,10 +170,13 @@ class DeviceTopology:
                 self.enc_select.append(True)
                 self.enc_rows.append(_dev(_i32(sub), self.device))
                 self.enc_inv.append(tuple(_dev(a, self.device) for a in inverse_spiral(sub, v)))
+                fl, width = inverse_flat(sub, v)
+                self.enc_flat.append((_dev(fl, self.device), width) if fl is not None else None)
             else:
                 self.enc_select.append(False)
                 self.enc_rows.append(self.spiral[-1])
                 self.enc_inv.append(self.spiral_inv[-1])
+                self.enc_flat.append(None)
             self.down_csr.append(self._csr(csr_from_coo(drow, dcol, dval, dshape[0])))
             self.downT_csr.append(self._csr(csr_transpose_from_coo(drow, dcol, dval, dshape[1])))
             urow, ucol, uval, ushape = up[l]

@@ -126,6 +126,25 @@ size_t cfsd_spiral_conv_bwd_workspace(int batch, int vsrc, int rows, int seq, in
  * launch for this shape (no reference counterpart: a scheduling query). */
 int cfsd_spiral_conv_bwd_paired(int batch, int vsrc, int rows, int seq, int cin, int cout);
 
+/* Backward (dx and dW/db) of a conv evaluated on a ROW SUBSET (the Enblock
+ * convs: `rows` = the kept vertices), in the reference's own two steps
+ * (autograd of model.py:40 then :34): dG = dpre.W at the kept rows only
+ * (MFMA, in the workspace), then dx[b,u,:] = g(b,u,:) * sum_{p in flat(u)}
+ * dG[b, p, :] with flat(u) = the flattened spiral positions p = r*seq + s
+ * having idx[r,s] == u, in ascending p (the sequential index_add_ order).
+ * inv_flat [vsrc][flat_width] int32, -1 padded, 16-B aligned rows,
+ * flat_width in {4, 8, 12, 16} (>= the largest fan-in).  dw/db exactly as
+ * cfsd_spiral_conv_bwd_weight (dw == db == NULL defers: cfsd_dw_reduce_batch
+ * item with fused = 1).  cin = 32, cout in {32, 64}.
+ * workspace: cfsd_spiral_conv_bwd_rowsub_workspace() bytes (0 = unsupported). */
+size_t cfsd_spiral_conv_bwd_rowsub_workspace(int batch, int vsrc, int rows, int seq, int cin,
+                                             int cout);
+int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, const float* dpre,
+                                const int32_t* inv_flat, int flat_width, const float* w,
+                                const float* elu_y, float* dx, float* dw, float* db,
+                                float* workspace, size_t workspace_bytes, int batch, int vsrc,
+                                int rows, int seq, int cin, int cout, void* stream);
+
 /* Materialising spiral gather, g[b,r,s*cin+c] = x[b, idx[r,s], c]
  * (model.py:34 index_select + view).  Used as the HBM-roofline probe. */
 int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, int batch, int vsrc, int rows,

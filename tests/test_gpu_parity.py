@@ -618,3 +618,43 @@ def test_encode_all_and_latent_stats_c1(dtopo):
     for k, v in {"means": ref.mean(0), "stds": ref.std(0), "mins": ref.min(0)[0],
                  "maxs": ref.max(0)[0]}.items():
         assert np.abs(st[k].cpu().numpy() - v.numpy()).max() <= 1e-4, k
+
+
+@pytest.mark.parametrize("level,cout,bsz", [(1, 32, 2), (1, 32, 16), (2, 32, 16), (3, 64, 16), (3, 64, 3)])
+@pytest.mark.parametrize("elu,deferred", [(False, False), (True, True)])
+def test_rowsub_backward(otopo, dtopo, level, cout, bsz, elu, deferred):
+    """Enblock backward on the kept rows (dG = dpre.W, then the ascending
+    flat-list gather) vs autograd of conv -> row subset (model.py:34,40)."""
+    g = torch.Generator().manual_seed(level * 10 + cout + bsz)
+    sp = otopo.spirals[level]
+    sel = torch.from_numpy(otopo.down[level][1])
+    v = sp.shape[0]
+    x = torch.randn(bsz, v, 32, generator=g).requires_grad_()
+    w = (torch.randn(cout, 288, generator=g) * 0.1).requires_grad_()
+    b = (torch.randn(cout, generator=g) * 0.1).requires_grad_()
+    y = O.spiral_conv(x, sp, w, b)[:, sel]
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy)
+    ey = O.elu(torch.randn(bsz, v, 32, generator=g))
+    ref_dx = x.grad * torch.where(ey > 0, torch.ones_like(ey), ey + 1) if elu else x.grad
+    rows = sel.numel()
+    need = ops.spiral_conv_bwd_rowsub_workspace(bsz, v, rows, 9, 32, cout)
+    assert need > 0 and dtopo.enc_flat[level] is not None
+    ws = torch.empty(need // 4 + 1, device=DEV)
+    dx = torch.full((bsz, v, 32), float("nan"), device=DEV)
+    dw = torch.empty(cout, 288, device=DEV)
+    db = torch.empty(cout, device=DEV)
+    args = (x.detach().to(DEV), dtopo.enc_rows[level], dy.to(DEV), dtopo.enc_flat[level], w.detach().to(DEV))
+    if deferred:
+        _, d = ops.spiral_conv_bwd_rowsub(*args, None, None, dx, elu_y=ey.to(DEV) if elu else None,
+                                          workspace=ws)
+        ops.dw_reduce_batch([(d, dw, db)])
+    else:
+        ops.spiral_conv_bwd_rowsub(*args, dw, db, dx, elu_y=ey.to(DEV) if elu else None, workspace=ws)
+    close(dx, ref_dx, 1e-5, f"rowsub dx L{level}")
+    close(dw, w.grad, 1e-5, f"rowsub dw L{level}")
+    close(db, b.grad, 1e-5, f"rowsub db L{level}")
+    # run-to-run bit-identical (fixed summation order, no atomics)
+    dx2 = torch.empty_like(dx)
+    ops.spiral_conv_bwd_rowsub(*args, dw, db, dx2, elu_y=ey.to(DEV) if elu else None, workspace=ws)
+    assert torch.equal(dx, dx2)

@@ -66,6 +66,24 @@ def test_inverse_spiral_matches_bruteforce():
     assert longest > topology.INV_HEAD  # the overflow path is exercised
 
 
+def test_inverse_flat_matches_bruteforce(topo_npz):
+    """Flattened spiral positions p = r*9 + s per source vertex, ascending
+    (the reference's index_add_ order), -1 padded to a multiple of 4."""
+    rs = np.random.RandomState(1)
+    idx = rs.randint(0, 60, size=(30, 9))
+    flat, width = topology.inverse_flat(idx, 60)
+    assert width % 4 == 0 and flat.shape == (60, width)
+    for u in range(60):
+        exp = [p for p in range(30 * 9) if idx.reshape(-1)[p] == u]
+        assert flat[u].tolist() == exp + [-1] * (width - len(exp))
+    # the craniofacial Enblock subsets (levels 1-3) fit in 8 entries
+    T = topology.DeviceTopology.from_npz(topo_npz, device="cpu")
+    for lv in (1, 2, 3):
+        tab, w = T.enc_flat[lv]
+        assert w == 8 and tuple(tab.shape) == (T.n_verts[lv], 8)
+    assert topology.inverse_flat(np.zeros((20, 9), np.int64), 1) == (None, 0)
+
+
 def test_csr_keeps_file_order_and_transpose():
     row = np.array([2, 0, 2, 1, 0, 2])
     col = np.array([5, 1, 0, 3, 4, 2])

@@ -10,6 +10,7 @@ import csv
 import glob
 import json
 import sys
+import time
 
 d = sys.argv[1]
 pat = sys.argv[2] if len(sys.argv) > 2 else "conv_fwd_mfma<32, 32, 1, 9>"
@@ -24,5 +25,6 @@ write = sum(vals["WRITE_SIZE"]) / max(1, len(vals["WRITE_SIZE"]))
 out = {"kernel": pat, "launches": [len(vals["FETCH_SIZE"]), len(vals["WRITE_SIZE"])],
        "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
        "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
+       "created": time.time(),
        "note": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE half-count correction)"}
 print(json.dumps(out))

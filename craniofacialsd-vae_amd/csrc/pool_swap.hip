@@ -90,6 +90,92 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   st4f(y + t * 4, acc);
 }
 
+// The same SpMM for matrices with long, skewed rows (the transposes of the
+// up-sampling matrices: level 0 has 12 entries per row on average but up to
+// 96).  A row is a sequential fp32 fold in entry order (kept for
+// bit-exactness), so the kernel cannot end before its longest row's chain of
+// dependent chunks; spmm_csr_k's plain chunk loop paid two memory latencies
+// (column list, then x rows) per 8 entries.  Here:
+//  * rows are visited in `order` (rows by decreasing length, a host-built
+//    schedule), slot-major inside each XCD's contiguous mesh group, so the
+//    longest rows of every mesh start first and a wave's 8 rows have similar
+//    lengths;
+//  * the next chunk's columns / values are loaded while the current chunk's
+//    x rows are in flight: one latency per chunk.
+// one row's sequential fold, the next chunk's list prefetched
+template <int CK, typename TX>
+__device__ __forceinline__ void spmm_fold_prefetch(int beg, int end, const int* __restrict__ col,
+                                                   const float* __restrict__ val,
+                                                   const TX* __restrict__ xb, int c4, f32x4& acc) {
+#pragma clang fp contract(off)
+  int cc[CK];
+  float vv[CK];
+#pragma unroll
+  for (int j = 0; j < CK; ++j) {
+    const int e = min(beg + j, end - 1);
+    cc[j] = col[e];
+    vv[j] = val[e];
+  }
+  for (int e0 = beg; e0 < end; e0 += CK) {
+    f32x4 xv[CK];
+#pragma unroll
+    for (int j = 0; j < CK; ++j) xv[j] = ld4f(xb + (long)cc[j] * c4 * 4);
+    float vc[CK];
+#pragma unroll
+    for (int j = 0; j < CK; ++j) vc[j] = vv[j];
+    if (e0 + CK < end) {  // next chunk's list while the x rows are in flight
+#pragma unroll
+      for (int j = 0; j < CK; ++j) {
+        const int e = min(e0 + CK + j, end - 1);
+        cc[j] = col[e];
+        vv[j] = val[e];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CK; ++j) {
+      if (e0 + j < end) {
+        acc.x = acc.x + xv[j].x * vc[j];
+        acc.y = acc.y + xv[j].y * vc[j];
+        acc.z = acc.z + xv[j].z * vc[j];
+        acc.w = acc.w + xv[j].w * vc[j];
+      }
+    }
+  }
+}
+
+template <typename TX, typename TY>
+__global__ __launch_bounds__(256) void spmm_sched_k(const int* __restrict__ row_ptr,
+                                                    const int* __restrict__ col,
+                                                    const float* __restrict__ val,
+                                                    const int* __restrict__ order,
+                                                    const TX* __restrict__ x,
+                                                    const TY* __restrict__ elu_y,
+                                                    TY* __restrict__ y, int m, int n, int c4,
+                                                    int groups, int bpg, int per) {
+  const int g = (int)blockIdx.x % groups;
+  const int t = (int)(blockIdx.x / groups) * (int)blockDim.x + (int)threadIdx.x;
+  if (t >= per) return;
+  const int rowq = bpg * c4;  // threads per schedule slot
+  const int slot = t / rowq, rem = t - slot * rowq;
+  const int bl = rem / c4, q = rem - bl * c4;
+  const int b = g * bpg + bl, r = order[slot];
+  const TX* xb = x + (long)b * n * c4 * 4 + 4 * q;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int beg = row_ptr[r], end = row_ptr[r + 1];
+  // (16-entry chunks for the > 32-entry rows measured no faster at level 0
+  // and slower elsewhere: the wider branch's registers cost occupancy)
+  spmm_fold_prefetch<8>(beg, end, col, val, xb, c4, acc);
+  const long o = ((long)b * m + r) * c4 + q;
+  if (elu_y) {
+    f32x4 gy = ld4f(elu_y + o * 4);
+    acc.x *= elu_grad_from_out(gy.x);
+    acc.y *= elu_grad_from_out(gy.y);
+    acc.z *= elu_grad_from_out(gy.z);
+    acc.w *= elu_grad_from_out(gy.w);
+  }
+  st4f(y + o * 4, acc);
+}
+
 // out[(i*bs + j), v, :] = x[mesh(i or j), v, :]; one thread per (out mesh,
 // vertex); c <= 4 channels per vertex (xyz) are copied as scalars, larger c
 // in 16-B chunks.  Device-side indices are range-guarded so a bad value can
@@ -241,9 +327,9 @@ extern "C" int cfsd_vertex_errors(const float* out, const float* gt, const float
   return launch_status("vertex_errors");
 }
 
-static int spmm_launch(const int32_t* row_ptr, const int32_t* col, const float* val, const void* x,
-                       int x_dt, const void* elu_y, void* y, int y_dt, int batch, int m, int n, int c,
-                       void* stream) {
+static int spmm_launch(const int32_t* row_ptr, const int32_t* col, const float* val,
+                       const int32_t* order, const void* x, int x_dt, const void* elu_y, void* y,
+                       int y_dt, int batch, int m, int n, int c, void* stream) {
   if (!row_ptr || !col || !val || !x || !y) return set_error(CFSD_EINVAL, "spmm_csr: null pointer");
   if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
     return set_error(CFSD_EINVAL, "spmm_csr: bad sizes batch=%d m=%d n=%d c=%d", batch, m, n, c);
@@ -252,6 +338,21 @@ static int spmm_launch(const int32_t* row_ptr, const int32_t* col, const float* 
   const long total = (long)batch * m * (c / 4);
   if (total >= (1L << 31) || (long)batch * n >= (1L << 31))
     return set_error(CFSD_EINVAL, "spmm_csr: batch x rows >= 2^31 (32-bit indices)");
+  const hipStream_t st0 = (hipStream_t)stream;
+  if (order) {  // scheduled rows: XCD groups of whole meshes
+    const int groups = batch % 8 == 0 ? 8 : 1, bpg = batch / groups;
+    const int per = bpg * m * (c / 4);
+    const unsigned nb = (unsigned)(groups * ((per + 255) / 256));
+#define SPMS(TX, TY)                                                                             \
+  hipLaunchKernelGGL((spmm_sched_k<TX, TY>), dim3(nb), dim3(256), 0, st0, row_ptr, col, val,     \
+                     order, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, groups, bpg, per)
+    if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPMS(float, float);
+    else if (x_dt == CFSD_DT_F32) SPMS(float, bf16_t);
+    else if (y_dt == CFSD_DT_F32) SPMS(bf16_t, float);
+    else SPMS(bf16_t, bf16_t);
+#undef SPMS
+    return launch_status("spmm_csr_sched");
+  }
   const long per_grp = (total + 7) / 8;  // 8 XCD groups of equal block count
   const unsigned nblk = (unsigned)(8 * ((per_grp + 255) / 256));
   const hipStream_t st = (hipStream_t)stream;
@@ -269,13 +370,21 @@ static int spmm_launch(const int32_t* row_ptr, const int32_t* col, const float* 
 extern "C" int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const float* val,
                              const float* x, const float* elu_y, float* y, int batch, int m,
                              int n, int c, void* stream) {
-  return spmm_launch(row_ptr, col, val, x, CFSD_DT_F32, elu_y, y, CFSD_DT_F32, batch, m, n, c, stream);
+  return spmm_launch(row_ptr, col, val, nullptr, x, CFSD_DT_F32, elu_y, y, CFSD_DT_F32, batch, m, n, c,
+                     stream);
+}
+
+extern "C" int cfsd_spmm_csr_sched(const int32_t* row_ptr, const int32_t* col, const float* val,
+                                   const int32_t* order, const void* x, int x_dt, const void* elu_y,
+                                   void* y, int y_dt, int batch, int m, int n, int c, void* stream) {
+  if (!order) return set_error(CFSD_EINVAL, "spmm_csr_sched: null order");
+  return spmm_launch(row_ptr, col, val, order, x, x_dt, elu_y, y, y_dt, batch, m, n, c, stream);
 }
 
 extern "C" int cfsd_spmm_csr_x(const int32_t* row_ptr, const int32_t* col, const float* val,
                                const void* x, int x_dt, const void* elu_y, void* y, int y_dt,
                                int batch, int m, int n, int c, void* stream) {
-  return spmm_launch(row_ptr, col, val, x, x_dt, elu_y, y, y_dt, batch, m, n, c, stream);
+  return spmm_launch(row_ptr, col, val, nullptr, x, x_dt, elu_y, y, y_dt, batch, m, n, c, stream);
 }
 
 extern "C" int cfsd_cast(const void* src, int src_dt, void* dst, int dst_dt, size_t n, void* stream) {

@@ -542,6 +542,12 @@ __global__ __launch_bounds__(256, dx_occ(CIN, COUT)) void conv_dx_mfma(
 // Tasks are numbered column-tile fastest, so the waves of a workgroup
 // gather the same rows (L1 hits).
 constexpr int kLatSB = 3;  // slots per batch
+#ifndef CFSD_FWD_LAT_SB
+#define CFSD_FWD_LAT_SB 3
+#endif
+#ifndef CFSD_DX_LAT_SB
+#define CFSD_DX_LAT_SB 3
+#endif
 template <int CIN, int COUT, int ACT, int CTW>
 __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
                                                     const int* __restrict__ idx,
@@ -551,6 +557,8 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
                                                     long total_rows) {
   // CTW column tiles per wave share the wave's A gathers
   constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN, NTW = NCT / CTW;
+  constexpr int FSB = CFSD_FWD_LAT_SB;
+  static_assert(kSeq % FSB == 0, "slot batches");
   static_assert(NCT % CTW == 0, "column tiles per wave");
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
   const long task = (long)xcd_block() * 4 + (threadIdx.x >> 6);
@@ -572,10 +580,10 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
 #pragma unroll
   for (int t = 0; t < CTW; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s0 = 0; s0 < kSeq; s0 += kLatSB) {
-    f32x4 av[kLatSB][CH], bw[kLatSB][CH][CTW];
+  for (int s0 = 0; s0 < kSeq; s0 += FSB) {
+    f32x4 av[FSB][CH], bw[FSB][CH][CTW];
 #pragma unroll
-    for (int sl = 0; sl < kLatSB; ++sl)
+    for (int sl = 0; sl < FSB; ++sl)
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
         av[sl][c] = ld4(xb + (long)src[s0 + sl] * CIN + 16 * c);
@@ -584,10 +592,10 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
       }
     // keep the batch's loads ahead of its MFMAs (hipcc otherwise interleaves
     // them with vmcnt waits to save registers, re-exposing the latency)
-    __builtin_amdgcn_sched_group_barrier(0x020, (1 + CTW) * kLatSB * CH, 0);  // VMEM reads
-    __builtin_amdgcn_sched_group_barrier(0x008, 4 * CTW * kLatSB * CH, 0);    // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x020, (1 + CTW) * FSB * CH, 0);  // VMEM reads
+    __builtin_amdgcn_sched_group_barrier(0x008, 4 * CTW * FSB * CH, 0);    // MFMA
 #pragma unroll
-    for (int sl = 0; sl < kLatSB; ++sl)
+    for (int sl = 0; sl < FSB; ++sl)
 #pragma unroll
       for (int c = 0; c < CH; ++c)
 #pragma unroll
@@ -634,6 +642,8 @@ __device__ __forceinline__ void conv_dx_lat_body(int vb, int vnb, const float* _
                                                  float* __restrict__ dx, int vsrc, int rows,
                                                  long total_rows) {
   constexpr int CH = COUT / 16, NCT = CIN / 16, K = kSeq * CIN, NTW = NCT / CTW;
+  constexpr int DSB = CFSD_DX_LAT_SB;
+  static_assert(kSeq % DSB == 0, "slot batches");
   static_assert(NCT % CTW == 0, "column tiles per wave");
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
   const long task = (long)xcd_block_of(vb, vnb) * 4 + (threadIdx.x >> 6);
@@ -656,13 +666,13 @@ __device__ __forceinline__ void conv_dx_lat_body(int vb, int vnb, const float* _
 #pragma unroll
   for (int t = 0; t < CTW; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s0 = 0; s0 < kSeq; s0 += kLatSB) {
-    int4 pr[kLatSB];
+  for (int s0 = 0; s0 < kSeq; s0 += DSB) {
+    int4 pr[DSB];
 #pragma unroll
-    for (int sl = 0; sl < kLatSB; ++sl) pr[sl] = pu[s0 + sl];
-    f32x4 bw[kLatSB][CH][CTW];
+    for (int sl = 0; sl < DSB; ++sl) pr[sl] = pu[s0 + sl];
+    f32x4 bw[DSB][CH][CTW];
 #pragma unroll
-    for (int sl = 0; sl < kLatSB; ++sl)
+    for (int sl = 0; sl < DSB; ++sl)
 #pragma unroll
       for (int c = 0; c < CH; ++c)
 #pragma unroll
@@ -672,9 +682,9 @@ __device__ __forceinline__ void conv_dx_lat_body(int vb, int vnb, const float* _
         }
     // list rows 0..2 of the batch's keys: unconditional buffer loads, absent
     // rows out of range (read as 0, no traffic), all in flight together
-    f32x4 a[kLatSB][CH];
+    f32x4 a[DSB][CH];
 #pragma unroll
-    for (int sl = 0; sl < kLatSB; ++sl) {
+    for (int sl = 0; sl < DSB; ++sl) {
       f32x4 r[3][CH];
       const int hr[3] = {pr[sl].x, pr[sl].y, pr[sl].z};
 #pragma unroll
@@ -687,7 +697,7 @@ __device__ __forceinline__ void conv_dx_lat_body(int vb, int vnb, const float* _
     }
     // rows 3.. (0.3 % of keys): exec branch
 #pragma unroll
-    for (int sl = 0; sl < kLatSB; ++sl) {
+    for (int sl = 0; sl < DSB; ++sl) {
       {
         if (pr[sl].w >= 0) {
 #pragma unroll
@@ -702,7 +712,7 @@ __device__ __forceinline__ void conv_dx_lat_body(int vb, int vnb, const float* _
       }
     }
 #pragma unroll
-    for (int sl = 0; sl < kLatSB; ++sl)
+    for (int sl = 0; sl < DSB; ++sl)
 #pragma unroll
       for (int c = 0; c < CH; ++c)
 #pragma unroll

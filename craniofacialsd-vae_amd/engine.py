@@ -449,11 +449,11 @@ class SDVAEEngine:
             ops.spiral_conv_fwd_x(x, idx, w, self._w16(wname + ".weight"), bias, act, out)
 
     @staticmethod
-    def _spmm(csr, x, m, out, elu_y=None):
+    def _spmm(csr, x, m, out, elu_y=None, order=None):
         if x.dtype == torch.float32 and out.dtype == torch.float32:
-            ops.spmm(csr, x, m, elu_y=elu_y, out=out)
+            ops.spmm(csr, x, m, elu_y=elu_y, out=out, order=order)
         else:
-            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out)
+            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out, order=order)
 
     def _lin_names(self):
         n = self.spec.n
@@ -610,9 +610,10 @@ class SDVAEEngine:
                                          out=b.g_dec_up[i], workspace=b.ws)
             if i > 0:  # through Pool(up) into the previous Deblock's ELU
                 self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dpre_dec[i - 1],
-                           elu_y=b.dec_out[i - 1])
+                           elu_y=b.dec_out[i - 1], order=T.upT_order[ui])
             else:
-                self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh)
+                self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh,
+                           order=T.upT_order[ui])
         # decoder Linear
         ops.linear_bwd(b.z, P.view("de_layers.0.weight"), b.dh.view(b.bsz, -1), dx=b.dz,
                        dw=P.gview("de_layers.0.weight"), db=P.gview("de_layers.0.bias"),

@@ -244,8 +244,10 @@ def spiral_gather(x, idx, out=None):
 
 
 # ------------------------------------------------------------------ pool / swap
-def spmm(csr, x, m, elu_y=None, out=None):
-    """y[b, r] = g * sum_{k in row r} val[k] x[b, col[k]]   (Pool, model.py:50-55)."""
+def spmm(csr, x, m, elu_y=None, out=None, order=None):
+    """y[b, r] = g * sum_{k in row r} val[k] x[b, col[k]]   (Pool, model.py:50-55).
+    ``order``: optional row schedule (a permutation of the rows by decreasing
+    length, for matrices with long skewed rows); same results bit for bit."""
     row_ptr, col, val = csr
     bsz, n, c = x.shape
     _need(x, None, name="x")
@@ -255,9 +257,19 @@ def spmm(csr, x, m, elu_y=None, out=None):
     if elu_y is not None:
         _need(elu_y, (bsz, m, c), name="elu_y")
     y = _out(out, (bsz, m, c), x)
+    if order is not None:
+        _spmm_sched(row_ptr, col, val, order, x, elu_y, y, bsz, m, n, c)
+        return y
     call("cfsd_spmm_csr", ptr(row_ptr), ptr(col), ptr(val), ptr(x), ptr(elu_y), ptr(y), bsz, m, n,
          c, stream_ptr())
     return y
+
+
+def _spmm_sched(row_ptr, col, val, order, x, elu_y, y, bsz, m, n, c):
+    """cfsd_spmm_csr_sched: rows visited in ``order`` (``topology.row_schedule``)."""
+    _need(order, (m,), torch.int32, "order")
+    call("cfsd_spmm_csr_sched", ptr(row_ptr), ptr(col), ptr(val), ptr(order), ptr(x), _dt(x),
+         ptr(elu_y), ptr(y), _dt(y), bsz, m, n, c, stream_ptr())
 
 
 def swap_features(x_all, batch_idx, region_mask, key, bs, out=None):
@@ -629,7 +641,7 @@ def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspa
     return dx
 
 
-def spmm_x(csr, x, m, elu_y=None, out=None):
+def spmm_x(csr, x, m, elu_y=None, out=None, order=None):
     """Pool SpMM with fp32 or bf16 operands (fp32 sums, file order)."""
     row_ptr, col, val = csr
     bsz, n, c = x.shape
@@ -640,6 +652,9 @@ def spmm_x(csr, x, m, elu_y=None, out=None):
     _needx(out, (bsz, m, c), "out")
     if elu_y is not None:
         _need(elu_y, (bsz, m, c), out.dtype, "elu_y")
+    if order is not None:
+        _spmm_sched(row_ptr, col, val, order, x, elu_y, out, bsz, m, n, c)
+        return out
     call("cfsd_spmm_csr_x", ptr(row_ptr), ptr(col), ptr(val), ptr(x), _dt(x), ptr(elu_y), ptr(out),
          _dt(out), bsz, m, n, c, stream_ptr())
     return out

@@ -97,6 +97,16 @@ def inverse_flat(idx, vsrc, max_width=16):
     return _i32(out), width
 
 
+def row_schedule(ptr, min_max_len=16):
+    """Rows by decreasing length (stable), the visiting order of
+    ``cfsd_spmm_csr_sched``; None when no row is longer than ``min_max_len``
+    (the plain kernel then has no long fold to start early)."""
+    cnt = np.diff(np.asarray(ptr, np.int64))
+    if cnt.size == 0 or cnt.max() <= min_max_len:
+        return None
+    return _i32(np.argsort(-cnt, kind="stable"))
+
+
 def selection_rows(row, col, val, m):
     """Return the kept-vertex list if the COO transform is a 0/1 row
     selection (exactly one entry of value 1.0 per row), else None."""
@@ -155,6 +165,7 @@ class DeviceTopology:
         self.enc_flat = []      # per Enblock on a row subset: (inverse_flat table, width)
         self.down_csr, self.downT_csr = [], []
         self.up_csr, self.upT_csr = [], []
+        self.upT_order = []     # row schedule of each up transpose (None: short rows)
         self.np_spirals = [np.asarray(s, np.int64) for s in spirals]
         for l in range(self.n_levels):
             sp = np.asarray(spirals[l], np.int64)
@@ -182,6 +193,8 @@ class DeviceTopology:
             urow, ucol, uval, ushape = up[l]
             self.up_csr.append(self._csr(csr_from_coo(urow, ucol, uval, ushape[0])))
             self.upT_csr.append(self._csr(csr_transpose_from_coo(urow, ucol, uval, ushape[1])))
+            sched = row_schedule(self.upT_csr[-1][0].cpu().numpy())
+            self.upT_order.append(_dev(sched, self.device) if sched is not None else None)
         self.lap_csr = self.lapT_csr = None
         if lap is not None:
             lr, lc, lv, lshape = lap

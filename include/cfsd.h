@@ -162,6 +162,15 @@ int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, int batch, 
 int cfsd_spmm_csr(const int32_t* row_ptr, const int32_t* col, const float* val, const float* x,
                   const float* elu_y, float* y, int batch, int m, int n, int c, void* stream);
 
+/* cfsd_spmm_csr(_x) for matrices with long, skewed rows (the up-sampling
+ * transposes): same results bit for bit; rows are visited in `order` (a
+ * permutation of [0, m), rows by decreasing length: the longest sequential
+ * folds start first) and each row's entry list is prefetched one chunk ahead.
+ * x / elu_y / y storage types as cfsd_spmm_csr_x. */
+int cfsd_spmm_csr_sched(const int32_t* row_ptr, const int32_t* col, const float* val,
+                        const int32_t* order, const void* x, int x_dt, const void* elu_y, void* y,
+                        int y_dt, int batch, int m, int n, int c, void* stream);
+
 /* ---------------------------------------------------------------- feature swap
  * Replaces SwapFeatures.__call__ / swap (swap_batch_transform.py:13-52):
  *   out[i*bs+j, v, :] = x[mesh[(i != j && mask[key*nv + v]) ? j : i], v, :]

@@ -228,6 +228,28 @@ def test_pool_bit_exact(otopo, dtopo, level, kind):
     np.testing.assert_array_equal(y.cpu().numpy(), out.detach().numpy())
     dx = ops.spmm(csrT, dout.to(DEV), n)
     np.testing.assert_array_equal(dx.cpu().numpy(), x.grad.numpy())
+    if kind == "up":  # long-row schedule of the transpose: same bits
+        assert dtopo.upT_order[level] is not None
+        dxs = ops.spmm(csrT, dout.to(DEV), n, order=dtopo.upT_order[level])
+        np.testing.assert_array_equal(dxs.cpu().numpy(), x.grad.numpy())
+
+
+@pytest.mark.parametrize("bsz", [16, 3])
+@pytest.mark.parametrize("dts", [("f32", "f32"), ("bf16", "bf16"), ("bf16", "f32")])
+def test_pool_scheduled_transpose(dtopo, bsz, dts):
+    """cfsd_spmm_csr_sched == cfsd_spmm_csr(_x) bit for bit (every level, with the
+    ELU-backward epilogue, XCD mesh groups and the single-group fallback)."""
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16}
+    g = torch.Generator().manual_seed(bsz)
+    for level in range(4):
+        m, n = dtopo.n_verts[level + 1], dtopo.n_verts[level]
+        x = torch.randn(bsz, n, 32, generator=g).to(DEV, dt[dts[0]])
+        ey = O.elu(torch.randn(bsz, m, 32, generator=g)).to(DEV, dt[dts[1]])
+        a = torch.empty(bsz, m, 32, device=DEV, dtype=dt[dts[1]])
+        b = torch.empty_like(a)
+        ops.spmm_x(dtopo.upT_csr[level], x, m, elu_y=ey, out=a)
+        ops.spmm_x(dtopo.upT_csr[level], x, m, elu_y=ey, out=b, order=dtopo.upT_order[level])
+        assert torch.equal(a, b), f"level {level}"
 
 
 def test_pool_golden(dtopo):
@@ -658,3 +680,4 @@ def test_rowsub_backward(otopo, dtopo, level, cout, bsz, elu, deferred):
     dx2 = torch.empty_like(dx)
     ops.spiral_conv_bwd_rowsub(*args, dw, db, dx2, elu_y=ey.to(DEV) if elu else None, workspace=ws)
     assert torch.equal(dx, dx2)
+

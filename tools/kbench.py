@@ -66,6 +66,35 @@ def main():
                                                    P.gview("en_layers.0.conv.layer.weight"),
                                                    P.gview("en_layers.0.conv.layer.bias"), b.ws),
     }
+    for lv, (gin, outb, ey) in enumerate([(b.g_dec_up[3], b.dpre_dec[2], b.dec_out[2]),
+                                           (b.g_dec_up[2], b.dpre_dec[1], b.dec_out[1]),
+                                           (b.g_dec_up[1], b.dpre_dec[0], b.dec_out[0]),
+                                           (b.g_dec_up[0], b.dh, None)]):
+        cases[f"spmm_up{lv}T_s"] = (lambda lv=lv, gin=gin, outb=outb, ey=ey: ops.spmm(
+            T.upT_csr[lv], gin, T.n_verts[lv + 1], elu_y=ey, out=outb, order=T.upT_order[lv]))
+    cases["fwd_d2"] = lambda: ops.spiral_conv_fwd(b.dec_up[2], T.spiral[1], *eng._dec_w(2), 1, out=b.dec_out[2],
+                                                  workspace=b.ws)
+    # coarse decoder / encoder layers (latency-shaped kernels)
+    w0, b0 = eng._dec_w(0)
+    w1, b1 = eng._dec_w(1)
+    for t in (b.dec_up[0], b.dec_up[1], b.dpre_dec[0], b.dpre_dec[1], b.enc_out[0], b.dpre_enc[1]):
+        t.copy_(torch.randn(t.shape, device="cuda", generator=g))
+    cases["fwd_d0"] = lambda: ops.spiral_conv_fwd(b.dec_up[0], T.spiral[3], w0, b0, 1, out=b.dec_out[0], workspace=b.ws)
+    cases["dx_d0"] = lambda: ops.spiral_conv_bwd_data(b.dpre_dec[0], T.spiral_inv[3], w0, T.n_verts[3],
+                                                      out=b.g_dec_up[0], workspace=b.ws)
+    cases["dw_d0"] = lambda: ops.spiral_conv_bwd_weight(b.dec_up[0], T.spiral[3], b.dpre_dec[0],
+                                                       P.gview("de_layers.1.conv.layer.weight"),
+                                                       P.gview("de_layers.1.conv.layer.bias"), b.ws)
+    cases["fwd_d1"] = lambda: ops.spiral_conv_fwd(b.dec_up[1], T.spiral[2], w1, b1, 1, out=b.dec_out[1], workspace=b.ws)
+    cases["pair_d1"] = lambda: ops.spiral_conv_bwd(b.dec_up[1], T.spiral[2], b.dpre_dec[1], T.spiral_inv[2], w1,
+                                                   P.gview("de_layers.2.conv.layer.weight"),
+                                                   P.gview("de_layers.2.conv.layer.bias"), dx=b.g_dec_up[1],
+                                                   workspace=b.ws_dw[("dec", 1)])
+    we1, be1 = eng._enc_w(1)
+    cases["fwd_e1"] = lambda: ops.spiral_conv_fwd(b.enc_out[0], T.enc_rows[1], we1, be1, 1, out=b.enc_out[1], workspace=b.ws)
+    cases["rowsub_e1"] = lambda: ops.spiral_conv_bwd_rowsub(b.enc_out[0], T.enc_rows[1], b.dpre_enc[1], T.enc_flat[1],
+                                                            we1, None, None, dx=b.dpre_enc[0], elu_y=b.enc_out[0],
+                                                            workspace=b.ws_dw[("enc", 1)])
     self_idx = torch.arange(T.n_verts[0], dtype=torch.int32, device="cuda").view(-1, 1).repeat(1, 9).contiguous()
     shift_idx = ((torch.arange(T.n_verts[0], device="cuda").view(-1, 1) + torch.arange(9, device="cuda").view(1, -1))
                  % T.n_verts[0]).to(torch.int32).contiguous()

@@ -1233,11 +1233,11 @@ __global__ __launch_bounds__(256) void conv_bwd_rowsub_pair(const DgArgs a, cons
 // broadcast), every dG load is an unconditional buffer load (an absent entry
 // is an out-of-range offset: 0.0, no memory access), all in flight together;
 // summed in list order; elu'(elu_y) epilogue.
-template <int CIN, int G>
+template <int CIN, int G, typename TY = float>
 __global__ __launch_bounds__(256) void conv_dx_rowsub_gather(const float* __restrict__ dg,
                                                              const int4* __restrict__ flat,
-                                                             const float* __restrict__ elu_y,
-                                                             float* __restrict__ dx, int vsrc,
+                                                             const TY* __restrict__ elu_y,
+                                                             TY* __restrict__ dx, int vsrc,
                                                              int rows, int total_src,
                                                              int dg_bytes) {
   constexpr int Q = CIN / 4;
@@ -1263,13 +1263,13 @@ __global__ __launch_bounds__(256) void conv_dx_rowsub_gather(const float* __rest
 #pragma unroll
   for (int k = 1; k < 4 * G; ++k) s += v[k];
   if (elu_y) {
-    const f32x4 y = ld4(elu_y + (long)m * CIN + 4 * q);
+    const f32x4 y = ld4f(elu_y + (long)m * CIN + 4 * q);
     s.x *= elu_grad_from_out(y.x);
     s.y *= elu_grad_from_out(y.y);
     s.z *= elu_grad_from_out(y.z);
     s.w *= elu_grad_from_out(y.w);
   }
-  st4(dx + (long)m * CIN + 4 * q, s);
+  st4f(dx + (long)m * CIN + 4 * q, s);  // bf16 storage: one rounding of the fp32 sum
 }
 
 // Batched weight-gradient reduction: ONE launch reduces the deferred slab
@@ -2306,7 +2306,10 @@ DwGeom dw_geom(int batch, int rows, int cin, int cout) {
     g.kind = kDwMfma;
     const long n_tiles = (M + 31) / 32;
     long gx = (n_tiles + 3) / 4;  // >= 4 tiles per block keeps the slab traffic bounded
-    if (gx > 768) gx = 768;       // 3 blocks of 9 waves per CU
+#ifndef CFSD_DW_MAX_WG
+#define CFSD_DW_MAX_WG 512  // (768: same time, 1.5x the slab traffic)
+#endif
+    if (gx > CFSD_DW_MAX_WG) gx = CFSD_DW_MAX_WG;  // 2 blocks of 9 waves per CU
     g.gx = (int)(gx > 0 ? gx : 1);
     g.ws_floats = (size_t)g.gx * dw_units(cin, cout) * 1024 + (size_t)g.gx * cout;
   } else if (cin <= 3 && (cout == 32 || cout == 64)) {
@@ -2619,6 +2622,61 @@ extern "C" int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, c
   RSG(32, 1) RSG(32, 2) RSG(32, 3) RSG(32, 4)
 #undef RSG
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub: unsupported channels %d -> %d", cin, cout);
+}
+
+extern "C" size_t cfsd_spiral_conv_bwd_data_rowsub_workspace(int batch, int rows, int seq, int cin) {
+  if (batch <= 0 || rows <= 0 || seq != kSeq || cin != 32) return 0;
+  return rowsub_dg_floats(batch, rows, cin) * sizeof(float);
+}
+
+extern "C" int cfsd_spiral_conv_bwd_data_rowsub(const float* dpre, const int32_t* inv_flat,
+                                                int flat_width, const float* w, const void* elu_y,
+                                                void* dx, int dx_dt, float* workspace,
+                                                size_t workspace_bytes, int batch, int vsrc, int rows,
+                                                int seq, int cin, int cout, void* stream) {
+  int rc = check_conv_args(dpre, inv_flat, w, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!dx || !workspace) return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_rowsub: null dx / workspace");
+  if (!rowsub_shape(cin, cout))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_rowsub: unsupported channels %d -> %d", cin, cout);
+  if (dx_dt != CFSD_DT_F32 && dx_dt != CFSD_DT_BF16) return set_error(CFSD_EINVAL, "bad dx dtype %d", dx_dt);
+  if (flat_width <= 0 || flat_width > 16 || flat_width % 4)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_rowsub: flat_width %d not in {4, 8, 12, 16}", flat_width);
+  if ((uintptr_t)inv_flat & 15) return set_error(CFSD_EINVAL, "inv_flat must be 16-B aligned");
+  const size_t dg_el = (size_t)batch * rows * kSeq * cin;
+  if (workspace_bytes < rowsub_dg_floats(batch, rows, cin) * sizeof(float))
+    return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes,
+                     rowsub_dg_floats(batch, rows, cin) * sizeof(float));
+  if (dg_el * sizeof(float) >= (size_t)kAbsentRow)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_rowsub: dG exceeds 32-bit buffer offsets");
+  hipStream_t st = (hipStream_t)stream;
+  const int total = batch * rows;
+  DgArgs a{dpre, w, workspace, total, rowsub_groups((total + 15) / 16, kSeq * cin / 16), 0};
+  a.nb = (int)(((total + 15) / 16 + 3) / 4) * a.n_groups;
+  DwLatArgs d{};  // no dW half
+  if (cout == 32)
+    hipLaunchKernelGGL((conv_bwd_rowsub_pair<32, 32>), dim3(a.nb), dim3(256),
+                       (dg_lds_floats<32, 32>(a.n_groups) * sizeof(float)), st, a, d);
+  else
+    hipLaunchKernelGGL((conv_bwd_rowsub_pair<32, 64>), dim3(a.nb), dim3(256),
+                       (dg_lds_floats<32, 64>(a.n_groups) * sizeof(float)), st, a, d);
+  if ((rc = launch_status("spiral_conv_bwd_data_rowsub_dg"))) return rc;
+  const long threads = (long)batch * vsrc * (cin / 4);
+  const dim3 gg((unsigned)((threads + 255) / 256));
+  const int G = flat_width / 4, M = batch * vsrc, dgb = (int)(dg_el * sizeof(float));
+#define RSG2(G_)                                                                                   \
+  if (G == G_) {                                                                                   \
+    if (dx_dt == CFSD_DT_BF16)                                                                     \
+      hipLaunchKernelGGL((conv_dx_rowsub_gather<32, G_, bf16_t>), gg, dim3(256), 0, st, workspace, \
+                         (const int4*)inv_flat, (const bf16_t*)elu_y, (bf16_t*)dx, vsrc, rows, M, dgb); \
+    else                                                                                           \
+      hipLaunchKernelGGL((conv_dx_rowsub_gather<32, G_, float>), gg, dim3(256), 0, st, workspace,  \
+                         (const int4*)inv_flat, (const float*)elu_y, (float*)dx, vsrc, rows, M, dgb); \
+    return launch_status("spiral_conv_bwd_data_rowsub_gather");                                   \
+  }
+  RSG2(1) RSG2(2) RSG2(3) RSG2(4)
+#undef RSG2
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_rowsub: bad flat_width");
 }
 
 extern "C" int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, int batch,

@@ -378,6 +378,13 @@ class SDVAEEngine:
             ws = max(ws, ops.spiral_conv_workspace(bsz, nv[lv], nv[lv], T.seq[lv], cin, cout))
         ws = max(ws, ops.spiral_conv_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
         ws = max(ws, ops.spiral_conv_bwd_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
+        # bf16 Enblocks whose dpre is fp32: dx by the row-subset dG + gather
+        b.rowsub_x = {}
+        for (cin, cout, lv) in S.enc_layers():
+            if lv in lp and lv > 0 and T.enc_select[lv] and T.enc_flat[lv] is not None and lv + 1 not in lp:
+                need = ops.spiral_conv_bwd_data_rowsub_workspace(bsz, nv[lv + 1], T.seq[lv], cin)
+                b.rowsub_x[lv] = need > 0
+                ws = max(ws, need)
         b.ws = torch.empty(ws // 4 + 64, dtype=torch.float32, device=dev)
         # weight-gradient partials: one region per layer, all reduced by ONE
         # cfsd_dw_reduce_batch launch at the end of the backward
@@ -656,7 +663,13 @@ class SDVAEEngine:
             if lv in self.lp_levels:  # bf16 operands (selection down-sampling)
                 defer(ops.spiral_conv_bwd_weight_x(x_in, rows_tab, b.dpre_enc[lv], None, None,
                                                    b.ws_dw[("enc", lv)]), f"en_layers.{lv}.conv.layer")
-                if lv > 0:
+                if lv > 0 and b.dpre_enc[lv].dtype == torch.float32 and b.rowsub_x.get(lv):
+                    # fp32 dpre: dG = dpre.W at the kept rows (fp32), then the
+                    # flat gather rounded once to bf16
+                    ops.spiral_conv_bwd_data_rowsub(b.dpre_enc[lv], T.enc_flat[lv], w, T.n_verts[lv],
+                                                    elu_y=b.enc_out[prev], out=b.dpre_enc[prev],
+                                                    workspace=b.ws)
+                elif lv > 0:
                     ops.spiral_conv_bwd_data_x(b.dpre_enc[lv], T.enc_inv[lv],
                                                self._w16(f"en_layers.{lv}.conv.layer.weight"), T.n_verts[lv],
                                                elu_y=b.enc_out[prev], out=b.dpre_enc[prev])

@@ -233,6 +233,31 @@ def spiral_conv_bwd_rowsub(x, idx, dpre, flat, w, dw, db, dx, elu_y=None, worksp
     return dx
 
 
+def spiral_conv_bwd_data_rowsub_workspace(bsz, rows, seq, cin):
+    return int(_abi.lib().cfsd_spiral_conv_bwd_data_rowsub_workspace(bsz, rows, seq, cin))
+
+
+def spiral_conv_bwd_data_rowsub(dpre, flat, w, vsrc, elu_y=None, out=None, workspace=None):
+    """dx of a row-subset conv (dG = dpre.W at the kept rows, then the
+    ascending flat gather); ``out``/``elu_y`` fp32 or bf16 (bf16 path)."""
+    bsz, rows, cout = dpre.shape
+    table, width = flat
+    cin = w.shape[1] // 9
+    _need(dpre, None, name="dpre")
+    _need(table, (vsrc, width), torch.int32, "inv_flat")
+    _need(w, (cout, 9 * cin), name="w")
+    _needx(out, (bsz, vsrc, cin), "out")
+    if elu_y is not None:
+        _need(elu_y, (bsz, vsrc, cin), out.dtype, "elu_y")
+    need = spiral_conv_bwd_data_rowsub_workspace(bsz, rows, 9, cin)
+    if need == 0:
+        raise ValueError(f"no row-subset backward for {cin} -> {cout} channels")
+    ws, nb = _conv_ws(workspace, dpre.device, need)
+    call("cfsd_spiral_conv_bwd_data_rowsub", ptr(dpre), ptr(table), width, ptr(w), ptr(elu_y), ptr(out),
+         _dt(out), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, 9, cin, cout, stream_ptr())
+    return out
+
+
 def spiral_gather(x, idx, out=None):
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape

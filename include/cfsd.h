@@ -145,6 +145,18 @@ int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, const float*
                                 float* workspace, size_t workspace_bytes, int batch, int vsrc,
                                 int rows, int seq, int cin, int cout, void* stream);
 
+/* dx alone of the row-subset backward (as cfsd_spiral_conv_bwd_rowsub):
+ * dG = dpre.W (fp32 dpre and W, fp32 MFMA) in `workspace`
+ * (cfsd_spiral_conv_bwd_data_rowsub_workspace() bytes), then the ascending
+ * flat-list gather-sum with elu'(elu_y); dx and elu_y stored as dx_dt
+ * (CFSD_DT_F32 or CFSD_DT_BF16: one rounding of the fp32 sum).  Used by the
+ * bf16 path, whose dW comes from cfsd_spiral_conv_bwd_weight_x. */
+size_t cfsd_spiral_conv_bwd_data_rowsub_workspace(int batch, int rows, int seq, int cin);
+int cfsd_spiral_conv_bwd_data_rowsub(const float* dpre, const int32_t* inv_flat, int flat_width,
+                                     const float* w, const void* elu_y, void* dx, int dx_dt,
+                                     float* workspace, size_t workspace_bytes, int batch, int vsrc,
+                                     int rows, int seq, int cin, int cout, void* stream);
+
 /* Materialising spiral gather, g[b,r,s*cin+c] = x[b, idx[r,s], c]
  * (model.py:34 index_select + view).  Used as the HBM-roofline probe. */
 int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, int batch, int vsrc, int rows,

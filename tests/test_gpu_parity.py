@@ -681,3 +681,26 @@ def test_rowsub_backward(otopo, dtopo, level, cout, bsz, elu, deferred):
     ops.spiral_conv_bwd_rowsub(*args, dw, db, dx2, elu_y=ey.to(DEV) if elu else None, workspace=ws)
     assert torch.equal(dx, dx2)
 
+
+
+@pytest.mark.parametrize("level,cout", [(1, 32), (2, 32), (3, 64)])
+def test_rowsub_data_bf16_storage(dtopo, level, cout):
+    """dx-only row-subset backward: bf16 storage = one rounding of the fp32
+    result (same dG, same gather order), so it equals the fp32 call cast."""
+    bsz = 16
+    g = torch.Generator().manual_seed(level + cout)
+    v, rows = dtopo.n_verts[level], dtopo.n_verts[level + 1]
+    dpre = torch.randn(bsz, rows, cout, generator=g).to(DEV)
+    w = (torch.randn(cout, 288, generator=g) * 0.1).to(DEV)
+    ey16 = O.elu(torch.randn(bsz, v, 32, generator=g)).to(DEV, torch.bfloat16)
+    d32 = torch.empty(bsz, v, 32, device=DEV)
+    d16 = torch.empty(bsz, v, 32, device=DEV, dtype=torch.bfloat16)
+    ops.spiral_conv_bwd_data_rowsub(dpre, dtopo.enc_flat[level], w, v, elu_y=ey16.float(), out=d32)
+    ops.spiral_conv_bwd_data_rowsub(dpre, dtopo.enc_flat[level], w, v, elu_y=ey16, out=d16)
+    assert torch.equal(d16, d32.to(torch.bfloat16))
+    # and the fp32 dx equals the fused rowsub backward's dx
+    x = torch.randn(bsz, v, 32, generator=g).to(DEV)
+    dxf = torch.empty_like(d32)
+    ops.spiral_conv_bwd_rowsub(x, dtopo.enc_rows[level], dpre, dtopo.enc_flat[level], w, None, None, dxf,
+                               elu_y=ey16.float())
+    assert torch.equal(dxf, d32)

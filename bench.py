@@ -180,6 +180,23 @@ def launch_cost(name, a):
         if dx:
             by += f4 * B * vs * ci * (2 if elu else 1) + 16 * vs * S
         return fl, by, FP32_PEAK_TFLOPS
+    if name == "cfsd_spiral_conv_bwd_rowsub":  # dx (dG + gather) and dW of a row-subset conv
+        B, vs, rows, S, ci, co = a[12:18]
+        elu = a[6] is not None
+        return (4.0 * B * rows * S * ci * co,
+                f4 * (B * vs * ci * (2 if elu else 1) + B * vs * ci + B * rows * co + co * S * ci) + 4 * rows * S
+                + 4 * vs * a[4], FP32_PEAK_TFLOPS)
+    if name == "cfsd_spiral_conv_bwd_data_rowsub":
+        B, vs, rows, S, ci, co = a[9:15]
+        sd = 4 if a[6] == 0 else 2
+        elu = a[4] is not None
+        return (2.0 * B * rows * S * ci * co, f4 * (B * rows * co + co * S * ci) + sd * B * vs * ci * (2 if elu else 1)
+                + 4 * vs * a[2], FP32_PEAK_TFLOPS)
+    if name == "cfsd_spmm_csr_sched":
+        sx, sy = (4 if a[5] == 0 else 2), (4 if a[8] == 0 else 2)
+        B, m, n, c = a[9:13]
+        elu = a[6] is not None
+        return 0.0, B * c * (sx * n + sy * m * (2 if elu else 1)), None
     if name == "cfsd_spiral_conv_fwd_x":
         sx, sy = (4 if a[1] == 0 else 2), (4 if a[7] == 0 else 2)
         B, vs, rows, S, ci, co = a[8:14]

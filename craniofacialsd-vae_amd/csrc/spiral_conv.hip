@@ -1186,23 +1186,24 @@ __device__ __forceinline__ void conv_dg_body(int vb, int vnb, const DgArgs& g, f
   }
   __syncthreads();
   if (rt * 16 >= g.total_rows) return;
-  const int mo0 = rt * 16 + 4 * kg;
+  // transposed orientation: D[i = n][j = row] (A = W^T from LDS, B = dpre),
+  // so a lane's 4 accumulator values are dG[row j][n 4kg .. 4kg+3], one 16-B
+  // store (the [row][n] orientation needed 4 dword stores per lane)
+  const int row_out = rt * 16 + j;
+  float* out = g.dg + (long)row_out * K + n0 + 4 * kg;
   for (int nt = 0; nt < ntg; ++nt) {
     const float* bp = wl + (nt * 16 + j) * LDW + kg * KP;
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int q = 0; q < KP / 4; ++q) {
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(bp + 4 * q);
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(bp + 4 * q);
       f32x4& ac = acc[q & 1];
-      ac = mfma16(a[q].x, bv.x, ac);
-      ac = mfma16(a[q].y, bv.y, ac);
-      ac = mfma16(a[q].z, bv.z, ac);
-      ac = mfma16(a[q].w, bv.w, ac);
+      ac = mfma16(wv.x, a[q].x, ac);
+      ac = mfma16(wv.y, a[q].y, ac);
+      ac = mfma16(wv.z, a[q].z, ac);
+      ac = mfma16(wv.w, a[q].w, ac);
     }
-    float* out = g.dg + (long)mo0 * K + n0 + nt * 16 + j;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
-      if (mo0 + rr < g.total_rows) out[(long)rr * K] = acc[0][rr] + acc[1][rr];
+    if (row_out < g.total_rows) st4(out + nt * 16, acc[0] + acc[1]);
   }
 }
 

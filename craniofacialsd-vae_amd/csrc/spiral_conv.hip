@@ -586,9 +586,18 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
     for (int sl = 0; sl < FSB; ++sl)
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
+#ifdef CFSD_EXP_NOA
+        av[sl][c] = ld4(xb + 16 * c);
+#else
         av[sl][c] = ld4(xb + (long)src[s0 + sl] * CIN + 16 * c);
+#endif
 #pragma unroll
-        for (int t = 0; t < CTW; ++t) bw[sl][c][t] = ld4(wb + (long)t * 16 * K + (s0 + sl) * CIN + 16 * c);
+        for (int t = 0; t < CTW; ++t)
+#ifdef CFSD_EXP_NOW
+          bw[sl][c][t] = ld4(w + 4 * kg + 16 * c);
+#else
+          bw[sl][c][t] = ld4(wb + (long)t * 16 * K + (s0 + sl) * CIN + 16 * c);
+#endif
       }
     // keep the batch's loads ahead of its MFMAs (hipcc otherwise interleaves
     // them with vmcnt waits to save registers, re-exposing the latency)
@@ -2076,14 +2085,19 @@ static int dispatch_fwd_mfma(const float* x, const int* idx, const float* w, con
                              float* y, float* ws, size_t ws_floats, int vsrc, int rows, long M,
                              hipStream_t st) {
   // (64 -> 32 excepted: measured slower there than slot groups + combine)
-  if (M < CFSD_LAT_FWD_MAX && !(CIN == 64 && COUT == 32)) {
+#ifndef CFSD_FWD_LAT_6432
+#define CFSD_FWD_LAT_6432 0
+#endif
+  if (M < CFSD_LAT_FWD_MAX && (CFSD_FWD_LAT_6432 || !(CIN == 64 && COUT == 32))) {
 #ifndef CFSD_FWD_LAT_CTW
 #define CFSD_FWD_LAT_CTW 1
 #endif
     // one wave per column tile: sharing the A gathers across both 32 -> 32
     // column tiles (CTW 2) measured slower here (E1 16.8 vs 16.1 us, E2 11.0
     // vs 7.8 us, same-box A/B) -- unlike the dx, whose A is a list gather-sum
-    constexpr int ctw = (CIN == 32 && COUT == 32) ? CFSD_FWD_LAT_CTW : 1;
+    // 64 -> 64 (the level-3 Deblock): two column tiles per wave, each A
+    // gather feeding twice the MFMAs (D0 forward 19.1 -> 16.3 us)
+    constexpr int ctw = (CIN == 32 && COUT == 32) ? CFSD_FWD_LAT_CTW : (CIN == 64 ? 2 : 1);
     const long tasks = (M + 15) / 16 * (COUT / 16 / ctw);
     hipLaunchKernelGGL((conv_fwd_lat<CIN, COUT, ACT, ctw>), dim3((unsigned)((tasks + 3) / 4)),
                        dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M);
@@ -2197,7 +2211,17 @@ static bool dx_is_lat(long m_dx, long dpre_rows) {
 // 32 -> 32 with >= 32k rows: one wave covers both 16-column tiles (the list
 // gathers are shared instead of repeated per column tile; measured E1 dx
 // 33 -> 29 us; the fewer, fatter waves lose on the smaller levels)
+#ifndef CFSD_DX_LAT_CTW64
+#define CFSD_DX_LAT_CTW64 2
+#endif
+#ifndef CFSD_DX_LAT_CTW6432
+#define CFSD_DX_LAT_CTW6432 2
+#endif
 static int dx_lat_ctw(int cin, int cout, long m_dx) {
+  // 64-wide inputs: two column tiles per wave share the list gather-sums
+  // (D0 dx 18.6 -> 15.2 us; the D1 paired backward 40.7 -> 36.9 us)
+  if (cin == 64 && cout == 64) return CFSD_DX_LAT_CTW64;
+  if (cin == 64 && cout == 32) return CFSD_DX_LAT_CTW6432;
   return (cin == 32 && cout == 32 && m_dx >= 32768) ? 2 : 1;
 }
 
@@ -2208,8 +2232,9 @@ static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* in
                             hipStream_t st) {
   if (dx_is_lat(M, M / vsrc * rows)) {
     if (dx_lat_ctw(CIN, COUT, M) == 2) {
-      const long tasks = (M + 15) / 16;
-      hipLaunchKernelGGL((conv_dx_lat<CIN, COUT, CIN / 16>), dim3((unsigned)((tasks + 3) / 4)), dim3(256),
+      constexpr int CTW2 = CIN / 16 >= 2 ? 2 : 1;
+      const long tasks = (M + 15) / 16 * (CIN / 16 / CTW2);
+      hipLaunchKernelGGL((conv_dx_lat<CIN, COUT, CTW2>), dim3((unsigned)((tasks + 3) / 4)), dim3(256),
                          0, st, dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M);
       return launch_status("spiral_conv_bwd_data_lat");
     }
@@ -2498,7 +2523,7 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
                        dim3(1024), 0, st, workspace, ws_db, dw, db, g.gx);                      \
     return launch_status("spiral_conv_bwd_weight_reduce");                                      \
   }
-    PAIR(32, 32, 1) PAIR(32, 32, 2) PAIR(64, 32, 1)
+    PAIR(32, 32, 1) PAIR(32, 32, 2) PAIR(64, 32, 1) PAIR(64, 32, 2)
 #undef PAIR
     return set_error(CFSD_EINVAL, "spiral_conv_bwd: unsupported channels %d -> %d", cin, cout);
   }

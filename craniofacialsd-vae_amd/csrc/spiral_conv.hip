@@ -1302,17 +1302,23 @@ struct DwRedBatch {
   int n;
 };
 
+// Items whose slab length is a multiple of 4 (every conv_dw_mfma / lat
+// item: U*1024 + cout) are reduced four consecutive elements per lane with
+// 16-B loads (256 elements per workgroup); the others (small-channel slabs)
+// one element per lane.  Same per-element summation order either way.
 __global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
   int li = 0;
   while (li + 1 < B.n && (int)blockIdx.x >= B.it[li + 1].blk0) ++li;
   const DwRedItem d = B.it[li];
-  __shared__ float part[16][64];
+  __shared__ f32x4 part[16][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int f = ((int)blockIdx.x - d.blk0) * 64 + lane;
-  const bool valid = f < d.n_el;
-  if (!valid) f = d.n_el - 1;
   const int K = kSeq * d.cin;
   const int nw = d.n_el - d.cout;  // kind 0: dW part of a slab
+  const bool vec = d.kind == 0;     // n_el, nw and cout are multiples of 4
+  const int per_blk = vec ? 256 : 64;
+  int f = ((int)blockIdx.x - d.blk0) * per_blk + (vec ? 4 * lane : lane);
+  const bool valid = f < d.n_el;
+  if (!valid) f = vec ? d.n_el - 4 : d.n_el - 1;
   const float* src;
   long stride;
   if (d.kind == 0) {
@@ -1323,38 +1329,50 @@ __global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
     stride = d.n_el;
   }
   // slabs p = wv, wv + 16, ... summed in that order; 16 loads in flight per
-  // batch (the level-0 items have ~768 slabs: 48 per wave, which as a
-  // 4-unrolled chain was 12 memory latencies back to back)
-  float sum = 0.f;
+  // batch (the level-0 items have ~512 slabs: 32 per wave)
+  f32x4 sum = {0.f, 0.f, 0.f, 0.f};
   int p = wv;
-#ifndef CFSD_RED_BATCH
-#define CFSD_RED_BATCH 1
-#endif
-  for (; CFSD_RED_BATCH && p + 16 * 15 < d.n_slabs; p += 16 * 16) {
-    float t[16];
+  if (vec) {
+    for (; p + 16 * 15 < d.n_slabs; p += 16 * 16) {
+      f32x4 t[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) t[j] = src[(long)(p + 16 * j) * stride];
+      for (int j = 0; j < 16; ++j) t[j] = ld4(src + (long)(p + 16 * j) * stride);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) sum += t[j];
+      for (int j = 0; j < 16; ++j) sum += t[j];
+    }
+    for (; p < d.n_slabs; p += 16) sum += ld4(src + (long)p * stride);
+  } else {
+    for (; p + 16 * 15 < d.n_slabs; p += 16 * 16) {
+      float t[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) t[j] = src[(long)(p + 16 * j) * stride];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) sum.x += t[j];
+    }
+    for (; p < d.n_slabs; p += 16) sum.x += src[(long)p * stride];
   }
-  for (; p < d.n_slabs; p += 16) sum += src[(long)p * stride];
   part[wv][lane] = sum;
   __syncthreads();
   if (wv == 0 && valid) {
-    float t = part[0][lane];
+    f32x4 t = part[0][lane];
 #pragma unroll
     for (int q = 1; q < 16; ++q) t += part[q][lane];
-    if (f >= nw) {
-      d.db[f - nw] = t;
-    } else if (d.kind == 0) {
+    if (!vec) {
+      if (f >= nw) d.db[f - nw] = t.x;
+      else d.dw[f] = t.x;
+    } else if (f >= nw) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d.db[f - nw + e] = t[e];
+    } else {
+      // 4 consecutive elements of one 32-wide unit row: 4 consecutive c
       const int CT = d.cin / 32, OT = d.cout / 32;
       const int un = f >> 10, within = f & 1023;
       const int cc = (un % CT) * 32 + (within & 31);
       const int o = ((un / CT) % OT) * 32 + (within >> 5);
       const int sl = un / (CT * OT);
-      d.dw[(long)o * K + sl * d.cin + cc] = t;
-    } else {
-      d.dw[f] = t;
+      float* dst = d.dw + (long)o * K + sl * d.cin + cc;  // 8-B aligned in the flat buffer
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[e] = t[e];
     }
   }
 }
@@ -2943,7 +2961,7 @@ extern "C" int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* str
       }
     }
     d.blk0 = blk;
-    blk += (d.n_el + 63) / 64;
+    blk += d.kind == 0 ? (d.n_el + 255) / 256 : (d.n_el + 63) / 64;
   }
   hipLaunchKernelGGL(dw_reduce_batch_k, dim3(blk), dim3(1024), 0, (hipStream_t)stream, B);
   return launch_status("dw_reduce_batch");

@@ -246,6 +246,9 @@ def launch_cost(name, a):
         fl = 2.0 * m * k * n * (int(dx) + int(dw))
         by = f4 * (m * n + n * k + m * k * (int(dx) + int(dw) + int(elu)) + n * k * int(dw))
         return fl, by, FP32_PEAK_TFLOPS
+    if name == "cfsd_linear_bwd_split":
+        m, k, n = a[6:9]
+        return 4.0 * m * k * n, f4 * (m * n + 2 * n * k + m * k), FP32_PEAK_TFLOPS
     if name == "cfsd_adam":
         n = a[5].value if hasattr(a[5], "value") else a[5]
         return 0.0, 7.0 * f4 * n, None

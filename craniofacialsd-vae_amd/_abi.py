@@ -40,6 +40,9 @@ SIGNATURES = {
     "cfsd_spiral_conv_bwd_data_rowsub": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _Z, _I, _I, _I, _I, _I, _I,
                                               _P]),
     "cfsd_spiral_conv_bwd_data_rowsub_workspace": (_Z, [_I, _I, _I, _I]),
+    "cfsd_linear_bwd_split_parts": (_I, [_I]),
+    "cfsd_linear_bwd_split": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "cfsd_latent_bwd_parts": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_gather": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spmm_csr_sched": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spmm_csr": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),

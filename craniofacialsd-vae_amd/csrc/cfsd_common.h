@@ -120,6 +120,27 @@ __device__ __forceinline__ f32x4 mfma_bf16(u32x4 a, u32x4 b, f32x4 c) {
                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
+// Cooperative global -> LDS copy of n items: item e is loaded by ld(e) and
+// stored by st(e, v), NB loads per thread issued before the first store.  (A
+// load -> store loop waits out one memory latency per item; these copies open
+// the persistent kernels, where every workgroup pays them at once.)
+template <int NB, typename T, typename LD, typename ST>
+__device__ __forceinline__ void coop_copy(int n, LD ld, ST st) {
+  for (int e0 = threadIdx.x; e0 < n; e0 += NB * (int)blockDim.x) {
+    T v[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int e = e0 + j * (int)blockDim.x;
+      v[j] = ld(e < n ? e : n - 1);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int e = e0 + j * (int)blockDim.x;
+      if (e < n) st(e, v[j]);
+    }
+  }
+}
+
 // Flattened row / element indices are < 2^31 (checked at every entry point),
 // so per-thread index splits use 32-bit division: a 64-bit division is a
 // ~100-instruction software sequence on CDNA, which showed up as VALU time

@@ -55,10 +55,9 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = blockIdx.y, s0 = g * SPG;
-  for (int e = threadIdx.x; e < COUT * (KG / 4); e += 256) {
-    const int n = e / (KG / 4), k4 = e % (KG / 4);
-    st4(&lds_w[n * KP + 4 * k4], ld4(&w[(long)n * K + s0 * CIN + 4 * k4]));
-  }
+  coop_copy<8, f32x4>(
+      COUT * (KG / 4), [&](int e) { return ld4(&w[(long)(e / (KG / 4)) * K + s0 * CIN + 4 * (e % (KG / 4))]); },
+      [&](int e, f32x4 v) { st4(&lds_w[(e / (KG / 4)) * KP + 4 * (e % (KG / 4))], v); });
   __syncthreads();
   const int r16 = lane & 15, kg = lane >> 4;
   float bn[NCT];
@@ -434,10 +433,9 @@ __global__ __launch_bounds__(256, dx_occ(CIN, COUT)) void conv_dx_mfma(
   const int wave = threadIdx.x >> 6;
   const int g = blockIdx.y, s0 = g * SPG;
   // lds_wt[(sl*CIN + c) * OP + o] = w[o, (s0+sl)*CIN + c]
-  for (int e = threadIdx.x; e < COUT * SPG * CIN; e += 256) {
-    const int o = e / (SPG * CIN), k = e % (SPG * CIN);
-    lds_wt[k * OP + o] = w[(long)o * K + s0 * CIN + k];
-  }
+  coop_copy<12, float>(
+      COUT * SPG * CIN, [&](int e) { return w[(long)(e / (SPG * CIN)) * K + s0 * CIN + e % (SPG * CIN)]; },
+      [&](int e, float v) { lds_wt[(e % (SPG * CIN)) * OP + e / (SPG * CIN)] = v; });
   __syncthreads();
   const int nbytes = (int)(total_rows / vsrc * rows * RB);
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dpre), 0, nbytes, 0x00020000);
@@ -1185,13 +1183,26 @@ __device__ __forceinline__ void conv_dg_body(int vb, int vnb, const DgArgs& g, f
   // stage the group's W^T (A loads in flight); consecutive threads take
   // consecutive o (conflict-free LDS writes)
   const int n0 = grp * ntg * 16;
-  for (int e = threadIdx.x; e < COUT * ntg * 4; e += blockDim.x) {
-    const int o = e % COUT, n4 = (e / COUT) * 4;
-    const f32x4 v = ld4(g.w + o * K + n0 + n4);
-    wl[(n4 + 0) * LDW + o] = v.x;
-    wl[(n4 + 1) * LDW + o] = v.y;
-    wl[(n4 + 2) * LDW + o] = v.z;
-    wl[(n4 + 3) * LDW + o] = v.w;
+  // (4 loads per thread in flight per batch: a load -> store loop exposed one
+  // memory latency per element)
+  for (int e0 = threadIdx.x; e0 < COUT * ntg * 4; e0 += 4 * (int)blockDim.x) {
+    f32x4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = min(e0 + q * (int)blockDim.x, COUT * ntg * 4 - 1);
+      v[q] = ld4(g.w + (e % COUT) * K + n0 + (e / COUT) * 4);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = e0 + q * (int)blockDim.x;
+      if (e < COUT * ntg * 4) {
+        const int o = e % COUT, n4 = (e / COUT) * 4;
+        wl[(n4 + 0) * LDW + o] = v[q].x;
+        wl[(n4 + 1) * LDW + o] = v[q].y;
+        wl[(n4 + 2) * LDW + o] = v[q].z;
+        wl[(n4 + 3) * LDW + o] = v[q].w;
+      }
+    }
   }
   __syncthreads();
   if (rt * 16 >= g.total_rows) return;

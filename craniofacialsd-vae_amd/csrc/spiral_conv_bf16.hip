@@ -35,10 +35,10 @@ __global__ __launch_bounds__(256) void conv_fwd_b16(const bf16_t* __restrict__ x
                                                     long total_rows) {
   constexpr int K = kS * CIN, KP = K + 8, KC = CIN / 32, NT = COUT / 16;
   extern __shared__ bf16_t lw[];  // [COUT][KP]
-  for (int e = threadIdx.x; e < COUT * K / 8; e += 256) {
-    const int n = e / (K / 8), k8 = e - n * (K / 8);
-    *reinterpret_cast<u32x4*>(&lw[n * KP + 8 * k8]) = *reinterpret_cast<const u32x4*>(&w[n * K + 8 * k8]);
-  }
+  coop_copy<8, u32x4>(
+      COUT * K / 8,
+      [&](int e) { return *reinterpret_cast<const u32x4*>(&w[(e / (K / 8)) * K + 8 * (e % (K / 8))]); },
+      [&](int e, u32x4 v) { *reinterpret_cast<u32x4*>(&lw[(e / (K / 8)) * KP + 8 * (e % (K / 8))]) = v; });
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;
@@ -123,10 +123,8 @@ __global__ __launch_bounds__(256) void conv_dx_b16(const TD* __restrict__ dpre,
   constexpr int K = kS * CIN, OP = COUT + 8, OC = COUT / 32, NT = CIN / 16;
   constexpr int RB = COUT * (int)sizeof(TD);  // dpre row bytes
   extern __shared__ bf16_t lwt[];             // [kS*CIN][OP]: lwt[k*OP + o] = w[o*K + k]
-  for (int e = threadIdx.x; e < COUT * K; e += 256) {
-    const int o = e / K, k = e - o * K;
-    lwt[k * OP + o] = w[e];
-  }
+  coop_copy<12, bf16_t>(
+      COUT * K, [&](int e) { return w[e]; }, [&](int e, bf16_t v) { lwt[(e % K) * OP + e / K] = v; });
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;

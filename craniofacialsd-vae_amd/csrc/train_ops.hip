@@ -351,11 +351,22 @@ __global__ __launch_bounds__(256) void latent_bwd_k(const float* __restrict__ mu
                                                     const float* __restrict__ dlat,
                                                     float* __restrict__ dmulv, int B, int L,
                                                     int train, int is_vae, int sigmoid,
-                                                    const float* __restrict__ zval) {
+                                                    const float* __restrict__ zval, int n_parts) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B * L) return;
   const int i = e / L, l = e % L;
-  const float dz = dz_dec[e] + dlat[i * 3 * L + l];
+  float dzd = dz_dec[e];
+  // decoder-Linear dx as split partial products: summed here in slice order,
+  // 16 loads in flight per batch (a load-add chain per part was 4x slower)
+  for (int p0 = 1; p0 < n_parts; p0 += 16) {
+    float t[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = dz_dec[(long)min(p0 + j, n_parts - 1) * B * L + e];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (p0 + j < n_parts) dzd += t[j];
+  }
+  const float dz = dzd + dlat[i * 3 * L + l];
   if (is_vae) {
     const float lv = mulv[i * 2 * L + l];
     const float dmu = dz + dlat[i * 3 * L + L + l];
@@ -497,18 +508,18 @@ __global__ __launch_bounds__(256) void linear_fwd_nred(const float* __restrict__
 // quad (blockIdx.y) with dy staged in LDS and W[c][k] coalesced (all of a
 // wave's W loads in flight together); the 4 wave partials are added in order.
 constexpr int kLinDxChunk = 40;  // c terms per wave and pass
-__global__ __launch_bounds__(256) void linear_dx_nsmall(const float* __restrict__ dy,
-                                                        const float* __restrict__ w,
-                                                        const float* __restrict__ elu_y,
-                                                        float* __restrict__ dx, int m, int k,
-                                                        int n, int accumulate) {
+__device__ __forceinline__ void linear_dx_nsmall_body(int bx, int by, const float* __restrict__ dy,
+                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ elu_y,
+                                                      float* __restrict__ dx, int m, int k, int n,
+                                                      int accumulate) {
   __shared__ float ds[4 * kLinSmallK];
   __shared__ float part[4][4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i0 = blockIdx.y * 4, mr = min(4, m - i0);
+  const int i0 = by * 4, mr = min(4, m - i0);
   for (int e = threadIdx.x; e < mr * n; e += 256) ds[e] = dy[(long)i0 * n + e];
   __syncthreads();
-  const int kk = blockIdx.x * 64 + lane;
+  const int kk = bx * 64 + lane;
   const int kc = kk < k ? kk : k - 1;
   const int per = (n + 3) / 4, c0 = wave * per, c1 = min(n, c0 + per);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -533,6 +544,13 @@ __global__ __launch_bounds__(256) void linear_dx_nsmall(const float* __restrict_
     if (elu_y) v *= elu_grad_from_out(elu_y[o]);
     dx[o] = accumulate ? dx[o] + v : v;
   }
+}
+__global__ __launch_bounds__(256) void linear_dx_nsmall(const float* __restrict__ dy,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ elu_y,
+                                                        float* __restrict__ dx, int m, int k,
+                                                        int n, int accumulate) {
+  linear_dx_nsmall_body(blockIdx.x, blockIdx.y, dy, w, elu_y, dx, m, k, n, accumulate);
 }
 
 // dx, long n (decoder Linear: dz [16 x 75] = dh [16 x 4288] . W [4288 x 75]):
@@ -582,12 +600,11 @@ __global__ __launch_bounds__(kLinRedThreads) void linear_dx_nred(const float* __
 // dw[n,k] = sum_i dy[i,n] x[i,k], db[n] = sum_i dy[i,n]: block row n =
 // blockIdx.y (dy[., n] wave-uniform -> scalar loads), thread per k
 // (coalesced x loads), the m terms unrolled by 16 so their loads overlap.
-__global__ __launch_bounds__(256) void linear_dw_k(const float* __restrict__ x,
-                                                   const float* __restrict__ dy,
-                                                   float* __restrict__ dw,
-                                                   float* __restrict__ db, int m, int k, int n) {
-  const int nn = blockIdx.y;
-  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void linear_dw_body(int bx, int nn, const float* __restrict__ x,
+                                               const float* __restrict__ dy,
+                                               float* __restrict__ dw, float* __restrict__ db,
+                                               int m, int k, int n) {
+  const int kk = bx * blockDim.x + threadIdx.x;
   if (dw && kk < k) {
     float s = 0.f;
     int i = 0;
@@ -601,10 +618,112 @@ __global__ __launch_bounds__(256) void linear_dw_k(const float* __restrict__ x,
     for (; i < m; ++i) s = fmaf(dy[(long)i * n + nn], x[(long)i * k + kk], s);
     dw[(long)nn * k + kk] = s;
   }
-  if (db && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (db && bx == 0 && threadIdx.x == 0) {
     float s = 0.f;
     for (int i = 0; i < m; ++i) s += dy[(long)i * n + nn];
     db[nn] = s;
+  }
+}
+__global__ __launch_bounds__(256) void linear_dw_k(const float* __restrict__ x,
+                                                   const float* __restrict__ dy,
+                                                   float* __restrict__ dw,
+                                                   float* __restrict__ db, int m, int k, int n) {
+  linear_dw_body(blockIdx.x, blockIdx.y, x, dy, dw, db, m, k, n);
+}
+
+// dx and dW of one Linear in ONE launch (independent halves; the horizontal
+// fusion saves a dependent kernel boundary): blocks [0, ndx) run the dx body
+// (dx_nsmall), the rest the dW body.
+constexpr int kLinSplitN = 64;   // rows of W per dx-partial block
+constexpr int kLinSplitK = 128;  // max Linear input width of the split dx
+constexpr int kLinSplitM = 16;   // max batch of the split dx
+// Decoder-Linear backward, one launch of two block kinds:
+//  * blocks [0, ndx): 64-row slices of W ([n][k] row-major, rows contiguous),
+//    W slice + dy's columns staged in LDS with coalesced loads (the
+//    column-per-block nred kernel read W in 4-B pieces at a k-float stride):
+//    dx partial parts[p][i][kk] = sum_{c in slice p} dy[i][c] w[c][kk] (c ascending);
+//  * the rest: 16 rows c of dW per block, dw[c][kk] = sum_i dy[i][c] x[i][kk],
+//    db[c] = sum_i dy[i][c] (i ascending), dy's columns and x staged in LDS.
+constexpr int kLinDwRows = 16;
+// global -> LDS copy of n floats, 8 loads per thread in flight per batch (a
+// load -> store loop exposes one memory latency per element)
+__device__ __forceinline__ void stage_lds(const float* __restrict__ src, float* dst, int n) {
+  constexpr int B = 8;
+  for (int e0 = threadIdx.x; e0 < n; e0 += B * (int)blockDim.x) {
+    float v[B];
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int e = e0 + j * (int)blockDim.x;
+      v[j] = src[e < n ? e : n - 1];
+    }
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int e = e0 + j * (int)blockDim.x;
+      if (e < n) dst[e] = v[j];
+    }
+  }
+}
+__global__ __launch_bounds__(256) void linear_bwd_split_k(const float* __restrict__ x,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ dy,
+                                                          float* __restrict__ parts,
+                                                          float* __restrict__ dw,
+                                                          float* __restrict__ db, int m, int k,
+                                                          int n, int ndx) {
+  __shared__ float wl[kLinSplitN * kLinSplitK];
+  __shared__ float dl[kLinSplitM * kLinSplitN];
+  const int bid = blockIdx.x;
+  if (bid < ndx) {
+    const int c0 = bid * kLinSplitN, nc = min(kLinSplitN, n - c0);
+    stage_lds(w + (long)c0 * k, wl, nc * k);
+    for (int e = threadIdx.x; e < m * kLinSplitN; e += blockDim.x) {
+      const int i = e / kLinSplitN, c = e % kLinSplitN;
+      dl[e] = c < nc ? dy[(long)i * n + c0 + c] : 0.f;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < m * k; e += blockDim.x) {
+      const int i = e / k, kk = e % k;
+      float acc = 0.f;
+      for (int c = 0; c < nc; ++c) acc = fmaf(dl[i * kLinSplitN + c], wl[c * k + kk], acc);
+      parts[(long)bid * m * k + e] = acc;
+    }
+    return;
+  }
+  float* xl = wl;  // [m][k]
+  const int c0 = (bid - ndx) * kLinDwRows, nc = min(kLinDwRows, n - c0);
+  stage_lds(x, xl, m * k);
+  for (int e = threadIdx.x; e < m * kLinDwRows; e += blockDim.x) {
+    const int i = e / kLinDwRows, c = e % kLinDwRows;
+    dl[e] = c < nc ? dy[(long)i * n + c0 + c] : 0.f;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < nc * k; e += blockDim.x) {
+    const int c = e / k, kk = e % k;
+    float acc = 0.f;
+    for (int i = 0; i < m; ++i) acc = fmaf(dl[i * kLinDwRows + c], xl[i * k + kk], acc);
+    dw[(long)c0 * k + e] = acc;
+  }
+  for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+    float acc = 0.f;
+    for (int i = 0; i < m; ++i) acc += dl[i * kLinDwRows + c];
+    db[c0 + c] = acc;
+  }
+}
+__global__ __launch_bounds__(256) void linear_bwd_pair_k(const float* __restrict__ x,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ dy,
+                                                         const float* __restrict__ elu_y,
+                                                         float* __restrict__ dx,
+                                                         float* __restrict__ dw,
+                                                         float* __restrict__ db, int m, int k,
+                                                         int n, int accumulate, int ndx_x,
+                                                         int ndx, int ndw_x) {
+  const int bid = blockIdx.x;
+  if (bid < ndx) {
+    linear_dx_nsmall_body(bid % ndx_x, bid / ndx_x, dy, w, elu_y, dx, m, k, n, accumulate);
+  } else {
+    const int j = bid - ndx;
+    linear_dw_body(j % ndw_x, j / ndw_x, x, dy, dw, db, m, k, n);
   }
 }
 
@@ -832,8 +951,21 @@ extern "C" int cfsd_latent_bwd(const float* mulv, const float* eps, const float*
   if (is_vae && train && !eps) return set_error(CFSD_EINVAL, "latent_bwd: eps required");
   const int n = batch * latent;
   hipLaunchKernelGGL(latent_bwd_k, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, mulv,
-                     eps, dz_dec, dlat, dmulv, batch, latent, train, is_vae, sigmoid, z);
+                     eps, dz_dec, dlat, dmulv, batch, latent, train, is_vae, sigmoid, z, 1);
   return launch_status("latent_bwd");
+}
+
+extern "C" int cfsd_latent_bwd_parts(const float* mulv, const float* eps, const float* z,
+                                     const float* dz_parts, int n_parts, const float* dlat,
+                                     float* dmulv, int batch, int latent, int train, int is_vae,
+                                     int sigmoid, void* stream) {
+  if (!mulv || !dz_parts || !dlat || !dmulv) return set_error(CFSD_EINVAL, "latent_bwd_parts: null pointer");
+  if (n_parts <= 0) return set_error(CFSD_EINVAL, "latent_bwd_parts: n_parts %d", n_parts);
+  if (is_vae && train && !eps) return set_error(CFSD_EINVAL, "latent_bwd_parts: eps required");
+  const int n = batch * latent;
+  hipLaunchKernelGGL(latent_bwd_k, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, mulv,
+                     eps, dz_parts, dlat, dmulv, batch, latent, train, is_vae, sigmoid, z, n_parts);
+  return launch_status("latent_bwd_parts");
 }
 
 extern "C" int cfsd_loss_finalize(const float* partials, int nblocks, const float* terms,
@@ -879,6 +1011,13 @@ extern "C" int cfsd_linear_bwd(const float* x, const float* w, const float* dy, 
   (void)workspace;
   (void)workspace_bytes;
   hipStream_t st = (hipStream_t)stream;
+  const int bt = k >= 256 ? 256 : ((k + 63) / 64) * 64;
+  if (dx && dw && x && w && n <= kLinSmallK && bt == 256) {  // dx + dW in one launch
+    const int ndx_x = (k + 63) / 64, ndx = ndx_x * ((m + 3) / 4), ndw_x = (k + 255) / 256;
+    hipLaunchKernelGGL(linear_bwd_pair_k, dim3(ndx + ndw_x * n), dim3(256), 0, st, x, w, dy,
+                       elu_y, dx, dw, db, m, k, n, accumulate, ndx_x, ndx, ndw_x);
+    return launch_status("linear_bwd_pair");
+  }
   if (dx) {
     if (!w) return set_error(CFSD_EINVAL, "linear_bwd: null w");
     int rc;
@@ -895,12 +1034,25 @@ extern "C" int cfsd_linear_bwd(const float* x, const float* w, const float* dy, 
   }
   if (dw || db) {
     if (dw && !x) return set_error(CFSD_EINVAL, "linear_bwd: null x");
-    const int bt = k >= 256 ? 256 : ((k + 63) / 64) * 64;
     hipLaunchKernelGGL(linear_dw_k, dim3((k + bt - 1) / bt, n), dim3(bt), 0, st, x, dy, dw, db, m,
                        k, n);
     return launch_status("linear_bwd_dw");
   }
   return CFSD_OK;
+}
+
+extern "C" int cfsd_linear_bwd_split_parts(int n) { return n > 0 ? (n + kLinSplitN - 1) / kLinSplitN : 0; }
+
+extern "C" int cfsd_linear_bwd_split(const float* x, const float* w, const float* dy, float* dx_parts,
+                                     float* dw, float* db, int m, int k, int n, void* stream) {
+  if (!x || !w || !dy || !dx_parts || !dw || !db) return set_error(CFSD_EINVAL, "linear_bwd_split: null pointer");
+  if (m <= 0 || k <= 0 || n <= 0 || m > kLinSplitM || k > kLinSplitK)
+    return set_error(CFSD_EINVAL, "linear_bwd_split: sizes m=%d k=%d n=%d (m <= %d, k <= %d)", m, k, n,
+                     kLinSplitM, kLinSplitK);
+  const int ndx = cfsd_linear_bwd_split_parts(n), ndw = (n + kLinDwRows - 1) / kLinDwRows;
+  hipLaunchKernelGGL(linear_bwd_split_k, dim3(ndx + ndw), dim3(256), 0, (hipStream_t)stream, x, w, dy,
+                     dx_parts, dw, db, m, k, n, ndx);
+  return launch_status("linear_bwd_split");
 }
 
 extern "C" int cfsd_adam(float* param, const float* grad, float* m, float* v,

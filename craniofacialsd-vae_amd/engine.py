@@ -357,6 +357,9 @@ class SDVAEEngine:
         b.dpre_dec = [torch.empty_like(t) for t in b.dec_out]   # grad wrt pre-ELU dec conv
         b.dh = torch.empty_like(b.h)
         b.dz = f(bsz, lat)
+        flat_out = self.num_vert * S.out_ch[-1]
+        b.dz_parts = (f(ops.linear_bwd_split_parts(flat_out), bsz, lat)
+                      if bsz <= 16 and lat <= 128 else None)
         b.dmulv = torch.empty_like(b.mulv)
         b.dpre_enc = [f(bsz, nv[lv + 1], cout) if (lv == last_enc or not T.enc_select[lv])
                       else fl(lv + 1, bsz, nv[lv + 1], cout) for (cin, cout, lv) in S.enc_layers()]
@@ -621,11 +624,18 @@ class SDVAEEngine:
             else:
                 self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh,
                            order=T.upT_order[ui])
-        # decoder Linear
-        ops.linear_bwd(b.z, P.view("de_layers.0.weight"), b.dh.view(b.bsz, -1), dx=b.dz,
-                       dw=P.gview("de_layers.0.weight"), db=P.gview("de_layers.0.bias"),
-                       workspace=b.lin_ws)
-        ops.latent_bwd(b.mulv, b.eps, b.z, b.dz, b.dlat, b.dmulv, S.latent, True, S.is_vae, S.sigmoid)
+        # decoder Linear: dW/db and dz (as 64-row-slice partial products,
+        # summed by the latent head's backward) in one launch
+        if b.dz_parts is not None:
+            ops.linear_bwd_split(b.z, P.view("de_layers.0.weight"), b.dh.view(b.bsz, -1), b.dz_parts,
+                                 P.gview("de_layers.0.weight"), P.gview("de_layers.0.bias"))
+            dz = b.dz_parts
+        else:
+            ops.linear_bwd(b.z, P.view("de_layers.0.weight"), b.dh.view(b.bsz, -1), dx=b.dz,
+                           dw=P.gview("de_layers.0.weight"), db=P.gview("de_layers.0.bias"),
+                           workspace=b.lin_ws)
+            dz = b.dz
+        ops.latent_bwd(b.mulv, b.eps, b.z, dz, b.dlat, b.dmulv, S.latent, True, S.is_vae, S.sigmoid)
         if split:
             ops.dw_reduce_batch(deferred)
             deferred = []

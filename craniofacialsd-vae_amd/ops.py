@@ -459,11 +459,39 @@ def latent_fwd(mulv, eps, key, z, dlat, terms, latent, region_size, train, is_va
 
 
 def latent_bwd(mulv, eps, z, dz_dec, dlat, dmulv, latent, train, is_vae, sigmoid):
+    """``dz_dec`` [B, latent], or [parts, B, latent] partial products (summed
+    in part order: cfsd_latent_bwd_parts)."""
+    _need(dmulv, tuple(mulv.shape), name="dmulv")
+    if dz_dec.dim() == 3:
+        parts, bsz = dz_dec.shape[:2]
+        _need(dz_dec, (parts, bsz, latent), name="dz_parts")
+        call("cfsd_latent_bwd_parts", ptr(mulv), ptr(eps), ptr(z), ptr(dz_dec), parts, ptr(dlat),
+             ptr(dmulv), bsz, latent, int(train), int(is_vae), int(sigmoid), stream_ptr())
+        return
     bsz = dz_dec.shape[0]
     _need(dz_dec, (bsz, latent), name="dz_dec")
-    _need(dmulv, tuple(mulv.shape), name="dmulv")
     call("cfsd_latent_bwd", ptr(mulv), ptr(eps), ptr(z), ptr(dz_dec), ptr(dlat), ptr(dmulv), bsz,
          latent, int(train), int(is_vae), int(sigmoid), stream_ptr())
+
+
+def linear_bwd_split_parts(n):
+    return int(_abi.lib().cfsd_linear_bwd_split_parts(n))
+
+
+def linear_bwd_split(x, w, dy, dx_parts, dw, db):
+    """Decoder-Linear backward in one launch: dW/db and dx as partial
+    products over 64-row slices of W (``dx_parts`` [parts, m, k], summed by
+    :func:`latent_bwd` with ``n_parts``)."""
+    m, k = x.shape
+    n = dy.shape[1]
+    _need(x, (m, k), name="x")
+    _need(w, (n, k), name="w")
+    _need(dy, (m, n), name="dy")
+    _need(dx_parts, (linear_bwd_split_parts(n), m, k), name="dx_parts")
+    _need(dw, (n, k), name="dw")
+    _need(db, (n,), name="db")
+    call("cfsd_linear_bwd_split", ptr(x), ptr(w), ptr(dy), ptr(dx_parts), ptr(dw), ptr(db), m, k, n,
+         stream_ptr())
 
 
 def loss_finalize(partials, terms, out, acc, bsz, nv, c, w_kl, w_lc, w_lap):

@@ -223,6 +223,15 @@ int cfsd_linear_bwd(const float* x, const float* w, const float* dy, const float
                     float* dw, float* db, float* workspace, size_t workspace_bytes, int m, int k,
                     int n, int accumulate, void* stream);
 
+/* Linear backward with a long output (the decoder Linear, dz = dh.W with
+ * W [n][k], n = 4288): dW / db as cfsd_linear_bwd and, in the SAME launch,
+ * dx as cfsd_linear_bwd_split_parts(n) partial products over 64-row slices of
+ * W, dx_parts [parts][m][k] (summed by cfsd_latent_bwd_parts, slice order).
+ * m <= 16, k <= 128. */
+int cfsd_linear_bwd_split_parts(int n);
+int cfsd_linear_bwd_split(const float* x, const float* w, const float* dy, float* dx_parts,
+                          float* dw, float* db, int m, int k, int n, void* stream);
+
 /* ---------------------------------------------------------------- losses
  * compute_mse_loss + _compute_laplacian_regularizer (model_manager.py:333-349,
  * utils.py:153-165) fused.  Pass 1 computes, per (b,v), Lx = sum_k L[v,k] pred[b,k,:]
@@ -267,6 +276,11 @@ int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_t* key, flo
 int cfsd_latent_bwd(const float* mulv, const float* eps, const float* z, const float* dz_dec,
                     const float* dlat, float* dmulv, int batch, int latent, int train, int is_vae,
                     int sigmoid, void* stream);
+/* cfsd_latent_bwd with dz_dec given as n_parts partial products
+ * [n_parts][batch][latent] (from cfsd_linear_bwd_split), summed in part order. */
+int cfsd_latent_bwd_parts(const float* mulv, const float* eps, const float* z,
+                          const float* dz_parts, int n_parts, const float* dlat, float* dmulv,
+                          int batch, int latent, int train, int is_vae, int sigmoid, void* stream);
 /* Reduce the recon partials + latent terms into out[5] = {rec, kl, lc, lap, tot}
  * (tot = rec + w_kl*kl + w_lc*lc + w_lap*lap, model_manager.py:308-312) and,
  * when acc != NULL, add them to acc[0..4] and 1 to acc[5] (per-epoch sums on

@@ -410,6 +410,34 @@ def test_linear_bwd(m, k, n, elu, accumulate):
     close(db, dy.double().sum(0), 1e-5, "linear db")
 
 
+@pytest.mark.parametrize("m,k,n", [(16, 75, 4288), (3, 33, 200), (16, 128, 65)])
+def test_linear_bwd_split(m, k, n):
+    """Decoder-Linear backward in one launch: dW/db exact-order sums, dx as
+    64-row-slice partial products that sum (in slice order) to dy.W."""
+    g = torch.Generator().manual_seed(m + k + n)
+    x, w = torch.randn(m, k, generator=g), torch.randn(n, k, generator=g) * 0.05
+    dy = torch.randn(m, n, generator=g)
+    parts = torch.empty(ops.linear_bwd_split_parts(n), m, k, device=DEV)
+    dw, db = torch.empty(n, k, device=DEV), torch.empty(n, device=DEV)
+    ops.linear_bwd_split(x.to(DEV), w.to(DEV), dy.to(DEV), parts, dw, db)
+    close(parts.sum(0), dy.double() @ w.double(), 1e-5, "split dx")
+    close(dw, dy.double().T @ x.double(), 1e-5, "split dw")
+    close(db, dy.double().sum(0), 1e-5, "split db")
+    # the latent head's backward sums the parts like one dz
+    L = k
+    mulv = torch.randn(m, 2 * L, generator=g).to(DEV)
+    eps = torch.randn(m, L, generator=g).to(DEV)
+    dlat = torch.randn(m, 3 * L, generator=g).to(DEV)
+    a, b = torch.empty(m, 2 * L, device=DEV), torch.empty(m, 2 * L, device=DEV)
+    z = torch.zeros(m, L, device=DEV)
+    ops.latent_bwd(mulv, eps, z, parts, dlat, a, L, True, True, False)
+    dz = torch.zeros(m, L, device=DEV)
+    for p in range(parts.shape[0]):
+        dz += parts[p]
+    ops.latent_bwd(mulv, eps, z, dz, dlat, b, L, True, True, False)
+    assert torch.equal(a, b)
+
+
 # --------------------------------------------------------------- latent head
 @pytest.mark.parametrize("key", [0, 7, 14])
 def test_latent_head_vs_oracle(key):

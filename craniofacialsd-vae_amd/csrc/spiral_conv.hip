@@ -2360,7 +2360,10 @@ DwGeom dw_geom(int batch, int rows, int cin, int cout) {
   } else if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64)) {
     g.kind = kDwMfma;
     const long n_tiles = (M + 31) / 32;
-    long gx = (n_tiles + 3) / 4;  // >= 4 tiles per block keeps the slab traffic bounded
+#ifndef CFSD_DW_TPB
+#define CFSD_DW_TPB 4
+#endif
+    long gx = (n_tiles + CFSD_DW_TPB - 1) / CFSD_DW_TPB;  // >= 4 tiles per block keeps the slab traffic bounded
 #ifndef CFSD_DW_MAX_WG
 #define CFSD_DW_MAX_WG 512  // (768: same time, 1.5x the slab traffic)
 #endif

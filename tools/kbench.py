@@ -91,6 +91,8 @@ def main():
                                                    P.gview("de_layers.2.conv.layer.bias"), dx=b.g_dec_up[1],
                                                    workspace=b.ws_dw[("dec", 1)])
     we1, be1 = eng._enc_w(1)
+    cases["dw_e1"] = lambda: ops.spiral_conv_bwd_weight(b.enc_out[0], T.enc_rows[1], b.dpre_enc[1], None, None,
+                                                       b.ws_dw[("enc", 1)])
     cases["fwd_e1"] = lambda: ops.spiral_conv_fwd(b.enc_out[0], T.enc_rows[1], we1, be1, 1, out=b.enc_out[1], workspace=b.ws)
     cases["rowsub_e1"] = lambda: ops.spiral_conv_bwd_rowsub(b.enc_out[0], T.enc_rows[1], b.dpre_enc[1], T.enc_flat[1],
                                                             we1, None, None, dx=b.dpre_enc[0], elu_y=b.enc_out[0],

@@ -63,7 +63,8 @@ __global__ __launch_bounds__(256, mfma_occ(CIN, COUT)) void conv_fwd_mfma(
   float bn[NCT];
 #pragma unroll
   for (int t = 0; t < NCT; ++t) bn[t] = (SPG == kSeq && bias) ? bias[t * 16 + r16] : 0.f;
-  const TileSweep sw = xcd_sweep((total_rows + 31) / 32, 4, wave);
+  const long n_tiles = (total_rows + 31) / 32;
+  const TileSweep sw = xcd_sweep(n_tiles, 4, wave, n_tiles < kContigTiles);
   for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
     const long m0 = tile * 32;
     const float* xb[2];
@@ -440,7 +441,8 @@ __global__ __launch_bounds__(256, dx_occ(CIN, COUT)) void conv_dx_mfma(
   const int nbytes = (int)(total_rows / vsrc * rows * RB);
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dpre), 0, nbytes, 0x00020000);
   const int i = lane & 31, h = lane >> 5;
-  const TileSweep sw = xcd_sweep((total_rows + 31) / 32, 4, wave);
+  const long n_tiles = (total_rows + 31) / 32;
+  const TileSweep sw = xcd_sweep(n_tiles, 4, wave, n_tiles < kContigTiles);
   for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
     const long m0 = tile * 32;
     long m = m0 + i;

@@ -18,11 +18,63 @@ from craniofacialsd_vae_amd import engine as E  # noqa: E402
 from craniofacialsd_vae_amd import ops, topology  # noqa: E402
 
 
+def locality_orders(spirals, n_coarsest=None):
+    """Experiment (measured: no kernel changed by more than noise, so the
+    product keeps the template numbering).  Per-level vertex orders with small spiral bandwidth (reverse
+    Cuthill-McKee on the spiral adjacency).  ``order[l][i]`` is the original
+    vertex stored at position i.  The template's own numbering spreads a
+    32-row tile's spiral neighbours over ~10k rows, so a level-0 sweep touches
+    the whole mesh and its L2 lines are evicted between reuses; in RCM order
+    the neighbours of a tile lie within ~1k rows."""
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    orders = []
+    for sp in spirals:
+        sp = np.asarray(sp, np.int64)
+        v = sp.shape[0]
+        a = coo_matrix((np.ones(sp.size), (np.repeat(np.arange(v), sp.shape[1]), sp.ravel())),
+                       shape=(v, v)).tocsr()
+        orders.append(np.asarray(reverse_cuthill_mckee((a + a.T).tocsr(), symmetric_mode=True), np.int64))
+    if n_coarsest is not None:
+        orders.append(np.arange(n_coarsest, dtype=np.int64))
+    return orders
+
+
+def relabel_npz(npz, orders):
+    """The arrays of a topology npz with level l's vertices renumbered so that
+    new vertex i is original vertex ``orders[l][i]`` (COO entries keep their
+    file order, so every per-row summation order is unchanged)."""
+    n = int(npz["n_levels"])
+    inv = []
+    for o in orders:
+        iv = np.empty(len(o), np.int64)
+        iv[o] = np.arange(len(o))
+        inv.append(iv)
+    out = dict(npz)
+    for l in range(n):
+        out[f"spiral_{l}"] = inv[l][np.asarray(npz[f"spiral_{l}"], np.int64)[orders[l]]]
+        out[f"down_{l}_row"] = inv[l + 1][np.asarray(npz[f"down_{l}_row"], np.int64)]
+        out[f"down_{l}_col"] = inv[l][np.asarray(npz[f"down_{l}_col"], np.int64)]
+        out[f"up_{l}_row"] = inv[l][np.asarray(npz[f"up_{l}_row"], np.int64)]
+        out[f"up_{l}_col"] = inv[l + 1][np.asarray(npz[f"up_{l}_col"], np.int64)]
+    if "lap_row" in npz:
+        out["lap_row"] = inv[0][np.asarray(npz["lap_row"], np.int64)]
+        out["lap_col"] = inv[0][np.asarray(npz["lap_col"], np.int64)]
+    for k in list(npz.keys()):
+        if k.startswith("region_") and (k.endswith("_feature") or k.endswith("_contour")):
+            out[k] = inv[0][np.asarray(npz[k], np.int64)]
+    return out
+
+
 def main():
     names = sys.argv[1:] or ["fwd_d3", "dx_d3", "dw_d3", "dout_fwd", "dout_dx", "dout_dw", "spmm_up0",
                              "spmm_up0T", "e0_fwd", "e0_dw"]
     iters = int(os.environ.get("KB_ITERS", "50"))
     npz = dict(np.load(os.path.join(ROOT, "tests", "golden", "topology_craniofacial.npz")))
+    if os.environ.get("KB_REORDER"):  # locality (RCM) vertex order on every level
+        n = int(npz["n_levels"])
+        orders = locality_orders([npz[f"spiral_{l}"] for l in range(n)], int(npz[f"down_{n - 1}_shape"][0]))
+        npz = relabel_npz(npz, orders)
     T = topology.DeviceTopology.from_npz(npz, device="cuda")
     eng = E.SDVAEEngine(T, E.ModelSpec(), device="cuda")
     b = eng.buffers(16)
@@ -72,6 +124,14 @@ def main():
                                            (b.g_dec_up[0], b.dh, None)]):
         cases[f"spmm_up{lv}T_s"] = (lambda lv=lv, gin=gin, outb=outb, ey=ey: ops.spmm(
             T.upT_csr[lv], gin, T.n_verts[lv + 1], elu_y=ey, out=outb, order=T.upT_order[lv]))
+    w2d, b2d = eng._dec_w(2)
+    for t in (b.dpre_dec[2], b.g_dec_up[2]):
+        t.copy_(torch.randn(t.shape, device="cuda", generator=g))
+    cases["dx_d2"] = lambda: ops.spiral_conv_bwd_data(b.dpre_dec[2], T.spiral_inv[1], w2d, T.n_verts[1],
+                                                      out=b.g_dec_up[2], workspace=b.ws)
+    cases["dw_d2"] = lambda: ops.spiral_conv_bwd_weight(b.dec_up[2], T.spiral[1], b.dpre_dec[2],
+                                                       P.gview("de_layers.3.conv.layer.weight"),
+                                                       P.gview("de_layers.3.conv.layer.bias"), b.ws)
     cases["fwd_d2"] = lambda: ops.spiral_conv_fwd(b.dec_up[2], T.spiral[1], *eng._dec_w(2), 1, out=b.dec_out[2],
                                                   workspace=b.ws)
     # coarse decoder / encoder layers (latency-shaped kernels)

@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void conv_fwd_b16(const bf16_t* __restrict__ x
   float bn[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) bn[t] = bias ? bias[t * 16 + i] : 0.f;
-  const TileSweep sw = xcd_sweep((total_rows + 15) / 16, 4, wave);
+  const long n_tiles = (total_rows + 15) / 16;
+  const TileSweep sw = xcd_sweep(n_tiles, 4, wave, n_tiles < 2 * kContigTiles);
   for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
     long m = tile * 16 + i;
     if (m >= total_rows) m = total_rows - 1;  // clamped loads, masked stores
@@ -130,7 +131,8 @@ __global__ __launch_bounds__(256) void conv_dx_b16(const TD* __restrict__ dpre,
   const int i = lane & 15, g = lane >> 4;
   const int nbytes = (int)(total_rows / vsrc * rows * RB);
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<TD*>(dpre), 0, nbytes, 0x00020000);
-  const TileSweep sw = xcd_sweep((total_rows + 15) / 16, 4, wave);
+  const long n_tiles = (total_rows + 15) / 16;
+  const TileSweep sw = xcd_sweep(n_tiles, 4, wave, n_tiles < 2 * kContigTiles);
   for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
     long m = tile * 16 + i;
     if (m >= total_rows) m = total_rows - 1;

@@ -90,6 +90,69 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   st4f(y + t * 4, acc);
 }
 
+// SpMM for a matrix whose rows all hold exactly K entries (the barycentric
+// up-sampling matrices: 3 per row), stored row-major in the CSR arrays:
+// row r's entries are [r*K, r*K + K), so there is no row_ptr load and the
+// dependent chain is column/value -> x rows (two memory latencies instead of
+// three).  A thread owns RPT chunks 256 apart (each load instruction still
+// covers 256 consecutive chunks), all their loads issued before the first
+// add; the adds are the CSR kernel's: 0 + x0*v0, then + x1*v1, ... un-fused
+// (bit-identical).  Same XCD grouping as spmm_csr_k.
+template <int K, int RPT, typename TX, typename TY>
+__global__ __launch_bounds__(256) void spmm_uniform_k(const int* __restrict__ col,
+                                                      const float* __restrict__ val,
+                                                      const TX* __restrict__ x,
+                                                      const TY* __restrict__ elu_y,
+                                                      TY* __restrict__ y, int m, int n, int c4,
+                                                      long total) {
+#pragma clang fp contract(off)
+  const long per = (total + 7) / 8;
+  const int grp = blockIdx.x & 7;
+  const long lim = min(total, (long)(grp + 1) * per);
+  const long t0 = (long)grp * per + (long)(blockIdx.x >> 3) * (256 * RPT) + threadIdx.x;
+  if (t0 >= lim) return;
+  int cc[RPT][K], bq[RPT], qq[RPT];
+  float vv[RPT][K];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const long t = min(t0 + 256 * j, lim - 1);  // clamped chunks: loads only
+    int br, r;
+    divmod32(t, c4, br, qq[j]);
+    divmod32(br, m, bq[j], r);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      cc[j][k] = col[r * K + k];
+      vv[j][k] = val[r * K + k];
+    }
+  }
+  f32x4 xv[RPT][K];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j)
+#pragma unroll
+    for (int k = 0; k < K; ++k) xv[j][k] = ld4f(x + ((long)bq[j] * n + cc[j][k]) * c4 * 4 + 4 * qq[j]);
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const long t = t0 + 256 * j;
+    if (t >= lim) break;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      acc.x = acc.x + xv[j][k].x * vv[j][k];
+      acc.y = acc.y + xv[j][k].y * vv[j][k];
+      acc.z = acc.z + xv[j][k].z * vv[j][k];
+      acc.w = acc.w + xv[j][k].w * vv[j][k];
+    }
+    if (elu_y) {
+      const f32x4 g = ld4f(elu_y + t * 4);
+      acc.x *= elu_grad_from_out(g.x);
+      acc.y *= elu_grad_from_out(g.y);
+      acc.z *= elu_grad_from_out(g.z);
+      acc.w *= elu_grad_from_out(g.w);
+    }
+    st4f(y + t * 4, acc);
+  }
+}
+
 // The same SpMM for matrices with long, skewed rows (the transposes of the
 // up-sampling matrices: level 0 has 12 entries per row on average but up to
 // 96).  A row is a sequential fp32 fold in entry order (kept for
@@ -385,6 +448,41 @@ extern "C" int cfsd_spmm_csr_x(const int32_t* row_ptr, const int32_t* col, const
                                const void* x, int x_dt, const void* elu_y, void* y, int y_dt,
                                int batch, int m, int n, int c, void* stream) {
   return spmm_launch(row_ptr, col, val, nullptr, x, x_dt, elu_y, y, y_dt, batch, m, n, c, stream);
+}
+
+#ifndef CFSD_SPMM_URPT
+#define CFSD_SPMM_URPT 4
+#endif
+extern "C" int cfsd_spmm_uniform(int k, const int32_t* col, const float* val, const void* x,
+                                 int x_dt, const void* elu_y, void* y, int y_dt, int batch, int m,
+                                 int n, int c, void* stream) {
+  if (!col || !val || !x || !y) return set_error(CFSD_EINVAL, "spmm_uniform: null pointer");
+  if (k < 1 || k > 4) return set_error(CFSD_EINVAL, "spmm_uniform: %d entries per row (1..4)", k);
+  if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
+    return set_error(CFSD_EINVAL, "spmm_uniform: bad sizes batch=%d m=%d n=%d c=%d", batch, m, n, c);
+  if ((x_dt != CFSD_DT_F32 && x_dt != CFSD_DT_BF16) || (y_dt != CFSD_DT_F32 && y_dt != CFSD_DT_BF16))
+    return set_error(CFSD_EINVAL, "spmm_uniform: bad dtype");
+  const long total = (long)batch * m * (c / 4);
+  if (total >= (1L << 31) || (long)batch * n >= (1L << 31) || (long)m * k >= (1L << 31))
+    return set_error(CFSD_EINVAL, "spmm_uniform: sizes >= 2^31 (32-bit indices)");
+  constexpr int RPT = CFSD_SPMM_URPT;
+  const long per_grp = (total + 7) / 8;
+  const unsigned nblk = (unsigned)(8 * ((per_grp + 256 * RPT - 1) / (256 * RPT)));
+  const hipStream_t st = (hipStream_t)stream;
+#define SPMU(K_, TX, TY)                                                                          \
+  hipLaunchKernelGGL((spmm_uniform_k<K_, RPT, TX, TY>), dim3(nblk), dim3(256), 0, st, col, val,    \
+                     (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, total)
+#define SPMU_K(K_)                                                                                \
+  if (k == K_) {                                                                                  \
+    if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPMU(K_, float, float);                        \
+    else if (x_dt == CFSD_DT_F32) SPMU(K_, float, bf16_t);                                         \
+    else if (y_dt == CFSD_DT_F32) SPMU(K_, bf16_t, float);                                         \
+    else SPMU(K_, bf16_t, bf16_t);                                                                 \
+  }
+  SPMU_K(1) SPMU_K(2) SPMU_K(3) SPMU_K(4)
+#undef SPMU_K
+#undef SPMU
+  return launch_status("spmm_uniform");
 }
 
 extern "C" int cfsd_cast(const void* src, int src_dt, void* dst, int dst_dt, size_t n, void* stream) {

@@ -459,11 +459,11 @@ class SDVAEEngine:
             ops.spiral_conv_fwd_x(x, idx, w, self._w16(wname + ".weight"), bias, act, out)
 
     @staticmethod
-    def _spmm(csr, x, m, out, elu_y=None, order=None):
+    def _spmm(csr, x, m, out, elu_y=None, order=None, uniform=0):
         if x.dtype == torch.float32 and out.dtype == torch.float32:
-            ops.spmm(csr, x, m, elu_y=elu_y, out=out, order=order)
+            ops.spmm(csr, x, m, elu_y=elu_y, out=out, order=order, uniform=uniform)
         else:
-            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out, order=order)
+            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out, order=order, uniform=uniform)
 
     def _lin_names(self):
         n = self.spec.n
@@ -519,7 +519,7 @@ class SDVAEEngine:
                        workspace=b.lin_ws)
         h = b.h
         for i, (cin, cout, lv, ui) in enumerate(S.dec_layers()):
-            self._spmm(T.up_csr[ui], h, T.n_verts[lv], out=b.dec_up[i])
+            self._spmm(T.up_csr[ui], h, T.n_verts[lv], out=b.dec_up[i], uniform=T.up_uniform[ui])
             self._conv_fwd(b, b.dec_up[i], T.spiral[lv], f"de_layers.{i + 1}.conv.layer", ACT_ELU,
                            b.dec_out[i])
             h = b.dec_out[i]

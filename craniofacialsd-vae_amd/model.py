@@ -87,8 +87,9 @@ class _PoolPlan:
         idx = t._indices().numpy()
         val = t._values().numpy()
         self.m, self.n = int(t.shape[0]), int(t.shape[1])
-        self.csr = tuple(torch.from_numpy(a).to(device)
-                         for a in topology.csr_from_coo(idx[0], idx[1], val, self.m))
+        csr = topology.csr_from_coo(idx[0], idx[1], val, self.m)
+        self.uniform = topology.uniform_rows(csr[0])
+        self.csr = tuple(torch.from_numpy(a).to(device) for a in csr)
         self.csrT = tuple(torch.from_numpy(a).to(device)
                           for a in topology.csr_transpose_from_coo(idx[0], idx[1], val, self.n))
         self.selection = topology.selection_rows(idx[0], idx[1], val, self.m)
@@ -132,7 +133,7 @@ class _PoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, plan):
         ctx.plan = plan
-        return ops.spmm(plan.csr, x.contiguous(), plan.m)
+        return ops.spmm(plan.csr, x.contiguous(), plan.m, uniform=plan.uniform)
 
     @staticmethod
     def backward(ctx, dy):

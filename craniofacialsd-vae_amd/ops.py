@@ -269,10 +269,12 @@ def spiral_gather(x, idx, out=None):
 
 
 # ------------------------------------------------------------------ pool / swap
-def spmm(csr, x, m, elu_y=None, out=None, order=None):
+def spmm(csr, x, m, elu_y=None, out=None, order=None, uniform=0):
     """y[b, r] = g * sum_{k in row r} val[k] x[b, col[k]]   (Pool, model.py:50-55).
     ``order``: optional row schedule (a permutation of the rows by decreasing
-    length, for matrices with long skewed rows); same results bit for bit."""
+    length, for matrices with long skewed rows); ``uniform``: every row holds
+    exactly that many entries (``topology.uniform_rows``; no row_ptr walk).
+    Same results bit for bit either way."""
     row_ptr, col, val = csr
     bsz, n, c = x.shape
     _need(x, None, name="x")
@@ -285,9 +287,20 @@ def spmm(csr, x, m, elu_y=None, out=None, order=None):
     if order is not None:
         _spmm_sched(row_ptr, col, val, order, x, elu_y, y, bsz, m, n, c)
         return y
+    if uniform:
+        _spmm_uniform(uniform, col, val, x, elu_y, y, bsz, m, n, c)
+        return y
     call("cfsd_spmm_csr", ptr(row_ptr), ptr(col), ptr(val), ptr(x), ptr(elu_y), ptr(y), bsz, m, n,
          c, stream_ptr())
     return y
+
+
+def _spmm_uniform(k, col, val, x, elu_y, y, bsz, m, n, c):
+    """cfsd_spmm_uniform: every row holds exactly ``k`` entries."""
+    if col.numel() != m * k:
+        raise ValueError(f"uniform SpMM: {col.numel()} entries != {m} rows x {k}")
+    call("cfsd_spmm_uniform", int(k), ptr(col), ptr(val), ptr(x), _dt(x), ptr(elu_y), ptr(y), _dt(y),
+         bsz, m, n, c, stream_ptr())
 
 
 def _spmm_sched(row_ptr, col, val, order, x, elu_y, y, bsz, m, n, c):
@@ -694,7 +707,7 @@ def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspa
     return dx
 
 
-def spmm_x(csr, x, m, elu_y=None, out=None, order=None):
+def spmm_x(csr, x, m, elu_y=None, out=None, order=None, uniform=0):
     """Pool SpMM with fp32 or bf16 operands (fp32 sums, file order)."""
     row_ptr, col, val = csr
     bsz, n, c = x.shape
@@ -707,6 +720,9 @@ def spmm_x(csr, x, m, elu_y=None, out=None, order=None):
         _need(elu_y, (bsz, m, c), out.dtype, "elu_y")
     if order is not None:
         _spmm_sched(row_ptr, col, val, order, x, elu_y, out, bsz, m, n, c)
+        return out
+    if uniform:
+        _spmm_uniform(uniform, col, val, x, elu_y, out, bsz, m, n, c)
         return out
     call("cfsd_spmm_csr_x", ptr(row_ptr), ptr(col), ptr(val), ptr(x), _dt(x), ptr(elu_y), ptr(out),
          _dt(out), bsz, m, n, c, stream_ptr())

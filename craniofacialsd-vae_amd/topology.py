@@ -107,6 +107,15 @@ def row_schedule(ptr, min_max_len=16):
     return _i32(np.argsort(-cnt, kind="stable"))
 
 
+def uniform_rows(ptr, max_k=4):
+    """k when every CSR row holds exactly k <= max_k entries (the barycentric
+    up-sampling matrices: 3), else 0 (``cfsd_spmm_uniform`` needs no row_ptr)."""
+    cnt = np.diff(np.asarray(ptr, np.int64))
+    if cnt.size == 0 or cnt[0] < 1 or cnt[0] > max_k or not np.all(cnt == cnt[0]):
+        return 0
+    return int(cnt[0])
+
+
 def selection_rows(row, col, val, m):
     """Return the kept-vertex list if the COO transform is a 0/1 row
     selection (exactly one entry of value 1.0 per row), else None."""
@@ -166,6 +175,7 @@ class DeviceTopology:
         self.down_csr, self.downT_csr = [], []
         self.up_csr, self.upT_csr = [], []
         self.upT_order = []     # row schedule of each up transpose (None: short rows)
+        self.up_uniform = []    # entries per row of each up matrix when uniform (else 0)
         self.np_spirals = [np.asarray(s, np.int64) for s in spirals]
         for l in range(self.n_levels):
             sp = np.asarray(spirals[l], np.int64)
@@ -191,7 +201,9 @@ class DeviceTopology:
             self.down_csr.append(self._csr(csr_from_coo(drow, dcol, dval, dshape[0])))
             self.downT_csr.append(self._csr(csr_transpose_from_coo(drow, dcol, dval, dshape[1])))
             urow, ucol, uval, ushape = up[l]
-            self.up_csr.append(self._csr(csr_from_coo(urow, ucol, uval, ushape[0])))
+            up_l = csr_from_coo(urow, ucol, uval, ushape[0])
+            self.up_uniform.append(uniform_rows(up_l[0]))
+            self.up_csr.append(self._csr(up_l))
             self.upT_csr.append(self._csr(csr_transpose_from_coo(urow, ucol, uval, ushape[1])))
             sched = row_schedule(self.upT_csr[-1][0].cpu().numpy())
             self.upT_order.append(_dev(sched, self.device) if sched is not None else None)

@@ -183,6 +183,15 @@ int cfsd_spmm_csr_sched(const int32_t* row_ptr, const int32_t* col, const float*
                         const int32_t* order, const void* x, int x_dt, const void* elu_y, void* y,
                         int y_dt, int batch, int m, int n, int c, void* stream);
 
+/* cfsd_spmm_csr_x for a matrix whose rows all hold exactly k (1..4) entries,
+ * row r's at [r*k, r*k + k) of col/val (the CSR arrays of the barycentric
+ * up-sampling matrices, Pool(up) at model.py:84 via model.py:50-55: 3 per
+ * row).  No row_ptr: one dependent load fewer per row.  Same results bit for
+ * bit as cfsd_spmm_csr_x on the same CSR. */
+int cfsd_spmm_uniform(int k, const int32_t* col, const float* val, const void* x, int x_dt,
+                      const void* elu_y, void* y, int y_dt, int batch, int m, int n, int c,
+                      void* stream);
+
 /* ---------------------------------------------------------------- feature swap
  * Replaces SwapFeatures.__call__ / swap (swap_batch_transform.py:13-52):
  *   out[i*bs+j, v, :] = x[mesh[(i != j && mask[key*nv + v]) ? j : i], v, :]

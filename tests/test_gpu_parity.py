@@ -228,7 +228,10 @@ def test_pool_bit_exact(otopo, dtopo, level, kind):
     np.testing.assert_array_equal(y.cpu().numpy(), out.detach().numpy())
     dx = ops.spmm(csrT, dout.to(DEV), n)
     np.testing.assert_array_equal(dx.cpu().numpy(), x.grad.numpy())
-    if kind == "up":  # long-row schedule of the transpose: same bits
+    if kind == "up":  # uniform-row forward and long-row schedule of the transpose: same bits
+        assert dtopo.up_uniform[level] == 3
+        yu = ops.spmm(csr, x.detach().to(DEV), m, uniform=dtopo.up_uniform[level])
+        np.testing.assert_array_equal(yu.cpu().numpy(), out.detach().numpy())
         assert dtopo.upT_order[level] is not None
         dxs = ops.spmm(csrT, dout.to(DEV), n, order=dtopo.upT_order[level])
         np.testing.assert_array_equal(dxs.cpu().numpy(), x.grad.numpy())
@@ -250,6 +253,28 @@ def test_pool_scheduled_transpose(dtopo, bsz, dts):
         ops.spmm_x(dtopo.upT_csr[level], x, m, elu_y=ey, out=a)
         ops.spmm_x(dtopo.upT_csr[level], x, m, elu_y=ey, out=b, order=dtopo.upT_order[level])
         assert torch.equal(a, b), f"level {level}"
+
+
+@pytest.mark.parametrize("bsz", [16, 3])
+@pytest.mark.parametrize("dts", [("f32", "f32"), ("bf16", "bf16"), ("f32", "bf16"), ("bf16", "f32")])
+def test_pool_uniform_rows(dtopo, bsz, dts):
+    """cfsd_spmm_uniform == cfsd_spmm_csr(_x) bit for bit on the 3-tap up-sampling
+    matrices (every level, with and without the ELU-backward epilogue, ragged
+    thread tails at bsz 3)."""
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16}
+    g = torch.Generator().manual_seed(100 + bsz)
+    for level in range(4):
+        m, n = dtopo.n_verts[level], dtopo.n_verts[level + 1]
+        k = dtopo.up_uniform[level]
+        assert k == 3
+        x = torch.randn(bsz, n, 32, generator=g).to(DEV, dt[dts[0]])
+        ey = O.elu(torch.randn(bsz, m, 32, generator=g)).to(DEV, dt[dts[1]])
+        for e in (None, ey):
+            a = torch.empty(bsz, m, 32, device=DEV, dtype=dt[dts[1]])
+            b = torch.empty_like(a)
+            ops.spmm_x(dtopo.up_csr[level], x, m, elu_y=e, out=a)
+            ops.spmm_x(dtopo.up_csr[level], x, m, elu_y=e, out=b, uniform=k)
+            assert torch.equal(a, b), f"level {level} elu {e is not None}"
 
 
 def test_pool_golden(dtopo):

@@ -104,6 +104,10 @@ def main():
                                                 elu_y=b.dec_out[3], workspace=b.ws),
         "spmm_up0": lambda: ops.spmm(T.up_csr[0], b.dec_out[2], T.n_verts[0], out=b.dec_up[3]),
         "spmm_up1": lambda: ops.spmm(T.up_csr[1], b.dec_out[1], T.n_verts[1], out=b.dec_up[2]),
+        "spmm_up0u": lambda: ops.spmm(T.up_csr[0], b.dec_out[2], T.n_verts[0], out=b.dec_up[3],
+                                      uniform=T.up_uniform[0]),
+        "spmm_up1u": lambda: ops.spmm(T.up_csr[1], b.dec_out[1], T.n_verts[1], out=b.dec_up[2],
+                                      uniform=T.up_uniform[1]),
         "spmm_up2": lambda: ops.spmm(T.up_csr[2], b.dec_out[0], T.n_verts[2], out=b.dec_up[1]),
         "spmm_up3": lambda: ops.spmm(T.up_csr[3], b.h, T.n_verts[3], out=b.dec_up[0]),
         "spmm_up1T": lambda: ops.spmm(T.upT_csr[1], b.g_dec_up[2], T.n_verts[2], elu_y=b.dec_out[1],

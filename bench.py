@@ -192,7 +192,7 @@ def launch_cost(name, a):
         elu = a[4] is not None
         return (2.0 * B * rows * S * ci * co, f4 * (B * rows * co + co * S * ci) + sd * B * vs * ci * (2 if elu else 1)
                 + 4 * vs * a[2], FP32_PEAK_TFLOPS)
-    if name == "cfsd_spmm_csr_sched":
+    if name in ("cfsd_spmm_csr_sched", "cfsd_spmm_sched_csr"):
         sx, sy = (4 if a[5] == 0 else 2), (4 if a[8] == 0 else 2)
         B, m, n, c = a[9:13]
         elu = a[6] is not None
@@ -219,7 +219,7 @@ def launch_cost(name, a):
         fl = 2.0 * B * rows * S * ci * co * (2 if dx else 1)
         by = 2 * B * vs * ci + 4 * B * rows * co + 4 * co * S * ci + (2 * B * vs * ci * (2 if elu else 1) if dx else 0)
         return fl, by, FP32_PEAK_TFLOPS
-    if name == "cfsd_spmm_csr_x":
+    if name in ("cfsd_spmm_csr_x", "cfsd_spmm_uniform"):
         sx, sy = (4 if a[4] == 0 else 2), (4 if a[7] == 0 else 2)
         B, m, n, c = a[8:12]
         elu = a[5] is not None

@@ -69,6 +69,7 @@ SIGNATURES = {
                                     _I, _I, _P]),
     "cfsd_spmm_csr_x": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spmm_uniform": (_I, [_I, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "cfsd_spmm_sched_csr": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_cast": (_I, [_P, _I, _P, _I, _Z, _P]),
     "cfsd_step_begin": (_I, [_P, _U64, _P, _I, _P, _I, _P, _I, _I, _P, _I, _I, _P, _P]),
     "cfsd_dw_reduce_batch": (_I, [_P, _I, _P]),

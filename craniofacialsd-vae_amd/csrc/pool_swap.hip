@@ -239,6 +239,43 @@ __global__ __launch_bounds__(256) void spmm_sched_k(const int* __restrict__ row_
   st4f(y + o * 4, acc);
 }
 
+// spmm_sched_k over a CSR stored in visiting order: slot i is output row
+// rows_s[i] with entries [ptr_s[i], ptr_s[i+1]) (the rows' entries in the
+// original per-row order, so the same sums bit for bit).  The slot's row id
+// and extent are independent loads, so the chain is extent -> list -> x rows
+// (spmm_sched_k: order -> row_ptr -> list -> x rows), and a wave's entry
+// lists are contiguous.
+template <typename TX, typename TY>
+__global__ __launch_bounds__(256) void spmm_sched_csr_k(const int* __restrict__ ptr_s,
+                                                        const int* __restrict__ col_s,
+                                                        const float* __restrict__ val_s,
+                                                        const int* __restrict__ rows_s,
+                                                        const TX* __restrict__ x,
+                                                        const TY* __restrict__ elu_y,
+                                                        TY* __restrict__ y, int m, int n, int c4,
+                                                        int groups, int bpg, int per) {
+  const int g = (int)blockIdx.x % groups;
+  const int t = (int)(blockIdx.x / groups) * (int)blockDim.x + (int)threadIdx.x;
+  if (t >= per) return;
+  const int rowq = bpg * c4;  // threads per schedule slot
+  const int slot = t / rowq, rem = t - slot * rowq;
+  const int bl = rem / c4, q = rem - bl * c4;
+  const int b = g * bpg + bl;
+  const int r = rows_s[slot], beg = ptr_s[slot], end = ptr_s[slot + 1];
+  const TX* xb = x + (long)b * n * c4 * 4 + 4 * q;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  spmm_fold_prefetch<8>(beg, end, col_s, val_s, xb, c4, acc);
+  const long o = ((long)b * m + r) * c4 + q;
+  if (elu_y) {
+    f32x4 gy = ld4f(elu_y + o * 4);
+    acc.x *= elu_grad_from_out(gy.x);
+    acc.y *= elu_grad_from_out(gy.y);
+    acc.z *= elu_grad_from_out(gy.z);
+    acc.w *= elu_grad_from_out(gy.w);
+  }
+  st4f(y + o * 4, acc);
+}
+
 // out[(i*bs + j), v, :] = x[mesh(i or j), v, :]; one thread per (out mesh,
 // vertex); c <= 4 channels per vertex (xyz) are copied as scalars, larger c
 // in 16-B chunks.  Device-side indices are range-guarded so a bad value can
@@ -483,6 +520,33 @@ extern "C" int cfsd_spmm_uniform(int k, const int32_t* col, const float* val, co
 #undef SPMU_K
 #undef SPMU
   return launch_status("spmm_uniform");
+}
+
+extern "C" int cfsd_spmm_sched_csr(const int32_t* ptr_s, const int32_t* col_s, const float* val_s,
+                                   const int32_t* rows_s, const void* x, int x_dt,
+                                   const void* elu_y, void* y, int y_dt, int batch, int m, int n,
+                                   int c, void* stream) {
+  if (!ptr_s || !col_s || !val_s || !rows_s || !x || !y)
+    return set_error(CFSD_EINVAL, "spmm_sched_csr: null pointer");
+  if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
+    return set_error(CFSD_EINVAL, "spmm_sched_csr: bad sizes batch=%d m=%d n=%d c=%d", batch, m, n, c);
+  if ((x_dt != CFSD_DT_F32 && x_dt != CFSD_DT_BF16) || (y_dt != CFSD_DT_F32 && y_dt != CFSD_DT_BF16))
+    return set_error(CFSD_EINVAL, "spmm_sched_csr: bad dtype");
+  if ((long)batch * m * (c / 4) >= (1L << 31) || (long)batch * n >= (1L << 31))
+    return set_error(CFSD_EINVAL, "spmm_sched_csr: batch x rows >= 2^31 (32-bit indices)");
+  const int groups = batch % 8 == 0 ? 8 : 1, bpg = batch / groups;
+  const int per = bpg * m * (c / 4);
+  const unsigned nb = (unsigned)(groups * ((per + 255) / 256));
+  const hipStream_t st = (hipStream_t)stream;
+#define SPSC(TX, TY)                                                                             \
+  hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY>), dim3(nb), dim3(256), 0, st, ptr_s, col_s, val_s, \
+                     rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, groups, bpg, per)
+  if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPSC(float, float);
+  else if (x_dt == CFSD_DT_F32) SPSC(float, bf16_t);
+  else if (y_dt == CFSD_DT_F32) SPSC(bf16_t, float);
+  else SPSC(bf16_t, bf16_t);
+#undef SPSC
+  return launch_status("spmm_sched_csr");
 }
 
 extern "C" int cfsd_cast(const void* src, int src_dt, void* dst, int dst_dt, size_t n, void* stream) {

@@ -459,11 +459,11 @@ class SDVAEEngine:
             ops.spiral_conv_fwd_x(x, idx, w, self._w16(wname + ".weight"), bias, act, out)
 
     @staticmethod
-    def _spmm(csr, x, m, out, elu_y=None, order=None, uniform=0):
+    def _spmm(csr, x, m, out, elu_y=None, sched=None, uniform=0):
         if x.dtype == torch.float32 and out.dtype == torch.float32:
-            ops.spmm(csr, x, m, elu_y=elu_y, out=out, order=order, uniform=uniform)
+            ops.spmm(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform)
         else:
-            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out, order=order, uniform=uniform)
+            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform)
 
     def _lin_names(self):
         n = self.spec.n
@@ -620,10 +620,10 @@ class SDVAEEngine:
                                          out=b.g_dec_up[i], workspace=b.ws)
             if i > 0:  # through Pool(up) into the previous Deblock's ELU
                 self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dpre_dec[i - 1],
-                           elu_y=b.dec_out[i - 1], order=T.upT_order[ui])
+                           elu_y=b.dec_out[i - 1], sched=T.upT_sched[ui])
             else:
                 self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh,
-                           order=T.upT_order[ui])
+                           sched=T.upT_sched[ui])
         # decoder Linear: dW/db and dz (as 64-row-slice partial products,
         # summed by the latent head's backward) in one launch
         if b.dz_parts is not None:

@@ -269,12 +269,13 @@ def spiral_gather(x, idx, out=None):
 
 
 # ------------------------------------------------------------------ pool / swap
-def spmm(csr, x, m, elu_y=None, out=None, order=None, uniform=0):
+def spmm(csr, x, m, elu_y=None, out=None, order=None, uniform=0, sched=None):
     """y[b, r] = g * sum_{k in row r} val[k] x[b, col[k]]   (Pool, model.py:50-55).
     ``order``: optional row schedule (a permutation of the rows by decreasing
     length, for matrices with long skewed rows); ``uniform``: every row holds
-    exactly that many entries (``topology.uniform_rows``; no row_ptr walk).
-    Same results bit for bit either way."""
+    exactly that many entries (``topology.uniform_rows``; no row_ptr walk);
+    ``sched``: the CSR re-stored in a visiting order (``topology.scheduled_csr``,
+    replaces ``csr``/``order``).  Same results bit for bit in every form."""
     row_ptr, col, val = csr
     bsz, n, c = x.shape
     _need(x, None, name="x")
@@ -284,6 +285,9 @@ def spmm(csr, x, m, elu_y=None, out=None, order=None, uniform=0):
     if elu_y is not None:
         _need(elu_y, (bsz, m, c), name="elu_y")
     y = _out(out, (bsz, m, c), x)
+    if sched is not None:
+        _spmm_sched_csr(sched, x, elu_y, y, bsz, m, n, c)
+        return y
     if order is not None:
         _spmm_sched(row_ptr, col, val, order, x, elu_y, y, bsz, m, n, c)
         return y
@@ -301,6 +305,17 @@ def _spmm_uniform(k, col, val, x, elu_y, y, bsz, m, n, c):
         raise ValueError(f"uniform SpMM: {col.numel()} entries != {m} rows x {k}")
     call("cfsd_spmm_uniform", int(k), ptr(col), ptr(val), ptr(x), _dt(x), ptr(elu_y), ptr(y), _dt(y),
          bsz, m, n, c, stream_ptr())
+
+
+def _spmm_sched_csr(sched, x, elu_y, y, bsz, m, n, c):
+    """cfsd_spmm_sched_csr over a CSR stored in visiting order."""
+    ptr_s, col_s, val_s, rows_s = sched
+    _need(ptr_s, (m + 1,), torch.int32, "ptr_s")
+    _need(rows_s, (m,), torch.int32, "rows_s")
+    _need(col_s, None, torch.int32, "col_s")
+    _need(val_s, (col_s.numel(),), name="val_s")
+    call("cfsd_spmm_sched_csr", ptr(ptr_s), ptr(col_s), ptr(val_s), ptr(rows_s), ptr(x), _dt(x), ptr(elu_y),
+         ptr(y), _dt(y), bsz, m, n, c, stream_ptr())
 
 
 def _spmm_sched(row_ptr, col, val, order, x, elu_y, y, bsz, m, n, c):
@@ -707,7 +722,7 @@ def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspa
     return dx
 
 
-def spmm_x(csr, x, m, elu_y=None, out=None, order=None, uniform=0):
+def spmm_x(csr, x, m, elu_y=None, out=None, order=None, uniform=0, sched=None):
     """Pool SpMM with fp32 or bf16 operands (fp32 sums, file order)."""
     row_ptr, col, val = csr
     bsz, n, c = x.shape
@@ -718,6 +733,9 @@ def spmm_x(csr, x, m, elu_y=None, out=None, order=None, uniform=0):
     _needx(out, (bsz, m, c), "out")
     if elu_y is not None:
         _need(elu_y, (bsz, m, c), out.dtype, "elu_y")
+    if sched is not None:
+        _spmm_sched_csr(sched, x, elu_y, out, bsz, m, n, c)
+        return out
     if order is not None:
         _spmm_sched(row_ptr, col, val, order, x, elu_y, out, bsz, m, n, c)
         return out

@@ -107,6 +107,19 @@ def row_schedule(ptr, min_max_len=16):
     return _i32(np.argsort(-cnt, kind="stable"))
 
 
+def scheduled_csr(ptr, col, val, order):
+    """The CSR re-stored in visiting order ``order`` (``row_schedule``): returns
+    (ptr_s [m+1], col_s, val_s, rows_s [m]) with slot i = row order[i], its
+    entries in the original per-row order (``cfsd_spmm_sched_csr``)."""
+    ptr = np.asarray(ptr, np.int64)
+    order = np.asarray(order, np.int64)
+    cnt = np.diff(ptr)[order]
+    ptr_s = np.concatenate([[0], np.cumsum(cnt)])
+    take = np.concatenate([np.arange(ptr[r], ptr[r + 1]) for r in order]) if len(order) else np.zeros(0, np.int64)
+    return (_i32(ptr_s), _i32(np.asarray(col)[take]), np.ascontiguousarray(np.asarray(val, np.float32)[take]),
+            _i32(order))
+
+
 def uniform_rows(ptr, max_k=4):
     """k when every CSR row holds exactly k <= max_k entries (the barycentric
     up-sampling matrices: 3), else 0 (``cfsd_spmm_uniform`` needs no row_ptr)."""
@@ -176,6 +189,7 @@ class DeviceTopology:
         self.up_csr, self.upT_csr = [], []
         self.upT_order = []     # row schedule of each up transpose (None: short rows)
         self.up_uniform = []    # entries per row of each up matrix when uniform (else 0)
+        self.upT_sched = []     # each up transpose stored in its visiting order (None: short rows)
         self.np_spirals = [np.asarray(s, np.int64) for s in spirals]
         for l in range(self.n_levels):
             sp = np.asarray(spirals[l], np.int64)
@@ -205,8 +219,11 @@ class DeviceTopology:
             self.up_uniform.append(uniform_rows(up_l[0]))
             self.up_csr.append(self._csr(up_l))
             self.upT_csr.append(self._csr(csr_transpose_from_coo(urow, ucol, uval, ushape[1])))
-            sched = row_schedule(self.upT_csr[-1][0].cpu().numpy())
+            upT = csr_transpose_from_coo(urow, ucol, uval, ushape[1])
+            sched = row_schedule(upT[0])
             self.upT_order.append(_dev(sched, self.device) if sched is not None else None)
+            self.upT_sched.append(tuple(_dev(a, self.device) for a in scheduled_csr(*upT, sched))
+                                  if sched is not None else None)
         self.lap_csr = self.lapT_csr = None
         if lap is not None:
             lr, lc, lv, lshape = lap

@@ -183,6 +183,15 @@ int cfsd_spmm_csr_sched(const int32_t* row_ptr, const int32_t* col, const float*
                         const int32_t* order, const void* x, int x_dt, const void* elu_y, void* y,
                         int y_dt, int batch, int m, int n, int c, void* stream);
 
+/* cfsd_spmm_csr_sched with the CSR stored in visiting order: slot i (0..m-1)
+ * is output row rows_s[i] (a permutation of [0, m)) with entries
+ * [ptr_s[i], ptr_s[i+1]) of col_s / val_s, each row's entries in the original
+ * per-row (file) order (topology.scheduled_csr).  Same results bit for bit as
+ * cfsd_spmm_csr_x; one dependent index load fewer than cfsd_spmm_csr_sched. */
+int cfsd_spmm_sched_csr(const int32_t* ptr_s, const int32_t* col_s, const float* val_s,
+                        const int32_t* rows_s, const void* x, int x_dt, const void* elu_y, void* y,
+                        int y_dt, int batch, int m, int n, int c, void* stream);
+
 /* cfsd_spmm_csr_x for a matrix whose rows all hold exactly k (1..4) entries,
  * row r's at [r*k, r*k + k) of col/val (the CSR arrays of the barycentric
  * up-sampling matrices, Pool(up) at model.py:84 via model.py:50-55: 3 per

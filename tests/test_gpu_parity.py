@@ -240,7 +240,7 @@ def test_pool_bit_exact(otopo, dtopo, level, kind):
 @pytest.mark.parametrize("bsz", [16, 3])
 @pytest.mark.parametrize("dts", [("f32", "f32"), ("bf16", "bf16"), ("bf16", "f32")])
 def test_pool_scheduled_transpose(dtopo, bsz, dts):
-    """cfsd_spmm_csr_sched == cfsd_spmm_csr(_x) bit for bit (every level, with the
+    """cfsd_spmm_csr_sched and cfsd_spmm_sched_csr == cfsd_spmm_csr(_x) bit for bit (every level, with the
     ELU-backward epilogue, XCD mesh groups and the single-group fallback)."""
     dt = {"f32": torch.float32, "bf16": torch.bfloat16}
     g = torch.Generator().manual_seed(bsz)
@@ -253,6 +253,9 @@ def test_pool_scheduled_transpose(dtopo, bsz, dts):
         ops.spmm_x(dtopo.upT_csr[level], x, m, elu_y=ey, out=a)
         ops.spmm_x(dtopo.upT_csr[level], x, m, elu_y=ey, out=b, order=dtopo.upT_order[level])
         assert torch.equal(a, b), f"level {level}"
+        b.zero_()
+        ops.spmm_x(dtopo.upT_csr[level], x, m, elu_y=ey, out=b, sched=dtopo.upT_sched[level])
+        assert torch.equal(a, b), f"level {level} (visiting-order CSR)"
 
 
 @pytest.mark.parametrize("bsz", [16, 3])

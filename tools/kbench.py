@@ -128,6 +128,8 @@ def main():
                                            (b.g_dec_up[0], b.dh, None)]):
         cases[f"spmm_up{lv}T_s"] = (lambda lv=lv, gin=gin, outb=outb, ey=ey: ops.spmm(
             T.upT_csr[lv], gin, T.n_verts[lv + 1], elu_y=ey, out=outb, order=T.upT_order[lv]))
+        cases[f"spmm_up{lv}T_c"] = (lambda lv=lv, gin=gin, outb=outb, ey=ey: ops.spmm(
+            T.upT_csr[lv], gin, T.n_verts[lv + 1], elu_y=ey, out=outb, sched=T.upT_sched[lv]))
     w2d, b2d = eng._dec_w(2)
     for t in (b.dpre_dec[2], b.g_dec_up[2]):
         t.copy_(torch.randn(t.shape, device="cuda", generator=g))

@@ -2347,13 +2347,16 @@ int dw_mfma_slabs(int cin, int cout, int gx) {
   return gx < cap ? gx : cap;
 }
 
+#ifndef CFSD_DW_LAT_WAVES
+#define CFSD_DW_LAT_WAVES 2048
+#endif
 DwGeom dw_geom(int batch, int rows, int cin, int cout) {
   DwGeom g{kDwNone, 0, 0, 0};
   const long M = (long)batch * rows;
   if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64) && M < CFSD_LAT_DW_MAX) {
     // few rows: one wave per (dW unit, row chunk); ~2k waves
     const long U = (long)dw_units(cin, cout);
-    long R = (M * U / 2048 + 15) / 16 * 16;
+    long R = (M * U / CFSD_DW_LAT_WAVES + 15) / 16 * 16;
     R = R < 32 ? 32 : (R > 512 ? 512 : R);
     g.kind = kDwLat;
     g.rchunk = (int)R;

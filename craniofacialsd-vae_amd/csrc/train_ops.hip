@@ -211,8 +211,10 @@ __global__ __launch_bounds__(CFSD_LAT_THREADS) void latent_fwd_k(const float* __
                                                     int region_size, int train, int is_vae,
                                                     int sigmoid, float w_kl, float w_lc,
                                                     float eta1, float eta2, int bs) {
-  __shared__ float zs[64 * 256];
-  __shared__ float dist[4 * 64 * 8];  // [kind][pair][t]
+  // dynamic LDS: z [B][L], then the distances [kind][pair][t] (4 npairs bs)
+  extern __shared__ float lat_lds[];
+  float* zs = lat_lds;
+  float* dist = lat_lds + B * L;
   __shared__ float2 red[CFSD_LAT_THREADS / 64];
   const int tid = threadIdx.x;
   const int ldm = is_vae ? 2 * L : L;
@@ -936,9 +938,19 @@ extern "C" int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_
   int bs = (int)lrint(sqrt((double)batch));
   if (w_lc != 0.f && bs * bs != batch) return set_error(CFSD_EINVAL, "latent_fwd: batch %d is not bs^2", batch);
   if (w_lc == 0.f) bs = 1;
-  if (batch > 64 || latent > 256 || batch * latent > 64 * 256)
-    return set_error(CFSD_EINVAL, "latent_fwd: batch %d / latent %d too large", batch, latent);
-  hipLaunchKernelGGL(latent_fwd_k, dim3(1), dim3(CFSD_LAT_THREADS), 0, (hipStream_t)stream, mulv, eps, key, z,
+  if (batch <= 0 || latent <= 0) return set_error(CFSD_EINVAL, "latent_fwd: bad sizes");
+  // one workgroup holds z and the pair distances in LDS (up to 160 KB:
+  // e.g. batch 256 = 16^2 at latent 75 takes 105 KB)
+  const size_t lds = ((size_t)batch * latent + (size_t)4 * (bs * (bs - 1) / 2) * bs) * sizeof(float);
+  constexpr size_t kLatLdsMax = 160 * 1024 - 1024;  // minus the static reduction array
+  if (lds > kLatLdsMax)
+    return set_error(CFSD_EINVAL, "latent_fwd: batch %d x latent %d needs %zu B of LDS (> %zu)", batch,
+                     latent, lds, kLatLdsMax);
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)latent_fwd_k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)kLatLdsMax) != hipSuccess)
+    return set_error(CFSD_EINVAL, "latent_fwd: cannot raise the dynamic LDS limit");
+  hipLaunchKernelGGL(latent_fwd_k, dim3(1), dim3(CFSD_LAT_THREADS), lds, (hipStream_t)stream, mulv, eps, key, z,
                      dlat, terms, batch, latent, region_size, train, is_vae, sigmoid, w_kl, w_lc,
                      eta1, eta2, bs);
   return launch_status("latent_fwd");

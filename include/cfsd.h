@@ -284,7 +284,9 @@ int cfsd_recon_lap_bwd_finalize(const float* pred, const float* gt, const float*
  * [key*region_size, +region_size) (key: device scalar; bs = sqrt(batch)).
  * Writes z [batch, latent]; terms[2] = {kl, lc}; and the head's own gradient
  * parts dlat [batch, 3*latent] = {w_lc*dLC/dz | w_kl*dKL/dmu | w_kl*dKL/dlogvar}.
- * Single workgroup (batch <= 64, latent <= 256). */
+ * Single workgroup holding z and the pair distances in LDS: needs
+ * 4 (batch*latent + 4*npairs*bs) bytes <= 159 KB (batch 256 at latent 75:
+ * 105 KB); larger shapes return CFSD_EINVAL. */
 int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_t* key, float* z,
                     float* dlat, float* terms, int batch, int latent, int region_size, int train,
                     int is_vae, int sigmoid, float w_kl, float w_lc, float eta1, float eta2,

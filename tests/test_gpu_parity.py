@@ -467,28 +467,30 @@ def test_linear_bwd_split(m, k, n):
 
 
 # --------------------------------------------------------------- latent head
-@pytest.mark.parametrize("key", [0, 7, 14])
-def test_latent_head_vs_oracle(key):
-    """Reparameterisation + KL + latent consistency (fwd terms and dz/dmu/dlogvar)."""
+@pytest.mark.parametrize("key,bs", [(0, 4), (7, 4), (14, 4), (3, 9), (11, 16)])
+def test_latent_head_vs_oracle(key, bs):
+    """Reparameterisation + KL + latent consistency (fwd terms and dz/dmu/dlogvar);
+    bs 9 and 16 (batch 81 / 256) run the head with > 64 KB of dynamic LDS."""
     g = torch.Generator().manual_seed(key)
-    L, bs = 75, 4
-    mu = torch.randn(16, L, generator=g).double().requires_grad_()
-    lv = (torch.randn(16, L, generator=g) * 0.3).double().requires_grad_()
-    eps = torch.randn(16, L, generator=g)
+    L = 75
+    B = bs * bs
+    mu = torch.randn(B, L, generator=g).double().requires_grad_()
+    lv = (torch.randn(B, L, generator=g) * 0.3).double().requires_grad_()
+    eps = torch.randn(B, L, generator=g)
     z = mu + eps.double() * torch.exp(0.5 * lv)
     regions = O.latent_regions(15, L)
     kl = O.kl_loss(mu, lv)
     lc = O.latent_consistency(z, regions[key], bs)
     (1e-4 * kl + 0.5 * lc).backward()
     mulv = torch.cat([lv, mu], 1).detach().float().to(DEV)
-    zz, dlat, terms = torch.empty(16, L, device=DEV), torch.empty(16, 3 * L, device=DEV), torch.empty(2, device=DEV)
+    zz, dlat, terms = torch.empty(B, L, device=DEV), torch.empty(B, 3 * L, device=DEV), torch.empty(2, device=DEV)
     keyt = torch.full((1,), key, dtype=torch.int32, device=DEV)
     ops.latent_fwd(mulv, eps.to(DEV), keyt, zz, dlat, terms, L, 5, True, True, False, 1e-4, 0.5, 0.5, 0.5)
     close(zz, z.detach(), 1e-5, "z")
     close(terms[0], kl.detach(), 1e-5, "kl")
     close(terms[1], lc.detach(), 1e-5, "lc")
     dmulv = torch.empty_like(mulv)
-    ops.latent_bwd(mulv, eps.to(DEV), zz, torch.zeros(16, L, device=DEV), dlat, dmulv, L, True, True, False)
+    ops.latent_bwd(mulv, eps.to(DEV), zz, torch.zeros(B, L, device=DEV), dlat, dmulv, L, True, True, False)
     close(dmulv[:, L:], mu.grad, 1e-5, "dmu")
     close(dmulv[:, :L], lv.grad, 1e-5, "dlogvar")
 

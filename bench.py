@@ -46,7 +46,7 @@ BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--steps", type=int, default=5000)
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--dataset", type=int, default=256, help="resident synthetic meshes per rank")
     p.add_argument("--topology", default="craniofacial", choices=["craniofacial", "synth5k"])

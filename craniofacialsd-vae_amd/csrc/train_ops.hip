@@ -69,6 +69,32 @@ __device__ __forceinline__ float2 block_sum2(float a, float b, float2* sh) {
 }
 
 // ----------------------------------------------------------- recon + Laplacian
+// C consecutive floats of one vertex row (C = 3: xyz) as ONE dwordx3 access
+// (per-channel dword accesses cost a texture-path cycle per line per
+// instruction three times over); rows are only dword-aligned.
+typedef float f32x3u __attribute__((ext_vector_type(3), aligned(4)));
+template <int C>
+__device__ __forceinline__ void ld_row(const float* __restrict__ p, float (&v)[C]) {
+  if constexpr (C == 3) {
+    const f32x3u t = *reinterpret_cast<const f32x3u*>(p);
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+  } else {
+#pragma unroll
+    for (int q = 0; q < C; ++q) v[q] = p[q];
+  }
+}
+template <int C>
+__device__ __forceinline__ void st_row(float* __restrict__ p, const float (&v)[C]) {
+  if constexpr (C == 3) {
+    *reinterpret_cast<f32x3u*>(p) = (f32x3u){v[0], v[1], v[2]};
+  } else {
+#pragma unroll
+    for (int q = 0; q < C; ++q) p[q] = v[q];
+  }
+}
+
 // Sparse row dot products of the Laplacian passes: entries in chunks of 8
 // whose column/value loads, then whose C-wide row loads, are issued together
 // (2 memory round trips per chunk instead of 2 per entry); past-the-end
@@ -89,9 +115,7 @@ __device__ __forceinline__ void lap_row_dot(int beg, int end, const int* __restr
     }
     float xv[CK][C];
 #pragma unroll
-    for (int j = 0; j < CK; ++j)
-#pragma unroll
-      for (int q = 0; q < C; ++q) xv[j][q] = xb[(long)cc[j] * C + q];
+    for (int j = 0; j < CK; ++j) ld_row<C>(xb + (long)cc[j] * C, xv[j]);
 #pragma unroll
     for (int j = 0; j < CK; ++j)
 #pragma unroll
@@ -116,17 +140,21 @@ __global__ __launch_bounds__(kLapThreads) void recon_lap_fwd_k(
 #pragma unroll
     for (int q = 0; q < C; ++q) lx[q] = 0.f;
     lap_row_dot<C>(l_ptr[v], l_ptr[v + 1], l_col, l_val, pred + b * nv * C, lx);
-    float n2 = 0.f;
+    float n2 = 0.f, pv[C], gv[C];
+    ld_row<C>(pred + t * C, pv);
+    ld_row<C>(gt + t * C, gv);
 #pragma unroll
     for (int q = 0; q < C; ++q) {
-      const float d = pred[t * C + q] - gt[t * C + q];
+      const float d = pv[q] - gv[q];
       sq = fmaf(d, d, sq);
       n2 = fmaf(lx[q], lx[q], n2);
     }
     nrm = sqrtf(n2);
     const float inv = nrm > 0.f ? 1.f / nrm : 0.f;
+    float un[C];
 #pragma unroll
-    for (int q = 0; q < C; ++q) unit[t * C + q] = lx[q] * inv;
+    for (int q = 0; q < C; ++q) un[q] = lx[q] * inv;
+    st_row<C>(unit + t * C, un);
   }
   float2 r = block_sum2(sq, nrm, sh);
   if (threadIdx.x == 0) {
@@ -187,9 +215,12 @@ __global__ __launch_bounds__(256) void recon_lap_bwd_k(
 #pragma unroll
   for (int q = 0; q < C; ++q) g[q] = 0.f;
   lap_row_dot<C>(lt_ptr[u], lt_ptr[u + 1], lt_col, lt_val, unit + b * nv * C, g);
+  float pv[C], gv[C], dv[C];
+  ld_row<C>(pred + t * C, pv);
+  ld_row<C>(gt + t * C, gv);
 #pragma unroll
-  for (int q = 0; q < C; ++q)
-    dpred[t * C + q] = k_rec * (pred[t * C + q] - gt[t * C + q]) + k_lap * g[q];
+  for (int q = 0; q < C; ++q) dv[q] = k_rec * (pv[q] - gv[q]) + k_lap * g[q];
+  st_row<C>(dpred + t * C, dv);
 }
 
 // ----------------------------------------------------------- latent head

@@ -87,6 +87,32 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// CS consecutive floats of one small-channel row (CS = 3: xyz) as ONE
+// dwordx3 access: per-channel dword loads cost the texture path a cycle per
+// cache line per instruction three times over.  Rows are only dword-aligned.
+typedef float f32x3u __attribute__((ext_vector_type(3), aligned(4)));
+template <int CS>
+__device__ __forceinline__ void ld_row(const float* __restrict__ p, float* v) {
+  if constexpr (CS == 3) {
+    const f32x3u t = *reinterpret_cast<const f32x3u*>(p);
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+  } else {
+#pragma unroll
+    for (int q = 0; q < CS; ++q) v[q] = p[q];
+  }
+}
+template <int CS>
+__device__ __forceinline__ void st_row(float* __restrict__ p, const float* v) {
+  if constexpr (CS == 3) {
+    *reinterpret_cast<f32x3u*>(p) = (f32x3u){v[0], v[1], v[2]};
+  } else {
+#pragma unroll
+    for (int q = 0; q < CS; ++q) p[q] = v[q];
+  }
+}
+
 constexpr int kMaxBatch = 1 << 20;
 
 // ---------------------------------------------------------------- bf16 storage

@@ -298,7 +298,13 @@ __global__ __launch_bounds__(256) void swap_k(const float* __restrict__ x,
   const long src_mesh = min(max(batch_idx[take ? j : i], 0), n_meshes - 1);
   const float* src = x + (src_mesh * nv + v) * c;
   float* dst = out + t * c;
-  for (int q = 0; q < c; ++q) dst[q] = src[q];
+  if (c == 3) {  // xyz: one dwordx3 load and store
+    float v3[3];
+    ld_row<3>(src, v3);
+    st_row<3>(dst, v3);
+  } else {
+    for (int q = 0; q < c; ++q) dst[q] = src[q];
+  }
 }
 
 // Storage conversion fp32 <-> bf16 (round to nearest even), 4 elements per

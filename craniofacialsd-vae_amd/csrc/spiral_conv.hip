@@ -330,9 +330,7 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
     float g[2 * KH];
 #pragma unroll
     for (int s = 0; s < kSeq; ++s) {
-      const float* p = xb + (long)ir[s] * CS;
-#pragma unroll
-      for (int c = 0; c < CS; ++c) g[s * CS + c] = p[c];
+      ld_row<CS>(xb + (long)ir[s] * CS, &g[s * CS]);
     }
 #pragma unroll
     for (int k = K; k < 2 * KH; ++k) g[k] = 0.f;
@@ -1608,9 +1606,7 @@ __global__ __launch_bounds__(256) void conv_dw_in_mfma(const float* __restrict__
     float xv[K];
 #pragma unroll
     for (int s = 0; s < kSeq; ++s) {
-      const float* p = xb + (long)ir[s] * CS;
-#pragma unroll
-      for (int c = 0; c < CS; ++c) xv[s * CS + c] = p[c];
+      ld_row<CS>(xb + (long)ir[s] * CS, &xv[s * CS]);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) At[k * kAts + lane] = valid ? xv[k] : 0.f;

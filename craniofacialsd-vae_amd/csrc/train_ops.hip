@@ -69,36 +69,6 @@ __device__ __forceinline__ float2 block_sum2(float a, float b, float2* sh) {
 }
 
 // ----------------------------------------------------------- recon + Laplacian
-// C consecutive floats of one vertex row (C = 3: xyz) as ONE dwordx3 access
-// (per-channel dword accesses cost a texture-path cycle per line per
-// instruction three times over); rows are only dword-aligned.
-typedef float f32x3u __attribute__((ext_vector_type(3), aligned(4)));
-template <int C>
-__device__ __forceinline__ void ld_row(const float* __restrict__ p, float (&v)[C]) {
-  if constexpr (C == 3) {
-    const f32x3u t = *reinterpret_cast<const f32x3u*>(p);
-    v[0] = t.x;
-    v[1] = t.y;
-    v[2] = t.z;
-  } else {
-#pragma unroll
-    for (int q = 0; q < C; ++q) v[q] = p[q];
-  }
-}
-template <int C>
-__device__ __forceinline__ void st_row(float* __restrict__ p, const float (&v)[C]) {
-  if constexpr (C == 3) {
-    *reinterpret_cast<f32x3u*>(p) = (f32x3u){v[0], v[1], v[2]};
-  } else {
-#pragma unroll
-    for (int q = 0; q < C; ++q) p[q] = v[q];
-  }
-}
-
-// Sparse row dot products of the Laplacian passes: entries in chunks of 8
-// whose column/value loads, then whose C-wide row loads, are issued together
-// (2 memory round trips per chunk instead of 2 per entry); past-the-end
-// entries are clamped to the row's last one and weighted 0.
 template <int C>
 __device__ __forceinline__ void lap_row_dot(int beg, int end, const int* __restrict__ col,
                                             const float* __restrict__ val,

@@ -102,10 +102,12 @@ class Runner:
         eng.backward_head(b, split=self.world > 1)
 
     def part_b(self):
-        self.eng.backward_tail(self.b)
+        # one process: the Adam step rides in the final weight-gradient reduce
+        self.eng.backward_tail(self.b, fuse_adam=self.world == 1)
 
     def part_c(self):
-        self.eng.adam_step()
+        if self.world > 1:
+            self.eng.adam_step()
 
     def eager_step(self):
         self.part_a()

@@ -73,6 +73,7 @@ SIGNATURES = {
     "cfsd_cast": (_I, [_P, _I, _P, _I, _Z, _P]),
     "cfsd_step_begin": (_I, [_P, _U64, _P, _I, _P, _I, _P, _I, _I, _P, _I, _I, _P, _P]),
     "cfsd_dw_reduce_batch": (_I, [_P, _I, _P]),
+    "cfsd_dw_reduce_batch_adam": (_I, [_P, _I, _P, _P, _P, _P, _P, _Z, _F, _F, _F, _F, _F, _P, _P]),
     "cfsd_scale": (_I, [_P, _Z, _F, _P]),
     "cfsd_elu_bwd": (_I, [_P, _P, _P, _Z, _P]),
     "cfsd_vertex_errors": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P]),

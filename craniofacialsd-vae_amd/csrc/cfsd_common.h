@@ -113,6 +113,17 @@ __device__ __forceinline__ void st_row(float* __restrict__ p, const float* v) {
   }
 }
 
+// torch.optim.Adam (non-amsgrad) update of one element.
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1,
+                                          float b2, float eps, float wd, float step_size,
+                                          float sqrt_bc2) {
+  if (wd != 0.f) g = fmaf(wd, p, g);
+  m = fmaf(b1, m, (1.f - b1) * g);
+  v = fmaf(b2, v, (1.f - b2) * g * g);
+  const float denom = sqrtf(v) / sqrt_bc2 + eps;
+  p -= step_size * (m / denom);
+}
+
 constexpr int kMaxBatch = 1 << 20;
 
 // ---------------------------------------------------------------- bf16 storage

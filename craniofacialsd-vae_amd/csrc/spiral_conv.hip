@@ -1308,16 +1308,68 @@ struct DwRedItem {
   int kind, cin, cout, n_slabs, n_el, blk0;
 };
 constexpr int kMaxDwRed = 16;
+// Optional Adam step fused into the reduction (single-process training: no
+// gradient exchange between the reduce and the update).  Every reduced
+// element is updated by the thread that produced its gradient; the elements
+// no item covers ([lo, hi) ranges of the flat buffers, e.g. the Linears)
+// by the workgroups past the reduction's.
+constexpr int kMaxAdamRest = 2 * kMaxDwRed + 2;
+struct DwAdam {
+  float* p;
+  const float* g;  // flat gradient buffer the items' dw/db point into
+  float* m;
+  float* v;
+  bf16_t* shadow;
+  const int* step;
+  float lr, b1, b2, eps, wd;
+  int n_rest;
+  long rest_lo[kMaxAdamRest], rest_hi[kMaxAdamRest], rest_blk0[kMaxAdamRest + 1];
+};
 struct DwRedBatch {
   DwRedItem it[kMaxDwRed];
   int n;
+  int blk_end;  // first workgroup past the reductions
+  DwAdam adam;  // adam.p == nullptr: no fused update
 };
+
+__device__ __forceinline__ void adam_consts(const DwAdam& a, float& step_size, float& sqrt_bc2) {
+  const int t = *a.step;
+  step_size = a.lr / (1.f - powf(a.b1, (float)t));
+  sqrt_bc2 = sqrtf(1.f - powf(a.b2, (float)t));
+}
+// Adam on the element whose gradient (value g) was just written at gp.
+__device__ __forceinline__ void adam_at(const DwAdam& a, const float* gp, float g, float step_size,
+                                        float sqrt_bc2) {
+  const long o = gp - a.g;
+  float pv = a.p[o], mv = a.m[o], vv = a.v[o];
+  adam_elem(pv, g, mv, vv, a.b1, a.b2, a.eps, a.wd, step_size, sqrt_bc2);
+  a.p[o] = pv;
+  a.m[o] = mv;
+  a.v[o] = vv;
+  if (a.shadow) stf(a.shadow + o, pv);
+}
 
 // Items whose slab length is a multiple of 4 (every conv_dw_mfma / lat
 // item: U*1024 + cout) are reduced four consecutive elements per lane with
 // 16-B loads (256 elements per workgroup); the others (small-channel slabs)
 // one element per lane.  Same per-element summation order either way.
 __global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
+  const bool fuse = B.adam.p != nullptr;
+  if (fuse && (int)blockIdx.x >= B.blk_end) {  // Adam on the elements no item covers
+    const DwAdam& a = B.adam;
+    float step_size, sqrt_bc2;
+    adam_consts(a, step_size, sqrt_bc2);
+    const int rb = (int)blockIdx.x - B.blk_end;
+    int ri = 0;
+    while (ri + 1 < a.n_rest && rb >= a.rest_blk0[ri + 1]) ++ri;
+    const long base = a.rest_lo[ri] + (long)(rb - a.rest_blk0[ri]) * 4096;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long o = base + k * 1024 + threadIdx.x;
+      if (o < a.rest_hi[ri]) adam_at(a, a.g + o, a.g[o], step_size, sqrt_bc2);
+    }
+    return;
+  }
   int li = 0;
   while (li + 1 < B.n && (int)blockIdx.x >= B.it[li + 1].blk0) ++li;
   const DwRedItem d = B.it[li];
@@ -1368,12 +1420,18 @@ __global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
     f32x4 t = part[0][lane];
 #pragma unroll
     for (int q = 1; q < 16; ++q) t += part[q][lane];
+    float step_size = 0.f, sqrt_bc2 = 1.f;
+    if (fuse) adam_consts(B.adam, step_size, sqrt_bc2);
     if (!vec) {
-      if (f >= nw) d.db[f - nw] = t.x;
-      else d.dw[f] = t.x;
+      float* dst = f >= nw ? d.db + (f - nw) : d.dw + f;
+      *dst = t.x;
+      if (fuse) adam_at(B.adam, dst, t.x, step_size, sqrt_bc2);
     } else if (f >= nw) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) d.db[f - nw + e] = t[e];
+      for (int e = 0; e < 4; ++e) {
+        d.db[f - nw + e] = t[e];
+        if (fuse) adam_at(B.adam, d.db + f - nw + e, t[e], step_size, sqrt_bc2);
+      }
     } else {
       // 4 consecutive elements of one 32-wide unit row: 4 consecutive c
       const int CT = d.cin / 32, OT = d.cout / 32;
@@ -1383,7 +1441,10 @@ __global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
       const int sl = un / (CT * OT);
       float* dst = d.dw + (long)o * K + sl * d.cin + cc;  // 8-B aligned in the flat buffer
 #pragma unroll
-      for (int e = 0; e < 4; ++e) dst[e] = t[e];
+      for (int e = 0; e < 4; ++e) {
+        dst[e] = t[e];
+        if (fuse) adam_at(B.adam, dst + e, t[e], step_size, sqrt_bc2);
+      }
     }
   }
 }
@@ -2931,8 +2992,9 @@ extern "C" int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* id
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: unsupported channels %d -> %d", cin, cout);
 }
 
-extern "C" int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* stream) {
-  if (n <= 0) return CFSD_OK;
+static int dw_reduce_batch_launch(const cfsd_dw_slabs* items, int n, const DwAdam* adam, long n_params,
+                                  void* stream) {
+  if (n <= 0 && !adam) return CFSD_OK;
   if (!items) return set_error(CFSD_EINVAL, "dw_reduce_batch: null items");
   if (n > kMaxDwRed) return set_error(CFSD_EINVAL, "dw_reduce_batch: %d items > %d", n, kMaxDwRed);
   DwRedBatch B{};
@@ -2978,6 +3040,77 @@ extern "C" int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* str
     d.blk0 = blk;
     blk += d.kind == 0 ? (d.n_el + 255) / 256 : (d.n_el + 63) / 64;
   }
+  B.blk_end = blk;
+  B.adam.p = nullptr;
+  if (adam) {
+    // the items' dw/db ranges inside [0, n_params) of the flat gradient, sorted;
+    // everything else is updated by the rest workgroups
+    B.adam = *adam;
+    long lo[2 * kMaxDwRed], hi[2 * kMaxDwRed];
+    int nr = 0;
+    for (int i = 0; i < n; ++i) {
+      const long K = (long)kSeq * items[i].cin;
+      const long w0 = items[i].dw - adam->g, b0 = items[i].db - adam->g;
+      const long wn = (long)items[i].cout * K, bn = items[i].cout;
+      if (w0 < 0 || w0 + wn > n_params || b0 < 0 || b0 + bn > n_params)
+        return set_error(CFSD_EINVAL, "dw_reduce_batch_adam: item %d outside the flat gradient", i);
+      lo[nr] = w0; hi[nr++] = w0 + wn;
+      lo[nr] = b0; hi[nr++] = b0 + bn;
+    }
+    for (int i = 1; i < nr; ++i)  // insertion sort by start
+      for (int j = i; j > 0 && lo[j] < lo[j - 1]; --j) {
+        long t = lo[j]; lo[j] = lo[j - 1]; lo[j - 1] = t;
+        t = hi[j]; hi[j] = hi[j - 1]; hi[j - 1] = t;
+      }
+    long cur = 0;
+    int nrest = 0, rblk = 0;
+    auto add_rest = [&](long a0, long a1) {
+      if (a1 <= a0) return true;
+      if (nrest >= kMaxAdamRest) return false;
+      B.adam.rest_lo[nrest] = a0;
+      B.adam.rest_hi[nrest] = a1;
+      B.adam.rest_blk0[nrest] = rblk;
+      rblk += (int)((a1 - a0 + 4095) / 4096);
+      ++nrest;
+      return true;
+    };
+    for (int i = 0; i < nr; ++i) {
+      if (lo[i] < cur) return set_error(CFSD_EINVAL, "dw_reduce_batch_adam: overlapping items");
+      if (!add_rest(cur, lo[i])) return set_error(CFSD_EINVAL, "dw_reduce_batch_adam: too many gaps");
+      cur = hi[i];
+    }
+    if (!add_rest(cur, n_params)) return set_error(CFSD_EINVAL, "dw_reduce_batch_adam: too many gaps");
+    B.adam.n_rest = nrest;
+    B.adam.rest_blk0[nrest] = rblk;
+    blk += rblk;
+  }
+  if (blk == 0) return CFSD_OK;
   hipLaunchKernelGGL(dw_reduce_batch_k, dim3(blk), dim3(1024), 0, (hipStream_t)stream, B);
   return launch_status("dw_reduce_batch");
+}
+
+extern "C" int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* stream) {
+  return dw_reduce_batch_launch(items, n, nullptr, 0, stream);
+}
+
+extern "C" int cfsd_dw_reduce_batch_adam(const cfsd_dw_slabs* items, int n, float* param,
+                                         const float* grad, float* exp_avg, float* exp_avg_sq,
+                                         const int32_t* step, size_t n_params, float lr, float beta1,
+                                         float beta2, float eps, float weight_decay,
+                                         uint16_t* param_bf16, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !step || n_params <= 0)
+    return set_error(CFSD_EINVAL, "dw_reduce_batch_adam: null buffer / bad size");
+  DwAdam a{};
+  a.p = param;
+  a.g = grad;
+  a.m = exp_avg;
+  a.v = exp_avg_sq;
+  a.shadow = reinterpret_cast<bf16_t*>(param_bf16);
+  a.step = step;
+  a.lr = lr;
+  a.b1 = beta1;
+  a.b2 = beta2;
+  a.eps = eps;
+  a.wd = weight_decay;
+  return dw_reduce_batch_launch(items, n, &a, (long)n_params, stream);
 }

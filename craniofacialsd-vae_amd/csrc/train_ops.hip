@@ -731,16 +731,6 @@ __global__ __launch_bounds__(256) void linear_bwd_pair_k(const float* __restrict
 }
 
 // ----------------------------------------------------------- Adam
-// torch.optim.Adam (non-amsgrad) update of one element.
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1,
-                                          float b2, float eps, float wd, float step_size,
-                                          float sqrt_bc2) {
-  if (wd != 0.f) g = fmaf(wd, p, g);
-  m = fmaf(b1, m, (1.f - b1) * g);
-  v = fmaf(b2, v, (1.f - b2) * g * g);
-  const float denom = sqrtf(v) / sqrt_bc2 + eps;
-  p -= step_size * (m / denom);
-}
 // Four elements per thread in 16-B accesses (the four state arrays are
 // streamed once: 7 x 4 B per element of HBM traffic); the n % 4 tail goes to
 // the last thread.  Same per-element arithmetic as a scalar loop.

@@ -549,18 +549,19 @@ class SDVAEEngine:
         parameters (the last gradients the backward produces)."""
         return self.params.offsets[f"en_layers.{self.spec.n}.weight"][0]
 
-    def backward(self, b, bucket_hook=None):
+    def backward(self, b, bucket_hook=None, fuse_adam=False):
         """Hand-derived backward of forward() (the reference's
         ``loss_tot.backward()``).  With ``bucket_hook`` the gradient becomes
         final in two contiguous buckets and the hook is called on each as soon
         as it is (data-parallel all-reduce overlapped with the rest of the
         backward): first everything from the encoder Linear on (decoder,
         bottleneck: ~96 % of the parameters), after the encoder-Linear
-        backward; then the encoder convs at the end."""
+        backward; then the encoder convs at the end.  ``fuse_adam`` (no hook):
+        the Adam step runs in the final weight-gradient reduce launch."""
         self.backward_head(b, split=bucket_hook is not None)
         if bucket_hook is not None:
             bucket_hook(self.params.grad[self.enc_conv_numel():])
-        self.backward_tail(b)
+        self.backward_tail(b, fuse_adam=fuse_adam and bucket_hook is None)
         if bucket_hook is not None:
             bucket_hook(self.params.grad[:self.enc_conv_numel()])
 
@@ -655,9 +656,17 @@ class SDVAEEngine:
             ops.spmm(T.downT_csr[last], b.g_pooled[last], T.n_verts[last], elu_y=b.enc_full[last],
                      out=b.dpre_enc[last])
 
-    def backward_tail(self, b):
+    def adam_args(self):
+        P = self.params
+        return dict(param=P.data, grad=P.grad, m=P.exp_avg, v=P.exp_avg_sq, step=P.step, lr=self.lr,
+                    beta1=self.betas[0], beta2=self.betas[1], eps=self.adam_eps,
+                    weight_decay=self.weight_decay, shadow=P.shadow)
+
+    def backward_tail(self, b, fuse_adam=False):
         """Encoder convs (E_{n-1} .. E0), then ONE batched reduce of every
-        still-deferred conv weight gradient."""
+        still-deferred conv weight gradient -- with ``fuse_adam`` (nothing
+        exchanges the gradient before the update) the Adam step runs in the
+        same launch (``cfsd_dw_reduce_batch_adam``) and adam_step is skipped."""
         T, S, P = self.topo, self.spec, self.params
         deferred, b.deferred = b.deferred, []
 
@@ -719,7 +728,7 @@ class SDVAEEngine:
                                          out=b.g_pooled[prev], workspace=b.ws)
                 ops.spmm(T.downT_csr[prev], b.g_pooled[prev], T.n_verts[prev], elu_y=b.enc_full[prev],
                          out=b.dpre_enc[prev])
-        ops.dw_reduce_batch(deferred)
+        ops.dw_reduce_batch(deferred, adam=self.adam_args() if fuse_adam else None)
 
     def adam_step(self):
         P = self.params
@@ -764,10 +773,12 @@ class SDVAEEngine:
         if hasattr(grad_hook, "bucket_ready"):  # dist.GradientAverager: overlapped buckets
             self.backward(b, bucket_hook=grad_hook.bucket_ready)
             grad_hook.finish(self.params.grad)
-        else:
+        elif grad_hook is not None:
             self.backward(b)
-            if grad_hook is not None:
-                grad_hook(self.params.grad)
+            grad_hook(self.params.grad)
+        else:  # nothing between the gradient and the update: Adam fused into the reduce
+            self.backward(b, fuse_adam=True)
+            return
         self.adam_step()
 
     def resident_step(self, b, data, acc=None, grad_hook=None):

@@ -149,13 +149,28 @@ class DeferredDw:
         return _abi.DwSlabs(self.workspace.data_ptr(), dw.data_ptr(), db.data_ptr(), *self.sizes)
 
 
-def dw_reduce_batch(items):
+def dw_reduce_batch(items, adam=None):
     """Reduce several deferred weight gradients in ONE launch.
-    ``items``: list of (DeferredDw, dw, db)."""
-    if not items:
+    ``items``: list of (DeferredDw, dw, db).  ``adam``: optional dict(param,
+    grad, m, v, step, lr, beta1, beta2, eps, weight_decay, shadow) -- the Adam
+    step over the whole flat buffers fused into the same launch (the items'
+    dw/db must be views of ``grad``)."""
+    if not items and adam is None:
         return
-    arr = (_abi.DwSlabs * len(items))(*[d.desc(dw, db) for d, dw, db in items])
-    call("cfsd_dw_reduce_batch", arr, len(items), stream_ptr())
+    arr = (_abi.DwSlabs * max(len(items), 1))(*[d.desc(dw, db) for d, dw, db in items])
+    if adam is None:
+        call("cfsd_dw_reduce_batch", arr, len(items), stream_ptr())
+        return
+    a = adam
+    n = a["param"].numel()
+    for t, nm in ((a["param"], "param"), (a["grad"], "grad"), (a["m"], "m"), (a["v"], "v")):
+        _need(t, (n,), name=nm)
+    _need(a["step"], (1,), torch.int32, "step")
+    if a.get("shadow") is not None:
+        _need(a["shadow"], (n,), torch.bfloat16, "shadow")
+    call("cfsd_dw_reduce_batch_adam", arr, len(items), ptr(a["param"]), ptr(a["grad"]), ptr(a["m"]),
+         ptr(a["v"]), ptr(a["step"]), ctypes.c_size_t(n), float(a["lr"]), float(a["beta1"]),
+         float(a["beta2"]), float(a["eps"]), float(a["weight_decay"]), ptr(a.get("shadow")), stream_ptr())
 
 
 def spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout):

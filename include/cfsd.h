@@ -104,6 +104,17 @@ typedef struct {
   int batch, vsrc, rows, cin, cout, fused;
 } cfsd_dw_slabs;
 int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* stream);
+/* cfsd_dw_reduce_batch fused with the Adam step of cfsd_adam (single-process
+ * training, model_manager.py:316 after :315's backward): every item's dw/db
+ * must lie inside the flat gradient `grad` [n_params]; each reduced element
+ * is written to grad and updated in param / exp_avg / exp_avg_sq (and
+ * param_bf16) by the thread that reduced it, every other element of the flat
+ * buffers by extra workgroups of the same launch.  Same values as
+ * cfsd_dw_reduce_batch followed by cfsd_adam. */
+int cfsd_dw_reduce_batch_adam(const cfsd_dw_slabs* items, int n, float* param, const float* grad,
+                              float* exp_avg, float* exp_avg_sq, const int32_t* step,
+                              size_t n_params, float lr, float beta1, float beta2, float eps,
+                              float weight_decay, uint16_t* param_bf16, void* stream);
 
 /* Fused backward of one SpiralConv (model.py:27-41 autograd, dX and dW/db of
  * the same layer in one call): dx exactly as cfsd_spiral_conv_bwd_data

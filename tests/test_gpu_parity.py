@@ -400,6 +400,33 @@ def test_train_step_deterministic(dtopo):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+def test_fused_reduce_adam_matches_separate(dtopo):
+    """cfsd_dw_reduce_batch_adam (train_step_on without a gradient hook) ==
+    cfsd_dw_reduce_batch + cfsd_adam, bit for bit: parameters, gradients and
+    both Adam moments after two steps."""
+    w = recipe.golden_weights()
+    x = torch.from_numpy(O.swap_features(recipe.normalized_meshes(4), [np.asarray(r) for r in
+                                         O.Topology(recipe.load_topology()).region_features], 2)).to(DEV)
+    eps = torch.from_numpy(recipe.train_eps(0)).to(DEV)
+    outs = []
+    for fused in (True, False):
+        eng = make_engine(dtopo, w)
+        for _ in range(2):
+            b = eng.set_batch(x, key_index=2, eps=eps)
+            if fused:
+                eng.train_step_on(b)
+            else:
+                eng.advance_step(b)
+                eng.forward(b, train=True, finalize=False)
+                eng.backward(b)
+                eng.adam_step()
+        torch.cuda.synchronize()
+        P = eng.params
+        outs.append([t.cpu().clone() for t in (P.data, P.grad, P.exp_avg, P.exp_avg_sq)])
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+
+
 # --------------------------------------------------------------- dense Linears
 # Both bottleneck shapes of the model (encoder [m x 4288] -> 150 stacked
 # mu/logvar, decoder 75 -> 4288) plus ragged m (not a multiple of the 4-row /

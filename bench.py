@@ -34,6 +34,7 @@ cfsd_loader.load()
 from craniofacialsd_vae_amd import _abi, ops, topology  # noqa: E402
 from craniofacialsd_vae_amd import dist as cdist  # noqa: E402
 from craniofacialsd_vae_amd import engine as E  # noqa: E402
+from craniofacialsd_vae_amd.step import TrainStep  # noqa: E402
 
 METRIC = "train meshes/sec + per-vertex L1, craniofacial SD-VAE @1/2/4/8 MI355X"
 TOPO_NPZ = os.path.join(ROOT, "tests", "golden", "topology_craniofacial.npz")
@@ -54,11 +55,45 @@ def parse():
                    help="fp32 (reference arithmetic) or bf16 (configs C3/C5: bf16 level-0/1 tensors on "
                         "bf16 MFMA, fp32 accumulation and master weights)")
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
+    p.add_argument("--augmented", type=int, default=0,
+                   help="configuration C5: train on N spectral-interpolation meshes (k = 1000 eigenvectors of "
+                        "the template, pairs of the demo meshes) generated on the device and resident in HBM, "
+                        "N / world per rank, instead of N(0, 1) meshes")
     p.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU-baseline sample budget")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-extras", action="store_true",
                    help="skip the secondary measurements (synthetic ~5k line, kernel trace)")
     return p.parse_args()
+
+
+def augmented_set(n, device, seed):
+    """C5's training set (BASELINE config 5): ``n`` meshes generated on the
+    device by spectral interpolation (utils.py:256-267) of same-class pairs of
+    the 12 demo meshes (data_loading.py:292-374), k = 1000 eigenvectors of
+    the template Laplacian, normalised by their own per-vertex mean / std
+    (data_loading.py:231-252).  Returns (meshes, norm, timing)."""
+    from craniofacialsd_vae_amd import augment as A
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import recipe
+    npz = np.load(TOPO_NPZ)
+    faces, nv = npz["face_0"].astype(np.int64), int(npz["pos_0"].shape[0])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, u = A.laplacian_eigendecomposition(faces, nv, k=1000, device=device)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    m = recipe.load_meshes()
+    raw = torch.from_numpy(m["verts"]).to(device)
+    aug, cls = A.synthesize(u, raw, [str(x)[0] for x in m["names"]], n, seed=seed)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    std = torch.std(aug, dim=0)
+    norm = {"mean": torch.mean(aug, dim=0), "std": torch.where(std > 0, std, torch.full_like(std, 1e-8))}
+    del u, raw
+    return aug, norm, {"meshes": n, "classes": {c: cls.count(c) for c in sorted(set(cls))},
+                       "eigendecomposition_s": t1 - t0, "generation_s": t2 - t1,
+                       "k": 1000, "source": "12 demo meshes (tests/golden/demo_meshes.npz), same-class pairs",
+                       "finite": bool(torch.isfinite(aug).all())}
 
 
 def load_topology(name, device):
@@ -69,8 +104,12 @@ def load_topology(name, device):
 
 
 class Runner:
+    """The benchmarked step is :class:`step.TrainStep` -- the same object
+    the data-parallel GPU tests (tests/test_gpu_dist.py) and the training
+    driver (manager.ModelManager) run."""
+
     def __init__(self, world, rank, device, n_meshes, use_graph, topo_name="craniofacial",
-                 precision="fp32"):
+                 precision="fp32", meshes=None, norm=None):
         self.topo = load_topology(topo_name, device)
         self.topo_name = topo_name
         self.precision = precision
@@ -79,81 +118,26 @@ class Runner:
         self.eng.reset_parameters()  # same init on every rank (broadcast below)
         self.world, self.rank = world, rank
         nv = self.topo.n_verts[0]
-        gen = torch.Generator(device=device).manual_seed(1234 + rank)
-        self.data = E.ResidentData(torch.randn(n_meshes, nv, 3, device=device, generator=gen), bs=4,
-                                   shuffle=True)
-        self.b = self.eng.buffers(16)
+        if meshes is None:
+            gen = torch.Generator(device=device).manual_seed(1234 + rank)
+            meshes = torch.randn(n_meshes, nv, 3, device=device, generator=gen)
+        self.data = E.ResidentData(meshes, bs=4, shuffle=True, norm=norm)
         self.avg = cdist.GradientAverager(world)
         if world > 1:
             cdist.broadcast_parameters(self.eng.params.data, 0)
             self.eng.sync_shadow()
+        self.ts = TrainStep(self.eng, self.data, self.avg)
+        self.b = self.ts.b
         self.use_graph = use_graph
-        self.graphs = None
-
-    # --- the step, split where the collective buckets go
-    def part_a(self):
-        """step_begin + swap + forward + backward up to the encoder Linear."""
-        eng, b, T, d = self.eng, self.b, self.topo, self.data
-        ops.step_begin(eng.counter, eng.seed, eps=b.eps, key=b.key, n_regions=T.n_regions,
-                       batch_idx=b.batch_idx, bs=4, n_batches=d.n_batches, perm=d.rows,
-                       n_items=d.n_items, shuffle=d.shuffle, adam_step=eng.params.step)
-        ops.swap_features(d.meshes, b.batch_idx, T.region_mask, b.key, 4, out=b.x)
-        eng.forward(b, train=True, acc=eng.loss_acc, finalize=False)
-        eng.backward_head(b, split=self.world > 1)
-
-    def part_b(self):
-        # one process: the Adam step rides in the final weight-gradient reduce
-        self.eng.backward_tail(self.b, fuse_adam=self.world == 1)
-
-    def part_c(self):
-        if self.world > 1:
-            self.eng.adam_step()
 
     def eager_step(self):
-        self.part_a()
-        if self.world > 1:
-            self.avg.bucket_ready(self.eng.params.grad[self.eng.enc_conv_numel():])
-        self.part_b()
-        if self.world > 1:
-            self.avg.bucket_ready(self.eng.params.grad[:self.eng.enc_conv_numel()])
-            self.avg.finish(self.eng.params.grad)
-        self.part_c()
+        self.ts.eager_step()
 
     def capture(self):
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                self.eager_step()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        if self.world == 1:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self.part_a()
-                self.part_b()
-                self.part_c()
-            self.graphs = [g]
-        else:
-            self.graphs = [torch.cuda.CUDAGraph() for _ in range(3)]
-            for g, fn in zip(self.graphs, (self.part_a, self.part_b, self.part_c)):
-                with torch.cuda.graph(g):
-                    fn()
+        self.ts.capture()
 
     def step(self):
-        if self.graphs is None:
-            return self.eager_step()
-        if self.world == 1:
-            self.graphs[0].replay()
-            return
-        ga, gb, gc = self.graphs
-        grad = self.eng.params.grad
-        ga.replay()
-        self.avg.bucket_ready(grad[self.eng.enc_conv_numel():])  # overlaps with gb
-        gb.replay()
-        self.avg.bucket_ready(grad[:self.eng.enc_conv_numel()])
-        self.avg.finish(grad)
-        gc.replay()
+        self.ts.step()
 
 
 # ------------------------------------------------------------------ roofline
@@ -504,7 +488,13 @@ def main():
             dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    runner = Runner(world, rank, device, args.dataset, not args.no_graph, args.topology, args.precision)
+    aug_info, meshes, norm = None, None, None
+    if args.augmented:
+        per_rank = args.augmented // world
+        meshes, norm, aug_info = augmented_set(per_rank, device, seed=77 + rank)
+    runner = Runner(world, rank, device, args.dataset, not args.no_graph, args.topology, args.precision,
+                    meshes=meshes, norm=norm)
+    del meshes
     if runner.use_graph:
         runner.capture()
     for _ in range(args.warmup):
@@ -581,12 +571,16 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if bf else "fp32",
-            "data": "synthetic N(0,1) meshes resident in HBM, random-init weights",
+            "data": ("spectral-interpolation augmented meshes generated on the device, resident in HBM, "
+                     "random-init weights" if aug_info else
+                     "synthetic N(0,1) meshes resident in HBM, random-init weights"),
+            "augmented_set": aug_info,
             "config": {"workload": "craniofacial.yaml SD-VAE train step (swap bs 4->16, fwd, "
                                    "MSE+Laplacian+KL+latent-consistency, bwd, Adam)",
                        "precision": runner.precision,
                        "topology": args.topology, "template_vertices": nv, "levels": runner.topo.n_verts,
                        "global_batch": 16 * world, "per_gpu_batch": 16,
+                       "resident_meshes_per_gpu": runner.data.n_items,
                        "parallelism": f"dp{world}", "graph": runner.use_graph,
                        "collective": None if world == 1 else
                        (("rccl" if backend == "nccl" else backend) + " all_reduce, 2 buckets overlapped")},

@@ -69,7 +69,11 @@ def choose_pairs(labels, ages, n_aug, rng, split_3years=True):
     """Pair draws of ``_augment`` (data_loading.py:314-358) as indices: for
     each class, ``n_aug[class]`` pairs of distinct meshes of the same class,
     from one age group (< 48 / >= 48 months, picked at random) when ages are
-    known and both groups are non-empty.  Returns (i1, i2, class) arrays."""
+    known and both groups hold >= 2 meshes (the reference would fail on a
+    group of < 2 at ``np.random.choice(len(group), 2, replace=False)``; here
+    the whole class is used instead).  Returns (i1, i2, class, i) arrays,
+    ``i`` = the draw's index within its class (the reference's name suffix,
+    data_loading.py:342-371)."""
     labels = np.asarray(labels)
     ages = np.asarray(ages, np.float64) if ages is not None else None
     out = []
@@ -80,37 +84,56 @@ def choose_pairs(labels, ages, n_aug, rng, split_3years=True):
             g = [members[ages[members] < 48], members[ages[members] >= 48]]
             if all(len(x) >= 2 for x in g):
                 groups = g
-        for _ in range(n):
+        if n > 0 and len(members) < 2:
+            raise ValueError(f"class {cl!r} has {len(members)} mesh(es): augmentation pairs need 2")
+        for i in range(n):
             grp = groups[rng.randint(len(groups))]
             a, b = rng.choice(len(grp), 2, replace=False)
-            out.append((grp[a], grp[b], cl))
+            out.append((grp[a], grp[b], cl, i))
     if not out:
-        return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, labels.dtype)
-    i1, i2, cls = zip(*out)
-    return np.asarray(i1), np.asarray(i2), np.asarray(cls)
+        e = np.zeros(0, np.int64)
+        return e, e, np.zeros(0, labels.dtype), e
+    i1, i2, cls, idx = zip(*out)
+    return np.asarray(i1), np.asarray(i2), np.asarray(cls), np.asarray(idx)
 
 
 def balanced_counts(labels, aug_factor, balanced=True):
-    """Augmented meshes per class (data_loading.py:329-335; 'b' merged into 'n')."""
-    labels = ["n" if y == "b" else y for y in labels]
-    classes = sorted(set(labels))
-    cnt = {c: labels.count(c) for c in classes}
+    """Augmented meshes per class (data_loading.py:314-335).  The classes are
+    the merged ones ('b' paediatric folded into 'n', :322-324), but the
+    balanced target divides by the number of class letters BEFORE the merge
+    (``data_classes``, :314, :332), exactly as the reference does."""
+    n_letters = len(set(labels))
+    merged = ["n" if y == "b" else y for y in labels]
+    classes = sorted(set(merged))
+    cnt = {c: merged.count(c) for c in classes}
     if balanced:
-        target = aug_factor * len(labels) // len(classes)
-        return {c: max(0, target - cnt[c]) for c in classes}
+        target = aug_factor * len(merged) // n_letters
+        return {c: target - cnt[c] for c in classes}
     return {c: (aug_factor - 1) * cnt[c] for c in classes}
 
 
 def augment(u, meshes, labels, ages=None, aug_factor=5, balanced=True, mode="spectral_interp", seed=0,
-            batch=1024, n_interp=30):
+            batch=1024, n_interp=30, split_3years=True):
     """The augmented training meshes ``_augment`` writes to disk, produced on
     the device: meshes [N, V, 3] (raw, un-normalised, device fp32), labels [N]
-    class letters.  Returns (augmented [M, V, 3] device, labels [M], pairs)."""
+    class letters.  Returns (augmented [M, V, 3] device, labels [M],
+    (i1, i2, i, t)) with ``i`` the index of each draw within its class and
+    ``t`` the interpolation values of mode 'interpolate' (else None).
+    A negative balanced count (a class already above the target) draws
+    nothing, as ``range(negative)`` does in the reference."""
     rng = np.random.RandomState(seed)
-    i1, i2, cls = choose_pairs(["n" if y == "b" else y for y in labels], ages,
-                               balanced_counts(labels, aug_factor, balanced), rng)
-    k = u.shape[1]
-    outs = []
+    counts = {c: max(0, n) for c, n in balanced_counts(labels, aug_factor, balanced).items()}
+    i1, i2, cls, idx = choose_pairs(["n" if y == "b" else y for y in labels], ages, counts, rng,
+                                    split_3years)
+    aug, tv = _generate(u, meshes, i1, i2, mode, rng, batch, n_interp)
+    return aug, list(cls), (i1, i2, idx, tv)
+
+
+def _generate(u, meshes, i1, i2, mode, rng, batch=1024, n_interp=30):
+    """The meshes of the pairs (i1, i2), ``batch`` pairs per launch group;
+    coefficients drawn from ``rng`` batch by batch."""
+    k = u.shape[1] if u is not None else 0
+    outs, tvals = [], []
     for s in range(0, len(i1), batch):
         a, b = i1[s:s + batch], i2[s:s + batch]
         x1 = meshes[torch.as_tensor(a, device=meshes.device)]
@@ -119,10 +142,28 @@ def augment(u, meshes, labels, ages=None, aug_factor=5, balanced=True, mode="spe
             vals = rng.normal(loc=0.5, scale=0.5, size=(len(a), k)).astype(np.float32)
         elif mode == "spectral_comb":
             vals = spectral_combination_values(rng, len(a), k, n_interp)
-        else:  # 'interpolate' (utils.py:234-235): one value per pair, full mesh
-            t = torch.as_tensor(rng.uniform(size=(len(a), 1, 1)).astype(np.float32), device=meshes.device)
+        elif mode == "interpolate":  # utils.py:234-235: one value per pair, whole mesh
+            tv = rng.uniform(size=(len(a), 1, 1)).astype(np.float32)
+            tvals.append(tv.ravel())
+            t = torch.as_tensor(tv, device=meshes.device)
             outs.append(x1 + t * (x2 - x1))
             continue
+        else:
+            raise ValueError(f"unknown augmentation_mode {mode!r}")
         outs.append(spectral_interpolation(u, x1, x2, torch.from_numpy(vals).to(meshes.device), n_interp))
     aug = torch.cat(outs) if outs else meshes[:0]
-    return aug, list(cls), (i1, i2)
+    return aug, (np.concatenate(tvals) if tvals else None)
+
+
+def synthesize(u, meshes, labels, n, seed=0, mode="spectral_interp", batch=1024):
+    """``n`` augmented meshes drawn as ``_augment`` draws them (same-class
+    pairs, spectral interpolation) with the classes taking turns -- the
+    generator of configuration C5's synthetic set (50 000 meshes from the
+    demo meshes).  Returns (meshes [n, V, 3] device, class letters)."""
+    rng = np.random.RandomState(seed)
+    merged = ["n" if y == "b" else y for y in labels]
+    classes = sorted(set(merged))
+    per = {c: n // len(classes) + (1 if i < n % len(classes) else 0) for i, c in enumerate(classes)}
+    i1, i2, cls, _ = choose_pairs(merged, None, per, rng, split_3years=False)
+    aug, _ = _generate(u, meshes, i1, i2, mode, rng, batch)
+    return aug, list(cls)

@@ -584,18 +584,10 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
     for (int sl = 0; sl < FSB; ++sl)
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
-#ifdef CFSD_EXP_NOA
-        av[sl][c] = ld4(xb + 16 * c);
-#else
         av[sl][c] = ld4(xb + (long)src[s0 + sl] * CIN + 16 * c);
-#endif
 #pragma unroll
         for (int t = 0; t < CTW; ++t)
-#ifdef CFSD_EXP_NOW
-          bw[sl][c][t] = ld4(w + 4 * kg + 16 * c);
-#else
           bw[sl][c][t] = ld4(wb + (long)t * 16 * K + (s0 + sl) * CIN + 16 * c);
-#endif
       }
     // keep the batch's loads ahead of its MFMAs (hipcc otherwise interleaves
     // them with vmcnt waits to save registers, re-exposing the latency)

@@ -145,6 +145,18 @@ def read_obj_vertices(path):
     return np.asarray(vs, np.float64)
 
 
+def write_obj(path, verts, faces=None):
+    """OBJ with ``v`` lines (9 significant digits: fp32 round-trips) and
+    1-based ``f`` lines (what ``mesh1.export`` of the augmented mesh writes,
+    data_loading.py:369-372)."""
+    v = np.asarray(verts, np.float64)
+    lines = ["v %.9g %.9g %.9g" % tuple(p) for p in v]
+    if faces is not None:
+        lines += ["f %d %d %d" % tuple(t) for t in (np.asarray(faces, np.int64) + 1)]
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
 def load_mesh(path):
     """``MeshInMemoryDataset.load_mesh`` (data_loading.py:220-229): vertices
     as float32."""
@@ -154,29 +166,149 @@ def load_mesh(path):
     return torch.tensor(read_obj_vertices(path), dtype=torch.float)
 
 
-def find_filenames(root):
-    """``find_filenames(find_augmented=False)`` without a dataset summary
-    (data_loading.py:166-178): every .ply / .obj outside 'aug' folders."""
+# ------------------------------------------------------------------ dataset summary
+def get_dataset_summary(data_config, data_type="heads"):
+    """``utils.get_dataset_summary`` (utils.py:193-208): the spreadsheet of
+    subjects (Dataset / ID|PID / AgeMonths / AgeYears / Gender / "Head Used"|
+    "Face Used") with a ``mesh_name`` column '<class letter>_<id>'; ``None``
+    without ``dataset_summary_path``.  ``.xlsx`` goes through pandas'
+    ``read_excel`` (needs openpyxl, absent from this image: the error is
+    pandas' own); a ``.csv`` with the same columns is read with
+    ``read_csv``."""
+    path = data_config.get("dataset_summary_path")
+    if not path:
+        return None
+    import pandas as pd
+    d = pd.read_csv(path) if path.endswith(".csv") else pd.read_excel(path)
+    d["mesh_name"] = "nan"
+    for ds, letter in (("Paeds", "b"), ("Apert", "a"), ("Crouzon", "c"), ("Muenke", "m"), ("LSFM", "n"),
+                       ("LYHM", "n")):
+        d.loc[d["Dataset"] == ds, "mesh_name"] = letter
+    id_column = "ID" if data_type == "heads" else "PID"
+    d["mesh_name"] = d["mesh_name"] + "_" + d[id_column].fillna(-1).astype(int).astype(str)
+    return d
+
+
+def find_data_used_from_summary(summary, data_type="heads"):
+    """``utils.find_data_used_from_summary`` (utils.py:211-217)."""
+    if summary is None:
+        return None
+    col = "Head Used" if data_type == "heads" else "Face Used"
+    return list(summary.loc[summary[col] == "y"]["mesh_name"])
+
+
+def get_age_and_gender_from_summary(summary, mesh_id):
+    """``utils.get_age_and_gender_from_summary`` (utils.py:220-231): age in
+    months (years * 12 + 6 when only years are known), gender; (-1, 'n/a')
+    for meshes the summary does not list (augmented meshes) -- and, here,
+    when there is no summary at all (the reference would raise)."""
+    if summary is None:
+        return -1, "n/a"
+    try:
+        rows = summary.loc[summary["mesh_name"] == mesh_id]
+        age = rows["AgeMonths"].values[0]
+        if np.isnan(age):
+            age = rows["AgeYears"].values[0] * 12 + 6
+        gender = rows["Gender"].values[0]
+    except IndexError:
+        age, gender = -1, "n/a"
+    return age, gender
+
+
+def find_filenames(root, data_to_use=None, find_augmented=False):
+    """``MeshInMemoryDataset.find_filenames`` (data_loading.py:166-178): every
+    .ply / .obj outside 'aug' folders whose stem the dataset summary marks as
+    used (all of them without a summary); with ``find_augmented`` also those
+    inside, as 'augmented/<name>'."""
     files = []
     for dirpath, _, fnames in os.walk(root):
         for f in fnames:
-            if (f.endswith(".ply") or f.endswith(".obj")) and "aug" not in dirpath:
-                files.append(f)
+            if f.endswith(".ply") or f.endswith(".obj"):
+                if "aug" not in dirpath:
+                    if data_to_use is None or f[:-4] in data_to_use:
+                        files.append(f)
+                elif find_augmented:
+                    files.append(os.path.join("augmented", f))
     return files
 
 
-def split_data(root, split_path, stratified=False):
+# ------------------------------------------------------------------ augmentation
+def augment_train_list(root, train_list, data_config, template=None, device="cuda", summary=None,
+                       precomputed_path=None, seed=0):
+    """``MeshInMemoryDataset._augment`` (data_loading.py:292-374) with the
+    meshes generated on the GPU (:mod:`augment`).
+
+    * ``<root>/augmented`` exists and is non-empty: its meshes are appended
+      (in sorted order; the reference takes ``os.listdir`` order) and nothing
+      is generated (:295-303);
+    * else: pairs per (merged) class and age group, balanced counts
+      (:314-335), eigenpairs k = 1000 of the template's combinatorial
+      Laplacian (cached as ``laplacian_eig_k1000.npz`` in the precomputed
+      folder), one batched GPU blend per 1024 pairs, and every result is
+      written to ``<root>/augmented/<name1>_<id2><_spectral_interp|..><i><ext>``
+      (:371-373) with the template's faces, then appended to the list.
+    Returns the extended train list (a new list)."""
+    from . import augment as A
+    train_list = list(train_list)
+    aug_dir = os.path.join(root, "augmented")
+    if os.path.isdir(aug_dir) and os.listdir(aug_dir):
+        for name in sorted(os.listdir(aug_dir)):
+            if name.endswith(".obj") or name.endswith(".ply"):
+                train_list.append(os.path.join("augmented", name))
+        return train_list
+    mode = data_config.get("augmentation_mode", "interpolate")
+    factor = int(data_config["augmentation_factor"])
+    balanced = bool(data_config.get("augmentation_balanced", True))
+    if template is None:
+        from .precompute import load_template
+        template = load_template(data_config["template_path"])
+    initial = list(train_list)
+    raw = torch.stack([load_mesh(os.path.join(root, n)) for n in initial]).to(device)
+    letters = [n[0] for n in initial]
+    ages = [get_age_and_gender_from_summary(summary, n[:-4])[0] for n in initial]
+    ages = None if summary is None else ages
+    u = None
+    if mode in ("spectral_interp", "spectral_comb"):
+        cache = os.path.join(precomputed_path, "laplacian_eig_k1000.npz") if precomputed_path else None
+        k = min(1000, template.num_nodes - 1)
+        _, u = A.laplacian_eigendecomposition(template.faces, template.num_nodes, k=k, device=device,
+                                              cache=cache)
+    aug, cls, (i1, i2, idx, tv) = A.augment(u, raw, letters, ages, aug_factor=factor, balanced=balanced,
+                                        mode=mode, seed=seed)
+    os.makedirs(aug_dir, exist_ok=True)
+    suffix = {"spectral_comb": "_spectral_comb", "spectral_interp": "_spectral_interp"}
+    host = aug.cpu().numpy()
+    for j in range(len(cls)):
+        n1, n2 = initial[int(i1[j])], initial[int(i2[j])]
+        tag = (suffix[mode] + str(int(idx[j]))) if mode in suffix else f"_interp{float(tv[j]):.2f}"
+        name = n1[:-4] + "_" + n2[2:-4] + tag + n1[-4:]
+        path = os.path.join(aug_dir, name)
+        if name.endswith(".ply"):
+            from .precompute import write_ply
+            write_ply(path, host[j], template.faces)
+        else:
+            write_obj(path, host[j], template.faces)
+        train_list.append(os.path.join("augmented", name))
+    return train_list
+
+
+def split_data(root, split_path, stratified=False, data_config=None, template=None, device="cuda",
+               summary=None, seed=0):
     """``MeshInMemoryDataset.split_data`` (data_loading.py:180-218): reuse
     ``data_split.json`` when present, else sort the file names and split
     (stratified 80/10/10 by class letter with sklearn, or the reference's
-    ``i % 100`` rule: <= 5 test, <= 10 validation, else train) and write it."""
+    ``i % 100`` rule: <= 5 test, <= 10 validation, else train), augment the
+    training list when ``augmentation_factor > 0`` (:207-213) and write the
+    json."""
     try:
         with open(split_path) as fp:
             d = json.load(fp)
         return d["train"], d["test"], d["val"]
     except FileNotFoundError:
         pass
-    names = sorted(find_filenames(root))
+    data_config = data_config or {}
+    data_to_use = find_data_used_from_summary(summary, data_config.get("data_type", "heads"))
+    names = sorted(find_filenames(root, data_to_use))
     if stratified:
         from sklearn.model_selection import train_test_split
         y = [n[0] for n in names]
@@ -186,6 +318,9 @@ def split_data(root, split_path, stratified=False):
         train, test, val = [], [], []
         for i, f in enumerate(names):
             (test if i % 100 <= 5 else val if i % 100 <= 10 else train).append(f)
+    if int(data_config.get("augmentation_factor", 0) or 0) > 0:
+        train = augment_train_list(root, train, data_config, template, device, summary,
+                                   os.path.dirname(split_path), seed)
     with open(split_path, "w") as fp:
         json.dump({"train": train, "test": test, "val": val}, fp)
     return train, test, val
@@ -202,7 +337,7 @@ def labels_of(name):
 def compute_mean_and_std(root, train_names, norm_path):
     """``compute_mean_and_std`` (data_loading.py:231-252): load ``norm.pt``
     (weights_only) or compute the per-vertex mean / std (torch, CPU) of the
-    training meshes and save it."""
+    training meshes -- augmented ones included -- and save it."""
     try:
         return torch.load(norm_path, weights_only=True)
     except FileNotFoundError:
@@ -215,27 +350,53 @@ def compute_mean_and_std(root, train_names, norm_path):
         return norm
 
 
-def load_mesh_dataset(data_config, batch_size, device="cuda"):
+def prepare_split(data_config, template=None, device="cuda", seed=0):
+    """The files the data sets are defined by: ``data_split.json`` (with
+    augmentation, :func:`split_data`) and ``norm.pt`` in the precomputed
+    folder, made once (data-parallel: by rank 0 before the others load).
+    Returns (train, test, val, norm, summary)."""
+    root = data_config["dataset_path"]
+    pre = data_config["precomputed_path"]
+    os.makedirs(pre, exist_ok=True)
+    summary = get_dataset_summary(data_config, data_config.get("data_type", "heads"))
+    train, test, val = split_data(root, os.path.join(pre, "data_split.json"),
+                                  data_config.get("stratified_split", False), data_config, template, device,
+                                  summary, seed)
+    norm = compute_mean_and_std(root, train, os.path.join(pre, "norm.pt"))
+    return train, test, val, norm, summary
+
+
+def load_mesh_dataset(data_config, batch_size, device="cuda", template=None, shard=None, seed=0):
     """``get_data_loaders`` (data_loading.py:23-51) for the resident path:
     train / validation / test :class:`engine.ResidentData` sets (meshes
     normalised on the device with norm.pt, data_loading.py:259-260; train and
     validation shuffled every epoch with drop_last, test in file order) plus
-    the normalisation dict and the per-set file names and labels."""
+    the normalisation dict and the per-set file names and labels.
+
+    ``shard=(rank, world)`` (data-parallel training): the train and
+    validation sets iterate over this rank's contiguous shard only (the whole
+    set stays resident; the test set is not sharded)."""
     root = data_config["dataset_path"]
-    pre = data_config["precomputed_path"]
-    os.makedirs(pre, exist_ok=True)
-    train, test, val = split_data(root, os.path.join(pre, "data_split.json"),
-                                  data_config.get("stratified_split", False))
-    norm = compute_mean_and_std(root, train, os.path.join(pre, "norm.pt"))
+    train, test, val, norm, summary = prepare_split(data_config, template, device, seed)
     sets = {}
     for kind, names, shuffle in (("train", train, True), ("val", val, True), ("test", test, False)):
         if len(names) < batch_size:
             sets[kind] = None
             continue
         meshes = torch.stack([load_mesh(os.path.join(root, n)) for n in names]).to(device)
-        rd = ResidentData(meshes, bs=batch_size, shuffle=shuffle,
+        rows = None
+        # (a shard smaller than one batch: every rank iterates the whole set;
+        # the decision depends on the sizes only, so all ranks agree)
+        if shard is not None and kind != "test" and shard[1] > 1 and len(names) // shard[1] >= batch_size:
+            from .dist import shard_range
+            lo, hi = shard_range(len(names), shard[0], shard[1])
+            rows = torch.arange(lo, hi, dtype=torch.int32)
+        rd = ResidentData(meshes, bs=batch_size, rows=rows, shuffle=shuffle,
                           norm=norm if data_config.get("normalize_data", True) else None)
         rd.names = list(names)
         rd.labels = [labels_of(n) for n in names]
+        ag = [get_age_and_gender_from_summary(summary, n[:-4]) for n in names]
+        rd.ages = [a for a, _ in ag]
+        rd.genders = [g for _, g in ag]
         sets[kind] = rd
     return sets["train"], sets["val"], sets["test"], norm

@@ -34,6 +34,16 @@ def init_from_env(backend=None, device_id=None):
     return world, rank, local
 
 
+def barrier():
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()
+
+
+def destroy():
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def broadcast_parameters(flat, src=0):
     """Make every rank start from rank ``src``'s parameters."""
     if dist.is_initialized() and dist.get_world_size() > 1:

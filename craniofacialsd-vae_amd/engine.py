@@ -808,11 +808,13 @@ class ResidentData:
     def __init__(self, meshes, bs, rows=None, shuffle=True, norm=None):
         if not meshes.is_cuda or meshes.dim() != 3:
             raise ValueError("meshes must be a [N, V, C] device tensor")
-        self.meshes = meshes.contiguous()
-        if norm is not None:
+        if norm is not None:  # into a buffer of its own: the caller's tensor is left unchanged
             mean = norm["mean"].to(meshes.device, torch.float32).contiguous()
             std = norm["std"].to(meshes.device, torch.float32).contiguous()
-            ops.normalize(self.meshes, mean, std, out=self.meshes)
+            self.meshes = ops.normalize(meshes.contiguous(), mean, std,
+                                        out=torch.empty(meshes.shape, dtype=torch.float32, device=meshes.device))
+        else:
+            self.meshes = meshes.contiguous()
         n = meshes.shape[0]
         if rows is not None:
             rows = torch.as_tensor(rows).to(torch.int64).cpu()

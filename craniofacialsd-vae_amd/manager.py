@@ -19,6 +19,7 @@ import torch
 
 from . import engine as E
 from . import ops, precompute, refcache, topology
+from .step import TrainStep
 
 LOSS_KEYS = ["reconstruction", "kl", "latent_consistency", "laplacian", "classification",
              "classification_acc", "tot"]
@@ -84,7 +85,7 @@ class JsonlWriter:
 
 class ModelManager:
     def __init__(self, configurations, device="cuda", precomputed_storage_path="precomputed",
-                 precision="fp32", seed=0, use_graph=True):
+                 precision="fp32", seed=0, use_graph=True, averager=None):
         self._model_params = configurations["model"]
         self._optimization_params = op = configurations["optimization"]
         self._precomputed_storage_path = precomputed_storage_path
@@ -114,8 +115,14 @@ class ModelManager:
         self._batch_diagonal_idx = [(self.bs + 1) * i for i in range(self.bs)]
         self._losses = None
         self.use_graph = use_graph
-        self._graph = None
-        self._graph_data = None
+        self._steps = {}
+        # data-parallel (one process per GPU, train.py under torchrun): every
+        # rank starts from rank 0's parameters and averages the gradient
+        self.averager = averager
+        if averager is not None and averager.world > 1:
+            from .dist import broadcast_parameters
+            broadcast_parameters(self.engine.params.data, 0)
+            self.engine.sync_shadow()
         self.val_acc = torch.zeros(6, dtype=torch.float32, device=self.device)
         self.val_counter = torch.zeros(1, dtype=torch.int32, device=self.device)
 
@@ -146,23 +153,18 @@ class ModelManager:
 
     # ------------------------------------------------------------ epochs
     def _train_step(self, b, data):
-        if not self.use_graph:
-            return self.engine.resident_step(b, data, acc=self.engine.loss_acc)
-        if self._graph is None or self._graph_data is not data:
-            s = torch.cuda.Stream(self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            # the warm-up launch on a side stream (allocations, lazy loading)
-            # is a REAL step of the epoch; the capture only records (nothing
-            # runs while capturing), later replays execute
-            with torch.cuda.stream(s):
-                self.engine.resident_step(b, data, acc=self.engine.loss_acc)
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self.engine.resident_step(b, data, acc=self.engine.loss_acc)
-            self._graph, self._graph_data = g, data
-            return "captured"
-        self._graph.replay()
+        """One training step from ``data`` through :class:`step.TrainStep`
+        (the object bench.py times).  With ``use_graph`` the first step of a
+        data set runs eagerly on a side stream and is captured; later steps
+        replay the graph(s)."""
+        ts = self._steps.get(id(data))
+        if ts is None or ts.data is not data:
+            ts = TrainStep(self.engine, data, self.averager, acc=self.engine.loss_acc)
+            self._steps[id(data)] = ts
+            if self.use_graph:
+                ts.capture()  # includes one real (eager) step
+                return "captured"
+        ts.step()
 
     def _eval_step(self, b, data):
         """_do_iteration(train=False) (model_manager.py:274-326 under
@@ -196,6 +198,9 @@ class ModelManager:
             if record is not None:
                 record.append((b.batch_idx.cpu().numpy().copy(), int(b.key.item()),
                                b.eps.cpu().numpy().copy() if (train and self.is_vae) else None))
+        if self.averager is not None and self.averager.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(acc)  # every rank's batches: sums and the batch count
         a = acc.cpu().numpy().astype(np.float64)
         n = max(a[5], 1.0)
         self._losses = {"reconstruction": a[0] / n, "kl": a[1] / n, "latent_consistency": a[2] / n,
@@ -203,10 +208,12 @@ class ModelManager:
                         "tot": a[4] / n}
         return dict(self._losses)
 
-    def log_losses(self, writer, epoch, phase="train"):
-        """model_manager.py:587-592."""
+    def log_losses(self, writer, epoch, phase="train", losses=None):
+        """model_manager.py:587-592 (``losses``: a run_epoch result; default
+        the last one)."""
+        losses = self._losses if losses is None else losses
         for k in self.loss_keys:
-            writer.add_scalar(phase + "/" + str(k), self._losses[k], epoch + 1)
+            writer.add_scalar(phase + "/" + str(k), losses[k], epoch + 1)
 
     # ------------------------------------------------------------ model access
     def encode(self, x):

@@ -1,0 +1,138 @@
+"""The replayable training step: one ``ModelManager._do_iteration``
+(``model_manager.py:274-326``) from an HBM-resident dataset, on one GPU or
+data-parallel over the GPUs of a node, captured as hipGraphs.
+
+This is the object ``bench.py``, ``manager.ModelManager`` (and so
+``train.py``) and the data-parallel GPU tests all run, so the step that is
+timed is the step that is tested.
+
+Step anatomy (every launch on one stream; nothing synchronises with the host):
+
+* ``part_a``: ``cfsd_step_begin`` (device counter -> epoch-shuffled batch
+  pick, swap key, VAE noise, Adam's t), the feature swap, the forward with its
+  four losses, and the backward from the losses through the decoder, the
+  latent head and the encoder Linear.  After it the gradient of everything
+  from the encoder Linear on (~96 % of the parameters) is final;
+* ``part_b``: the encoder conv backward and the batched weight-gradient
+  reduce.  On one GPU Adam rides in that reduce (``cfsd_dw_reduce_batch_adam``);
+* ``part_c``: (data-parallel only) Adam, after the gradient all-reduce.
+
+One GPU: the three parts are ONE graph.  Data-parallel: three graphs, with
+the two RCCL all-reduce buckets issued between the replays -- the decoder /
+bottleneck bucket right after ``part_a`` so it overlaps ``part_b`` (RCCL runs
+on its own stream, ordered after the work already queued), the encoder-conv
+bucket after ``part_b`` -- then ``cfsd_scale(1/world)`` and Adam.  The
+justification for data parallelism is that every loss term is intra-swap-group
+(``model_manager.py:360-393``): each rank trains its own groups and the only
+exchange is the flat fp32 gradient.
+"""
+import torch
+
+from . import ops
+
+
+class TrainStep:
+    """``TrainStep(engine, data, averager=None, acc=None)``.
+
+    ``engine``: :class:`engine.SDVAEEngine`; ``data``: :class:`engine.
+    ResidentData` (this rank's shard); ``averager``: a
+    :class:`dist.GradientAverager` (``None`` or world 1: single GPU);
+    ``acc``: the device loss accumulator (default ``engine.loss_acc``).
+
+    ``step()`` runs one training step -- eagerly until :meth:`capture` was
+    called, then by graph replay.  ``capture()`` first runs ONE real step
+    eagerly on a side stream (that step counts: it advances the counter,
+    the parameters and the epoch position exactly like any other), then
+    records the graphs; nothing executes while recording, so the k-th step
+    of a captured runner equals the k-th step of an eager one, bit for bit."""
+
+    def __init__(self, engine, data, averager=None, acc=None):
+        self.eng = engine
+        self.data = data
+        self.avg = averager if (averager is not None and averager.world > 1) else None
+        self.b = engine.buffers(engine.swap_bs ** 2)
+        self.acc = engine.loss_acc if acc is None else acc
+        self.graphs = None
+        self._split = engine.enc_conv_numel()
+
+    @property
+    def world(self):
+        return self.avg.world if self.avg is not None else 1
+
+    @property
+    def captured(self):
+        return self.graphs is not None
+
+    # ------------------------------------------------------------ the parts
+    def part_a(self):
+        eng, b, T, d = self.eng, self.b, self.eng.topo, self.data
+        ops.step_begin(eng.counter, eng.seed, eps=b.eps if eng.spec.is_vae else None, key=b.key,
+                       n_regions=max(T.n_regions, 1), batch_idx=b.batch_idx, bs=eng.swap_bs,
+                       n_batches=d.n_batches, perm=d.rows, n_items=d.n_items, shuffle=d.shuffle,
+                       adam_step=eng.params.step)
+        ops.swap_features(d.meshes, b.batch_idx, T.region_mask, b.key, eng.swap_bs, out=b.x)
+        eng.forward(b, train=True, acc=self.acc, finalize=False)
+        eng.backward_head(b, split=self.avg is not None)
+
+    def part_b(self):
+        self.eng.backward_tail(self.b, fuse_adam=self.avg is None)
+
+    def part_c(self):
+        if self.avg is not None:
+            self.eng.adam_step()
+
+    # ------------------------------------------------------------ buckets
+    def _bucket_dec(self):
+        self.avg.bucket_ready(self.eng.params.grad[self._split:])
+
+    def _bucket_enc_and_finish(self):
+        grad = self.eng.params.grad
+        self.avg.bucket_ready(grad[:self._split])
+        self.avg.finish(grad)
+
+    # ------------------------------------------------------------ running
+    def eager_step(self):
+        self.part_a()
+        if self.avg is not None:
+            self._bucket_dec()
+        self.part_b()
+        if self.avg is not None:
+            self._bucket_enc_and_finish()
+        self.part_c()
+
+    def capture(self):
+        """One real eager step on a side stream (lazy initialisation of
+        everything the launches touch), then record the graph(s)."""
+        dev = self.eng.device
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            self.eager_step()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        if self.avg is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.part_a()
+                self.part_b()
+            self.graphs = [g]
+        else:
+            self.graphs = [torch.cuda.CUDAGraph() for _ in range(3)]
+            for g, fn in zip(self.graphs, (self.part_a, self.part_b, self.part_c)):
+                with torch.cuda.graph(g):
+                    fn()
+
+    def step(self):
+        if self.graphs is None:
+            return self.eager_step()
+        if self.avg is None:
+            self.graphs[0].replay()
+            return
+        ga, gb, gc = self.graphs
+        ga.replay()
+        self._bucket_dec()          # overlaps with gb
+        gb.replay()
+        self._bucket_enc_and_finish()
+        gc.replay()
+
+    __call__ = step

@@ -386,3 +386,37 @@ def spectral_interpolation(u, x1, x2, values, interp_until=30):
     s4 = s1.copy()
     s4[:interp_until] = s3[:interp_until]
     return u @ s4
+
+
+def augment_counts(train_names, aug_factor, balanced=True):
+    """Augmented meshes per class of ``_augment`` (data_loading.py:314-335):
+    classes are first letters, 'b' merged into 'n' (:322-324); the balanced
+    target is aug_factor * len(initial_list) // len(data_classes) with
+    data_classes taken BEFORE the merge (:314, :331-333); range(negative)
+    draws nothing."""
+    data_classes = set(n[0] for n in train_names)
+    per = {c: [n for n in train_names if n[0] == c] for c in data_classes}
+    per["n"] = per.get("n", []) + per.pop("b", [])
+    out = {}
+    for c, info in per.items():
+        if balanced:
+            n = aug_factor * len(train_names) // len(data_classes) - len(info)
+        else:
+            n = (aug_factor - 1) * len(info)
+        out[c] = max(0, n)
+    return out
+
+
+def augmented_name(name1, name2, mode, i):
+    """data_loading.py:359-371: name1[:-4] + '_' + name2[2:-4] + tag + ext."""
+    tag = {"spectral_comb": "_spectral_comb", "spectral_interp": "_spectral_interp"}.get(mode)
+    if tag is None:
+        raise ValueError("interpolate names carry the drawn value, not an index")
+    return name1[:-4] + "_" + name2[2:-4] + tag + str(i) + name1[-4:]
+
+
+def mean_std(verts):
+    """compute_mean_and_std (data_loading.py:247-249) over a [N, V, 3] fp32 stack."""
+    verts = torch.as_tensor(verts)
+    std = torch.std(verts, dim=0)
+    return torch.mean(verts, dim=0), torch.where(std > 0, std, torch.tensor(1e-8))

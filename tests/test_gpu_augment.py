@@ -78,8 +78,58 @@ def test_augment_counts(mods, eig, topo_npz):
     sel = topo_npz["down_0_col"][np.argsort(topo_npz["down_0_row"])]
     m = torch.from_numpy(recipe.load_meshes()["verts"][:, sel]).float().cuda()
     labels = list("nnnaaacccmmm")
-    aug, cls, (i1, i2) = A.augment(u, m, labels, aug_factor=5, balanced=True, seed=1, batch=7)
+    aug, cls, (i1, i2, _, _) = A.augment(u, m, labels, aug_factor=5, balanced=True, seed=1, batch=7)
     exp = A.balanced_counts(labels, 5, True)
     assert {c: cls.count(c) for c in set(cls)} == {c: v for c, v in exp.items() if v}
     assert aug.shape == (len(cls), n, 3) and torch.isfinite(aug).all()
     assert all(labels[a] == labels[b] and a != b for a, b in zip(i1, i2))
+
+
+# ------------------------------------------------ full template, k = 1000 (C5)
+@pytest.fixture(scope="module")
+def eig_full(mods, topo_npz, tmp_path_factory):
+    """The reference's eigendecomposition size (data_loading.py:309-310:
+    k = 1000 of the 17 039-vertex template), device fp64, cached in a file
+    and read back from the cache."""
+    A, _ = mods
+    faces = topo_npz["face_0"].astype(np.int64)
+    n = int(topo_npz["pos_0"].shape[0])
+    cache = str(tmp_path_factory.mktemp("eig") / "laplacian_eig_k1000.npz")
+    s, u = A.laplacian_eigendecomposition(faces, n, k=1000, device="cuda", cache=cache)
+    s2, u2 = A.laplacian_eigendecomposition(faces, n, k=1000, device="cuda", cache=cache)
+    assert np.array_equal(s, s2) and torch.equal(u.cpu(), u2.cpu())
+    return faces, n, s, u
+
+
+def test_full_template_eigenpairs(mods, eig_full):
+    A, P = mods
+    faces, n, s, u = eig_full
+    assert u.shape == (17039, 1000)
+    L = P.combinatorial_laplacian(faces, n)
+    U = u.double().cpu().numpy()
+    res = np.abs(L @ U - U * s[None]).max()
+    assert res <= 1e-4 * max(1.0, float(np.abs(s).max())), res
+    assert np.abs(U.T @ U - np.eye(U.shape[1])).max() <= 1e-4
+    ref = np.sort(sla.eigsh(L.astype(np.float64), k=12, sigma=-1e-3, which="LM")[0])
+    np.testing.assert_allclose(s[:12], ref, rtol=1e-6, atol=1e-9)
+    assert np.all(np.diff(s) >= -1e-9)  # ascending: the k SMALLEST (eigsh which='SM')
+
+
+def test_full_template_spectral_interpolation_vs_oracle(mods, eig_full):
+    """C5's generator at full size: batched GEMMs + cfsd_spectral_blend ==
+    the oracle's float64 spectral_interpolation (utils.py:256-267) with the
+    same U and coefficients, on demo pairs of the 17 039-vertex template."""
+    A, _ = mods
+    faces, n, s, u = eig_full
+    m = recipe.load_meshes()["verts"]
+    rs = np.random.RandomState(1)
+    pairs = [(0, 1), (2, 3), (4, 5), (6, 11), (7, 9)]
+    vals = rs.normal(0.5, 0.5, size=(len(pairs), u.shape[1])).astype(np.float32)
+    x1 = torch.from_numpy(np.stack([m[a] for a, _ in pairs])).float().cuda()
+    x2 = torch.from_numpy(np.stack([m[b] for _, b in pairs])).float().cuda()
+    got = A.spectral_interpolation(u, x1, x2, torch.from_numpy(vals).cuda()).cpu().numpy()
+    U = u.double().cpu().numpy()
+    for i, (a, b) in enumerate(pairs):
+        ref = O.spectral_interpolation(U, m[a], m[b], vals[i])
+        err = np.abs(got[i] - ref).max() / np.abs(ref).max()
+        assert err <= 1e-4, f"pair {i}: rel {err}"

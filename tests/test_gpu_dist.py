@@ -93,16 +93,134 @@ dist.destroy_process_group()
 '''
 
 
-def test_dp2_hip_step_matches_single_rank_mean(tmp_path):
+def _run2(tmp_path, script, *args):
     wfile = tmp_path / "dp_worker.py"
-    wfile.write_text(WORKER)
+    wfile.write_text(script)
     out = tmp_path / "res.json"
     env = dict(os.environ, CFSD_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(wfile), ROOT, str(out)]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(wfile), ROOT, str(out),
+           *args]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    res = json.loads(out.read_text())
+    return json.loads(out.read_text())
+
+
+def test_dp2_hip_step_matches_single_rank_mean(tmp_path):
+    res = _run2(tmp_path, WORKER)
     assert res["groups_differ"]
     assert res["grad_equal_mean"], res
     assert res["params_equal_0"] and res["params_equal_1"], res
+
+
+# The step bench.py times at N > 1 (configuration C3): step.TrainStep with a
+# GradientAverager, captured as three hipGraphs replayed around the two
+# all-reduce buckets, trained from a resident, device-shuffled data shard.
+GRAPH_WORKER = r'''
+import json, os, sys
+ROOT, OUT, PREC = sys.argv[1], sys.argv[2], sys.argv[3]
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests", "golden")]
+import numpy as np, torch, torch.distributed as dist
+import cfsd_loader, recipe
+cfsd_loader.load()
+from craniofacialsd_vae_amd import engine as E, dist as D, topology
+from craniofacialsd_vae_amd.step import TrainStep
+world, rank, _ = D.init_from_env(backend="gloo")
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+T = topology.DeviceTopology.from_npz(recipe.load_topology(), device=dev)
+w = {k: torch.from_numpy(v) for k, v in recipe.golden_weights().items()}
+nv = T.n_verts[0]
+meshes = torch.randn(16, nv, 3, generator=torch.Generator().manual_seed(99)).to(dev)
+
+def make(r, perturb=False):
+    eng = E.SDVAEEngine(T, E.ModelSpec(), seed=1234 + r, device=dev, precision=PREC)
+    eng.load_state_dict(w)
+    if perturb:  # rank 1 starts elsewhere: the broadcast must fix it
+        eng.params.data.mul_(0.5)
+    lo, hi = D.shard_range(16, r, world)
+    data = E.ResidentData(meshes, bs=4, rows=torch.arange(lo, hi), shuffle=True)
+    return eng, data
+
+def state(eng):
+    P = eng.params
+    out = [P.data, P.grad, P.exp_avg, P.exp_avg_sq, P.step, eng.counter]
+    if P.shadow is not None:
+        out.append(P.shadow)
+    return [t.detach().cpu().clone() for t in out]
+
+def gather_equal(t):
+    gs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(gs, t.contiguous())
+    return all(torch.equal(gs[0], x) for x in gs)
+
+eng_g, data_g = make(rank, perturb=rank == 1)
+D.broadcast_parameters(eng_g.params.data, 0)
+eng_g.sync_shadow()
+ts = TrainStep(eng_g, data_g, D.GradientAverager(world))
+eng_e, data_e = make(rank)
+avg_e = D.GradientAverager(world)
+b_e = eng_e.buffers(16)
+res = {"steps": []}
+ts.capture()                       # step 1 runs eagerly inside capture()
+eng_e.resident_step(b_e, data_e, acc=eng_e.loss_acc, grad_hook=avg_e)
+torch.cuda.synchronize()
+g1 = eng_g.params.grad.detach().cpu().clone()
+for step in range(1, 4):
+    if step > 1:
+        ts.step()                  # graph replays
+        eng_e.resident_step(b_e, data_e, acc=eng_e.loss_acc, grad_hook=avg_e)
+        torch.cuda.synchronize()
+    sg, se = state(eng_g), state(eng_e)
+    rec = {"graph_equals_eager": all(torch.equal(a, b) for a, b in zip(sg, se)),
+           "params_equal_ranks": gather_equal(eng_g.params.data.cpu()),
+           "moments_equal_ranks": gather_equal(eng_g.params.exp_avg_sq.cpu()),
+           "batch_idx": ts.b.batch_idx.cpu().tolist()}
+    if eng_g.params.shadow is not None:
+        rec["shadow_equal_ranks"] = gather_equal(eng_g.params.shadow.view(torch.int16).cpu())
+        rec["shadow_is_cast"] = bool(torch.equal(eng_g.params.shadow.cpu(),
+                                                 eng_g.params.data.cpu().to(torch.bfloat16)))
+    rec["losses_finite"] = bool(torch.isfinite(eng_g.loss_acc).all())
+    res["steps"].append(rec)
+rows = [torch.tensor(s["batch_idx"]) for s in res["steps"]]
+res["rows_in_shard"] = all(((r >= D.shard_range(16, rank, world)[0]) &
+                            (r < D.shard_range(16, rank, world)[1])).all().item() for r in rows)
+if rank == 0:
+    singles = []
+    for r in range(world):
+        e1, d1 = make(r)
+        t1 = TrainStep(e1, d1)       # single GPU: Adam fused into the reduce
+        t1.step()
+        torch.cuda.synchronize()
+        singles.append(e1.params.grad.cpu())
+    mean = (singles[0] + singles[1]) * 0.5
+    res["grad_equal_mean"] = bool(torch.equal(g1, mean))
+    res["grad_max_abs_diff"] = float((g1 - mean).abs().max())
+    res["groups_differ"] = not torch.equal(singles[0], singles[1])
+    with open(OUT, "w") as f:
+        json.dump(res, f)
+dist.barrier()
+dist.destroy_process_group()
+'''
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_dp2_graph_trainstep(tmp_path, precision):
+    """C3 path: 2 ranks x 16 meshes, graph-replayed TrainStep (the object the
+    N > 1 bench replays) -- (1) the averaged gradient of the first step is
+    bit-equal to the mean of the two single-GPU gradients of the same batches;
+    (2) after every step parameters, Adam moments and the bf16 shadows are
+    bit-identical across ranks; (3) every graph-replayed step is bit-identical
+    to the eager ``resident_step(grad_hook=GradientAverager)`` step
+    (train_step_on's overlapped buckets) -- parameters, gradient, moments,
+    Adam t, device counter, shadow; (4) each rank only draws its shard."""
+    res = _run2(tmp_path, GRAPH_WORKER, precision)
+    assert res["groups_differ"]
+    assert res["grad_equal_mean"], res
+    assert res["rows_in_shard"], res
+    for i, s in enumerate(res["steps"]):
+        assert s["graph_equals_eager"], (i, s)
+        assert s["params_equal_ranks"] and s["moments_equal_ranks"], (i, s)
+        assert s["losses_finite"], (i, s)
+        if precision == "bf16":
+            assert s["shadow_equal_ranks"] and s["shadow_is_cast"], (i, s)

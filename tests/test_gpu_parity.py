@@ -324,8 +324,8 @@ def test_swap_bit_exact(otopo, dtopo):
 
 
 # --------------------------------------------------------------- full model
-def make_engine(dtopo, weights, bs=4):
-    eng = E.SDVAEEngine(dtopo, E.ModelSpec(), swap_bs=bs, device=DEV)
+def make_engine(dtopo, weights, bs=4, precision="fp32"):
+    eng = E.SDVAEEngine(dtopo, E.ModelSpec(), swap_bs=bs, device=DEV, precision=precision)
     eng.load_state_dict({k: torch.from_numpy(v) for k, v in weights.items()})
     return eng
 
@@ -400,17 +400,19 @@ def test_train_step_deterministic(dtopo):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
-def test_fused_reduce_adam_matches_separate(dtopo):
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_fused_reduce_adam_matches_separate(dtopo, precision):
     """cfsd_dw_reduce_batch_adam (train_step_on without a gradient hook) ==
-    cfsd_dw_reduce_batch + cfsd_adam, bit for bit: parameters, gradients and
-    both Adam moments after two steps."""
+    cfsd_dw_reduce_batch + cfsd_adam, bit for bit: parameters, gradients,
+    both Adam moments and (bf16) the weight shadow after two steps -- in bf16
+    also the bf16-MFMA weight-gradient items of the fused reduce."""
     w = recipe.golden_weights()
     x = torch.from_numpy(O.swap_features(recipe.normalized_meshes(4), [np.asarray(r) for r in
                                          O.Topology(recipe.load_topology()).region_features], 2)).to(DEV)
     eps = torch.from_numpy(recipe.train_eps(0)).to(DEV)
     outs = []
     for fused in (True, False):
-        eng = make_engine(dtopo, w)
+        eng = make_engine(dtopo, w, precision=precision)
         for _ in range(2):
             b = eng.set_batch(x, key_index=2, eps=eps)
             if fused:
@@ -422,7 +424,9 @@ def test_fused_reduce_adam_matches_separate(dtopo):
                 eng.adam_step()
         torch.cuda.synchronize()
         P = eng.params
-        outs.append([t.cpu().clone() for t in (P.data, P.grad, P.exp_avg, P.exp_avg_sq)])
+        bufs = [P.data, P.grad, P.exp_avg, P.exp_avg_sq] + ([P.shadow] if P.shadow is not None else [])
+        outs.append([t.cpu().clone() for t in bufs])
+    assert len(outs[0]) == (5 if precision == "bf16" else 4)
     for a, c in zip(*outs):
         assert torch.equal(a, c)
 

@@ -150,3 +150,125 @@ def test_swap_features_dropin_labels(workspace):
     assert batch.y == ny and batch.gender == ng
     assert np.array_equal(batch.augmented.cpu().numpy().astype(bool), na.astype(bool))
     assert np.array_equal(batch.age.cpu().numpy(), nage.astype(np.float64))
+
+
+# ----------------------------------------------- augmented data set (C5 shape)
+@pytest.fixture(scope="module")
+def aug_workspace(tmp_path_factory, topo_npz):
+    """Demo workspace with augmentation_factor 2 / spectral_interp /
+    balanced (craniofacial.yaml uses 5; 2 keeps the written files few), 45
+    meshes with the classes a / b / c / m / n."""
+    cfsd_loader.load()
+    from craniofacialsd_vae_amd import precompute
+    d = tmp_path_factory.mktemp("demo_sp")
+    precompute.write_ply(str(d / "template.ply"), topo_npz["pos_0"], topo_npz["face_0"],
+                         topo_npz["template_colors"])
+    (d / "pre").mkdir()
+    np.savez(d / "pre" / "topology.npz", **topo_npz)
+    (d / "meshes").mkdir()
+    m = recipe.load_meshes()
+    rs = np.random.RandomState(4)
+    for i in range(45):
+        v = m["verts"][i % 12] + rs.normal(0, 0.002, m["verts"][0].shape)
+        write_obj(d / "meshes" / f"{'nacmb'[i % 5]}_{i:03d}.obj", v.astype(np.float32))
+    cfg = dict(CONFIG, data={"template_path": str(d / "template.ply"), "precomputed_path": str(d / "pre"),
+                             "dataset_path": str(d / "meshes"), "normalize_data": True, "to_mm_constant": 89.11,
+                             "swap_features": True, "stratified_split": False, "augmentation_factor": 2,
+                             "augmentation_mode": "spectral_interp", "augmentation_balanced": True})
+    return d, cfg
+
+
+def test_augmented_split_counts_norm_and_spectra(aug_workspace):
+    """split_data -> _augment wiring (data_loading.py:207-213, 292-374,
+    231-252): per-class counts of the reference's balanced rule (5 letters
+    before the b -> n merge), reference names in the train split and
+    data_split.json, norm.pt over the augmented train list, augmented=True
+    labels, and -- per written mesh -- the spectral signature of
+    spectral_interpolation (utils.py:256-267): with U the cached k = 1000
+    eigenvectors, U^T x_aug equals U^T x1 beyond the first 30 components,
+    each of the first 30 is s1 + v (s2 - s1) with ONE v for x, y and z, and
+    x_aug lies in span(U)."""
+    from craniofacialsd_vae_amd import data as D
+    d, cfg = aug_workspace
+    tr, va, te, norm = D.load_mesh_dataset(cfg["data"], 4, "cuda")
+    names = tr.names
+    orig = [n for n in names if not n.startswith("augmented/")]
+    augn = [n for n in names if n.startswith("augmented/")]
+    exp = O.augment_counts(orig, 2, True)
+    got = {}
+    for n in augn:
+        got[D.labels_of(n)[0]] = got.get(D.labels_of(n)[0], 0) + 1
+    assert got == {c: v for c, v in exp.items() if v} and sum(got.values()) > 0
+    assert json.load(open(d / "pre" / "data_split.json"))["train"] == names
+    assert all(lab[1] for lab, n in zip(tr.labels, names) if n.startswith("augmented/"))
+    raw = torch.stack([D.load_mesh(str(d / "meshes" / n)) for n in names])
+    m, s = O.mean_std(raw)
+    assert torch.equal(norm["mean"], m) and torch.equal(norm["std"], s)
+    assert torch.equal(tr.meshes.cpu(), O.normalize(raw, m, s))
+    e = np.load(d / "pre" / "laplacian_eig_k1000.npz")
+    U = e["u"].astype(np.float64)
+    assert U.shape == (17039, 1000)
+    by_id = {n[2:-4]: n for n in orig}
+    for n in augn[:6]:
+        stem = n.split("/")[1][:-4]
+        name1 = stem[:5] + ".obj"
+        id2 = stem[6:9]
+        x1 = D.load_mesh(str(d / "meshes" / name1)).double().numpy()
+        x2 = D.load_mesh(str(d / "meshes" / by_id[id2])).double().numpy()
+        xa = D.load_mesh(str(d / "meshes" / n)).double().numpy()
+        s1, s2, sa = U.T @ x1, U.T @ x2, U.T @ xa
+        scale = np.abs(s1).max()
+        assert np.abs(sa[30:] - s1[30:]).max() <= 1e-4 * scale, n
+        v = (sa[:30] - s1[:30]) / np.where(np.abs(s2[:30] - s1[:30]) > 1e-3 * scale, s2[:30] - s1[:30], np.nan)
+        spread = np.nanmax(v, axis=1) - np.nanmin(v, axis=1)
+        assert np.nanmax(spread) <= 1e-2, (n, np.nanmax(spread))
+        assert np.abs(xa - U @ sa).max() <= 1e-4 * np.abs(xa).max(), n
+
+
+def test_bf16_epochs_on_augmented_set(aug_workspace):
+    """C5-shaped training: the bf16 step on the resident augmented set --
+    one eager epoch (each training mesh drawn at most once, drop_last, every
+    batch from the augmented-inclusive set) and one graph-replayed epoch
+    through step.TrainStep; all losses finite."""
+    from craniofacialsd_vae_amd import data as D
+    from craniofacialsd_vae_amd import manager as M
+    d, cfg = aug_workspace
+    man = M.ModelManager(cfg, device="cuda", precomputed_storage_path=cfg["data"]["precomputed_path"],
+                         seed=5, use_graph=False, precision="bf16")
+    tr, va, te, norm = D.load_mesh_dataset(cfg["data"], 4, "cuda")
+    rec = []
+    got = man.run_epoch(tr, train=True, record=rec)
+    assert len(rec) == tr.n_batches == tr.n_items // 4
+    seen = np.concatenate([r[0] for r in rec])
+    assert len(np.unique(seen)) == len(seen) == tr.n_batches * 4
+    assert any(tr.names[i].startswith("augmented/") for i in seen)
+    assert all(np.isfinite(v) for v in got.values())
+    man.use_graph = True
+    got2 = man.run_epoch(tr, train=True)
+    assert all(np.isfinite(v) for v in got2.values())
+    assert int(man.engine.params.step.item()) == 2 * tr.n_batches
+
+
+def test_cli_data_parallel_two_ranks(workspace, tmp_path):
+    """train.py under torch.distributed.run with 2 ranks (C3's driver; here
+    gloo with both ranks on the one test GPU): each rank trains its shard,
+    epoch losses are the all-reduced means, rank 0 logs and checkpoints."""
+    import socket
+    d, cfg = workspace
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    out = tmp_path / "runs"
+    env = dict(os.environ, CFSD_DIST_BACKEND="gloo", CFSD_SHARE_DEVICE="1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "train.py"),
+           "--config", str(d / "config.yaml"), "--id", "dp", "--output_path", str(out), "--precision", "bf16"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    od = out / "outputs" / "dp"
+    assert sorted(os.listdir(od / "checkpoints")) == ["model_00000001.pt", "model_00000002.pt", "optimizer.pt"]
+    logs = [json.loads(ln) for ln in open(od / "logs" / "scalars.jsonl")]
+    assert len([x for x in logs if x["tag"] == "train/tot"]) == 2
+    assert all(np.isfinite(x["value"]) for x in logs)
+    assert r.stdout.count("epoch 2:") == 1  # rank 0 only

@@ -177,7 +177,7 @@ for step in range(1, 4):
            "moments_equal_ranks": gather_equal(eng_g.params.exp_avg_sq.cpu()),
            "batch_idx": ts.b.batch_idx.cpu().tolist()}
     if eng_g.params.shadow is not None:
-        rec["shadow_equal_ranks"] = gather_equal(eng_g.params.shadow.view(torch.int16).cpu())
+        rec["shadow_equal_ranks"] = gather_equal(eng_g.params.shadow.float().cpu())  # exact widening (gloo has no 16-bit types)
         rec["shadow_is_cast"] = bool(torch.equal(eng_g.params.shadow.cpu(),
                                                  eng_g.params.data.cpu().to(torch.bfloat16)))
     rec["losses_finite"] = bool(torch.isfinite(eng_g.loss_acc).all())

@@ -203,6 +203,18 @@ def main():
                                                  db=P.gview("de_layers.0.bias"))
     cases["lin_enc_dx"] = lambda: ops.linear_bwd(flat, W_enc, b.dmulv, dx=b.dpre_enc[3].view(16, -1), elu_y=flat)
     cases["lin_enc_dw"] = lambda: ops.linear_bwd(flat, None, b.dmulv, dw=gW_enc.view(W_enc.shape), db=gB_enc)
+    # bf16 D3 kernels (configs C3/C5), the step's own launch arguments
+    e16 = E.SDVAEEngine(T, E.ModelSpec(), device="cuda", precision="bf16")
+    c = e16.buffers(16)
+    for t in (c.dec_up[3], c.dec_out[3], c.dpre_dec[3]):
+        t.copy_(torch.randn(t.shape, device="cuda", generator=g))
+    w3h, b3h = e16._dec_w(3)
+    w16 = e16._w16("de_layers.4.conv.layer.weight")
+    cases["fwd_d3_b16"] = lambda: ops.spiral_conv_fwd_x(c.dec_up[3], T.spiral[0], w3h, w16, b3h, 1, c.dec_out[3])
+    cases["dx_d3_b16"] = lambda: ops.spiral_conv_bwd_data_x(c.dpre_dec[3], T.spiral_inv[0], w16, T.n_verts[0],
+                                                            out=c.g_dec_up[3])
+    cases["dw_d3_b16"] = lambda: ops.spiral_conv_bwd_weight_x(c.dec_up[3], T.spiral[0], c.dpre_dec[3], None, None,
+                                                              c.ws_dw[("dec", 3)])
     if "step" in names:
         eng.set_batch(b.x, key_index=3)
         cases["step"] = lambda: eng.train_step_on(b)

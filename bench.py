@@ -147,6 +147,10 @@ def launch_cost(name, a):
     that do no work the algorithm requires (step counter, latent head,
     loss finalisation, slab reduction, gradient scaling)."""
     f4 = 4
+
+    def sz(dt):  # bytes per element of a storage descriptor (type | CFSD_VM)
+        return 4 if (dt & 0xf) == 0 else 2
+
     if name == "cfsd_spiral_conv_fwd":
         B, vs, rows, S, ci, co = a[7:13]
         return 2.0 * B * rows * S * ci * co, f4 * (B * vs * ci + B * rows * co + co * S * ci) + 4 * rows * S, FP32_PEAK_TFLOPS
@@ -174,39 +178,39 @@ def launch_cost(name, a):
                 + 4 * vs * a[4], FP32_PEAK_TFLOPS)
     if name == "cfsd_spiral_conv_bwd_data_rowsub":
         B, vs, rows, S, ci, co = a[9:15]
-        sd = 4 if a[6] == 0 else 2
+        sd = sz(a[6])
         elu = a[4] is not None
         return (2.0 * B * rows * S * ci * co, f4 * (B * rows * co + co * S * ci) + sd * B * vs * ci * (2 if elu else 1)
                 + 4 * vs * a[2], FP32_PEAK_TFLOPS)
     if name in ("cfsd_spmm_csr_sched", "cfsd_spmm_sched_csr"):
-        sx, sy = (4 if a[5] == 0 else 2), (4 if a[8] == 0 else 2)
+        sx, sy = sz(a[5]), sz(a[8])
         B, m, n, c = a[9:13]
         elu = a[6] is not None
         return 0.0, B * c * (sx * n + sy * m * (2 if elu else 1)), None
     if name == "cfsd_spiral_conv_fwd_x":
-        sx, sy = (4 if a[1] == 0 else 2), (4 if a[7] == 0 else 2)
+        sx, sy = sz(a[1]), sz(a[7])
         B, vs, rows, S, ci, co = a[8:14]
         peak = BF16_PEAK_TFLOPS if (ci >= 16 and co >= 16) else FP32_PEAK_TFLOPS
         return 2.0 * B * rows * S * ci * co, sx * B * vs * ci + sy * B * rows * co + 2 * co * S * ci + 4 * rows * S, peak
     if name == "cfsd_spiral_conv_bwd_data_x":
-        sd = 4 if a[1] == 0 else 2
-        B, vs, rows, S, ci, co = a[8:14]
+        sd = sz(a[1])
+        B, vs, rows, S, ci, co = a[9:15]
         elu = a[6] is not None
         return (2.0 * B * rows * S * ci * co, sd * B * rows * co + 2 * B * vs * ci * (2 if elu else 1)
                 + 2 * co * S * ci + 16 * vs * S, BF16_PEAK_TFLOPS)
     if name == "cfsd_spiral_conv_bwd_weight_x":
-        sx, sd = (4 if a[1] == 0 else 2), (4 if a[4] == 0 else 2)
+        sx, sd = sz(a[1]), sz(a[4])
         B, vs, rows, S, ci, co = a[9:15]
         peak = BF16_PEAK_TFLOPS if ci >= 16 else FP32_PEAK_TFLOPS
         return 2.0 * B * rows * S * ci * co, sx * B * vs * ci + sd * B * rows * co + 4 * co * S * ci + 4 * rows * S, peak
     if name == "cfsd_spiral_conv_bwd_x":
-        B, vs, rows, S, ci, co = a[14:20]
-        dx, elu = a[9] is not None, a[8] is not None
+        B, vs, rows, S, ci, co = a[15:21]
+        dx, elu = a[10] is not None, a[9] is not None
         fl = 2.0 * B * rows * S * ci * co * (2 if dx else 1)
         by = 2 * B * vs * ci + 4 * B * rows * co + 4 * co * S * ci + (2 * B * vs * ci * (2 if elu else 1) if dx else 0)
         return fl, by, FP32_PEAK_TFLOPS
     if name in ("cfsd_spmm_csr_x", "cfsd_spmm_uniform"):
-        sx, sy = (4 if a[4] == 0 else 2), (4 if a[7] == 0 else 2)
+        sx, sy = sz(a[4]), sz(a[7])
         B, m, n, c = a[8:12]
         elu = a[5] is not None
         return 0.0, B * c * (sx * n + sy * m * (2 if elu else 1)), None
@@ -319,7 +323,7 @@ def kernel_probe(runner, n_iter=20):
         timed("conv_dw_D3", lambda: ops.spiral_conv_bwd_weight(b.dec_up[i3], T.spiral[0], b.dpre_dec[i3],
                                                                None, None, b.ws_dw[("dec", i3)]))
     g = torch.empty(16, T.n_verts[0], 9 * 32, device=b.x.device)
-    xg = b.dec_up[i3] if b.dec_up[i3].dtype == torch.float32 else b.dec_up[i3].float()
+    xg = b.dec_up[i3] if b.dec_up[i3].dtype == torch.float32 else b.dec_up[i3].float().contiguous()
     timed("spiral_gather_L0", lambda: ops.spiral_gather(xg, T.spiral[0], out=g))
     del g
     return res

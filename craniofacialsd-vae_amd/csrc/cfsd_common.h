@@ -201,6 +201,26 @@ __device__ __forceinline__ void divmod32(long v, int d, int& q, int& r) {
   r = vi - q * d;
 }
 
+// Row layout of a [batch, nv, c] activation (CFSD_VM storage flag, cfsd.h).
+// BM (the reference's [B, V, C]): row (b, v) is b*nv + v.  VM (vertex-major):
+// v*batch + b -- the rows of one vertex in every mesh of the batch form ONE
+// contiguous block, so a spiral neighbour is gathered for all meshes by a
+// single coalesced wave load (16 meshes x 32 bf16 channels = 1 KiB, 8 full
+// cache lines) instead of 16 scattered 64-B rows.  Kernels iterate flat rows
+// m in one operand's layout (split_row) and address the others with row_of.
+struct Lay {
+  int bs, vs;  // row index = b*bs + v*vs
+};
+__host__ __device__ inline Lay make_lay(bool vm, int batch, int nv) {
+  return vm ? Lay{1, batch} : Lay{nv, 1};
+}
+__device__ __forceinline__ int row_of(const Lay& L, int b, int v) { return b * L.bs + v * L.vs; }
+// flat row m of a tensor stored in layout (vm, batch, nv) -> (b, v)
+__device__ __forceinline__ void split_row(long m, bool vm, int batch, int nv, int& b, int& v) {
+  if (vm) divmod32(m, batch, v, b);
+  else divmod32(m, nv, b, v);
+}
+
 // Workgroups of `kernel` that can be resident on the whole device at once
 // (occupancy API x CU count).  Persistent grids are sized to this so no
 // workgroup runs in a second, mostly idle, round.  Cached per kernel.

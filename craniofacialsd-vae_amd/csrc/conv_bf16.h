@@ -12,18 +12,20 @@ namespace bf {
 constexpr int DT_F32 = CFSD_DT_F32;
 constexpr int DT_BF16 = CFSD_DT_BF16;
 
+// Layouts: xvm / dxvm (0/1) and the CFSD_VM bit of y_dt / dpre_dt (cfsd.h).
 // y[m, :] = act(bias + W . gather(x)), x bf16, y bf16 or fp32 (y_dt).
-int launch_fwd(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, void* y,
+int launch_fwd(const bf16_t* x, int xvm, const int* idx, const bf16_t* w, const float* bias, void* y,
                int y_dt, int vsrc, int rows, long total_rows, int cin, int cout, int act,
                hipStream_t st);
-// dx bf16 (times elu'(elu_y) when elu_y != NULL), dpre bf16 or fp32.
+// dx bf16 (times elu'(elu_y) when elu_y != NULL; elu_y in dx's layout), dpre
+// bf16 or fp32.
 int launch_dx(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_row,
-              const int* inv_head, const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int vsrc,
+              const int* inv_head, const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int dxvm, int vsrc,
               int rows, long total_src_rows, int cin, int cout, hipStream_t st);
 // dW / db partial slabs [n_slabs][cout*9*cin + cout] (plain layout), x bf16,
 // dpre bf16 or fp32.
 int dw_slabs(int batch, int rows, int cin, int cout);
-int launch_dw(const bf16_t* x, const int* idx, const void* dpre, int dpre_dt, float* ws, int vsrc,
+int launch_dw(const bf16_t* x, int xvm, const int* idx, const void* dpre, int dpre_dt, float* ws, int vsrc,
               int rows, long total_rows, int cin, int cout, hipStream_t st);
 
 }  // namespace bf

@@ -13,10 +13,12 @@
 namespace cfsd {
 
 
+// xb: the mesh's x base; rs: elements between consecutive vertices of one
+// mesh (c for batch-major x, batch * c for vertex-major x).
 template <int CK, typename TX>
 __device__ __forceinline__ void spmm_row_chunks(int beg, int end, const int* __restrict__ col,
                                                 const float* __restrict__ val,
-                                                const TX* __restrict__ xb, int c4, f32x4& acc) {
+                                                const TX* __restrict__ xb, long rs, f32x4& acc) {
 #pragma clang fp contract(off)
   for (int e0 = beg; e0 < end; e0 += CK) {
     float v[CK];
@@ -25,7 +27,7 @@ __device__ __forceinline__ void spmm_row_chunks(int beg, int end, const int* __r
     for (int j = 0; j < CK; ++j) {
       const int e = e0 + j < end ? e0 + j : end - 1;
       v[j] = val[e];
-      xv[j] = ld4f(xb + (long)col[e] * c4 * 4);
+      xv[j] = ld4f(xb + (long)col[e] * rs);
     }
 #pragma unroll
     for (int j = 0; j < CK; ++j) {
@@ -55,7 +57,7 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
                                                   const TX* __restrict__ x,
                                                   const TY* __restrict__ elu_y,
                                                   TY* __restrict__ y, int m, int n, int c4,
-                                                  long total) {
+                                                  long total, int batch, int xvm, int yvm) {
   // hipcc contracts a*b+c into fma by default; the reference rounds the
   // product and the sum separately (index_select*value, then scatter_add).
 #pragma clang fp contract(off)
@@ -64,8 +66,10 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   if (t >= total || t >= (long)((blockIdx.x & 7) + 1) * per) return;
   int br, q, b, r;
   divmod32(t, c4, br, q);
-  divmod32(br, m, b, r);
-  const TX* xb = x + (long)b * n * c4 * 4 + 4 * q;
+  split_row(br, yvm, batch, m, b, r);  // output rows in y's layout
+  const Lay lx = make_lay(xvm, batch, n);
+  const long rs = (long)lx.vs * c4 * 4;
+  const TX* xb = x + (long)b * lx.bs * c4 * 4 + 4 * q;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const int beg = row_ptr[r], end = row_ptr[r + 1];
   // Entries in chunks: the chunk's column/value and x loads are all issued
@@ -75,9 +79,9 @@ __global__ __launch_bounds__(256) void spmm_csr_k(const int* __restrict__ row_pt
   // clamped to the row's last one (an L1 hit, not added) -- measured faster
   // than exec-masked loads.  The 3-tap rows get an exact 3-entry chunk
   // (no clamped 4th load: up0 16.4 -> 15.2 us, same add order).
-  if (end - beg == 3) spmm_row_chunks<3>(beg, end, col, val, xb, c4, acc);
-  else if (end - beg <= 4) spmm_row_chunks<4>(beg, end, col, val, xb, c4, acc);
-  else spmm_row_chunks<8>(beg, end, col, val, xb, c4, acc);
+  if (end - beg == 3) spmm_row_chunks<3>(beg, end, col, val, xb, rs, acc);
+  else if (end - beg <= 4) spmm_row_chunks<4>(beg, end, col, val, xb, rs, acc);
+  else spmm_row_chunks<8>(beg, end, col, val, xb, rs, acc);
   if (elu_y) {
     f32x4 g = ld4f(elu_y + t * 4);
     acc.x *= elu_grad_from_out(g.x);
@@ -104,8 +108,9 @@ __global__ __launch_bounds__(256) void spmm_uniform_k(const int* __restrict__ co
                                                       const TX* __restrict__ x,
                                                       const TY* __restrict__ elu_y,
                                                       TY* __restrict__ y, int m, int n, int c4,
-                                                      long total) {
+                                                      long total, int batch, int xvm, int yvm) {
 #pragma clang fp contract(off)
+  const Lay lx = make_lay(xvm, batch, n);
   const long per = (total + 7) / 8;
   const int grp = blockIdx.x & 7;
   const long lim = min(total, (long)(grp + 1) * per);
@@ -118,7 +123,7 @@ __global__ __launch_bounds__(256) void spmm_uniform_k(const int* __restrict__ co
     const long t = min(t0 + 256 * j, lim - 1);  // clamped chunks: loads only
     int br, r;
     divmod32(t, c4, br, qq[j]);
-    divmod32(br, m, bq[j], r);
+    split_row(br, yvm, batch, m, bq[j], r);  // output rows in y's layout
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       cc[j][k] = col[r * K + k];
@@ -129,7 +134,8 @@ __global__ __launch_bounds__(256) void spmm_uniform_k(const int* __restrict__ co
 #pragma unroll
   for (int j = 0; j < RPT; ++j)
 #pragma unroll
-    for (int k = 0; k < K; ++k) xv[j][k] = ld4f(x + ((long)bq[j] * n + cc[j][k]) * c4 * 4 + 4 * qq[j]);
+    for (int k = 0; k < K; ++k)
+      xv[j][k] = ld4f(x + ((long)bq[j] * lx.bs + (long)cc[j][k] * lx.vs) * c4 * 4 + 4 * qq[j]);
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
     const long t = t0 + 256 * j;
@@ -169,7 +175,7 @@ __global__ __launch_bounds__(256) void spmm_uniform_k(const int* __restrict__ co
 template <int CK, typename TX>
 __device__ __forceinline__ void spmm_fold_prefetch(int beg, int end, const int* __restrict__ col,
                                                    const float* __restrict__ val,
-                                                   const TX* __restrict__ xb, int c4, f32x4& acc) {
+                                                   const TX* __restrict__ xb, long rs, f32x4& acc) {
 #pragma clang fp contract(off)
   int cc[CK];
   float vv[CK];
@@ -182,7 +188,7 @@ __device__ __forceinline__ void spmm_fold_prefetch(int beg, int end, const int* 
   for (int e0 = beg; e0 < end; e0 += CK) {
     f32x4 xv[CK];
 #pragma unroll
-    for (int j = 0; j < CK; ++j) xv[j] = ld4f(xb + (long)cc[j] * c4 * 4);
+    for (int j = 0; j < CK; ++j) xv[j] = ld4f(xb + (long)cc[j] * rs);
     float vc[CK];
 #pragma unroll
     for (int j = 0; j < CK; ++j) vc[j] = vv[j];
@@ -227,7 +233,7 @@ __global__ __launch_bounds__(256) void spmm_sched_k(const int* __restrict__ row_
   const int beg = row_ptr[r], end = row_ptr[r + 1];
   // (16-entry chunks for the > 32-entry rows measured no faster at level 0
   // and slower elsewhere: the wider branch's registers cost occupancy)
-  spmm_fold_prefetch<8>(beg, end, col, val, xb, c4, acc);
+  spmm_fold_prefetch<8>(beg, end, col, val, xb, (long)c4 * 4, acc);
   const long o = ((long)b * m + r) * c4 + q;
   if (elu_y) {
     f32x4 gy = ld4f(elu_y + o * 4);
@@ -253,19 +259,21 @@ __global__ __launch_bounds__(256) void spmm_sched_csr_k(const int* __restrict__ 
                                                         const TX* __restrict__ x,
                                                         const TY* __restrict__ elu_y,
                                                         TY* __restrict__ y, int m, int n, int c4,
-                                                        int groups, int bpg, int per) {
+                                                        int groups, int bpg, int per, int xvm,
+                                                        int yvm) {
   const int g = (int)blockIdx.x % groups;
   const int t = (int)(blockIdx.x / groups) * (int)blockDim.x + (int)threadIdx.x;
   if (t >= per) return;
   const int rowq = bpg * c4;  // threads per schedule slot
   const int slot = t / rowq, rem = t - slot * rowq;
   const int bl = rem / c4, q = rem - bl * c4;
-  const int b = g * bpg + bl;
+  const int b = g * bpg + bl, batch = groups * bpg;
+  const Lay lx = make_lay(xvm, batch, n), ly = make_lay(yvm, batch, m);
   const int r = rows_s[slot], beg = ptr_s[slot], end = ptr_s[slot + 1];
-  const TX* xb = x + (long)b * n * c4 * 4 + 4 * q;
+  const TX* xb = x + (long)b * lx.bs * c4 * 4 + 4 * q;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  spmm_fold_prefetch<8>(beg, end, col_s, val_s, xb, c4, acc);
-  const long o = ((long)b * m + r) * c4 + q;
+  spmm_fold_prefetch<8>(beg, end, col_s, val_s, xb, (long)lx.vs * c4 * 4, acc);
+  const long o = (long)row_of(ly, b, r) * c4 + q;
   if (elu_y) {
     f32x4 gy = ld4f(elu_y + o * 4);
     acc.x *= elu_grad_from_out(gy.x);
@@ -433,10 +441,20 @@ extern "C" int cfsd_vertex_errors(const float* out, const float* gt, const float
   return launch_status("vertex_errors");
 }
 
+// storage descriptor (type | CFSD_VM) -> (type, vertex-major); false if invalid
+static bool split_dt(int dt, int& type, int& vm) {
+  type = CFSD_DT_TYPE(dt);
+  vm = (dt & CFSD_VM) != 0;
+  return (dt & ~(CFSD_VM | 0xf)) == 0 && (type == CFSD_DT_F32 || type == CFSD_DT_BF16);
+}
+
 static int spmm_launch(const int32_t* row_ptr, const int32_t* col, const float* val,
                        const int32_t* order, const void* x, int x_dt, const void* elu_y, void* y,
                        int y_dt, int batch, int m, int n, int c, void* stream) {
   if (!row_ptr || !col || !val || !x || !y) return set_error(CFSD_EINVAL, "spmm_csr: null pointer");
+  int xvm, yvm;
+  if (!split_dt(x_dt, x_dt, xvm) || !split_dt(y_dt, y_dt, yvm)) return set_error(CFSD_EINVAL, "spmm_csr: bad dtype");
+  if (order && (xvm || yvm)) return set_error(CFSD_EINVAL, "spmm_csr_sched: batch-major operands only");
   if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
     return set_error(CFSD_EINVAL, "spmm_csr: bad sizes batch=%d m=%d n=%d c=%d", batch, m, n, c);
   if ((x_dt != CFSD_DT_F32 && x_dt != CFSD_DT_BF16) || (y_dt != CFSD_DT_F32 && y_dt != CFSD_DT_BF16))
@@ -464,7 +482,7 @@ static int spmm_launch(const int32_t* row_ptr, const int32_t* col, const float* 
   const hipStream_t st = (hipStream_t)stream;
 #define SPMM(TX, TY)                                                                             \
   hipLaunchKernelGGL((spmm_csr_k<TX, TY>), dim3(nblk), dim3(256), 0, st, row_ptr, col, val,      \
-                     (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, total)
+                     (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, total, batch, xvm, yvm)
   if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPMM(float, float);
   else if (x_dt == CFSD_DT_F32) SPMM(float, bf16_t);
   else if (y_dt == CFSD_DT_F32) SPMM(bf16_t, float);
@@ -503,8 +521,8 @@ extern "C" int cfsd_spmm_uniform(int k, const int32_t* col, const float* val, co
   if (k < 1 || k > 4) return set_error(CFSD_EINVAL, "spmm_uniform: %d entries per row (1..4)", k);
   if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
     return set_error(CFSD_EINVAL, "spmm_uniform: bad sizes batch=%d m=%d n=%d c=%d", batch, m, n, c);
-  if ((x_dt != CFSD_DT_F32 && x_dt != CFSD_DT_BF16) || (y_dt != CFSD_DT_F32 && y_dt != CFSD_DT_BF16))
-    return set_error(CFSD_EINVAL, "spmm_uniform: bad dtype");
+  int xvm, yvm;
+  if (!split_dt(x_dt, x_dt, xvm) || !split_dt(y_dt, y_dt, yvm)) return set_error(CFSD_EINVAL, "spmm_uniform: bad dtype");
   const long total = (long)batch * m * (c / 4);
   if (total >= (1L << 31) || (long)batch * n >= (1L << 31) || (long)m * k >= (1L << 31))
     return set_error(CFSD_EINVAL, "spmm_uniform: sizes >= 2^31 (32-bit indices)");
@@ -514,7 +532,7 @@ extern "C" int cfsd_spmm_uniform(int k, const int32_t* col, const float* val, co
   const hipStream_t st = (hipStream_t)stream;
 #define SPMU(K_, TX, TY)                                                                          \
   hipLaunchKernelGGL((spmm_uniform_k<K_, RPT, TX, TY>), dim3(nblk), dim3(256), 0, st, col, val,    \
-                     (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, total)
+                     (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, total, batch, xvm, yvm)
 #define SPMU_K(K_)                                                                                \
   if (k == K_) {                                                                                  \
     if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPMU(K_, float, float);                        \
@@ -536,17 +554,22 @@ extern "C" int cfsd_spmm_sched_csr(const int32_t* ptr_s, const int32_t* col_s, c
     return set_error(CFSD_EINVAL, "spmm_sched_csr: null pointer");
   if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
     return set_error(CFSD_EINVAL, "spmm_sched_csr: bad sizes batch=%d m=%d n=%d c=%d", batch, m, n, c);
-  if ((x_dt != CFSD_DT_F32 && x_dt != CFSD_DT_BF16) || (y_dt != CFSD_DT_F32 && y_dt != CFSD_DT_BF16))
+  int xvm, yvm;
+  if (!split_dt(x_dt, x_dt, xvm) || !split_dt(y_dt, y_dt, yvm))
     return set_error(CFSD_EINVAL, "spmm_sched_csr: bad dtype");
   if ((long)batch * m * (c / 4) >= (1L << 31) || (long)batch * n >= (1L << 31))
     return set_error(CFSD_EINVAL, "spmm_sched_csr: batch x rows >= 2^31 (32-bit indices)");
-  const int groups = batch % 8 == 0 ? 8 : 1, bpg = batch / groups;
+  // batch-major x: XCD groups of whole meshes (their rows share an L2);
+  // vertex-major x: one group, a slot's threads cover every mesh, so each
+  // gathered vertex block is one contiguous load
+  const int groups = (!xvm && batch % 8 == 0) ? 8 : 1, bpg = batch / groups;
   const int per = bpg * m * (c / 4);
   const unsigned nb = (unsigned)(groups * ((per + 255) / 256));
   const hipStream_t st = (hipStream_t)stream;
 #define SPSC(TX, TY)                                                                             \
   hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY>), dim3(nb), dim3(256), 0, st, ptr_s, col_s, val_s, \
-                     rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, groups, bpg, per)
+                     rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, groups, bpg, per,   \
+                     xvm, yvm)
   if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPSC(float, float);
   else if (x_dt == CFSD_DT_F32) SPSC(float, bf16_t);
   else if (y_dt == CFSD_DT_F32) SPSC(bf16_t, float);

@@ -234,7 +234,8 @@ __global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(con
                                                           const float* __restrict__ w,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ y, int vsrc,
-                                                          int rows, long total_rows) {
+                                                          int rows, long total_rows, int batch,
+                                                          int xvm, int yvm) {
   constexpr int L = CIN / 4;
   constexpr int RPW = 64 / L;
   constexpr int K = kSeq * CIN;
@@ -256,9 +257,12 @@ __global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(con
     const long mm = grp * RPW + slot;
     const bool valid = mm < total_rows;
     const long m = valid ? mm : total_rows - 1;
+    // rows visited in x's layout (vertex-major: RPW meshes of one vertex, so
+    // the wave's neighbour loads are contiguous), y addressed in its own
     int b, r;
-    divmod32(m, rows, b, r);
-    const TX* xb = x + (long)b * vsrc * CIN + 4 * q;
+    split_row(m, xvm, batch, rows, b, r);
+    const Lay lx = make_lay(xvm, batch, vsrc);
+    const TX* xb = x + (long)b * lx.bs * CIN + 4 * q;
     const int* ir = idx + (long)r * kSeq;
     float acc[CO];
 #pragma unroll
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(con
     asm volatile("" : "+v"(wq));  // opaque per iteration: keeps the weight reads from being hoisted into VGPRs
 #pragma unroll
     for (int s = 0; s < kSeq; ++s) {
-      const f32x4 v = ld4f(xb + (long)ir[s] * CIN);
+      const f32x4 v = ld4f(xb + (long)ir[s] * lx.vs * CIN);
 #pragma unroll
       for (int o = 0; o < CO; ++o) {
         const f32x4 wv = lw[(o * K + s * CIN) / 4 + wq];
@@ -282,11 +286,12 @@ __global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(con
 #pragma unroll
       for (int d = L / 2; d >= 1; d >>= 1) acc[o] += __shfl_xor(acc[o], d);
     if (valid && q == 0) {
+      const long yo = xvm == yvm ? m : (long)row_of(make_lay(yvm, batch, rows), b, r);
 #pragma unroll
       for (int o = 0; o < CO; ++o) {
         float v = acc[o] + bo[o];
         if (ACT == CFSD_ACT_ELU) v = elu_f(v);
-        y[m * CO + o] = v;
+        y[yo * CO + o] = v;
       }
     }
   }
@@ -304,7 +309,8 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
                                                         const float* __restrict__ w,
                                                         const float* __restrict__ bias,
                                                         TY* __restrict__ y, int vsrc, int rows,
-                                                        long total_rows) {
+                                                        long total_rows, int batch, int xvm,
+                                                        int yvm) {
   constexpr int K = kSeq * CS, KH = (K + 1) / 2, NCT = COUT / 32;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
@@ -324,13 +330,14 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
     long m = tile * 32 + i;
     if (m >= total_rows) m = total_rows - 1;
     int b, r;
-    divmod32(m, rows, b, r);
-    const float* xb = x + (long)b * vsrc * CS;
+    split_row(m, yvm, batch, rows, b, r);  // rows visited (and stored) in y's layout
+    const Lay lx = make_lay(xvm, batch, vsrc);
+    const float* xb = x + (long)b * lx.bs * CS;
     const int* ir = idx + (long)r * kSeq;
     float g[2 * KH];
 #pragma unroll
     for (int s = 0; s < kSeq; ++s) {
-      ld_row<CS>(xb + (long)ir[s] * CS, &g[s * CS]);
+      ld_row<CS>(xb + (long)ir[s] * lx.vs * CS, &g[s * CS]);
     }
 #pragma unroll
     for (int k = K; k < 2 * KH; ++k) g[k] = 0.f;
@@ -539,7 +546,6 @@ __global__ __launch_bounds__(256, dx_occ(CIN, COUT)) void conv_dx_mfma(
 // two accumulators (even / odd chunk) halve the dependent-MFMA chain.
 // Tasks are numbered column-tile fastest, so the waves of a workgroup
 // gather the same rows (L1 hits).
-constexpr int kLatSB = 3;  // slots per batch
 #ifndef CFSD_FWD_LAT_SB
 #define CFSD_FWD_LAT_SB 3
 #endif
@@ -1252,12 +1258,13 @@ __global__ __launch_bounds__(256) void conv_dx_rowsub_gather(const float* __rest
                                                              const TY* __restrict__ elu_y,
                                                              TY* __restrict__ dx, int vsrc,
                                                              int rows, int total_src,
-                                                             int dg_bytes) {
+                                                             int dg_bytes, int batch, int dxvm) {
   constexpr int Q = CIN / 4;
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t >= total_src * Q) return;
   const int m = t / Q, q = t - m * Q;
-  const int b = m / vsrc, u = m - b * vsrc;
+  int b, u;
+  split_row(m, dxvm, batch, vsrc, b, u);  // dx / elu_y rows in dx's layout; dG batch-major
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dg), 0, dg_bytes, 0x00020000);
   const int base = (b * rows * kSeq * CIN + 4 * q) * (int)sizeof(float);
   int4 e[G];
@@ -1635,7 +1642,8 @@ __global__ __launch_bounds__(256) void conv_dw_in_mfma(const float* __restrict__
                                                        const int* __restrict__ idx,
                                                        const TD* __restrict__ dpre,
                                                        float* __restrict__ ws, int vsrc, int rows,
-                                                       long total_rows) {
+                                                       long total_rows, int batch, int xvm,
+                                                       int dpvm) {
   constexpr int K = kSeq * CS, NI = K + 1, NCT = COUT / 32, NEL = COUT * K + COUT;
   static_assert(NI <= 32 && COUT % 32 == 0, "shape");
   __shared__ float at_all[4 * 32 * kAts];
@@ -1653,13 +1661,14 @@ __global__ __launch_bounds__(256) void conv_dw_in_mfma(const float* __restrict__
     const bool valid = m < total_rows;
     const long mm = valid ? m : total_rows - 1;
     int b, r;
-    divmod32(mm, rows, b, r);
-    const float* xb = x + (long)b * vsrc * CS;
+    split_row(mm, dpvm, batch, rows, b, r);  // K (rows) in dpre's layout
+    const Lay lx = make_lay(xvm, batch, vsrc);
+    const float* xb = x + (long)b * lx.bs * CS;
     const int* ir = idx + (long)r * kSeq;
     float xv[K];
 #pragma unroll
     for (int s = 0; s < kSeq; ++s) {
-      ld_row<CS>(xb + (long)ir[s] * CS, &xv[s * CS]);
+      ld_row<CS>(xb + (long)ir[s] * lx.vs * CS, &xv[s * CS]);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) At[k * kAts + lane] = valid ? xv[k] : 0.f;
@@ -1851,7 +1860,8 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     const float* __restrict__ dpre, const int* __restrict__ inv_ptr,
     const int* __restrict__ inv_row, const int4* __restrict__ inv_head,
     const float* __restrict__ w, const TX* __restrict__ elu_y, const TX* __restrict__ x,
-    TX* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, long total_rows) {
+    TX* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, long total_rows, int batch,
+    int xvm, int dpvm) {
   constexpr int SPH = 5, KH = SPH * CO, K = kSeq * CIN, NCT = CIN / 32, NEL = CO * K + CO;
   static_assert(2 * KH <= 32 && CIN % 32 == 0, "shape");
   __shared__ float at_all[4 * 32 * kAtS];
@@ -1879,6 +1889,7 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
   const int ey_mode = elu_y == nullptr ? 0 : (elu_y == x ? 1 : 2);
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(dpre), 0, (int)(total_rows / vsrc * rows * CO * (long)sizeof(float)), 0x00020000);
+  const Lay ldp = make_lay(dpvm, batch, rows);
   const long n_tiles = (total_rows + 31) / 32;
   const TileSweep sw = xcd_sweep(n_tiles, 4, wave);
   for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
@@ -1888,7 +1899,7 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     const bool valid = m < total_rows;
     const long mm = valid ? m : total_rows - 1;
     int b, u;
-    divmod32(mm, vsrc, b, u);
+    split_row(mm, xvm, batch, vsrc, b, u);  // source rows (x, dx, elu_y) in x's layout
     // x tile in accumulator-row order (B operand of dW, elu' source); issued
     // first: independent of the inverse-spiral chain, so their latency hides
     // behind it
@@ -1901,7 +1912,8 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) xv[ct][j] = ldf(&xt[rr * CIN + ct * 32]);
     }
-    const float* db_ = dpre + (long)b * rows * CO;
+    const float* db_ = dpre + (long)b * ldp.bs * CO;
+    const int dstride = ldp.vs * CO;  // floats between consecutive rows of one mesh's dpre
     const int4 none = make_int4(-1, -1, -1, -1);
     int4 pr[SPH];
 #pragma unroll
@@ -1913,14 +1925,14 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     // flight together (absent rows out of range: 0, no traffic); rows 3..
     // (0.3 % of keys) through an exec branch
     float tt[SPH][CO];
-    const int base = b * rows * CO * (int)sizeof(float);
+    const int base = b * ldp.bs * CO * (int)sizeof(float);
 #pragma unroll
     for (int sl = 0; sl < SPH; ++sl) {
       const int hr[3] = {pr[sl].x, pr[sl].y, pr[sl].z};
       float v[3][CO];
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        const int off = hr[j] >= 0 ? base + hr[j] * CO * (int)sizeof(float) : kAbsentRow;
+        const int off = hr[j] >= 0 ? base + hr[j] * dstride * (int)sizeof(float) : kAbsentRow;
         // one load per list row: the texture path costs a cycle per distinct
         // cache line per instruction, so per-channel dword loads tripled it
         load_row<CO>(rsrc, off, v[j]);
@@ -1932,11 +1944,11 @@ __global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
     for (int sl = 0; sl < SPH; ++sl) {
       if (pr[sl].w >= 0) {
 #pragma unroll
-        for (int o = 0; o < CO; ++o) tt[sl][o] += db_[pr[sl].w * CO + o];
+        for (int o = 0; o < CO; ++o) tt[sl][o] += db_[pr[sl].w * dstride + o];
         const long key = (long)u * kSeq + h * SPH + sl;
         for (int e = inv_ptr[key] + kInvHead; e < inv_ptr[key + 1]; ++e) {
 #pragma unroll
-          for (int o = 0; o < CO; ++o) tt[sl][o] += db_[inv_row[e] * CO + o];
+          for (int o = 0; o < CO; ++o) tt[sl][o] += db_[inv_row[e] * dstride + o];
         }
       }
     }
@@ -2230,23 +2242,23 @@ extern "C" int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const fl
   if (cin == CS_ && cout == CO_) {                                                               \
     if (act == CFSD_ACT_ELU)                                                                     \
       hipLaunchKernelGGL((conv_fwd_in_mfma<CS_, CO_, CFSD_ACT_ELU>), dim3(gp), dim3(256), 0, st,  \
-                         x, idx, w, bias, y, vsrc, rows, M);                                     \
+                         x, idx, w, bias, y, vsrc, rows, M, batch, 0, 0);                        \
     else                                                                                         \
       hipLaunchKernelGGL((conv_fwd_in_mfma<CS_, CO_, CFSD_ACT_NONE>), dim3(gp), dim3(256), 0, st, \
-                         x, idx, w, bias, y, vsrc, rows, M);                                     \
+                         x, idx, w, bias, y, vsrc, rows, M, batch, 0, 0);                        \
     return launch_status("spiral_conv_fwd_in");                                                  \
   }
     FIN(1, 32) FIN(2, 32) FIN(3, 32) FIN(1, 64) FIN(2, 64) FIN(3, 64)
 #undef FIN
   }
-#define FWD_SMALL(KERNEL, A_, B_)                                                                \
+#define FWD_SMALL(KERNEL, A_, B_, ...)                                                           \
   if (cin == A_ && cout == B_) {                                                                 \
     if (act == CFSD_ACT_ELU) {                                                                   \
       auto k = KERNEL<A_, B_, CFSD_ACT_ELU>;                                                     \
-      hipLaunchKernelGGL(k, dim3(GRID(k)), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M); \
+      hipLaunchKernelGGL(k, dim3(GRID(k)), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M __VA_ARGS__); \
     } else {                                                                                     \
       auto k = KERNEL<A_, B_, CFSD_ACT_NONE>;                                                    \
-      hipLaunchKernelGGL(k, dim3(GRID(k)), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M); \
+      hipLaunchKernelGGL(k, dim3(GRID(k)), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M __VA_ARGS__); \
     }                                                                                            \
     return launch_status("spiral_conv_fwd_small");                                               \
   }
@@ -2254,8 +2266,8 @@ extern "C" int cfsd_spiral_conv_fwd(const float* x, const int32_t* idx, const fl
   FWD_SMALL(conv_fwd_in_small, 3, 16)
 #undef GRID
 #define GRID(k) small_grid(k, M)
-  FWD_SMALL(conv_fwd_out_small, 16, 3) FWD_SMALL(conv_fwd_out_small, 32, 3)
-  FWD_SMALL(conv_fwd_out_small, 64, 3)
+  FWD_SMALL(conv_fwd_out_small, 16, 3, , batch, 0, 0) FWD_SMALL(conv_fwd_out_small, 32, 3, , batch, 0, 0)
+  FWD_SMALL(conv_fwd_out_small, 64, 3, , batch, 0, 0)
 #undef GRID
 #undef FWD_SMALL
   return set_error(CFSD_EINVAL, "spiral_conv_fwd: unsupported channels %d -> %d", cin, cout);
@@ -2508,10 +2520,10 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
     DWM(32, 32) DWM(32, 64) DWM(64, 32) DWM(64, 64)
 #undef DWM
   }
-#define DWS(KERNEL, A_, B_)                                                                       \
+#define DWS(KERNEL, A_, B_, ...)                                                                  \
   if (cin == A_ && cout == B_) {                                                                  \
     hipLaunchKernelGGL((KERNEL<A_, B_>), dim3(g.gx), dim3(256), 0, st, x, idx, dpre, workspace,   \
-                       vsrc, rows, M);                                                            \
+                       vsrc, rows, M __VA_ARGS__);                                                \
     rc = launch_status("spiral_conv_bwd_weight_small");                                           \
     if (rc || deferred) return rc;                                                                \
     hipLaunchKernelGGL(slab_reduce, rg, dim3(1024), 0, st, workspace, g.gx, n_el, dw,             \
@@ -2519,9 +2531,9 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
     return launch_status("spiral_conv_bwd_weight_small_reduce");                                  \
   }
   if (g.kind == kDwInMfma) {
-    DWS(conv_dw_in_mfma, 3, 32) DWS(conv_dw_in_mfma, 3, 64)
-    DWS(conv_dw_in_mfma, 2, 32) DWS(conv_dw_in_mfma, 2, 64)
-    DWS(conv_dw_in_mfma, 1, 32) DWS(conv_dw_in_mfma, 1, 64)
+    DWS(conv_dw_in_mfma, 3, 32, , batch, 0, 0) DWS(conv_dw_in_mfma, 3, 64, , batch, 0, 0)
+    DWS(conv_dw_in_mfma, 2, 32, , batch, 0, 0) DWS(conv_dw_in_mfma, 2, 64, , batch, 0, 0)
+    DWS(conv_dw_in_mfma, 1, 32, , batch, 0, 0) DWS(conv_dw_in_mfma, 1, 64, , batch, 0, 0)
   } else if (g.kind == kDwInSmall) {
     DWS(conv_dw_in_small, 3, 16) DWS(conv_dw_in_small, 3, 32) DWS(conv_dw_in_small, 3, 64)
   } else {
@@ -2629,7 +2641,7 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
   if (cin == CIN_ && cout == CO_) {                                                              \
     hipLaunchKernelGGL((conv_bwd_out_mfma<CIN_, CO_>), dim3(gx), dim3(256), 0, st, dpre,         \
                        inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, x, dx, workspace, vsrc, \
-                       rows, Ms);                                                                \
+                       rows, Ms, batch, 0, 0);                                                   \
     rc = launch_status("spiral_conv_bwd_small");                                                 \
     if (rc || !dw) return rc;                                                                    \
     hipLaunchKernelGGL(slab_reduce, dim3((unsigned)((n_el + 63) / 64)), dim3(1024), 0, st,        \
@@ -2728,7 +2740,7 @@ extern "C" int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, c
 #define RSG(CIN_, G_)                                                                             \
   if (cin == CIN_ && G == G_) {                                                                   \
     hipLaunchKernelGGL((conv_dx_rowsub_gather<CIN_, G_>), gg, dim3(256), 0, st, dg,               \
-                       (const int4*)inv_flat, elu_y, dx, vsrc, rows, M, (int)(dg_el * sizeof(float))); \
+                       (const int4*)inv_flat, elu_y, dx, vsrc, rows, M, (int)(dg_el * sizeof(float)), batch, 0); \
     return launch_status("spiral_conv_bwd_rowsub_gather");                                       \
   }
   RSG(32, 1) RSG(32, 2) RSG(32, 3) RSG(32, 4)
@@ -2751,6 +2763,8 @@ extern "C" int cfsd_spiral_conv_bwd_data_rowsub(const float* dpre, const int32_t
   if (!dx || !workspace) return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_rowsub: null dx / workspace");
   if (!rowsub_shape(cin, cout))
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_rowsub: unsupported channels %d -> %d", cin, cout);
+  const int dxvm = (dx_dt & CFSD_VM) != 0;  // dx and elu_y vertex-major
+  dx_dt = CFSD_DT_TYPE(dx_dt);
   if (dx_dt != CFSD_DT_F32 && dx_dt != CFSD_DT_BF16) return set_error(CFSD_EINVAL, "bad dx dtype %d", dx_dt);
   if (flat_width <= 0 || flat_width > 16 || flat_width % 4)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_rowsub: flat_width %d not in {4, 8, 12, 16}", flat_width);
@@ -2780,10 +2794,10 @@ extern "C" int cfsd_spiral_conv_bwd_data_rowsub(const float* dpre, const int32_t
   if (G == G_) {                                                                                   \
     if (dx_dt == CFSD_DT_BF16)                                                                     \
       hipLaunchKernelGGL((conv_dx_rowsub_gather<32, G_, bf16_t>), gg, dim3(256), 0, st, workspace, \
-                         (const int4*)inv_flat, (const bf16_t*)elu_y, (bf16_t*)dx, vsrc, rows, M, dgb); \
+                         (const int4*)inv_flat, (const bf16_t*)elu_y, (bf16_t*)dx, vsrc, rows, M, dgb, batch, dxvm); \
     else                                                                                           \
       hipLaunchKernelGGL((conv_dx_rowsub_gather<32, G_, float>), gg, dim3(256), 0, st, workspace,  \
-                         (const int4*)inv_flat, (const float*)elu_y, (float*)dx, vsrc, rows, M, dgb); \
+                         (const int4*)inv_flat, (const float*)elu_y, (float*)dx, vsrc, rows, M, dgb, batch, dxvm); \
     return launch_status("spiral_conv_bwd_data_rowsub_gather");                                   \
   }
   RSG2(1) RSG2(2) RSG2(3) RSG2(4)
@@ -2822,7 +2836,10 @@ extern "C" int cfsd_spiral_gather(const float* x, const int32_t* idx, float* g, 
 static bool mfma_shape(int cin, int cout) {
   return (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
 }
-static bool dt_ok(int dt) { return dt == CFSD_DT_F32 || dt == CFSD_DT_BF16; }
+static bool dt_ok(int dt) {
+  return (dt & ~(CFSD_VM | 0xf)) == 0 && (CFSD_DT_TYPE(dt) == CFSD_DT_F32 || CFSD_DT_TYPE(dt) == CFSD_DT_BF16);
+}
+static int vm_of(int dt) { return (dt & CFSD_VM) != 0; }
 
 extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* idx, const float* w,
                                       const uint16_t* w_bf16, const float* bias, void* y, int y_dt,
@@ -2834,11 +2851,14 @@ extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* id
   if (act != CFSD_ACT_NONE && act != CFSD_ACT_ELU) return set_error(CFSD_EINVAL, "bad act %d", act);
   const hipStream_t st = (hipStream_t)stream;
   const long M = (long)batch * rows;
+  const int xvm = vm_of(x_dt), yvm = vm_of(y_dt);
+  x_dt = CFSD_DT_TYPE(x_dt);
   if (mfma_shape(cin, cout) && x_dt == CFSD_DT_BF16) {
     if (!w_bf16) return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: w_bf16 required");
-    return bf::launch_fwd((const bf16_t*)x, idx, (const bf16_t*)w_bf16, bias, y, y_dt, vsrc, rows, M, cin,
+    return bf::launch_fwd((const bf16_t*)x, xvm, idx, (const bf16_t*)w_bf16, bias, y, y_dt, vsrc, rows, M, cin,
                           cout, act, st);
   }
+  y_dt = CFSD_DT_TYPE(y_dt);
   if (!w) return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: w required");
   if (cin <= 3 && (cout == 32 || cout == 64) && x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_BF16) {
     const long tiles = (M + 31) / 32;
@@ -2847,10 +2867,12 @@ extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* id
   if (cin == CS_ && cout == CO_) {                                                               \
     if (act == CFSD_ACT_ELU)                                                                     \
       hipLaunchKernelGGL((conv_fwd_in_mfma<CS_, CO_, CFSD_ACT_ELU, bf16_t>), dim3(gp), dim3(256), \
-                         0, st, (const float*)x, idx, w, bias, (bf16_t*)y, vsrc, rows, M);       \
+                         0, st, (const float*)x, idx, w, bias, (bf16_t*)y, vsrc, rows, M, batch, \
+                         xvm, yvm);                                                              \
     else                                                                                         \
       hipLaunchKernelGGL((conv_fwd_in_mfma<CS_, CO_, CFSD_ACT_NONE, bf16_t>), dim3(gp), dim3(256), \
-                         0, st, (const float*)x, idx, w, bias, (bf16_t*)y, vsrc, rows, M);       \
+                         0, st, (const float*)x, idx, w, bias, (bf16_t*)y, vsrc, rows, M, batch, \
+                         xvm, yvm);                                                              \
     return launch_status("spiral_conv_fwd_in_bf16");                                             \
   }
     FINB(1, 32) FINB(2, 32) FINB(3, 32) FINB(1, 64) FINB(2, 64) FINB(3, 64)
@@ -2862,11 +2884,11 @@ extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* id
     if (act == CFSD_ACT_ELU) {                                                                    \
       auto k = conv_fwd_out_small<CI_, CO_, CFSD_ACT_ELU, bf16_t>;                                \
       hipLaunchKernelGGL(k, dim3(small_grid(k, M)), dim3(256), 0, st, (const bf16_t*)x, idx, w,   \
-                         bias, (float*)y, vsrc, rows, M);                                         \
+                         bias, (float*)y, vsrc, rows, M, batch, xvm, yvm);                        \
     } else {                                                                                      \
       auto k = conv_fwd_out_small<CI_, CO_, CFSD_ACT_NONE, bf16_t>;                               \
       hipLaunchKernelGGL(k, dim3(small_grid(k, M)), dim3(256), 0, st, (const bf16_t*)x, idx, w,   \
-                         bias, (float*)y, vsrc, rows, M);                                         \
+                         bias, (float*)y, vsrc, rows, M, batch, xvm, yvm);                        \
     }                                                                                             \
     return launch_status("spiral_conv_fwd_out_bf16");                                             \
   }
@@ -2880,20 +2902,21 @@ extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* id
 extern "C" int cfsd_spiral_conv_bwd_data_x(const void* dpre, int dpre_dt, const int32_t* inv_ptr,
                                            const int32_t* inv_row, const int32_t* inv_head,
                                            const uint16_t* w_bf16, const uint16_t* elu_y,
-                                           uint16_t* dx, int batch, int vsrc, int rows, int seq,
-                                           int cin, int cout, void* stream) {
+                                           uint16_t* dx, int dx_dt, int batch, int vsrc, int rows,
+                                           int seq, int cin, int cout, void* stream) {
   int rc = check_conv_args(dpre, inv_ptr, inv_row, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
   if (!w_bf16 || !dx || !inv_head) return set_error(CFSD_EINVAL, "null w_bf16/dx/inv_head");
-  if (!dt_ok(dpre_dt)) return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_x: bad dtype");
+  if (!dt_ok(dpre_dt) || !dt_ok(dx_dt) || CFSD_DT_TYPE(dx_dt) != CFSD_DT_BF16)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_x: bad dtype");
   if ((uintptr_t)inv_head & 15) return set_error(CFSD_EINVAL, "inv_head must be 16-B aligned");
-  if ((long)batch * rows * cout * (dpre_dt == CFSD_DT_F32 ? 4L : 2L) >= (1L << 31))
+  if ((long)batch * rows * cout * (CFSD_DT_TYPE(dpre_dt) == CFSD_DT_F32 ? 4L : 2L) >= (1L << 31))
     return set_error(CFSD_EINVAL, "dpre larger than 2 GiB (32-bit buffer offsets)");
   if (!mfma_shape(cin, cout))
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_x: unsupported channels %d -> %d", cin, cout);
   return bf::launch_dx(dpre, dpre_dt, inv_ptr, inv_row, inv_head, (const bf16_t*)w_bf16,
-                       (const bf16_t*)elu_y, (bf16_t*)dx, vsrc, rows, (long)batch * vsrc, cin, cout,
-                       (hipStream_t)stream);
+                       (const bf16_t*)elu_y, (bf16_t*)dx, vm_of(dx_dt), vsrc, rows, (long)batch * vsrc,
+                       cin, cout, (hipStream_t)stream);
 }
 
 extern "C" size_t cfsd_spiral_conv_bwd_weight_x_workspace(int batch, int rows, int seq, int cin,
@@ -2922,17 +2945,21 @@ extern "C" int cfsd_spiral_conv_bwd_weight_x(const void* x, int x_dt, const int3
   const long M = (long)batch * rows;
   const int n_el = cout * kSeq * cin + cout;
   const dim3 rg((unsigned)((n_el + 63) / 64));
+  const int xvm = vm_of(x_dt), dpvm = vm_of(dpre_dt);
+  x_dt = CFSD_DT_TYPE(x_dt);
   int n_slabs = 0;
   if (mfma_shape(cin, cout) && x_dt == CFSD_DT_BF16) {
-    rc = bf::launch_dw((const bf16_t*)x, idx, dpre, dpre_dt, workspace, vsrc, rows, M, cin, cout, st);
+    rc = bf::launch_dw((const bf16_t*)x, xvm, idx, dpre, dpre_dt, workspace, vsrc, rows, M, cin, cout, st);
     n_slabs = bf::dw_slabs(batch, rows, cin, cout);
-  } else if (cin <= 3 && (cout == 32 || cout == 64) && x_dt == CFSD_DT_F32 && dpre_dt == CFSD_DT_BF16) {
+  } else if (cin <= 3 && (cout == 32 || cout == 64) && x_dt == CFSD_DT_F32 &&
+             CFSD_DT_TYPE(dpre_dt) == CFSD_DT_BF16) {
     const DwGeom g = dw_geom(batch, rows, cin, cout);
     if (g.kind != kDwInMfma) return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_x: geometry");
 #define DWIB(CS_, CO_)                                                                             \
   if (cin == CS_ && cout == CO_)                                                                   \
     hipLaunchKernelGGL((conv_dw_in_mfma<CS_, CO_, bf16_t>), dim3(g.gx), dim3(256), 0, st,          \
-                       (const float*)x, idx, (const bf16_t*)dpre, workspace, vsrc, rows, M);
+                       (const float*)x, idx, (const bf16_t*)dpre, workspace, vsrc, rows, M, batch,  \
+                       xvm, dpvm);
     DWIB(1, 32) DWIB(2, 32) DWIB(3, 32) DWIB(1, 64) DWIB(2, 64) DWIB(3, 64)
 #undef DWIB
     rc = launch_status("spiral_conv_bwd_weight_in_bf16");
@@ -2947,14 +2974,16 @@ extern "C" int cfsd_spiral_conv_bwd_weight_x(const void* x, int x_dt, const int3
 }
 
 extern "C" int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* idx, const float* dpre,
-                                      const int32_t* inv_ptr, const int32_t* inv_row,
+                                      int dpre_dt, const int32_t* inv_ptr, const int32_t* inv_row,
                                       const int32_t* inv_head, const float* w, const void* elu_y,
                                       void* dx, float* dw, float* db, float* workspace,
                                       size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
                                       int cin, int cout, void* stream) {
   int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
-  if (x_dt != CFSD_DT_BF16) return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: x must be bf16");
+  if (!dt_ok(x_dt) || CFSD_DT_TYPE(x_dt) != CFSD_DT_BF16) return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: x must be bf16");
+  if (!dt_ok(dpre_dt) || CFSD_DT_TYPE(dpre_dt) != CFSD_DT_F32)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: dpre must be fp32");
   if (!fused_small(cin, cout))
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: small-output layers only (%d -> %d)", cin, cout);
   if (!inv_ptr || !inv_row || !inv_head || !w || !workspace)
@@ -2972,7 +3001,8 @@ extern "C" int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* id
   if (cin == CIN_ && cout == CO_) {                                                              \
     hipLaunchKernelGGL((conv_bwd_out_mfma<CIN_, CO_, bf16_t>), dim3(gx), dim3(256), 0, st, dpre, \
                        inv_ptr, inv_row, (const int4*)inv_head, w, (const bf16_t*)elu_y,          \
-                       (const bf16_t*)x, (bf16_t*)dx, workspace, vsrc, rows, Ms);                 \
+                       (const bf16_t*)x, (bf16_t*)dx, workspace, vsrc, rows, Ms, batch,           \
+                       vm_of(x_dt), vm_of(dpre_dt));                                              \
     rc = launch_status("spiral_conv_bwd_small_bf16");                                            \
     if (rc || !dw) return rc;                                                                    \
     hipLaunchKernelGGL(slab_reduce, dim3((unsigned)((n_el + 63) / 64)), dim3(1024), 0, st,        \

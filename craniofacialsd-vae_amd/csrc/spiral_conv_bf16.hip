@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void conv_fwd_b16(const bf16_t* __restrict__ x
                                                     const bf16_t* __restrict__ w,
                                                     const float* __restrict__ bias,
                                                     TY* __restrict__ y, int vsrc, int rows,
-                                                    long total_rows) {
+                                                    long total_rows, int batch, int xvm, int yvm) {
   constexpr int K = kS * CIN, KP = K + 8, KC = CIN / 32, NT = COUT / 16;
   extern __shared__ bf16_t lw[];  // [COUT][KP]
   coop_copy<8, u32x4>(
@@ -45,14 +45,17 @@ __global__ __launch_bounds__(256) void conv_fwd_b16(const bf16_t* __restrict__ x
   float bn[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) bn[t] = bias ? bias[t * 16 + i] : 0.f;
+  // rows are visited in x's layout (vertex-major: a 16-row tile is one
+  // vertex of 16 meshes, each neighbour gather one contiguous 1-KiB wave load)
+  const Lay lx = make_lay(xvm, batch, vsrc), ly = make_lay(yvm, batch, rows);
   const long n_tiles = (total_rows + 15) / 16;
   const TileSweep sw = xcd_sweep(n_tiles, 4, wave, n_tiles < 2 * kContigTiles);
   for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
     long m = tile * 16 + i;
     if (m >= total_rows) m = total_rows - 1;  // clamped loads, masked stores
     int b, r;
-    divmod32(m, rows, b, r);
-    const bf16_t* xb = x + (long)b * vsrc * CIN + 8 * g;
+    split_row(m, xvm, batch, rows, b, r);
+    const bf16_t* xb = x + (long)b * lx.bs * CIN + 8 * g;
     const int* ir = idx + r * kS;
     int src[kS];
 #pragma unroll
@@ -61,7 +64,7 @@ __global__ __launch_bounds__(256) void conv_fwd_b16(const bf16_t* __restrict__ x
 #pragma unroll
     for (int s = 0; s < kS; ++s)
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) a[s][kc] = ld8bf(xb + src[s] * CIN + 32 * kc);
+      for (int kc = 0; kc < KC; ++kc) a[s][kc] = ld8bf(xb + (long)src[s] * lx.vs * CIN + 32 * kc);
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -78,11 +81,17 @@ __global__ __launch_bounds__(256) void conv_fwd_b16(const bf16_t* __restrict__ x
     for (int rr = 0; rr < 4; ++rr) {
       const long mo = tile * 16 + 4 * g + rr;
       if (mo < total_rows) {
+        long yo = mo;
+        if (xvm != yvm) {
+          int bo, ro;
+          split_row(mo, xvm, batch, rows, bo, ro);
+          yo = row_of(ly, bo, ro);
+        }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           float v = acc[t][rr] + bn[t];
           if (ACT == CFSD_ACT_ELU) v = elu_f(v);
-          stf(&y[mo * COUT + t * 16 + i], v);
+          stf(&y[yo * COUT + t * 16 + i], v);
         }
       }
     }
@@ -120,7 +129,7 @@ __global__ __launch_bounds__(256) void conv_dx_b16(const TD* __restrict__ dpre,
                                                    const bf16_t* __restrict__ w,
                                                    const bf16_t* __restrict__ elu_y,
                                                    bf16_t* __restrict__ dx, int vsrc, int rows,
-                                                   long total_rows) {
+                                                   long total_rows, int batch, int dpvm, int dxvm) {
   constexpr int K = kS * CIN, OP = COUT + 8, OC = COUT / 32, NT = CIN / 16;
   constexpr int RB = COUT * (int)sizeof(TD);  // dpre row bytes
   extern __shared__ bf16_t lwt[];             // [kS*CIN][OP]: lwt[k*OP + o] = w[o*K + k]
@@ -131,14 +140,16 @@ __global__ __launch_bounds__(256) void conv_dx_b16(const TD* __restrict__ dpre,
   const int i = lane & 15, g = lane >> 4;
   const int nbytes = (int)(total_rows / vsrc * rows * RB);
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<TD*>(dpre), 0, nbytes, 0x00020000);
+  const Lay ld = make_lay(dpvm, batch, rows);
+  const int rstride = ld.vs * RB;  // bytes between consecutive vertices of one mesh's dpre
   const long n_tiles = (total_rows + 15) / 16;
   const TileSweep sw = xcd_sweep(n_tiles, 4, wave, n_tiles < 2 * kContigTiles);
   for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
     long m = tile * 16 + i;
     if (m >= total_rows) m = total_rows - 1;
     int b, u;
-    divmod32(m, vsrc, b, u);
-    const int base = b * rows * RB + 8 * g * (int)sizeof(TD);
+    split_row(m, dxvm, batch, vsrc, b, u);  // dx (and elu_y) rows in dx's layout
+    const int base = b * ld.bs * RB + 8 * g * (int)sizeof(TD);
     const int4* pu = inv_head + u * kS;
     f32x4 acc[NT];
 #pragma unroll
@@ -156,7 +167,7 @@ __global__ __launch_bounds__(256) void conv_dx_b16(const TD* __restrict__ dpre,
         for (int kc = 0; kc < OC; ++kc)
 #pragma unroll
           for (int j = 0; j < 3; ++j)
-            load_row8<TD>(rs, hr[j] >= 0 ? base + hr[j] * RB + 32 * kc * (int)sizeof(TD) : kAbsent,
+            load_row8<TD>(rs, hr[j] >= 0 ? base + hr[j] * rstride + 32 * kc * (int)sizeof(TD) : kAbsent,
                           v[q][kc][j]);
       }
 #pragma unroll
@@ -168,11 +179,11 @@ __global__ __launch_bounds__(256) void conv_dx_b16(const TD* __restrict__ dpre,
 #pragma unroll
           for (int e = 0; e < 8; ++e) a8[e] = (v[q][kc][0][e] + v[q][kc][1][e]) + v[q][kc][2][e];
           if (hd[q].w >= 0) {  // 0.3 % of keys: list rows 3..
-            const TD* db_ = dpre + (long)b * rows * COUT + 32 * kc + 8 * g;
-            for (int e = 0; e < 8; ++e) a8[e] += ldf(&db_[(long)hd[q].w * COUT + e]);
+            const TD* db_ = dpre + (long)b * ld.bs * COUT + 32 * kc + 8 * g;
+            for (int e = 0; e < 8; ++e) a8[e] += ldf(&db_[(long)hd[q].w * ld.vs * COUT + e]);
             const long key = (long)u * kS + s;
             for (int p = inv_ptr[key] + CFSD_INV_HEAD; p < inv_ptr[key + 1]; ++p) {
-              const TD* rp = db_ + (long)inv_row[p] * COUT;
+              const TD* rp = db_ + (long)inv_row[p] * ld.vs * COUT;
               for (int e = 0; e < 8; ++e) a8[e] += ldf(&rp[e]);
             }
           }
@@ -244,7 +255,7 @@ __global__ __launch_bounds__(1024) void conv_dw_b16(const bf16_t* __restrict__ x
                                                     const int* __restrict__ idx,
                                                     const TD* __restrict__ dpre,
                                                     float* __restrict__ ws, int vsrc, int rows,
-                                                    long total_rows) {
+                                                    long total_rows, int batch, int xvm, int dpvm) {
   using C = DwB16Cfg<CIN, COUT>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(lds_raw);
@@ -260,6 +271,9 @@ __global__ __launch_bounds__(1024) void conv_dw_b16(const bf16_t* __restrict__ x
   for (int s = 0; s < kS; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float db_acc = 0.f;
 
+  // K (rows) is visited in x's layout: a vertex-major x tile is 2 vertices x
+  // 16 meshes, its gathered rows two contiguous 1-KiB blocks per slot
+  const Lay lx = make_lay(xvm, batch, vsrc), ldp = make_lay(dpvm, batch, rows);
   u32x4 xs[C::XPT], ds[C::DPT];
   auto load_tile = [&](long tile) {
     const long m0 = tile * 32;
@@ -271,8 +285,8 @@ __global__ __launch_bounds__(1024) void conv_dw_b16(const bf16_t* __restrict__ x
         long m = m0 + row;
         if (m >= total_rows) m = total_rows - 1;  // its dpre row is zero
         int b, r;
-        divmod32(m, rows, b, r);
-        xs[e] = ld8bf(x + ((long)b * vsrc + idx[r * kS + s]) * CIN + 8 * c8);
+        split_row(m, xvm, batch, rows, b, r);
+        xs[e] = ld8bf(x + ((long)b * lx.bs + (long)idx[r * kS + s] * lx.vs) * CIN + 8 * c8);
       }
     }
 #pragma unroll
@@ -281,7 +295,13 @@ __global__ __launch_bounds__(1024) void conv_dw_b16(const bf16_t* __restrict__ x
       if (f < C::DCH) {
         const int row = f / (COUT / 8), c8 = f - row * (COUT / 8);
         const long m = m0 + row;
-        ds[e] = m < total_rows ? ld8bf(dpre + m * COUT + 8 * c8) : (u32x4){0u, 0u, 0u, 0u};
+        long dr = m;
+        if (xvm != dpvm && m < total_rows) {
+          int b, r;
+          split_row(m, xvm, batch, rows, b, r);
+          dr = row_of(ldp, b, r);
+        }
+        ds[e] = m < total_rows ? ld8bf(dpre + dr * COUT + 8 * c8) : (u32x4){0u, 0u, 0u, 0u};
       }
     }
   };
@@ -349,26 +369,28 @@ static int blocks_resident(K kern, int threads, size_t lds) {
 
 template <int CIN, int COUT, int ACT, typename TY>
 static int fwd_t(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, TY* y,
-                 int vsrc, int rows, long M, hipStream_t st) {
+                 int vsrc, int rows, long M, int xvm, int yvm, hipStream_t st) {
   constexpr size_t lds = (size_t)COUT * (kS * CIN + 8) * sizeof(bf16_t);
   auto kern = conv_fwd_b16<CIN, COUT, ACT, TY>;
   const long tiles = (M + 15) / 16;
   const unsigned grid = balanced_blocks(tiles, 4, blocks_resident(kern, 256, lds));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, M);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, M,
+                     (int)(M / rows), xvm, yvm);
   return launch_status("spiral_conv_fwd_bf16");
 }
 
-int launch_fwd(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, void* y,
+int launch_fwd(const bf16_t* x, int xvm, const int* idx, const bf16_t* w, const float* bias, void* y,
                int y_dt, int vsrc, int rows, long M, int cin, int cout, int act, hipStream_t st) {
+  const int yvm = (y_dt & CFSD_VM) != 0;
 #define F(CI, CO)                                                                                   \
   if (cin == CI && cout == CO) {                                                                    \
-    if (y_dt == DT_BF16)                                                                            \
+    if (CFSD_DT_TYPE(y_dt) == DT_BF16)                                                              \
       return act == CFSD_ACT_ELU                                                                    \
-                 ? fwd_t<CI, CO, CFSD_ACT_ELU, bf16_t>(x, idx, w, bias, (bf16_t*)y, vsrc, rows, M, st) \
-                 : fwd_t<CI, CO, CFSD_ACT_NONE, bf16_t>(x, idx, w, bias, (bf16_t*)y, vsrc, rows, M, st); \
+                 ? fwd_t<CI, CO, CFSD_ACT_ELU, bf16_t>(x, idx, w, bias, (bf16_t*)y, vsrc, rows, M, xvm, yvm, st) \
+                 : fwd_t<CI, CO, CFSD_ACT_NONE, bf16_t>(x, idx, w, bias, (bf16_t*)y, vsrc, rows, M, xvm, yvm, st); \
     return act == CFSD_ACT_ELU                                                                      \
-               ? fwd_t<CI, CO, CFSD_ACT_ELU, float>(x, idx, w, bias, (float*)y, vsrc, rows, M, st)  \
-               : fwd_t<CI, CO, CFSD_ACT_NONE, float>(x, idx, w, bias, (float*)y, vsrc, rows, M, st); \
+               ? fwd_t<CI, CO, CFSD_ACT_ELU, float>(x, idx, w, bias, (float*)y, vsrc, rows, M, xvm, yvm, st)  \
+               : fwd_t<CI, CO, CFSD_ACT_NONE, float>(x, idx, w, bias, (float*)y, vsrc, rows, M, xvm, yvm, st); \
   }
   F(32, 32) F(32, 64) F(64, 32) F(64, 64)
 #undef F
@@ -378,26 +400,27 @@ int launch_fwd(const bf16_t* x, const int* idx, const bf16_t* w, const float* bi
 template <int CIN, int COUT, typename TD>
 static int dx_t(const TD* dpre, const int* inv_ptr, const int* inv_row, const int* inv_head,
                 const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int vsrc, int rows, long M,
-                hipStream_t st) {
+                int dpvm, int dxvm, hipStream_t st) {
   constexpr size_t lds = (size_t)kS * CIN * (COUT + 8) * sizeof(bf16_t);
   auto kern = conv_dx_b16<CIN, COUT, TD>;
   const long tiles = (M + 15) / 16;
   const unsigned grid = balanced_blocks(tiles, 4, blocks_resident(kern, 256, lds));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, dpre, inv_ptr, inv_row,
-                     (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M);
+                     (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M, (int)(M / vsrc), dpvm, dxvm);
   return launch_status("spiral_conv_bwd_data_bf16");
 }
 
 int launch_dx(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_row,
-              const int* inv_head, const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int vsrc,
+              const int* inv_head, const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int dxvm, int vsrc,
               int rows, long M, int cin, int cout, hipStream_t st) {
+  const int dpvm = (dpre_dt & CFSD_VM) != 0;
 #define D(CI, CO)                                                                                 \
   if (cin == CI && cout == CO)                                                                    \
-    return dpre_dt == DT_BF16                                                                     \
+    return CFSD_DT_TYPE(dpre_dt) == DT_BF16                                                       \
                ? dx_t<CI, CO, bf16_t>((const bf16_t*)dpre, inv_ptr, inv_row, inv_head, w, elu_y,  \
-                                      dx, vsrc, rows, M, st)                                      \
+                                      dx, vsrc, rows, M, dpvm, dxvm, st)                          \
                : dx_t<CI, CO, float>((const float*)dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, \
-                                     vsrc, rows, M, st);
+                                     vsrc, rows, M, dpvm, dxvm, st);
   D(32, 32) D(32, 64) D(64, 32) D(64, 64)
 #undef D
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_data (bf16): unsupported channels %d -> %d", cin, cout);
@@ -413,21 +436,22 @@ int dw_slabs(int batch, int rows, int cin, int cout) {
 
 template <int CIN, int COUT, typename TD>
 static int dw_t(const bf16_t* x, const int* idx, const TD* dpre, float* ws, int vsrc, int rows,
-                long M, hipStream_t st) {
+                long M, int xvm, int dpvm, hipStream_t st) {
   using C = DwB16Cfg<CIN, COUT>;
   const int gx = dw_slabs((int)(M / rows), rows, CIN, COUT);
   hipLaunchKernelGGL((conv_dw_b16<CIN, COUT, TD>), dim3(gx), dim3(C::THREADS), C::LDS, st, x, idx,
-                     dpre, ws, vsrc, rows, M);
+                     dpre, ws, vsrc, rows, M, (int)(M / rows), xvm, dpvm);
   return launch_status("spiral_conv_bwd_weight_bf16");
 }
 
-int launch_dw(const bf16_t* x, const int* idx, const void* dpre, int dpre_dt, float* ws, int vsrc,
+int launch_dw(const bf16_t* x, int xvm, const int* idx, const void* dpre, int dpre_dt, float* ws, int vsrc,
               int rows, long M, int cin, int cout, hipStream_t st) {
+  const int dpvm = (dpre_dt & CFSD_VM) != 0;
 #define W(CI, CO)                                                                                 \
   if (cin == CI && cout == CO)                                                                    \
-    return dpre_dt == DT_BF16                                                                     \
-               ? dw_t<CI, CO, bf16_t>(x, idx, (const bf16_t*)dpre, ws, vsrc, rows, M, st)          \
-               : dw_t<CI, CO, float>(x, idx, (const float*)dpre, ws, vsrc, rows, M, st);
+    return CFSD_DT_TYPE(dpre_dt) == DT_BF16                                                       \
+               ? dw_t<CI, CO, bf16_t>(x, idx, (const bf16_t*)dpre, ws, vsrc, rows, M, xvm, dpvm, st) \
+               : dw_t<CI, CO, float>(x, idx, (const float*)dpre, ws, vsrc, rows, M, xvm, dpvm, st);
   W(32, 32) W(32, 64) W(64, 32) W(64, 64)
 #undef W
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight (bf16): unsupported channels %d -> %d", cin, cout);

@@ -136,10 +136,12 @@ class SDVAEEngine:
                  w_lap=0.1, eta1=0.5, eta2=0.5, swap_bs=4, seed=0, device="cuda", precision="fp32"):
         """``precision``: "fp32" (the reference's arithmetic, the parity
         configuration) or "bf16" (configs C3/C5: the level-0/1 activations
-        and gradients -- the large tensors -- stored in bf16, their convs on
-        bf16 MFMA with the bf16 shadow of the fp32 master weights, fp32
-        accumulation; coarse levels, bottleneck, losses, gradients and Adam
-        stay fp32)."""
+        and gradients -- the large tensors -- stored in bf16 and VERTEX-MAJOR
+        (``ops.is_vm``: the 16 mesh rows of a vertex are one contiguous 1-KiB
+        block, so every spiral gather is a coalesced wave load), their convs
+        on bf16 MFMA with the bf16 shadow of the fp32 master weights, fp32
+        accumulation; the network input / output, coarse levels, bottleneck,
+        losses, gradients and Adam stay fp32 batch-major)."""
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
         self.precision = precision
@@ -322,7 +324,9 @@ class SDVAEEngine:
         lp = self.lp_levels
 
         def fl(level, *shape):  # storage of a level's activation / gradient
-            return torch.empty(shape, dtype=torch.bfloat16 if level in lp else torch.float32, device=dev)
+            if level in lp:  # bf16, vertex-major (ops.is_vm): a vertex's 16 mesh rows = one 1-KiB block
+                return ops.vm_empty(*shape, dtype=torch.bfloat16, device=dev)
+            return torch.empty(shape, dtype=torch.float32, device=dev)
 
         b = _Buffers()
         b.bsz = bsz
@@ -353,8 +357,8 @@ class SDVAEEngine:
         b.losses = f(5)
         # backward
         b.dout = f(bsz, nv[0], S.in_ch)
-        b.g_dec_up = [torch.empty_like(t) for t in b.dec_up]    # grad wrt dec_up (conv dx)
-        b.dpre_dec = [torch.empty_like(t) for t in b.dec_out]   # grad wrt pre-ELU dec conv
+        b.g_dec_up = [fl(lv, bsz, nv[lv], cin) for (cin, cout, lv, ui) in S.dec_layers()]   # grad wrt dec_up
+        b.dpre_dec = [fl(lv, bsz, nv[lv], cout) for (cin, cout, lv, ui) in S.dec_layers()]  # grad wrt pre-ELU
         b.dh = torch.empty_like(b.h)
         b.dz = f(bsz, lat)
         flat_out = self.num_vert * S.out_ch[-1]

@@ -47,6 +47,57 @@ def _needx(t, shape, name="tensor"):
     return _need(t, shape, t.dtype if t.dtype in _DTYPES else torch.float32, name)
 
 
+# ------------------------------------------------------------------ layouts
+VM = 0x10  # CFSD_VM: vertex-major storage flag of a *_dt argument (include/cfsd.h)
+
+
+def is_vm(t):
+    """True for a logical [B, V, C] view of a VERTEX-MAJOR [V, B, C] buffer
+    (``vm_empty`` / ``to_vm``): element (b, v, c) at (v*B + b)*C + c, the
+    rows of one vertex in every mesh of the batch contiguous."""
+    if t is None or t.dim() != 3 or t.is_contiguous():
+        return False
+    b, v, c = t.shape
+    return t.stride() == (c, b * c, 1)
+
+
+def vm_empty(bsz, nv, c, dtype=torch.float32, device="cuda"):
+    """Uninitialised vertex-major tensor, seen as [bsz, nv, c]."""
+    return torch.empty((nv, bsz, c), dtype=dtype, device=device).permute(1, 0, 2)
+
+
+def to_vm(t):
+    """Vertex-major copy of a [B, V, C] tensor (same logical values)."""
+    return t.transpose(0, 1).contiguous().transpose(0, 1)
+
+
+def _needl(t, shape, name="tensor", dtype=None):
+    """A mixed-precision [B, V, C] operand in either layout: batch-major
+    (contiguous) or vertex-major (``is_vm``)."""
+    if t is None:
+        raise ValueError(f"{name} is required")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    want = dtype if dtype is not None else (t.dtype if t.dtype in _DTYPES else torch.float32)
+    if t.dtype != want:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {want}")
+    if not (t.is_contiguous() or is_vm(t)):
+        raise ValueError(f"{name} must be contiguous (batch-major) or a vertex-major view")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+    return t
+
+
+def _st(t, name="tensor"):
+    """Storage descriptor of a mixed-precision operand: type | CFSD_VM."""
+    return _dt(t, name) | (VM if is_vm(t) else 0)
+
+
+def _same_layout(a, b, what):
+    if a is not None and b is not None and is_vm(a) != is_vm(b):
+        raise ValueError(f"{what} must share one layout")
+
+
 def _out(out, shape, like, name="out"):
     if out is None:
         return torch.empty(shape, dtype=torch.float32, device=like.device)
@@ -261,15 +312,16 @@ def spiral_conv_bwd_data_rowsub(dpre, flat, w, vsrc, elu_y=None, out=None, works
     _need(dpre, None, name="dpre")
     _need(table, (vsrc, width), torch.int32, "inv_flat")
     _need(w, (cout, 9 * cin), name="w")
-    _needx(out, (bsz, vsrc, cin), "out")
+    _needl(out, (bsz, vsrc, cin), "out")
     if elu_y is not None:
-        _need(elu_y, (bsz, vsrc, cin), out.dtype, "elu_y")
+        _needl(elu_y, (bsz, vsrc, cin), "elu_y", out.dtype)
+        _same_layout(out, elu_y, "out and elu_y")
     need = spiral_conv_bwd_data_rowsub_workspace(bsz, rows, 9, cin)
     if need == 0:
         raise ValueError(f"no row-subset backward for {cin} -> {cout} channels")
     ws, nb = _conv_ws(workspace, dpre.device, need)
     call("cfsd_spiral_conv_bwd_data_rowsub", ptr(dpre), ptr(table), width, ptr(w), ptr(elu_y), ptr(out),
-         _dt(out), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, 9, cin, cout, stream_ptr())
+         _st(out), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, 9, cin, cout, stream_ptr())
     return out
 
 
@@ -318,7 +370,7 @@ def _spmm_uniform(k, col, val, x, elu_y, y, bsz, m, n, c):
     """cfsd_spmm_uniform: every row holds exactly ``k`` entries."""
     if col.numel() != m * k:
         raise ValueError(f"uniform SpMM: {col.numel()} entries != {m} rows x {k}")
-    call("cfsd_spmm_uniform", int(k), ptr(col), ptr(val), ptr(x), _dt(x), ptr(elu_y), ptr(y), _dt(y),
+    call("cfsd_spmm_uniform", int(k), ptr(col), ptr(val), ptr(x), _st(x), ptr(elu_y), ptr(y), _st(y),
          bsz, m, n, c, stream_ptr())
 
 
@@ -329,15 +381,15 @@ def _spmm_sched_csr(sched, x, elu_y, y, bsz, m, n, c):
     _need(rows_s, (m,), torch.int32, "rows_s")
     _need(col_s, None, torch.int32, "col_s")
     _need(val_s, (col_s.numel(),), name="val_s")
-    call("cfsd_spmm_sched_csr", ptr(ptr_s), ptr(col_s), ptr(val_s), ptr(rows_s), ptr(x), _dt(x), ptr(elu_y),
-         ptr(y), _dt(y), bsz, m, n, c, stream_ptr())
+    call("cfsd_spmm_sched_csr", ptr(ptr_s), ptr(col_s), ptr(val_s), ptr(rows_s), ptr(x), _st(x), ptr(elu_y),
+         ptr(y), _st(y), bsz, m, n, c, stream_ptr())
 
 
 def _spmm_sched(row_ptr, col, val, order, x, elu_y, y, bsz, m, n, c):
     """cfsd_spmm_csr_sched: rows visited in ``order`` (``topology.row_schedule``)."""
     _need(order, (m,), torch.int32, "order")
-    call("cfsd_spmm_csr_sched", ptr(row_ptr), ptr(col), ptr(val), ptr(order), ptr(x), _dt(x),
-         ptr(elu_y), ptr(y), _dt(y), bsz, m, n, c, stream_ptr())
+    call("cfsd_spmm_csr_sched", ptr(row_ptr), ptr(col), ptr(val), ptr(order), ptr(x), _st(x),
+         ptr(elu_y), ptr(y), _st(y), bsz, m, n, c, stream_ptr())
 
 
 def swap_features(x_all, batch_idx, region_mask, key, bs, out=None):
@@ -648,16 +700,16 @@ def spiral_conv_fwd_x(x, idx, w, w_bf16, b, act, out):
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape
     cout = w.shape[0]
-    _needx(x, None, "x")
+    _needl(x, None, "x")
     _need(idx, (rows, seq), torch.int32, "idx")
     _need(w, (cout, seq * cin), name="w")
     if w_bf16 is not None:
         _need(w_bf16, (cout, seq * cin), torch.bfloat16, "w_bf16")
     if b is not None:
         _need(b, (cout,), name="bias")
-    _needx(out, (bsz, rows, cout), "out")
-    call("cfsd_spiral_conv_fwd_x", ptr(x), _dt(x), ptr(idx), ptr(w), ptr(w_bf16), ptr(b), ptr(out),
-         _dt(out), bsz, vsrc, rows, seq, cin, cout, act, stream_ptr())
+    _needl(out, (bsz, rows, cout), "out")
+    call("cfsd_spiral_conv_fwd_x", ptr(x), _st(x), ptr(idx), ptr(w), ptr(w_bf16), ptr(b), ptr(out),
+         _st(out), bsz, vsrc, rows, seq, cin, cout, act, stream_ptr())
     return out
 
 
@@ -666,18 +718,19 @@ def spiral_conv_bwd_data_x(dpre, inv, w_bf16, vsrc, elu_y=None, out=None):
     inv_ptr, inv_row, inv_head = inv
     seq = (inv_ptr.numel() - 1) // vsrc
     cin = w_bf16.shape[1] // seq
-    _needx(dpre, None, "dpre")
+    _needl(dpre, None, "dpre")
     _need(inv_ptr, (vsrc * seq + 1,), torch.int32, "inv_ptr")
     _need(inv_row, (rows * seq,), torch.int32, "inv_row")
     _need(inv_head, (vsrc * seq, INV_HEAD), torch.int32, "inv_head")
     _need(w_bf16, (cout, seq * cin), torch.bfloat16, "w_bf16")
-    if elu_y is not None:
-        _need(elu_y, (bsz, vsrc, cin), torch.bfloat16, "elu_y")
     if out is None:
         out = torch.empty((bsz, vsrc, cin), dtype=torch.bfloat16, device=dpre.device)
-    _need(out, (bsz, vsrc, cin), torch.bfloat16, "dx")
-    call("cfsd_spiral_conv_bwd_data_x", ptr(dpre), _dt(dpre), ptr(inv_ptr), ptr(inv_row), ptr(inv_head),
-         ptr(w_bf16), ptr(elu_y), ptr(out), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    _needl(out, (bsz, vsrc, cin), "dx", torch.bfloat16)
+    if elu_y is not None:
+        _needl(elu_y, (bsz, vsrc, cin), "elu_y", torch.bfloat16)
+        _same_layout(out, elu_y, "dx and elu_y")
+    call("cfsd_spiral_conv_bwd_data_x", ptr(dpre), _st(dpre), ptr(inv_ptr), ptr(inv_row), ptr(inv_head),
+         ptr(w_bf16), ptr(elu_y), ptr(out), _st(out), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
     return out
 
 
@@ -691,9 +744,9 @@ def spiral_conv_bwd_weight_x(x, idx, dpre, dw, db, workspace):
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape
     cout = dpre.shape[2]
-    _needx(x, None, "x")
+    _needl(x, None, "x")
     _need(idx, (rows, seq), torch.int32, "idx")
-    _needx(dpre, (bsz, rows, cout), "dpre")
+    _needl(dpre, (bsz, rows, cout), "dpre")
     if dw is not None or db is not None:
         _need(dw, (cout, seq * cin), name="dw")
         _need(db, (cout,), name="db")
@@ -702,7 +755,7 @@ def spiral_conv_bwd_weight_x(x, idx, dpre, dw, db, workspace):
     nbytes = workspace.numel() * workspace.element_size()
     if nbytes < need:
         raise ValueError(f"workspace {nbytes} < {need} bytes")
-    call("cfsd_spiral_conv_bwd_weight_x", ptr(x), _dt(x), ptr(idx), ptr(dpre), _dt(dpre), ptr(dw), ptr(db),
+    call("cfsd_spiral_conv_bwd_weight_x", ptr(x), _st(x), ptr(idx), ptr(dpre), _st(dpre), ptr(dw), ptr(db),
          ptr(workspace), ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
     if dw is None:
         mfma = cin in (32, 64) and cout in (32, 64)
@@ -716,20 +769,22 @@ def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspa
     rows, seq = idx.shape
     cout = dpre.shape[2]
     inv_ptr, inv_row, inv_head = inv
-    _need(x, None, torch.bfloat16, "x")
+    _needl(x, None, "x", torch.bfloat16)
     _need(idx, (rows, seq), torch.int32, "idx")
-    _need(dpre, (bsz, rows, cout), name="dpre")
+    _needl(dpre, (bsz, rows, cout), "dpre", torch.float32)
     _need(inv_head, (vsrc * seq, INV_HEAD), torch.int32, "inv_head")
     _need(w, (cout, seq * cin), name="w")
     if dx is not None:
-        _need(dx, (bsz, vsrc, cin), torch.bfloat16, "dx")
+        _needl(dx, (bsz, vsrc, cin), "dx", torch.bfloat16)
+        _same_layout(x, dx, "x and dx")
     if elu_y is not None:
-        _need(elu_y, (bsz, vsrc, cin), torch.bfloat16, "elu_y")
+        _needl(elu_y, (bsz, vsrc, cin), "elu_y", torch.bfloat16)
+        _same_layout(x, elu_y, "x and elu_y")
     if dw is not None or db is not None:
         _need(dw, (cout, seq * cin), name="dw")
         _need(db, (cout,), name="db")
     ws, nb = _conv_ws(workspace, x.device, spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout))
-    call("cfsd_spiral_conv_bwd_x", ptr(x), DT_BF16, ptr(idx), ptr(dpre), ptr(inv_ptr), ptr(inv_row),
+    call("cfsd_spiral_conv_bwd_x", ptr(x), _st(x), ptr(idx), ptr(dpre), _st(dpre), ptr(inv_ptr), ptr(inv_row),
          ptr(inv_head), ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb),
          bsz, vsrc, rows, seq, cin, cout, stream_ptr())
     if dw is None:
@@ -741,13 +796,14 @@ def spmm_x(csr, x, m, elu_y=None, out=None, order=None, uniform=0, sched=None):
     """Pool SpMM with fp32 or bf16 operands (fp32 sums, file order)."""
     row_ptr, col, val = csr
     bsz, n, c = x.shape
-    _needx(x, None, "x")
+    _needl(x, None, "x")
     _need(row_ptr, (m + 1,), torch.int32, "row_ptr")
     _need(col, None, torch.int32, "col")
     _need(val, (col.numel(),), name="val")
-    _needx(out, (bsz, m, c), "out")
+    _needl(out, (bsz, m, c), "out")
     if elu_y is not None:
-        _need(elu_y, (bsz, m, c), out.dtype, "elu_y")
+        _needl(elu_y, (bsz, m, c), "elu_y", out.dtype)
+        _same_layout(out, elu_y, "out and elu_y")
     if sched is not None:
         _spmm_sched_csr(sched, x, elu_y, out, bsz, m, n, c)
         return out
@@ -757,6 +813,6 @@ def spmm_x(csr, x, m, elu_y=None, out=None, order=None, uniform=0, sched=None):
     if uniform:
         _spmm_uniform(uniform, col, val, x, elu_y, out, bsz, m, n, c)
         return out
-    call("cfsd_spmm_csr_x", ptr(row_ptr), ptr(col), ptr(val), ptr(x), _dt(x), ptr(elu_y), ptr(out),
-         _dt(out), bsz, m, n, c, stream_ptr())
+    call("cfsd_spmm_csr_x", ptr(row_ptr), ptr(col), ptr(val), ptr(x), _st(x), ptr(elu_y), ptr(out),
+         _st(out), bsz, m, n, c, stream_ptr())
     return out

@@ -41,6 +41,18 @@ extern "C" {
  * (bf16) entry points: fp32, or bfloat16 as raw uint16 (torch.bfloat16 bits). */
 #define CFSD_DT_F32 0
 #define CFSD_DT_BF16 1
+/* Storage flag OR-ed into a *_dt argument of the mixed-precision entry points
+ * (ABI 4.0): the operand is VERTEX-MAJOR.  A logical [batch, nv, c] tensor
+ * then has element (b, v, k) at ((size_t)v * batch + b) * c + k, so the rows
+ * of one vertex in every mesh of the batch are one contiguous block (torch:
+ * an empty [nv, batch, c] tensor viewed through .permute(1, 0, 2)).  Without
+ * the flag: batch-major, (b * nv + v) * c + k (the reference's [B, V, C]).
+ * Each operand's layout is independent (e.g. E1 reads a vertex-major level-1
+ * tensor and writes a batch-major level-2 one); results do not depend on the
+ * layout.  Where one descriptor covers several operands, the entry point says
+ * so. */
+#define CFSD_VM 0x10
+#define CFSD_DT_TYPE(dt) ((dt) & 0xf)
 
 /* ABI version: (major << 16) | minor. */
 int cfsd_version(void);
@@ -366,12 +378,13 @@ int cfsd_scale(float* y, size_t n, float alpha, void* stream);
 int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* idx, const float* w,
                            const uint16_t* w_bf16, const float* bias, void* y, int y_dt, int batch,
                            int vsrc, int rows, int seq, int cin, int cout, int act, void* stream);
-/* dx (bf16) of a 32/64-channel layer; dpre bf16 or fp32; elu_y bf16 or NULL. */
+/* dx (bf16) of a 32/64-channel layer; dpre bf16 or fp32; elu_y bf16 or NULL.
+ * dx_dt = CFSD_DT_BF16 [| CFSD_VM] (the layout of dx and elu_y). */
 int cfsd_spiral_conv_bwd_data_x(const void* dpre, int dpre_dt, const int32_t* inv_ptr,
                                 const int32_t* inv_row, const int32_t* inv_head,
                                 const uint16_t* w_bf16, const uint16_t* elu_y, uint16_t* dx,
-                                int batch, int vsrc, int rows, int seq, int cin, int cout,
-                                void* stream);
+                                int dx_dt, int batch, int vsrc, int rows, int seq, int cin,
+                                int cout, void* stream);
 /* dW/db (fp32): 32/64-channel layers (x bf16, dpre bf16/fp32) and the xyz
  * input layer (x fp32, dpre bf16).  dw == db == NULL defers the reduction
  * (cfsd_dw_reduce_batch item with fused = 2 for the 32/64-channel kind, 0
@@ -383,9 +396,10 @@ int cfsd_spiral_conv_bwd_weight_x(const void* x, int x_dt, const int32_t* idx, c
                                   int cin, int cout, void* stream);
 /* Fused dx + dW of the xyz output layer (cout*seq <= 32) with x, elu_y, dx
  * bf16 and dpre fp32 (workspace: cfsd_spiral_conv_bwd_workspace; deferred
- * items use fused = 1). */
+ * items use fused = 1).  x_dt's CFSD_VM flag is the layout of x, elu_y and
+ * dx; dpre_dt = CFSD_DT_F32 [| CFSD_VM]. */
 int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* idx, const float* dpre,
-                           const int32_t* inv_ptr, const int32_t* inv_row, const int32_t* inv_head,
+                           int dpre_dt, const int32_t* inv_ptr, const int32_t* inv_row, const int32_t* inv_head,
                            const float* w, const void* elu_y, void* dx, float* dw, float* db,
                            float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows,
                            int seq, int cin, int cout, void* stream);

@@ -49,6 +49,16 @@ def err_rel_max(got, ref):
     return float((got - ref).abs().max() / (ref.abs().max() + 1e-30))
 
 
+def lay(ops, t, vm):
+    """The operand in the requested layout: batch-major (contiguous) or
+    vertex-major (CFSD_VM, ``ops.to_vm``) -- same logical values."""
+    return ops.to_vm(t) if vm else t.contiguous()
+
+
+def empty(ops, shape, dtype, vm):
+    return ops.vm_empty(*shape, dtype=dtype, device=DEV) if vm else torch.empty(shape, dtype=dtype, device=DEV)
+
+
 def gather(x, sp):
     idx = torch.as_tensor(sp, dtype=torch.long)
     return torch.index_select(x, 1, idx.reshape(-1)).view(x.shape[0], idx.shape[0], -1)
@@ -59,10 +69,18 @@ MFMA_CASES = [(32, 32, 0, 2), (32, 32, 1, 16), (32, 32, 3, 3), (32, 64, 2, 3), (
               (64, 64, 3, 2)]
 
 
+# layouts of (x, y): batch-major / vertex-major / mixed (E1 reads a
+# vertex-major level-1 tensor and writes a batch-major level-2 one)
+LAYOUTS = [(False, False), (True, True), (True, False), (False, True)]
+
+
 @pytest.mark.parametrize("cin,cout,level,bsz", MFMA_CASES)
 @pytest.mark.parametrize("act", [0, 1])
 @pytest.mark.parametrize("out_bf16", [True, False])
-def test_conv_fwd_bf16(mods, otopo, dtopo, cin, cout, level, bsz, act, out_bf16):
+@pytest.mark.parametrize("xvm,yvm", LAYOUTS)
+def test_conv_fwd_bf16(mods, otopo, dtopo, cin, cout, level, bsz, act, out_bf16, xvm, yvm):
+    """Also: every layout gives the bit-identical result (same per-output
+    MFMA K order; only the addressing differs)."""
     _, ops, _ = mods
     g = torch.Generator().manual_seed(cin + cout + level + act)
     sp = otopo.spirals[level]
@@ -73,20 +91,28 @@ def test_conv_fwd_bf16(mods, otopo, dtopo, cin, cout, level, bsz, act, out_bf16)
     ref = gather(rb(x), sp) @ rb(w).T + b.double()
     if act:
         ref = torch.nn.functional.elu(ref)
-    out = torch.empty(bsz, v, cout, dtype=BF if out_bf16 else torch.float32, device=DEV)
-    ops.spiral_conv_fwd_x(x.to(BF).to(DEV), dtopo.spiral[level], w.to(DEV), w.to(BF).to(DEV), b.to(DEV),
-                          act, out)
+    odt = BF if out_bf16 else torch.float32
+    out = empty(ops, (bsz, v, cout), odt, yvm)
+    assert ops.is_vm(out) == (yvm and bsz > 1)
+    args = (dtopo.spiral[level], w.to(DEV), w.to(BF).to(DEV), b.to(DEV), act)
+    ops.spiral_conv_fwd_x(lay(ops, x.to(BF).to(DEV), xvm), *args, out)
     tol = 2.0 ** -8 if out_bf16 else 1e-5
     assert err_rel_max(out.float(), ref) <= tol
+    if xvm or yvm:
+        base = torch.empty(bsz, v, cout, dtype=odt, device=DEV)
+        ops.spiral_conv_fwd_x(x.to(BF).to(DEV), *args, base)
+        assert torch.equal(out, base)
 
 
 @pytest.mark.parametrize("table,cin,cout,level,bsz", [("dec", 32, 32, 0, 2), ("dec", 32, 32, 1, 16),
                                                       ("enc", 32, 32, 1, 16), ("dec", 64, 32, 2, 3),
                                                       ("dec", 32, 64, 3, 3), ("dec", 64, 64, 2, 2)])
 @pytest.mark.parametrize("dpre_f32", [False, True])
-def test_conv_bwd_bf16(mods, otopo, dtopo, table, cin, cout, level, bsz, dpre_f32):
+@pytest.mark.parametrize("xvm,dpvm", [(False, False), (True, True), (True, False)])
+def test_conv_bwd_bf16(mods, otopo, dtopo, table, cin, cout, level, bsz, dpre_f32, xvm, dpvm):
     """dx (bf16, with elu') and dW/db (fp32) of the bf16 MFMA kernels, on the
-    full spiral table and on the Enblock row subset (E1's shape)."""
+    full spiral table and on the Enblock row subset (E1's shape), with x /
+    dx / elu_y and dpre in either layout (dx bit-identical across layouts)."""
     _, ops, _ = mods
     g = torch.Generator().manual_seed(5 + cin + cout + level)
     sp = otopo.spirals[level]
@@ -109,10 +135,15 @@ def test_conv_bwd_bf16(mods, otopo, dtopo, table, cin, cout, level, bsz, dpre_f3
     wl = wb.clone().requires_grad_()
     bl = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
     (gather(yb, sp) @ wl.T + bl).backward(rb(dpre))
-    dpre_dev = (dpre if dpre_f32 else dpre.to(BF)).to(DEV)
-    y_dev = y.to(BF).to(DEV)
-    dx = ops.spiral_conv_bwd_data_x(dpre_dev, inv, w.to(BF).to(DEV), vsrc, elu_y=y_dev)
+    dpre_dev = lay(ops, (dpre if dpre_f32 else dpre.to(BF)).to(DEV), dpvm)
+    y_dev = lay(ops, y.to(BF).to(DEV), xvm)
+    dx = empty(ops, (bsz, vsrc, cin), BF, xvm)
+    ops.spiral_conv_bwd_data_x(dpre_dev, inv, w.to(BF).to(DEV), vsrc, elu_y=y_dev, out=dx)
     assert err_rel_max(dx.float(), dx_ref) <= 1e-2
+    if xvm or dpvm:
+        base = ops.spiral_conv_bwd_data_x(dpre_dev.contiguous(), inv, w.to(BF).to(DEV), vsrc,
+                                          elu_y=y_dev.contiguous())
+        assert torch.equal(dx, base)
     dw = torch.empty(cout, 9 * cin, device=DEV)
     db = torch.empty(cout, device=DEV)
     ws = torch.empty(ops.spiral_conv_bwd_weight_x_workspace(bsz, rows, 9, cin, cout) // 4 + 1, device=DEV)
@@ -131,7 +162,10 @@ def test_conv_bwd_bf16(mods, otopo, dtopo, table, cin, cout, level, bsz, dpre_f3
                                                        (0, "upT", True, True), (1, "upT", True, False),
                                                        (2, "down", True, True)])
 @pytest.mark.parametrize("with_elu", [False, True])
-def test_spmm_bf16_bit_exact(mods, otopo, dtopo, level, kind, x_bf16, y_bf16, with_elu):
+@pytest.mark.parametrize("xvm,yvm", LAYOUTS)
+def test_spmm_bf16_bit_exact(mods, otopo, dtopo, level, kind, x_bf16, y_bf16, with_elu, xvm, yvm):
+    """Bit-exact in every layout and in each of the step's SpMM forms (CSR,
+    uniform-row, visiting-order CSR)."""
     _, ops, _ = mods
     g = torch.Generator().manual_seed(level * 3 + len(kind))
     coo = otopo.up[level] if kind != "down" else otopo.down[level]
@@ -150,19 +184,30 @@ def test_spmm_bf16_bit_exact(mods, otopo, dtopo, level, kind, x_bf16, y_bf16, wi
     if with_elu:
         eyq = ey.to(BF).float() if y_bf16 else ey
         ref = ref * torch.where(eyq > 0, torch.ones_like(eyq), eyq + 1.0)
-    out = torch.empty(4, m, 32, dtype=BF if y_bf16 else torch.float32, device=DEV)
-    xd = (x.to(BF) if x_bf16 else x).to(DEV)
-    eyd = (ey.to(BF) if y_bf16 else ey).to(DEV) if with_elu else None
-    ops.spmm_x(csr, xd, m, elu_y=eyd, out=out)
+    ydt = BF if y_bf16 else torch.float32
+    xd = lay(ops, (x.to(BF) if x_bf16 else x).to(DEV), xvm)
+    eyd = lay(ops, (ey.to(BF) if y_bf16 else ey).to(DEV), yvm) if with_elu else None
     exp = ref.to(BF) if y_bf16 else ref
-    assert torch.equal(out.cpu(), exp)
+    forms = [{}]
+    if kind == "up":
+        forms.append({"uniform": dtopo.up_uniform[level]})
+    if kind == "upT":
+        forms.append({"sched": dtopo.upT_sched[level]})
+    for f in forms:
+        if not all(f.values()):
+            continue
+        out = empty(ops, (4, m, 32), ydt, yvm)
+        ops.spmm_x(csr, xd, m, elu_y=eyd, out=out, **f)
+        assert torch.equal(out.cpu(), exp), f
 
 
 @pytest.mark.parametrize("bsz", [2, 16])
-def test_xyz_layers_bf16(mods, otopo, dtopo, bsz):
+@pytest.mark.parametrize("vm", [False, True])
+def test_xyz_layers_bf16(mods, otopo, dtopo, bsz, vm):
     """The xyz layers of the bf16 step: input conv (fp32 x -> bf16 y) and
     its dW with bf16 dpre; output conv (bf16 x -> fp32 y) and its fused
-    dx (bf16) + dW."""
+    dx (bf16) + dW.  ``vm``: the 32-channel operands vertex-major (the
+    step's layout), the xyz tensors batch-major."""
     _, ops, _ = mods
     g = torch.Generator().manual_seed(bsz)
     sp0 = otopo.spirals[0]
@@ -171,13 +216,13 @@ def test_xyz_layers_bf16(mods, otopo, dtopo, bsz):
     w0 = torch.randn(32, 27, generator=g) * 0.1
     b0 = torch.randn(32, generator=g) * 0.1
     ref = torch.nn.functional.elu(gather(x.double(), sp0[sel]) @ w0.double().T + b0.double())
-    y = torch.empty(bsz, len(sel), 32, dtype=BF, device=DEV)
+    y = empty(ops, (bsz, len(sel), 32), BF, vm)
     ops.spiral_conv_fwd_x(x.to(DEV), dtopo.enc_rows[0], w0.to(DEV), None, b0.to(DEV), 1, y)
     assert err_rel_max(y.float(), ref) <= 2.0 ** -8
     dpre = torch.randn(bsz, len(sel), 32, generator=g)
     dw, db = torch.empty(32, 27, device=DEV), torch.empty(32, device=DEV)
     ws = torch.empty(ops.spiral_conv_bwd_weight_x_workspace(bsz, len(sel), 9, 3, 32) // 4 + 1, device=DEV)
-    ops.spiral_conv_bwd_weight_x(x.to(DEV), dtopo.enc_rows[0], dpre.to(BF).to(DEV), dw, db, ws)
+    ops.spiral_conv_bwd_weight_x(x.to(DEV), dtopo.enc_rows[0], lay(ops, dpre.to(BF).to(DEV), vm), dw, db, ws)
     gx = gather(x.double(), sp0[sel])
     assert err_rel_max(dw, torch.einsum("bro,brk->ok", rb(dpre), gx)) <= 1e-5
     assert err_rel_max(db, rb(dpre).sum((0, 1))) <= 1e-5
@@ -186,7 +231,7 @@ def test_xyz_layers_bf16(mods, otopo, dtopo, bsz):
     w5 = torch.randn(3, 288, generator=g) * 0.1
     b5 = torch.randn(3, generator=g) * 0.1
     out = torch.empty(bsz, sp0.shape[0], 3, device=DEV)
-    hd = h.to(BF).to(DEV)
+    hd = lay(ops, h.to(BF).to(DEV), vm)
     ops.spiral_conv_fwd_x(hd, dtopo.spiral[0], w5.to(DEV), None, b5.to(DEV), 0, out)
     hl = rb(h).requires_grad_()
     wl = w5.double().requires_grad_()
@@ -196,7 +241,7 @@ def test_xyz_layers_bf16(mods, otopo, dtopo, bsz):
     dout = torch.randn(ref.shape, generator=g)
     ref.backward(dout.double())
     dx_ref = hl.grad * torch.where(rb(h) > 0, 1.0, rb(h) + 1.0)
-    dx = torch.empty(bsz, sp0.shape[0], 32, dtype=BF, device=DEV)
+    dx = empty(ops, (bsz, sp0.shape[0], 32), BF, vm)
     dw, db = torch.empty(3, 288, device=DEV), torch.empty(3, device=DEV)
     ops.spiral_conv_bwd_x(hd, dtopo.spiral[0], dout.to(DEV), dtopo.spiral_inv[0], w5.to(DEV), dw, db,
                           dx=dx, elu_y=hd)

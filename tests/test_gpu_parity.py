@@ -787,6 +787,10 @@ def test_rowsub_data_bf16_storage(dtopo, level, cout):
     ops.spiral_conv_bwd_data_rowsub(dpre, dtopo.enc_flat[level], w, v, elu_y=ey16.float(), out=d32)
     ops.spiral_conv_bwd_data_rowsub(dpre, dtopo.enc_flat[level], w, v, elu_y=ey16, out=d16)
     assert torch.equal(d16, d32.to(torch.bfloat16))
+    # vertex-major dx / elu_y (the bf16 step's E1 layout): the same values
+    dvm = ops.vm_empty(bsz, v, 32, dtype=torch.bfloat16, device=DEV)
+    ops.spiral_conv_bwd_data_rowsub(dpre, dtopo.enc_flat[level], w, v, elu_y=ops.to_vm(ey16), out=dvm)
+    assert ops.is_vm(dvm) and torch.equal(dvm, d16)
     # and the fp32 dx equals the fused rowsub backward's dx
     x = torch.randn(bsz, v, 32, generator=g).to(DEV)
     dxf = torch.empty_like(d32)

@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_version_and_error_reporting(lib):
-    assert lib.cfsd_version() >> 16 == 3  # 3.0: per-epoch shuffle, bf16 path
+    assert lib.cfsd_version() >> 16 == 4  # 4.0: CFSD_VM vertex-major operands
     # argument validation happens before any HIP call: safe without a GPU
     rc = lib.cfsd_spiral_conv_fwd(None, None, None, None, None, None, 0, 1, 1, 1, 9, 32, 32, 0, None)
     assert rc == -1

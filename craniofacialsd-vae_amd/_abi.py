@@ -63,6 +63,7 @@ SIGNATURES = {
     "cfsd_adam": (_I, [_P, _P, _P, _P, _P, _Z, _F, _F, _F, _F, _F, _P, _P]),
     "cfsd_spiral_conv_fwd_x": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_data_x": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "cfsd_spiral_conv_bwd_data_flat": (_I, [_P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_weight_x_workspace": (_Z, [_I, _I, _I, _I, _I]),
     "cfsd_spiral_conv_bwd_weight_x": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_x": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I,

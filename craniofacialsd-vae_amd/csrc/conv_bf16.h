@@ -28,5 +28,17 @@ int dw_slabs(int batch, int rows, int cin, int cout);
 int launch_dw(const bf16_t* x, int xvm, const int* idx, const void* dpre, int dpre_dt, float* ws, int vsrc,
               int rows, long total_rows, int cin, int cout, hipStream_t st);
 
+// Vertex-major operands with batch % 16 == 0 (spiral_conv_vm16.hip): one
+// 16-row MFMA tile = one vertex x 16 meshes.
+bool vm16_ok(int batch, int cin, int cout);
+int launch_fwd_vm16(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, void* y, int y_dt,
+                    int vsrc, int rows, int batch, int cin, int cout, int act, hipStream_t st);
+int launch_dx_vm16(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_row, const int* inv_head,
+                   const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int vsrc, int rows, int batch, int cin,
+                   int cout, hipStream_t st);
+int launch_dx_flat_vm16(const void* dpre, int dpre_dt, const int* flat, int width, const bf16_t* w,
+                        const bf16_t* elu_y, bf16_t* dx, int vsrc, int rows, int batch, int cin, int cout,
+                        hipStream_t st);
+
 }  // namespace bf
 }  // namespace cfsd

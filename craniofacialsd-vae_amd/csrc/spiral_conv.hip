@@ -2919,6 +2919,25 @@ extern "C" int cfsd_spiral_conv_bwd_data_x(const void* dpre, int dpre_dt, const 
                        cin, cout, (hipStream_t)stream);
 }
 
+extern "C" int cfsd_spiral_conv_bwd_data_flat(const void* dpre, int dpre_dt, const int32_t* inv_flat,
+                                              int flat_width, const uint16_t* w_bf16, const uint16_t* elu_y,
+                                              uint16_t* dx, int dx_dt, int batch, int vsrc, int rows, int seq,
+                                              int cin, int cout, void* stream) {
+  int rc = check_conv_args(dpre, inv_flat, w_bf16, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!dx) return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat: null dx");
+  if (!dt_ok(dpre_dt) || !dt_ok(dx_dt) || CFSD_DT_TYPE(dx_dt) != CFSD_DT_BF16 || !vm_of(dpre_dt) || !vm_of(dx_dt))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat: dpre and dx must be vertex-major (CFSD_VM), dx bf16");
+  if (!bf::vm16_ok(batch, cin, cout))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat: batch %% 16 == 0 and 32 -> 32/64 channels only");
+  if ((uintptr_t)inv_flat & 15) return set_error(CFSD_EINVAL, "inv_flat must be 16-B aligned");
+  if ((long)batch * rows * cout * (CFSD_DT_TYPE(dpre_dt) == CFSD_DT_F32 ? 4L : 2L) >= (long)kAbsentRow)
+    return set_error(CFSD_EINVAL, "dpre exceeds 32-bit buffer offsets");
+  return bf::launch_dx_flat_vm16(dpre, dpre_dt, inv_flat, flat_width, (const bf16_t*)w_bf16,
+                                 (const bf16_t*)elu_y, (bf16_t*)dx, vsrc, rows, batch, cin, cout,
+                                 (hipStream_t)stream);
+}
+
 extern "C" size_t cfsd_spiral_conv_bwd_weight_x_workspace(int batch, int rows, int seq, int cin,
                                                           int cout) {
   if (batch <= 0 || rows <= 0 || seq != kSeq || cin <= 0 || cout <= 0) return 0;

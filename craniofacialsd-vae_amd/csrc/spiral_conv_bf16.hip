@@ -382,6 +382,8 @@ static int fwd_t(const bf16_t* x, const int* idx, const bf16_t* w, const float* 
 int launch_fwd(const bf16_t* x, int xvm, const int* idx, const bf16_t* w, const float* bias, void* y,
                int y_dt, int vsrc, int rows, long M, int cin, int cout, int act, hipStream_t st) {
   const int yvm = (y_dt & CFSD_VM) != 0;
+  if (xvm && vm16_ok((int)(M / rows), cin, cout))
+    return launch_fwd_vm16(x, idx, w, bias, y, y_dt, vsrc, rows, (int)(M / rows), cin, cout, act, st);
 #define F(CI, CO)                                                                                   \
   if (cin == CI && cout == CO) {                                                                    \
     if (CFSD_DT_TYPE(y_dt) == DT_BF16)                                                              \
@@ -414,6 +416,9 @@ int launch_dx(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_
               const int* inv_head, const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int dxvm, int vsrc,
               int rows, long M, int cin, int cout, hipStream_t st) {
   const int dpvm = (dpre_dt & CFSD_VM) != 0;
+  if (dxvm && dpvm && vm16_ok((int)(M / vsrc), cin, cout))
+    return launch_dx_vm16(dpre, dpre_dt, inv_ptr, inv_row, inv_head, w, elu_y, dx, vsrc, rows, (int)(M / vsrc),
+                          cin, cout, st);
 #define D(CI, CO)                                                                                 \
   if (cin == CI && cout == CO)                                                                    \
     return CFSD_DT_TYPE(dpre_dt) == DT_BF16                                                       \

@@ -1,0 +1,495 @@
+// SpiralConv forward / data gradient on bf16 MFMA for VERTEX-MAJOR operands
+// (CFSD_VM) with a batch that is a multiple of 16 -- the bf16 step's level-0/1
+// layers (configs C3/C5: 16 meshes per GPU).
+//
+// Reference: SpiralConv.forward (model.py:27-41) and the autograd of its
+// index_select / Linear (model.py:34, 40).
+//
+// Vertex-major storage puts the 16 mesh rows of one vertex side by side, so a
+// 16-row MFMA tile is ONE vertex x 16 meshes: every spiral index is the same
+// for the whole wave (scalar loads, scalar buffer offsets: no per-lane index
+// or address arithmetic), and every neighbour gather is one contiguous 1-KiB
+// wave load (16 meshes x 32 bf16 channels).  The MFMA runs transposed,
+// D^T[channel][mesh] = W . X^T, with the weight rows permuted in LDS so that a
+// lane's accumulators are 4*NT CONSECUTIVE output channels of one mesh: the
+// epilogue stores 16-B (bf16) / 32-B (fp32) vectors, a whole output block per
+// wave instruction group, instead of 2-byte scalars.  Persistent waves walk an
+// XCD-contiguous vertex range with the next tile's gathers in flight during
+// the current tile's MFMAs.
+//
+// Same products in the same K order per output as conv_fwd_b16 / conv_dx_b16
+// (spiral_conv_bf16.hip); the MFMA runs in the transposed orientation and the
+// ELU uses the hardware exp (elu_fast), so results agree with those kernels to
+// fp32 rounding, not bit for bit.
+#include "conv_bf16.h"
+
+namespace cfsd {
+namespace bf {
+
+namespace {
+constexpr int kS = 9;
+constexpr int kAbsent = 0x7ffff000;  // out-of-range buffer offset: reads 0, no traffic
+
+__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// output channel of row i (0..15) of MFMA tile t: lane group g's four rows of
+// every tile are channels CPL*g + 4t .. +3, so a lane owns CPL consecutive ones
+template <int NT>
+__device__ __forceinline__ int perm_ch(int t, int i) {
+  return 4 * NT * (i >> 2) + 4 * t + (i & 3);
+}
+
+// store CPL = 4*NT consecutive channels (fp32 values v[t][rr], channel 4t+rr)
+template <int NT>
+__device__ __forceinline__ void store_row(bf16_t* p, const float (&v)[NT][4]) {
+#pragma unroll
+  for (int h = 0; h < NT / 2; ++h)
+    *reinterpret_cast<u32x4*>(p + 8 * h) =
+        (u32x4){pack_bf2(v[2 * h][0], v[2 * h][1]), pack_bf2(v[2 * h][2], v[2 * h][3]),
+                pack_bf2(v[2 * h + 1][0], v[2 * h + 1][1]), pack_bf2(v[2 * h + 1][2], v[2 * h + 1][3])};
+}
+template <int NT>
+__device__ __forceinline__ void store_row(float* p, const float (&v)[NT][4]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) *reinterpret_cast<f32x4*>(p + 4 * t) = (f32x4){v[t][0], v[t][1], v[t][2], v[t][3]};
+}
+}  // namespace
+
+// ------------------------------------------------------------------ forward
+// Wave = tile (output row r, mesh group mg of 16).  Lane (j, g): mesh j,
+// input channels [32kc + 8g, +8) of every neighbour (B operand, one 16-B
+// buffer load per slot, the spiral offset in an SGPR); A = permuted W rows
+// from LDS.  y in either layout (E1 writes its batch-major level-2 output).
+template <int CIN, int COUT, int ACT, typename TY>
+__global__ __launch_bounds__(256) void conv_fwd_vm16(const bf16_t* __restrict__ x,
+                                                     const int* __restrict__ idx,
+                                                     const bf16_t* __restrict__ w,
+                                                     const float* __restrict__ bias,
+                                                     TY* __restrict__ y, int vsrc, int rows,
+                                                     int batch, int yvm) {
+  constexpr int K = kS * CIN, KP = K + 8, KC = CIN / 32, NT = COUT / 16, CPL = 4 * NT;
+  extern __shared__ bf16_t lw[];  // [NT*16][KP], row t*16 + i = W row perm_ch<NT>(t, i)
+  coop_copy<8, u32x4>(
+      COUT * K / 8,
+      [&](int e) { return *reinterpret_cast<const u32x4*>(&w[(e / (K / 8)) * K + 8 * (e % (K / 8))]); },
+      [&](int e, u32x4 v) {
+        const int o = e / (K / 8), rem = o % CPL;
+        const int row = (rem >> 2) * 16 + 4 * (o / CPL) + (rem & 3);
+        *reinterpret_cast<u32x4*>(&lw[row * KP + 8 * (e % (K / 8))]) = v;
+      });
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  float bn[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) bn[t][rr] = bias ? bias[CPL * g + 4 * t + rr] : 0.f;
+  const int G16 = batch >> 4;
+  const long n_tiles = (long)rows * G16;
+  const int xbytes = (int)((long)vsrc * batch * CIN * 2);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x), 0, xbytes, 0x00020000);
+  const int vstride = batch * CIN * 2;  // bytes between two vertices' blocks
+  const TileSweep sw = xcd_sweep(n_tiles, 4, wave, true);
+
+  auto gather = [&](long tile, u32x4 (&a)[kS][KC]) {
+    const int tl = uni((int)tile);
+    const int r = tl / G16, mg = tl - r * G16;
+    const int voff = ((mg * 16 + j) * CIN + 8 * g) * 2;
+#pragma unroll
+    for (int s = 0; s < kS; ++s) {
+      const int src = uni(idx[r * kS + s]);
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) a[s][kc] = bload16(rs, voff + 64 * kc, src * vstride);
+    }
+  };
+  auto compute_store = [&](long tile, const u32x4 (&a)[kS][KC]) {
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kS; ++s)
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const u32x4 wa = *reinterpret_cast<const u32x4*>(&lw[(t * 16 + j) * KP + s * CIN + 32 * kc + 8 * g]);
+          acc[t] = mfma_bf16(wa, a[s][kc], acc[t]);
+        }
+    float v[NT][4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        float z = acc[t][rr] + bn[t][rr];
+        if (ACT == CFSD_ACT_ELU) z = elu_fast(z);
+        v[t][rr] = z;
+      }
+    const int tl = (int)tile;
+    const int r = tl / G16, mesh = (tl - r * G16) * 16 + j;
+    const long row = yvm ? (long)r * batch + mesh : (long)mesh * rows + r;
+    store_row<NT>(y + row * COUT + CPL * g, v);
+  };
+
+  // two tiles per iteration, the next one's gathers always in flight
+  u32x4 a0[kS][KC], a1[kS][KC];
+  long t0 = sw.begin;
+  if (t0 < sw.end) gather(t0, a0);
+  while (t0 < sw.end) {
+    const long t1 = t0 + sw.step;
+    if (t1 < sw.end) gather(t1, a1);
+    compute_store(t0, a0);
+    if (t1 >= sw.end) break;
+    t0 = t1 + sw.step;
+    if (t0 < sw.end) gather(t0, a0);
+    compute_store(t1, a1);
+  }
+}
+
+// ------------------------------------------------------------------ data gradient
+// Wave = tile (source vertex u, mesh group).  Per slot s the B operand is
+// T_s[mesh][o] = sum of the dpre rows of the inverse-spiral list (u, s): the
+// list head (int4, scalar) gives rows 0-2 as unconditional buffer loads with
+// scalar offsets (absent rows out of range: 0, no traffic), rows 3.. (0.3 %
+// of keys) through a uniform branch; summed in fp32 in list order, rounded
+// once to bf16.  A = W_s^T with permuted channel rows (LDS).  dx and elu_y
+// vertex-major; dpre vertex-major (bf16 or fp32).
+template <int CIN, int COUT, typename TD>
+__global__ __launch_bounds__(256) void conv_dx_vm16(const TD* __restrict__ dpre,
+                                                    const int* __restrict__ inv_ptr,
+                                                    const int* __restrict__ inv_row,
+                                                    const int4* __restrict__ inv_head,
+                                                    const bf16_t* __restrict__ w,
+                                                    const bf16_t* __restrict__ elu_y,
+                                                    bf16_t* __restrict__ dx, int vsrc, int rows,
+                                                    int batch) {
+  constexpr int K = kS * CIN, OP = COUT + 8, OC = COUT / 32, NT = CIN / 16, CPL = 4 * NT;
+  constexpr int RB = COUT * (int)sizeof(TD);  // dpre row bytes
+  static_assert(OC >= 1, "shape");
+  // lwt[(s*NT + t)*16 + i][o] = W[o][s*CIN + perm_ch(t, i)]
+  extern __shared__ bf16_t lwt[];
+  coop_copy<12, bf16_t>(
+      COUT * K, [&](int e) { return w[e]; },
+      [&](int e, bf16_t v) {
+        const int o = e / K, k = e % K, s = k / CIN, c = k % CIN, rem = c % CPL;
+        const int row = (s * NT + (rem >> 2)) * 16 + 4 * (c / CPL) + (rem & 3);
+        lwt[row * OP + o] = v;
+      });
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const int G16 = batch >> 4;
+  const long n_tiles = (long)vsrc * G16;
+  const int nbytes = (int)((long)batch * rows * RB);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<TD*>(dpre), 0, nbytes, 0x00020000);
+  const int rstride = batch * RB;  // bytes between two rows' blocks
+  const TileSweep sw = xcd_sweep(n_tiles, 4, wave, true);
+  constexpr int NL = sizeof(TD) == 2 ? 1 : 2;  // 16-B loads per 8 channels of a row
+
+  for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
+    const int tl = uni((int)tile);
+    const int u = tl / G16, mg = tl - u * G16;
+    const int voff = (mg * 16 + j) * RB + 8 * g * (int)sizeof(TD);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s0 = 0; s0 < kS; s0 += 3) {
+      int4 hd[3];
+      u32x4 v[3][OC][3][NL];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int4 h = inv_head[u * kS + s0 + q];
+        hd[q] = make_int4(uni(h.x), uni(h.y), uni(h.z), uni(h.w));
+      }
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int hr[3] = {hd[q].x, hd[q].y, hd[q].z};
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+          const int so = hr[jj] >= 0 ? hr[jj] * rstride : kAbsent;
+#pragma unroll
+          for (int oc = 0; oc < OC; ++oc)
+#pragma unroll
+            for (int l = 0; l < NL; ++l) v[q][oc][jj][l] = bload16(rs, voff + 32 * oc * (int)sizeof(TD) + 16 * l, so);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int s = s0 + q;
+#pragma unroll
+        for (int oc = 0; oc < OC; ++oc) {
+          float a8[8];
+#pragma unroll
+          for (int jj = 0; jj < 3; ++jj) {
+            float r8[8];
+            if constexpr (sizeof(TD) == 2) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                r8[2 * e] = __uint_as_float(v[q][oc][jj][0][e] << 16);
+                r8[2 * e + 1] = __uint_as_float(v[q][oc][jj][0][e] & 0xffff0000u);
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                r8[e] = __uint_as_float(v[q][oc][jj][0][e]);
+                r8[4 + e] = __uint_as_float(v[q][oc][jj][NL - 1][e]);
+              }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a8[e] = jj == 0 ? r8[e] : a8[e] + r8[e];
+          }
+          if (hd[q].w >= 0) {  // 0.3 % of keys: list rows 3.. (uniform branch)
+            const long key = (long)u * kS + s;
+            const TD* db_ = dpre + (long)(mg * 16 + j) * COUT + 32 * oc + 8 * g;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a8[e] += ldf(&db_[(long)hd[q].w * batch * COUT + e]);
+            for (int p = inv_ptr[key] + CFSD_INV_HEAD; p < inv_ptr[key + 1]; ++p) {
+              const TD* rp = db_ + (long)inv_row[p] * batch * COUT;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) a8[e] += ldf(&rp[e]);
+            }
+          }
+          const u32x4 bt = {pack_bf2(a8[0], a8[1]), pack_bf2(a8[2], a8[3]), pack_bf2(a8[4], a8[5]),
+                            pack_bf2(a8[6], a8[7])};
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const u32x4 wa = *reinterpret_cast<const u32x4*>(&lwt[((s * NT + t) * 16 + j) * OP + 32 * oc + 8 * g]);
+            acc[t] = mfma_bf16(wa, bt, acc[t]);
+          }
+        }
+      }
+    }
+    const long row = (long)u * batch + mg * 16 + j;
+    float vv[NT][4];
+    float ey[CPL];
+    if (elu_y) {
+      const bf16_t* ep = elu_y + row * CIN + CPL * g;
+#pragma unroll
+      for (int h = 0; h < CPL / 8; ++h) {
+        const u32x4 q = *reinterpret_cast<const u32x4*>(ep + 8 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ey[8 * h + 2 * e] = __uint_as_float(q[e] << 16);
+          ey[8 * h + 2 * e + 1] = __uint_as_float(q[e] & 0xffff0000u);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        float z = acc[t][rr];
+        if (elu_y) z *= elu_grad_from_out(ey[4 * t + rr]);
+        vv[t][rr] = z;
+      }
+    store_row<NT>(dx + row * CIN + CPL * g, vv);
+  }
+}
+
+// ------------------------------------------------------------------ data gradient, flat lists
+// dx[u] = elu'(y[u]) * sum_e W_{s_e}^T dpre[r_e] over the FLAT inverse list of
+// u: the spiral positions p_e = 9 r_e + s_e with idx[r_e][s_e] == u, in
+// ascending p (topology.inverse_flat, the order IndexSelectBackward's
+// index_add_ visits them, model.py:34).  By linearity this equals the
+// per-slot form (sum the slot's rows, then W_s^T), but needs ONE load per
+// entry (9 per vertex on average, FW padded with out-of-range loads) instead
+// of 3 head rows per slot, and the products are exact bf16 x bf16 in fp32
+// (no bf16 rounding of row sums).  One MFMA per entry and 16-column tile.
+template <int CIN, int COUT, typename TD, int FW>
+__global__ __launch_bounds__(256) void conv_dx_flat_vm16(const TD* __restrict__ dpre,
+                                                         const int4* __restrict__ flat,
+                                                         const bf16_t* __restrict__ w,
+                                                         const bf16_t* __restrict__ elu_y,
+                                                         bf16_t* __restrict__ dx, int vsrc, int rows,
+                                                         int batch) {
+  constexpr int K = kS * CIN, OP = COUT + 8, OC = COUT / 32, NT = CIN / 16, CPL = 4 * NT;
+  constexpr int RB = COUT * (int)sizeof(TD);
+  constexpr int NL = sizeof(TD) == 2 ? 1 : 2;
+  extern __shared__ bf16_t lwt[];  // as conv_dx_vm16
+  coop_copy<12, bf16_t>(
+      COUT * K, [&](int e) { return w[e]; },
+      [&](int e, bf16_t v) {
+        const int o = e / K, k = e % K, s = k / CIN, c = k % CIN, rem = c % CPL;
+        const int row = (s * NT + (rem >> 2)) * 16 + 4 * (c / CPL) + (rem & 3);
+        lwt[row * OP + o] = v;
+      });
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const int G16 = batch >> 4;
+  const long n_tiles = (long)vsrc * G16;
+  const int nbytes = (int)((long)batch * rows * RB);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<TD*>(dpre), 0, nbytes, 0x00020000);
+  const int rstride = batch * RB;
+  const TileSweep sw = xcd_sweep(n_tiles, 4, wave, true);
+  for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
+    const int tl = uni((int)tile);
+    const int u = tl / G16, mg = tl - u * G16;
+    const int voff = (mg * 16 + j) * RB + 8 * g * (int)sizeof(TD);
+    int pe[FW];
+#pragma unroll
+    for (int q = 0; q < FW / 4; ++q) {
+      const int4 f = flat[u * (FW / 4) + q];
+      pe[4 * q] = uni(f.x);
+      pe[4 * q + 1] = uni(f.y);
+      pe[4 * q + 2] = uni(f.z);
+      pe[4 * q + 3] = uni(f.w);
+    }
+    u32x4 v[FW][OC][NL];
+#pragma unroll
+    for (int e = 0; e < FW; ++e) {
+      const int so = pe[e] >= 0 ? (pe[e] / kS) * rstride : kAbsent;
+#pragma unroll
+      for (int oc = 0; oc < OC; ++oc)
+#pragma unroll
+        for (int l = 0; l < NL; ++l) v[e][oc][l] = bload16(rs, voff + 32 * oc * (int)sizeof(TD) + 16 * l, so);
+    }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < FW; ++e) {
+      const int s = pe[e] >= 0 ? pe[e] % kS : 0;  // absent entries: B = 0, adds 0
+#pragma unroll
+      for (int oc = 0; oc < OC; ++oc) {
+        u32x4 bt;
+        if constexpr (sizeof(TD) == 2) {
+          bt = v[e][oc][0];
+        } else {
+          const f32x4 a = __builtin_bit_cast(f32x4, v[e][oc][0]), b = __builtin_bit_cast(f32x4, v[e][oc][1]);
+          bt = (u32x4){pack_bf2(a.x, a.y), pack_bf2(a.z, a.w), pack_bf2(b.x, b.y), pack_bf2(b.z, b.w)};
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const u32x4 wa = *reinterpret_cast<const u32x4*>(&lwt[((s * NT + t) * 16 + j) * OP + 32 * oc + 8 * g]);
+          acc[t] = mfma_bf16(wa, bt, acc[t]);
+        }
+      }
+    }
+    const long row = (long)u * batch + mg * 16 + j;
+    float vv[NT][4];
+    float ey[CPL];
+    if (elu_y) {
+      const bf16_t* ep = elu_y + row * CIN + CPL * g;
+#pragma unroll
+      for (int h = 0; h < CPL / 8; ++h) {
+        const u32x4 q = *reinterpret_cast<const u32x4*>(ep + 8 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ey[8 * h + 2 * e] = __uint_as_float(q[e] << 16);
+          ey[8 * h + 2 * e + 1] = __uint_as_float(q[e] & 0xffff0000u);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        float z = acc[t][rr];
+        if (elu_y) z *= elu_grad_from_out(ey[4 * t + rr]);
+        vv[t][rr] = z;
+      }
+    store_row<NT>(dx + row * CIN + CPL * g, vv);
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+template <typename Kern>
+static int resident(Kern k, size_t lds) {
+  const int r = resident_blocks_of(k, 256, lds);
+  return r > 0 ? r : 1;
+}
+
+template <int CIN, int COUT, int ACT, typename TY>
+static int fwd16_t(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, TY* y, int vsrc,
+                   int rows, int batch, int yvm, hipStream_t st) {
+  constexpr size_t lds = (size_t)COUT * (kS * CIN + 8) * sizeof(bf16_t);
+  auto kern = conv_fwd_vm16<CIN, COUT, ACT, TY>;
+  const long tiles = (long)rows * (batch / 16);
+  const unsigned grid = balanced_blocks(tiles, 8, resident(kern, lds));  // >= 2 tiles per wave
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
+  return launch_status("spiral_conv_fwd_vm16");
+}
+
+bool vm16_ok(int batch, int cin, int cout) {
+  return batch % 16 == 0 && cin == 32 && (cout == 32 || cout == 64);
+}
+
+int launch_fwd_vm16(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, void* y, int y_dt,
+                    int vsrc, int rows, int batch, int cin, int cout, int act, hipStream_t st) {
+  const int yvm = (y_dt & CFSD_VM) != 0;
+  const bool ybf = CFSD_DT_TYPE(y_dt) == DT_BF16;
+#define F16(CO)                                                                                          \
+  if (cout == CO) {                                                                                      \
+    if (ybf)                                                                                             \
+      return act == CFSD_ACT_ELU                                                                         \
+                 ? fwd16_t<32, CO, CFSD_ACT_ELU, bf16_t>(x, idx, w, bias, (bf16_t*)y, vsrc, rows, batch, yvm, st) \
+                 : fwd16_t<32, CO, CFSD_ACT_NONE, bf16_t>(x, idx, w, bias, (bf16_t*)y, vsrc, rows, batch, yvm, st); \
+    return act == CFSD_ACT_ELU                                                                           \
+               ? fwd16_t<32, CO, CFSD_ACT_ELU, float>(x, idx, w, bias, (float*)y, vsrc, rows, batch, yvm, st) \
+               : fwd16_t<32, CO, CFSD_ACT_NONE, float>(x, idx, w, bias, (float*)y, vsrc, rows, batch, yvm, st); \
+  }
+  F16(32) F16(64)
+#undef F16
+  return set_error(CFSD_EINVAL, "spiral_conv_fwd_vm16: unsupported channels %d -> %d", cin, cout);
+}
+
+template <int CIN, int COUT, typename TD>
+static int dx16_t(const TD* dpre, const int* inv_ptr, const int* inv_row, const int* inv_head, const bf16_t* w,
+                  const bf16_t* elu_y, bf16_t* dx, int vsrc, int rows, int batch, hipStream_t st) {
+  constexpr size_t lds = (size_t)kS * CIN * (COUT + 8) * sizeof(bf16_t);
+  auto kern = conv_dx_vm16<CIN, COUT, TD>;
+  const long tiles = (long)vsrc * (batch / 16);
+  const unsigned grid = balanced_blocks(tiles, 4, resident(kern, lds));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, dpre, inv_ptr, inv_row, (const int4*)inv_head, w,
+                     elu_y, dx, vsrc, rows, batch);
+  return launch_status("spiral_conv_bwd_data_vm16");
+}
+
+int launch_dx_vm16(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_row, const int* inv_head,
+                   const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int vsrc, int rows, int batch, int cin,
+                   int cout, hipStream_t st) {
+  const bool dbf = CFSD_DT_TYPE(dpre_dt) == DT_BF16;
+#define D16(CO)                                                                                          \
+  if (cout == CO)                                                                                        \
+    return dbf ? dx16_t<32, CO, bf16_t>((const bf16_t*)dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, vsrc, \
+                                        rows, batch, st)                                                 \
+               : dx16_t<32, CO, float>((const float*)dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, vsrc, \
+                                       rows, batch, st);
+  D16(32) D16(64)
+#undef D16
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_vm16: unsupported channels %d -> %d", cin, cout);
+}
+
+template <int CIN, int COUT, typename TD, int FW>
+static int dxf16_t(const TD* dpre, const int* flat, const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int vsrc,
+                   int rows, int batch, hipStream_t st) {
+  constexpr size_t lds = (size_t)kS * CIN * (COUT + 8) * sizeof(bf16_t);
+  auto kern = conv_dx_flat_vm16<CIN, COUT, TD, FW>;
+  const long tiles = (long)vsrc * (batch / 16);
+  const unsigned grid = balanced_blocks(tiles, 4, resident(kern, lds));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows,
+                     batch);
+  return launch_status("spiral_conv_bwd_data_flat");
+}
+
+int launch_dx_flat_vm16(const void* dpre, int dpre_dt, const int* flat, int width, const bf16_t* w,
+                        const bf16_t* elu_y, bf16_t* dx, int vsrc, int rows, int batch, int cin, int cout,
+                        hipStream_t st) {
+  const bool dbf = CFSD_DT_TYPE(dpre_dt) == DT_BF16;
+#define DF(CO, FW_)                                                                                       \
+  if (cout == CO && width == FW_)                                                                         \
+    return dbf ? dxf16_t<32, CO, bf16_t, FW_>((const bf16_t*)dpre, flat, w, elu_y, dx, vsrc, rows, batch, st) \
+               : dxf16_t<32, CO, float, FW_>((const float*)dpre, flat, w, elu_y, dx, vsrc, rows, batch, st);
+  DF(32, 8) DF(32, 12) DF(32, 16) DF(32, 20) DF(64, 8) DF(64, 12) DF(64, 16) DF(64, 20)
+#undef DF
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat: unsupported channels %d -> %d / width %d", cin,
+                   cout, width);
+}
+
+}  // namespace bf
+}  // namespace cfsd

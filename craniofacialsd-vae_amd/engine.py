@@ -611,9 +611,13 @@ class SDVAEEngine:
             if lv in self.lp_levels:  # bf16 operands: bf16 MFMA dW slabs + dx
                 defer(ops.spiral_conv_bwd_weight_x(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
                                                    b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
-                ops.spiral_conv_bwd_data_x(b.dpre_dec[i], T.spiral_inv[lv],
-                                           self._w16(f"de_layers.{i + 1}.conv.layer.weight"), T.n_verts[lv],
-                                           out=b.g_dec_up[i])
+                w16 = self._w16(f"de_layers.{i + 1}.conv.layer.weight")
+                if self._flat_dx(b, lv, cin, cout):  # vertex-major, batch % 16: one MFMA per list entry
+                    ops.spiral_conv_bwd_data_flat(b.dpre_dec[i], T.spiral_flat[lv], w16, T.n_verts[lv],
+                                                  out=b.g_dec_up[i])
+                else:
+                    ops.spiral_conv_bwd_data_x(b.dpre_dec[i], T.spiral_inv[lv], w16, T.n_verts[lv],
+                                               out=b.g_dec_up[i])
             elif b.paired[("dec", i)]:  # dx + dW slabs in one launch
                 _, d = ops.spiral_conv_bwd(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_inv[lv],
                                            w, None, None, dx=b.g_dec_up[i], workspace=b.ws_dw[("dec", i)])
@@ -659,6 +663,12 @@ class SDVAEEngine:
                            db=gB, workspace=b.lin_ws)
             ops.spmm(T.downT_csr[last], b.g_pooled[last], T.n_verts[last], elu_y=b.enc_full[last],
                      out=b.dpre_enc[last])
+
+    def _flat_dx(self, b, lv, cin, cout):
+        """The flat-list bf16 data gradient applies (vertex-major level,
+        batch a multiple of 16, 32 -> 32/64 channels, fan-in <= 20)."""
+        return (lv in self.lp_levels and b.bsz % 16 == 0 and cin == 32 and cout in (32, 64)
+                and self.topo.spiral_flat[lv] is not None)
 
     def adam_args(self):
         P = self.params

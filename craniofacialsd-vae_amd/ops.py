@@ -734,6 +734,27 @@ def spiral_conv_bwd_data_x(dpre, inv, w_bf16, vsrc, elu_y=None, out=None):
     return out
 
 
+def spiral_conv_bwd_data_flat(dpre, flat, w_bf16, vsrc, elu_y=None, out=None):
+    """dx of a vertex-major bf16 layer through the flat inverse list
+    (``topology.spiral_flat``), batch a multiple of 16."""
+    bsz, rows, cout = dpre.shape
+    table, width = flat
+    seq = 9
+    cin = w_bf16.shape[1] // seq
+    _needl(dpre, None, "dpre")
+    _need(table, (vsrc, width), torch.int32, "inv_flat")
+    _need(w_bf16, (cout, seq * cin), torch.bfloat16, "w_bf16")
+    if out is None:
+        out = vm_empty(bsz, vsrc, cin, dtype=torch.bfloat16, device=dpre.device)
+    _needl(out, (bsz, vsrc, cin), "dx", torch.bfloat16)
+    if elu_y is not None:
+        _needl(elu_y, (bsz, vsrc, cin), "elu_y", torch.bfloat16)
+        _same_layout(out, elu_y, "dx and elu_y")
+    call("cfsd_spiral_conv_bwd_data_flat", ptr(dpre), _st(dpre), ptr(table), width, ptr(w_bf16), ptr(elu_y),
+         ptr(out), _st(out), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    return out
+
+
 def spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout):
     return int(_abi.lib().cfsd_spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout))
 

@@ -181,6 +181,7 @@ class DeviceTopology:
         self.region_keys = list(region_keys) if region_keys is not None else None
         self.spiral = []        # full spiral tables [V_l, S]
         self.spiral_inv = []    # inverse CSR of the full table
+        self.spiral_flat = []   # (inverse_flat of the full table, width) or None (fan-in > 20)
         self.enc_rows = []      # per Enblock: evaluated spiral table (subset or full)
         self.enc_inv = []
         self.enc_select = []    # True when Pool(down) folds into the row subset
@@ -196,6 +197,8 @@ class DeviceTopology:
             v = sp.shape[0]
             self.spiral.append(_dev(_i32(sp), self.device))
             self.spiral_inv.append(tuple(_dev(a, self.device) for a in inverse_spiral(sp, v)))
+            fl, width = inverse_flat(sp, v, max_width=20)
+            self.spiral_flat.append((_dev(fl, self.device), width) if fl is not None else None)
             drow, dcol, dval, dshape = down[l]
             sel = selection_rows(drow, dcol, dval, dshape[0])
             if dshape[1] != v:

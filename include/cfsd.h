@@ -385,6 +385,16 @@ int cfsd_spiral_conv_bwd_data_x(const void* dpre, int dpre_dt, const int32_t* in
                                 const uint16_t* w_bf16, const uint16_t* elu_y, uint16_t* dx,
                                 int dx_dt, int batch, int vsrc, int rows, int seq, int cin,
                                 int cout, void* stream);
+/* The same dx through the FLAT inverse list (topology.inverse_flat: per
+ * source vertex the spiral positions p = r*seq + s naming it, ascending,
+ * -1 padded to flat_width in {8, 12, 16, 20}): one MFMA per entry, exact
+ * products (no bf16 rounding of per-slot row sums).  Vertex-major dpre / dx /
+ * elu_y, batch % 16 == 0, 32 -> 32/64 channels (the bf16 step's level-0/1
+ * Deblocks). */
+int cfsd_spiral_conv_bwd_data_flat(const void* dpre, int dpre_dt, const int32_t* inv_flat,
+                                   int flat_width, const uint16_t* w_bf16, const uint16_t* elu_y,
+                                   uint16_t* dx, int dx_dt, int batch, int vsrc, int rows, int seq,
+                                   int cin, int cout, void* stream);
 /* dW/db (fp32): 32/64-channel layers (x bf16, dpre bf16/fp32) and the xyz
  * input layer (x fp32, dpre bf16).  dw == db == NULL defers the reduction
  * (cfsd_dw_reduce_batch item with fused = 2 for the 32/64-channel kind, 0

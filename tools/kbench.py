@@ -213,6 +213,8 @@ def main():
     cases["fwd_d3_b16"] = lambda: ops.spiral_conv_fwd_x(c.dec_up[3], T.spiral[0], w3h, w16, b3h, 1, c.dec_out[3])
     cases["dx_d3_b16"] = lambda: ops.spiral_conv_bwd_data_x(c.dpre_dec[3], T.spiral_inv[0], w16, T.n_verts[0],
                                                             out=c.g_dec_up[3])
+    cases["dxf_d3_b16"] = lambda: ops.spiral_conv_bwd_data_flat(c.dpre_dec[3], T.spiral_flat[0], w16, T.n_verts[0],
+                                                                out=c.g_dec_up[3])
     cases["dw_d3_b16"] = lambda: ops.spiral_conv_bwd_weight_x(c.dec_up[3], T.spiral[0], c.dpre_dec[3], None, None,
                                                               c.ws_dw[("dec", 3)])
     if "step" in names:

@@ -217,6 +217,19 @@ def main():
                                                                 out=c.g_dec_up[3])
     cases["dw_d3_b16"] = lambda: ops.spiral_conv_bwd_weight_x(c.dec_up[3], T.spiral[0], c.dpre_dec[3], None, None,
                                                               c.ws_dw[("dec", 3)])
+    bm_up, bm_out = c.dec_up[3].contiguous(), c.dec_out[3].contiguous()
+    bm_dp, bm_g = c.dpre_dec[3].contiguous(), c.g_dec_up[3].contiguous()
+    cases["fwd_d3_b16_bm"] = lambda: ops.spiral_conv_fwd_x(bm_up, T.spiral[0], w3h, w16, b3h, 1, bm_out)
+    cases["dx_d3_b16_bm"] = lambda: ops.spiral_conv_bwd_data_x(bm_dp, T.spiral_inv[0], w16, T.n_verts[0], out=bm_g)
+    cases["dw_d3_b16_bm"] = lambda: ops.spiral_conv_bwd_weight_x(bm_up, T.spiral[0], bm_dp, None, None,
+                                                                 c.ws_dw[("dec", 3)])
+    for mult in (2, 4):  # work scaling of the vertex-major forward (fixed-cost check)
+        xin = ops.to_vm(torch.randn(16 * mult, T.n_verts[0], 32, device="cuda", generator=g).to(torch.bfloat16))
+        yout = ops.vm_empty(16 * mult, T.n_verts[0], 32, dtype=torch.bfloat16, device="cuda")
+        cases[f"fwd_d3_b16_x{mult}"] = (lambda xin=xin, yout=yout:
+                                        ops.spiral_conv_fwd_x(xin, T.spiral[0], w3h, w16, b3h, 1, yout))
+    cases["fwd_d3_b16_self"] = lambda: ops.spiral_conv_fwd_x(c.dec_up[3], self_idx, w3h, w16, b3h, 1, c.dec_out[3])
+    cases["fwd_d3_b16_shift"] = lambda: ops.spiral_conv_fwd_x(c.dec_up[3], shift_idx, w3h, w16, b3h, 1, c.dec_out[3])
     if "step" in names:
         eng.set_batch(b.x, key_index=3)
         cases["step"] = lambda: eng.train_step_on(b)

@@ -55,6 +55,9 @@ def parse():
                    help="fp32 (reference arithmetic) or bf16 (configs C3/C5: bf16 level-0/1 tensors on "
                         "bf16 MFMA, fp32 accumulation and master weights)")
     p.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
+    p.add_argument("--batch-major", action="store_true",
+                   help="fp32: keep every tensor batch-major (the reference's [B, V, C]) instead of storing "
+                        "the level-0/1 tensors vertex-major (A/B of the layouts)")
     p.add_argument("--augmented", type=int, default=0,
                    help="configuration C5: train on N spectral-interpolation meshes (k = 1000 eigenvectors of "
                         "the template, pairs of the demo meshes) generated on the device and resident in HBM, "
@@ -109,12 +112,13 @@ class Runner:
     driver (manager.ModelManager) run."""
 
     def __init__(self, world, rank, device, n_meshes, use_graph, topo_name="craniofacial",
-                 precision="fp32", meshes=None, norm=None):
+                 precision="fp32", meshes=None, norm=None, vertex_major=True):
         self.topo = load_topology(topo_name, device)
         self.topo_name = topo_name
         self.precision = precision
         self.eng = E.SDVAEEngine(self.topo, E.ModelSpec(latent_size=75), lr=1e-4, swap_bs=4,
-                                 seed=1234 + rank, device=device, precision=precision)
+                                 seed=1234 + rank, device=device, precision=precision,
+                                 vertex_major=vertex_major)
         self.eng.reset_parameters()  # same init on every rank (broadcast below)
         self.world, self.rank = world, rank
         nv = self.topo.n_verts[0]
@@ -190,7 +194,7 @@ def launch_cost(name, a):
     if name == "cfsd_spiral_conv_fwd_x":
         sx, sy = sz(a[1]), sz(a[7])
         B, vs, rows, S, ci, co = a[8:14]
-        peak = BF16_PEAK_TFLOPS if (ci >= 16 and co >= 16) else FP32_PEAK_TFLOPS
+        peak = BF16_PEAK_TFLOPS if (ci >= 16 and co >= 16 and sx == 2) else FP32_PEAK_TFLOPS
         return 2.0 * B * rows * S * ci * co, sx * B * vs * ci + sy * B * rows * co + 2 * co * S * ci + 4 * rows * S, peak
     if name == "cfsd_spiral_conv_bwd_data_x":
         sd = sz(a[1])
@@ -198,16 +202,23 @@ def launch_cost(name, a):
         elu = a[6] is not None
         return (2.0 * B * rows * S * ci * co, sd * B * rows * co + 2 * B * vs * ci * (2 if elu else 1)
                 + 2 * co * S * ci + 16 * vs * S, BF16_PEAK_TFLOPS)
+    if name == "cfsd_spiral_conv_bwd_data_flat":
+        sd, sx = sz(a[1]), sz(a[7])
+        B, vs, rows, S, ci, co = a[8:14]
+        elu = a[5] is not None
+        return (2.0 * B * rows * S * ci * co, sd * B * rows * co + sx * B * vs * ci * (2 if elu else 1)
+                + sx * co * S * ci + 4 * vs * a[3], BF16_PEAK_TFLOPS if sx == 2 else FP32_PEAK_TFLOPS)
     if name == "cfsd_spiral_conv_bwd_weight_x":
         sx, sd = sz(a[1]), sz(a[4])
         B, vs, rows, S, ci, co = a[9:15]
-        peak = BF16_PEAK_TFLOPS if ci >= 16 else FP32_PEAK_TFLOPS
+        peak = BF16_PEAK_TFLOPS if (ci >= 16 and sx == 2) else FP32_PEAK_TFLOPS
         return 2.0 * B * rows * S * ci * co, sx * B * vs * ci + sd * B * rows * co + 4 * co * S * ci + 4 * rows * S, peak
     if name == "cfsd_spiral_conv_bwd_x":
+        sx = sz(a[1])  # x, elu_y, dx storage
         B, vs, rows, S, ci, co = a[15:21]
         dx, elu = a[10] is not None, a[9] is not None
         fl = 2.0 * B * rows * S * ci * co * (2 if dx else 1)
-        by = 2 * B * vs * ci + 4 * B * rows * co + 4 * co * S * ci + (2 * B * vs * ci * (2 if elu else 1) if dx else 0)
+        by = sx * B * vs * ci + 4 * B * rows * co + 4 * co * S * ci + (sx * B * vs * ci * (2 if elu else 1) if dx else 0)
         return fl, by, FP32_PEAK_TFLOPS
     if name in ("cfsd_spmm_csr_x", "cfsd_spmm_uniform"):
         sx, sy = sz(a[4]), sz(a[7])
@@ -305,12 +316,19 @@ def kernel_probe(runner, n_iter=20):
     i3 = len(dec) - 1
     w3, bias3 = eng._dec_w(i3)
     wname = f"de_layers.{i3 + 1}.conv.layer.weight"
-    if runner.precision == "bf16":
-        w16 = eng._w16(wname)
+    # the D3 kernels exactly as the step launches them (dW deferred: slab
+    # kernel only, reduced by the batched reduce)
+    if 0 in b.xl:  # vertex-major level 0 (bf16, or fp32 at batch % 16 == 0)
+        w16 = eng._w16(wname) if runner.precision == "bf16" else None
+        wx = eng._wx(wname)
         timed("conv_fwd_D3", lambda: ops.spiral_conv_fwd_x(b.dec_up[i3], T.spiral[0], w3, w16, bias3, 1,
                                                             b.dec_out[i3]))
-        timed("conv_dx_D3", lambda: ops.spiral_conv_bwd_data_x(b.dpre_dec[i3], T.spiral_inv[0], w16,
-                                                               T.n_verts[0], out=b.g_dec_up[i3]))
+        if eng._flat_dx(b, 0, 32, 32):
+            timed("conv_dx_D3", lambda: ops.spiral_conv_bwd_data_flat(b.dpre_dec[i3], T.spiral_flat[0], wx,
+                                                                      T.n_verts[0], out=b.g_dec_up[i3]))
+        else:
+            timed("conv_dx_D3", lambda: ops.spiral_conv_bwd_data_x(b.dpre_dec[i3], T.spiral_inv[0], w16,
+                                                                   T.n_verts[0], out=b.g_dec_up[i3]))
         timed("conv_dw_D3", lambda: ops.spiral_conv_bwd_weight_x(b.dec_up[i3], T.spiral[0], b.dpre_dec[i3],
                                                                  None, None, b.ws_dw[("dec", i3)]))
     else:
@@ -323,7 +341,7 @@ def kernel_probe(runner, n_iter=20):
         timed("conv_dw_D3", lambda: ops.spiral_conv_bwd_weight(b.dec_up[i3], T.spiral[0], b.dpre_dec[i3],
                                                                None, None, b.ws_dw[("dec", i3)]))
     g = torch.empty(16, T.n_verts[0], 9 * 32, device=b.x.device)
-    xg = b.dec_up[i3] if b.dec_up[i3].dtype == torch.float32 else b.dec_up[i3].float().contiguous()
+    xg = b.dec_up[i3].float().contiguous()  # batch-major fp32 copy
     timed("spiral_gather_L0", lambda: ops.spiral_gather(xg, T.spiral[0], out=g))
     del g
     return res
@@ -497,7 +515,7 @@ def main():
         per_rank = args.augmented // world
         meshes, norm, aug_info = augmented_set(per_rank, device, seed=77 + rank)
     runner = Runner(world, rank, device, args.dataset, not args.no_graph, args.topology, args.precision,
-                    meshes=meshes, norm=norm)
+                    meshes=meshes, norm=norm, vertex_major=not args.batch_major)
     del meshes
     if runner.use_graph:
         runner.capture()
@@ -548,10 +566,11 @@ def main():
                     "conv_dx_D3": s_act * 16 * nv * 64 + nv * 9 * 16,
                     "conv_dw_D3": s_act * 16 * nv * 64 + nv * 36}
         d3 = {}
+        vm0 = 0 in runner.b.xl  # level-0 tensors vertex-major (the kernels below)
         for name, key in (("conv_fwd_D3", "conv_fwd_d3"), ("conv_dx_D3", "conv_dx_d3"),
                           ("conv_dw_D3", "conv_dw_d3")):
             t = probe[name]
-            key = key + ("_bf16" if bf else "")
+            key = key + ("_bf16" if bf else "") + ("_vm" if vm0 else "")
             traffic, traffic_src = pmc_traffic(key) if args.topology == "craniofacial" else (None, None)
             if bf:
                 d3[name] = {"us_per_launch": t * 1e6, "bound": "hbm", "achieved": d3_bytes[name] / t / 1e9,
@@ -564,12 +583,20 @@ def main():
                             "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS, "algorithmic_flop": flops,
                             "traffic": traffic, "traffic_source": traffic_src}
         dom = max(d3, key=lambda k: d3[k]["us_per_launch"])
-        kern_names = ({"conv_fwd_D3": "conv_fwd_b16<32,32> (decoder level 0 forward, bf16)",
-                       "conv_dx_D3": "conv_dx_b16<32,32> (decoder level 0 data gradient, bf16)",
-                       "conv_dw_D3": "conv_dw_b16<32,32> (decoder level 0 weight gradient, bf16)"} if bf else
-                      {"conv_fwd_D3": "conv_fwd_mfma<32,32> (decoder level 0 forward)",
-                       "conv_dx_D3": "conv_dx_mfma<32,32> (decoder level 0 data gradient)",
-                       "conv_dw_D3": "conv_dw_mfma<32,32> (decoder level 0 weight gradient)"})
+        if bf:
+            kern_names = {"conv_fwd_D3": "conv_fwd_vm16<32,32> (decoder level 0 forward, bf16, vertex-major)",
+                          "conv_dx_D3": "conv_dx_flat_vm16<32,32> (decoder level 0 data gradient, bf16, "
+                                        "vertex-major flat list)",
+                          "conv_dw_D3": "conv_dw_b16<32,32> (decoder level 0 weight gradient, bf16, vertex-major)"}
+        elif vm0:
+            kern_names = {"conv_fwd_D3": "conv_fwd_vm32<32,32> (decoder level 0 forward, vertex-major)",
+                          "conv_dx_D3": "conv_dx_flat_vm32<32,32> (decoder level 0 data gradient, vertex-major "
+                                        "flat list)",
+                          "conv_dw_D3": "conv_dw_mfma<32,32> (decoder level 0 weight gradient, vertex-major)"}
+        else:
+            kern_names = {"conv_fwd_D3": "conv_fwd_mfma<32,32> (decoder level 0 forward)",
+                          "conv_dx_D3": "conv_dx_mfma<32,32> (decoder level 0 data gradient)",
+                          "conv_dw_D3": "conv_dw_mfma<32,32> (decoder level 0 weight gradient)"}
         out = {
             "metric": METRIC, "value": meshes / el, "unit": "meshes/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
@@ -582,6 +609,7 @@ def main():
             "config": {"workload": "craniofacial.yaml SD-VAE train step (swap bs 4->16, fwd, "
                                    "MSE+Laplacian+KL+latent-consistency, bwd, Adam)",
                        "precision": runner.precision,
+                       "layout": "vertex-major levels 0-1" if 0 in runner.b.xl else "batch-major",
                        "topology": args.topology, "template_vertices": nv, "levels": runner.topo.n_verts,
                        "global_batch": 16 * world, "per_gpu_batch": 16,
                        "resident_meshes_per_gpu": runner.data.n_items,

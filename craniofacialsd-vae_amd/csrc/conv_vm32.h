@@ -1,0 +1,30 @@
+// Launchers of the fp32 SpiralConv kernels for VERTEX-MAJOR operands
+// (spiral_conv_vm32.hip), called by the C ABI in spiral_conv.hip.  A batch
+// that is a multiple of 16 makes one 16-row MFMA tile = one vertex x 16
+// meshes: every spiral index of the tile is wave-uniform and every gathered
+// neighbour is one contiguous 2-KiB block (16 meshes x 32 fp32 channels).
+#pragma once
+#include "cfsd_common.h"
+
+namespace cfsd {
+namespace vm32 {
+
+bool ok(int batch, int cin, int cout);
+// y[(b, r), :] = act(bias + W . gather(x)); x vertex-major [vsrc][batch][cin],
+// y vertex-major (yvm) or batch-major [batch][rows][cout].  Same products in
+// the same order as conv_fwd_mfma (bit-identical results).
+int launch_fwd(const float* x, const int* idx, const float* w, const float* bias, float* y, int yvm,
+               int vsrc, int rows, int batch, int cin, int cout, int act, hipStream_t st);
+// dx[u] = elu'(elu_y[u]) * sum over the flat inverse list of u (ascending
+// spiral position p = 9r + s) of W_s^T dpre[r]; dpre, dx, elu_y vertex-major.
+int launch_dx_flat(const float* dpre, const int* flat, int width, const float* w, const float* elu_y,
+                   float* dx, int vsrc, int rows, int batch, int cin, int cout, hipStream_t st);
+// dW / db partial slabs [n_slabs][cout*9*cin + cout] (plain layout, summed by
+// slab_reduce / dw_reduce_batch kind 2); x vertex-major, dpre vertex-major
+// (dpvm) or batch-major.
+int dw_slabs(int batch, int rows, int cin, int cout);
+int launch_dw(const float* x, const int* idx, const float* dpre, int dpvm, float* ws, int vsrc, int rows,
+              int batch, int cin, int cout, hipStream_t st);
+
+}  // namespace vm32
+}  // namespace cfsd

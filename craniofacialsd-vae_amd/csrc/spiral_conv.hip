@@ -19,6 +19,7 @@
 // kernels shaped for them (lane-per-output-channel or 8-lanes-per-row).
 #include "cfsd_common.h"
 #include "conv_bf16.h"
+#include "conv_vm32.h"
 
 namespace cfsd {
 
@@ -330,7 +331,9 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
     long m = tile * 32 + i;
     if (m >= total_rows) m = total_rows - 1;
     int b, r;
-    split_row(m, yvm, batch, rows, b, r);  // rows visited (and stored) in y's layout
+    // rows visited in x's layout (the xyz input is batch-major: a tile's
+    // neighbour rows are one mesh's), each 128-B output row stored in y's
+    split_row(m, xvm, batch, rows, b, r);
     const Lay lx = make_lay(xvm, batch, vsrc);
     const float* xb = x + (long)b * lx.bs * CS;
     const int* ir = idx + (long)r * kSeq;
@@ -356,8 +359,14 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
       for (int rr = 0; rr < 16; ++rr) {
         const long mo = tile * 32 + acc_row(rr, lane);
         if (mo < total_rows) {
+          long yo = mo;
+          if (xvm != yvm) {
+            int bo, ro;
+            split_row(mo, xvm, batch, rows, bo, ro);
+            yo = row_of(make_lay(yvm, batch, rows), bo, ro);
+          }
           const float v = acc[t][rr] + bn[t];
-          stf(&y[mo * COUT + t * 32 + i], ACT == CFSD_ACT_ELU ? elu_f(v) : v);
+          stf(&y[yo * COUT + t * 32 + i], ACT == CFSD_ACT_ELU ? elu_f(v) : v);
         }
       }
   }
@@ -558,7 +567,7 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
                                                     const float* __restrict__ w,
                                                     const float* __restrict__ bias,
                                                     float* __restrict__ y, int vsrc, int rows,
-                                                    long total_rows) {
+                                                    long total_rows, int batch, int xvm, int yvm) {
   // CTW column tiles per wave share the wave's A gathers
   constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN, NTW = NCT / CTW;
   constexpr int FSB = CFSD_FWD_LAT_SB;
@@ -573,13 +582,14 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
   long m = rt * 16 + r16;
   if (m >= total_rows) m = total_rows - 1;  // clamp loads, stores are masked
   int b, r;
-  divmod32(m, rows, b, r);
-  const float* xb = x + (long)b * vsrc * CIN + 4 * kg;
+  split_row(m, xvm, batch, rows, b, r);  // rows in x's layout (vertex-major: 16 meshes of a vertex)
+  const Lay lx = make_lay(xvm, batch, vsrc);
+  const float* xb = x + (long)b * lx.bs * CIN + 4 * kg;
   const int* ir = idx + (long)r * kSeq;
   const float* wb = w + (long)(ct0 * 16 + r16) * K + 4 * kg;  // + t*16*K
   int src[kSeq];
 #pragma unroll
-  for (int s = 0; s < kSeq; ++s) src[s] = ir[s];
+  for (int s = 0; s < kSeq; ++s) src[s] = ir[s] * lx.vs;
   f32x4 acc[CTW][2];
 #pragma unroll
   for (int t = 0; t < CTW; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -622,7 +632,13 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
       if (mo < total_rows) {
         float v = acc[t][0][rr] + acc[t][1][rr] + bn;
         if (ACT == CFSD_ACT_ELU) v = elu_f(v);
-        y[mo * COUT + n] = v;
+        long yo = mo;
+        if (xvm != yvm) {
+          int bo, ro;
+          split_row(mo, xvm, batch, rows, bo, ro);
+          yo = row_of(make_lay(yvm, batch, rows), bo, ro);
+        }
+        y[yo * COUT + n] = v;
       }
     }
   }
@@ -845,7 +861,8 @@ struct DwCfg {
 template <int CIN, int COUT>
 __global__ __launch_bounds__(768) void conv_dw_mfma(
     const float* __restrict__ x, const int* __restrict__ idx, const float* __restrict__ dpre,
-    float* __restrict__ ws, float* __restrict__ ws_db, int vsrc, int rows, long total_rows) {
+    float* __restrict__ ws, float* __restrict__ ws_db, int vsrc, int rows, long total_rows, int batch,
+    int xvm, int dpvm) {
   using C = DwCfg<CIN, COUT>;
   constexpr int OT = COUT / 32, CT = CIN / 32;
   extern __shared__ float lds[];
@@ -861,6 +878,10 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
   for (int q = 0; q < C::UPW; ++q) acc[q] = (f32x16){0.f};
   float db_acc = 0.f;
 
+  // K (rows) is visited in x's layout (vertex-major: a 32-row tile is 2
+  // vertices x 16 meshes, so each slot's gathered rows are two contiguous
+  // blocks); dpre rows are addressed in their own layout
+  const Lay lx = make_lay(xvm, batch, vsrc), ldp = make_lay(dpvm, batch, rows);
   f32x4 xs[C::XPT], ds[C::DPT];
   auto load_tile = [&](long tile) {
     const long m0 = tile * 32;
@@ -873,10 +894,10 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
         const int s = f / (32 * CIN / 4);
         long m = m0 + row;
         if (m >= total_rows) m = total_rows - 1;
-        const int mi = (int)m;  // < 2^31 rows: 32-bit division
-        const int b = mi / rows, r = mi - b * rows;
+        int b, r;  // < 2^31 rows: 32-bit division
+        split_row(m, xvm, batch, rows, b, r);
         const int src = idx[r * kSeq + s];
-        xs[e] = ld4(x + ((long)b * vsrc + src) * CIN + 4 * c4);
+        xs[e] = ld4(x + ((long)b * lx.bs + (long)src * lx.vs) * CIN + 4 * c4);
       }
     }
 #pragma unroll
@@ -885,7 +906,13 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
       if (f < C::DF4) {
         const int row = f / (COUT / 4);
         const long m = m0 + row;
-        ds[e] = m < total_rows ? ld4(dpre + m * COUT + 4 * (f % (COUT / 4)))
+        long dr = m;
+        if (xvm != dpvm && m < total_rows) {
+          int b, r;
+          split_row(m, xvm, batch, rows, b, r);
+          dr = row_of(ldp, b, r);
+        }
+        ds[e] = m < total_rows ? ld4(dpre + dr * COUT + 4 * (f % (COUT / 4)))
                                : (f32x4){0.f, 0.f, 0.f, 0.f};
       }
     }
@@ -989,7 +1016,8 @@ __device__ __forceinline__ void conv_dw_lat_body(int vb, int vnb, const float* _
                                                  const float* __restrict__ dpre,
                                                  float* __restrict__ ws,
                                                  float* __restrict__ ws_db, int vsrc, int rows,
-                                                 int total_rows, int rchunk, int n_chunks) {
+                                                 int total_rows, int rchunk, int n_chunks, int batch,
+                                                 int xvm, int dpvm) {
   constexpr int OT = COUT / 32, CT = CIN / 32, U = kSeq * OT * CT, NB = 8;
   const int lane = threadIdx.x & 63, li = lane & 31, h = lane >> 5;
   const long task = (long)xcd_block_of(vb, vnb) * 4 + (threadIdx.x >> 6);
@@ -997,9 +1025,13 @@ __device__ __forceinline__ void conv_dw_lat_body(int vb, int vnb, const float* _
   const int unit = (int)(task % U), chunk = (int)(task / U);
   const int ct = unit % CT, ot = (unit / CT) % OT, sl = unit / (CT * OT);
   const int r0 = chunk * rchunk, r1 = min(total_rows, r0 + rchunk);
-  // (b, r) of this lane's first row, advanced incrementally by 2 per step
+  // (b, r) of this lane's first row (flat dpre row m in dpre's layout:
+  // minor index mi of extent E, major ma), advanced incrementally by 2 per
+  // step; x rows are addressed in x's layout
+  const Lay lx = make_lay(xvm, batch, vsrc);
+  const int E = dpvm ? batch : rows;
   int m = r0 + h;
-  int b = m / rows, r = m - b * rows;
+  int ma = m / E, mi = m - ma * E;
   const float* dp = dpre + ot * 32 + li;
   const float* xs = x + ct * 32 + li;
   f32x16 acc[2];
@@ -1009,7 +1041,8 @@ __device__ __forceinline__ void conv_dw_lat_body(int vb, int vnb, const float* _
     for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
   float dbs = 0.f;
   const bool do_db = sl == 0 && ct == 0;
-  const int b_last = (r1 - 1) / rows, r_last = (r1 - 1) - b_last * rows;
+  int b_last, r_last;
+  split_row(r1 - 1, dpvm, batch, rows, b_last, r_last);
   static_assert(NB == 8, "vm_wait_arr8");
   // Rows past the chunk are clamped to its last row (loads stay in bounds,
   // no branches) and weighted 0.  Pipelined one batch ahead: while batch i's
@@ -1025,14 +1058,18 @@ __device__ __forceinline__ void conv_dw_lat_body(int vb, int vnb, const float* _
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const bool ok = m < r1;
+      const int b = dpvm ? mi : ma, r = dpvm ? ma : mi;
       ok_[j] = ok ? 1.f : 0.f;
-      bs[j] = (ok ? b : b_last) * vsrc;
-      sr[j] = idx[(ok ? r : r_last) * kSeq + sl];
+      bs[j] = (ok ? b : b_last) * lx.bs;
+      sr[j] = idx[(ok ? r : r_last) * kSeq + sl] * lx.vs;
       m += 2;
-      r += 2;
-      const bool wrap = r >= rows;
-      r = wrap ? r - rows : r;
-      b = wrap ? b + 1 : b;
+      mi += 2;
+      bool wrap = mi >= E;
+      mi = wrap ? mi - E : mi;
+      ma = wrap ? ma + 1 : ma;
+      wrap = mi >= E;  // extent 1
+      mi = wrap ? mi - E : mi;
+      ma = wrap ? ma + 1 : ma;
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) a_[j] = dp[(long)min(m0_ + h + 2 * j, r1 - 1) * COUT];
@@ -1081,9 +1118,10 @@ __global__ __launch_bounds__(256) void conv_dw_lat(const float* __restrict__ x,
                                                    const float* __restrict__ dpre,
                                                    float* __restrict__ ws,
                                                    float* __restrict__ ws_db, int vsrc, int rows,
-                                                   int total_rows, int rchunk, int n_chunks) {
+                                                   int total_rows, int rchunk, int n_chunks, int batch,
+                                                   int xvm, int dpvm) {
   conv_dw_lat_body<CIN, COUT>(blockIdx.x, gridDim.x, x, idx, dpre, ws, ws_db, vsrc, rows,
-                              total_rows, rchunk, n_chunks);
+                              total_rows, rchunk, n_chunks, batch, xvm, dpvm);
 }
 
 // Both gradients of one coarse-level conv in ONE launch (horizontal fusion):
@@ -1112,6 +1150,7 @@ struct DwLatArgs {
   float* ws_db;
   int vsrc, rows, total_rows, rchunk, n_chunks;
   int nb;
+  int batch, xvm, dpvm;  // layouts of x / dpre (cfsd.h CFSD_VM)
 };
 template <int CIN, int COUT, int CTW>
 __global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, const DwLatArgs d) {
@@ -1130,7 +1169,7 @@ __global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, cons
                                      a.elu_y, a.dx, a.vsrc, a.rows, a.total_rows);
   else
     conv_dw_lat_body<CIN, COUT>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows,
-                                d.total_rows, d.rchunk, d.n_chunks);
+                                d.total_rows, d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm);
 }
 
 // ==========================================================================
@@ -1244,7 +1283,7 @@ __global__ __launch_bounds__(256) void conv_bwd_rowsub_pair(const DgArgs a, cons
     conv_dg_body<CIN, COUT>(vb, a.nb, a, wl);
   else
     conv_dw_lat_body<CIN, COUT>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows,
-                                d.total_rows, d.rchunk, d.n_chunks);
+                                d.total_rows, d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm);
 }
 
 // (2): a thread per (source row, 16-B channel chunk); the row's flat list
@@ -2192,7 +2231,7 @@ static int dispatch_fwd_mfma(const float* x, const int* idx, const float* w, con
     constexpr int ctw = (CIN == 32 && COUT == 32) ? CFSD_FWD_LAT_CTW : (CIN == 64 ? 2 : 1);
     const long tasks = (M + 15) / 16 * (COUT / 16 / ctw);
     hipLaunchKernelGGL((conv_fwd_lat<CIN, COUT, ACT, ctw>), dim3((unsigned)((tasks + 3) / 4)),
-                       dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M);
+                       dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M, (int)(M / rows), 0, 0);
     return launch_status("spiral_conv_fwd_lat");
   }
   constexpr bool big = (size_t)COUT * (kSeq * CIN + 8) * sizeof(float) > 80 * 1024;
@@ -2464,12 +2503,12 @@ extern "C" size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int
   return dw_geom(batch, rows, cin, cout).ws_floats * sizeof(float);
 }
 
-extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, const float* dpre,
-                                           float* dw, float* db, float* workspace,
-                                           size_t workspace_bytes, int batch, int vsrc, int rows,
-                                           int seq, int cin, int cout, void* stream) {
-  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
-  if (rc) return rc;
+// dW / db of an fp32 conv, x and dpre each batch-major or vertex-major
+// (xvm / dpvm; the small-channel kernels are batch-major only).
+static int dw_f32(const float* x, int xvm, const int32_t* idx, const float* dpre, int dpvm, float* dw,
+                  float* db, float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows,
+                  int cin, int cout, hipStream_t st) {
+  int rc = CFSD_OK;
   if (!workspace) return set_error(CFSD_EINVAL, "null workspace");
   if ((dw == nullptr) != (db == nullptr))
     return set_error(CFSD_EINVAL, "dw and db must both be set (or both NULL: deferred)");
@@ -2480,7 +2519,8 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
   if (workspace_bytes < g.ws_floats * sizeof(float))
     return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes,
                      g.ws_floats * sizeof(float));
-  hipStream_t st = (hipStream_t)stream;
+  if ((xvm || dpvm) && g.kind != kDwLat && g.kind != kDwMfma)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight: vertex-major operands need 32/64 channels");
   const long M = (long)batch * rows;
   const int n_el = cout * kSeq * cin + cout;
   const dim3 rg((unsigned)((n_el + 63) / 64));
@@ -2491,7 +2531,7 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
   if (cin == CIN_ && cout == COUT_) {                                                           \
     hipLaunchKernelGGL((conv_dw_lat<CIN_, COUT_>), dim3((unsigned)((tasks + 3) / 4)), dim3(256), \
                        0, st, x, idx, dpre, workspace, ws_db, vsrc, rows, (int)M, g.rchunk,      \
-                       g.gx);                                                                   \
+                       g.gx, batch, xvm, dpvm);                                                 \
     rc = launch_status("spiral_conv_bwd_weight_lat");                                           \
     if (rc || deferred) return rc;                                                              \
     hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), rg, dim3(1024), 0, st, workspace, ws_db,  \
@@ -2510,7 +2550,7 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
     auto k = conv_dw_mfma<CIN_, COUT_>;                                                         \
     nslab = dw_mfma_slabs(cin, cout, g.gx);                                                     \
     hipLaunchKernelGGL(k, dim3(nslab), dim3(C::THREADS), C::LDS_FLOATS * sizeof(float), st, x,  \
-                       idx, dpre, workspace, ws_db, vsrc, rows, M);                             \
+                       idx, dpre, workspace, ws_db, vsrc, rows, M, batch, xvm, dpvm);           \
     rc = launch_status("spiral_conv_bwd_weight");                                               \
     if (rc || deferred) return rc;                                                              \
     hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), rg, dim3(1024), 0, st, workspace, ws_db,  \
@@ -2541,6 +2581,16 @@ extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, c
   }
 #undef DWS
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight: unsupported channels %d -> %d", cin, cout);
+}
+
+extern "C" int cfsd_spiral_conv_bwd_weight(const float* x, const int32_t* idx, const float* dpre,
+                                           float* dw, float* db, float* workspace,
+                                           size_t workspace_bytes, int batch, int vsrc, int rows,
+                                           int seq, int cin, int cout, void* stream) {
+  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  return dw_f32(x, 0, idx, dpre, 0, dw, db, workspace, workspace_bytes, batch, vsrc, rows, cin, cout,
+                (hipStream_t)stream);
 }
 
 // ---- fused backward (data + weight)
@@ -2607,7 +2657,7 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
     float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
     DxLatArgs a{dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M, 0};
     DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, batch * rows, g.rchunk, g.gx,
-                (int)((dw_tasks + 3) / 4)};
+                (int)((dw_tasks + 3) / 4), batch, 0, 0};
     const int ctw = dx_lat_ctw(cin, cout, M);
     a.nb = (int)(((M + 15) / 16 * (cin / 16 / ctw) + 3) / 4);
     const dim3 grid((unsigned)(a.nb + d.nb));
@@ -2713,7 +2763,7 @@ extern "C" int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, c
   a.nb = (int)(((total + 15) / 16 + 3) / 4) * a.n_groups;
   const bool lat = g.kind == kDwLat;
   float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
-  DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, total, g.rchunk, g.gx, 0};
+  DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, total, g.rchunk, g.gx, 0, batch, 0, 0};
   if (lat) d.nb = (int)(((long)g.gx * (long)dw_units(cin, cout) + 3) / 4);
   const dim3 grid((unsigned)(a.nb + d.nb));
   const int n_el = cout * kSeq * cin + cout;
@@ -2860,6 +2910,55 @@ extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* id
   }
   y_dt = CFSD_DT_TYPE(y_dt);
   if (!w) return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: w required");
+  if (mfma_shape(cin, cout) && x_dt == CFSD_DT_F32 && xvm) {  // fp32 vertex-major
+    if (y_dt != CFSD_DT_F32) return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: fp32 x needs fp32 y");
+    if (M < CFSD_LAT_FWD_MAX && cin == 32 && cout == 32) {  // few rows (an Enblock's kept rows): 16x16 tasks
+      const long tasks = (M + 15) / 16 * 2;
+      if (act == CFSD_ACT_ELU)
+        hipLaunchKernelGGL((conv_fwd_lat<32, 32, CFSD_ACT_ELU, 1>), dim3((unsigned)((tasks + 3) / 4)), dim3(256),
+                           0, st, (const float*)x, idx, w, bias, (float*)y, vsrc, rows, M, batch, xvm, yvm);
+      else
+        hipLaunchKernelGGL((conv_fwd_lat<32, 32, CFSD_ACT_NONE, 1>), dim3((unsigned)((tasks + 3) / 4)), dim3(256),
+                           0, st, (const float*)x, idx, w, bias, (float*)y, vsrc, rows, M, batch, xvm, yvm);
+      return launch_status("spiral_conv_fwd_lat_x");
+    }
+    return vm32::launch_fwd((const float*)x, idx, w, bias, (float*)y, yvm, vsrc, rows, batch, cin, cout, act, st);
+  }
+  if (cin <= 3 && (cout == 32 || cout == 64) && x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) {
+#define FINF(CS_, CO_)                                                                           \
+  if (cin == CS_ && cout == CO_) {                                                               \
+    if (act == CFSD_ACT_ELU)                                                                     \
+      hipLaunchKernelGGL((conv_fwd_in_mfma<CS_, CO_, CFSD_ACT_ELU, float>), dim3(gp), dim3(256),  \
+                         0, st, (const float*)x, idx, w, bias, (float*)y, vsrc, rows, M, batch,  \
+                         xvm, yvm);                                                              \
+    else                                                                                         \
+      hipLaunchKernelGGL((conv_fwd_in_mfma<CS_, CO_, CFSD_ACT_NONE, float>), dim3(gp), dim3(256), \
+                         0, st, (const float*)x, idx, w, bias, (float*)y, vsrc, rows, M, batch,  \
+                         xvm, yvm);                                                              \
+    return launch_status("spiral_conv_fwd_in_x");                                                \
+  }
+    const long tiles = (M + 31) / 32;
+    const unsigned gp = (unsigned)((tiles + 3) / 4 < 2048 ? (tiles + 3) / 4 : 2048);
+    FINF(1, 32) FINF(2, 32) FINF(3, 32) FINF(1, 64) FINF(2, 64) FINF(3, 64)
+#undef FINF
+  }
+  if (cout <= 3 && (cin == 16 || cin == 32 || cin == 64) && x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) {
+#define FOUTF(CI_, CO_)                                                                           \
+  if (cin == CI_ && cout == CO_) {                                                                \
+    if (act == CFSD_ACT_ELU) {                                                                    \
+      auto k = conv_fwd_out_small<CI_, CO_, CFSD_ACT_ELU, float>;                                 \
+      hipLaunchKernelGGL(k, dim3(small_grid(k, M)), dim3(256), 0, st, (const float*)x, idx, w,    \
+                         bias, (float*)y, vsrc, rows, M, batch, xvm, yvm);                        \
+    } else {                                                                                      \
+      auto k = conv_fwd_out_small<CI_, CO_, CFSD_ACT_NONE, float>;                                \
+      hipLaunchKernelGGL(k, dim3(small_grid(k, M)), dim3(256), 0, st, (const float*)x, idx, w,    \
+                         bias, (float*)y, vsrc, rows, M, batch, xvm, yvm);                        \
+    }                                                                                             \
+    return launch_status("spiral_conv_fwd_out_x");                                                \
+  }
+    FOUTF(16, 3) FOUTF(32, 3) FOUTF(64, 3) FOUTF(32, 1) FOUTF(32, 2)
+#undef FOUTF
+  }
   if (cin <= 3 && (cout == 32 || cout == 64) && x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_BF16) {
     const long tiles = (M + 31) / 32;
     const unsigned gp = (unsigned)((tiles + 3) / 4 < 2048 ? (tiles + 3) / 4 : 2048);
@@ -2920,20 +3019,27 @@ extern "C" int cfsd_spiral_conv_bwd_data_x(const void* dpre, int dpre_dt, const 
 }
 
 extern "C" int cfsd_spiral_conv_bwd_data_flat(const void* dpre, int dpre_dt, const int32_t* inv_flat,
-                                              int flat_width, const uint16_t* w_bf16, const uint16_t* elu_y,
-                                              uint16_t* dx, int dx_dt, int batch, int vsrc, int rows, int seq,
-                                              int cin, int cout, void* stream) {
-  int rc = check_conv_args(dpre, inv_flat, w_bf16, batch, vsrc, rows, seq, cin, cout);
+                                              int flat_width, const void* w, const void* elu_y, void* dx,
+                                              int dx_dt, int batch, int vsrc, int rows, int seq, int cin,
+                                              int cout, void* stream) {
+  int rc = check_conv_args(dpre, inv_flat, w, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
   if (!dx) return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat: null dx");
-  if (!dt_ok(dpre_dt) || !dt_ok(dx_dt) || CFSD_DT_TYPE(dx_dt) != CFSD_DT_BF16 || !vm_of(dpre_dt) || !vm_of(dx_dt))
-    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat: dpre and dx must be vertex-major (CFSD_VM), dx bf16");
+  if (!dt_ok(dpre_dt) || !dt_ok(dx_dt) || !vm_of(dpre_dt) || !vm_of(dx_dt))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat: dpre and dx must be vertex-major (CFSD_VM)");
+  if (CFSD_DT_TYPE(dx_dt) == CFSD_DT_F32) {  // fp32 operands and weights (spiral_conv_vm32.hip)
+    if (CFSD_DT_TYPE(dpre_dt) != CFSD_DT_F32)
+      return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat: fp32 dx needs fp32 dpre");
+    if ((uintptr_t)inv_flat & 15) return set_error(CFSD_EINVAL, "inv_flat must be 16-B aligned");
+    return vm32::launch_dx_flat((const float*)dpre, inv_flat, flat_width, (const float*)w, (const float*)elu_y,
+                                (float*)dx, vsrc, rows, batch, cin, cout, (hipStream_t)stream);
+  }
   if (!bf::vm16_ok(batch, cin, cout))
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat: batch %% 16 == 0 and 32 -> 32/64 channels only");
   if ((uintptr_t)inv_flat & 15) return set_error(CFSD_EINVAL, "inv_flat must be 16-B aligned");
   if ((long)batch * rows * cout * (CFSD_DT_TYPE(dpre_dt) == CFSD_DT_F32 ? 4L : 2L) >= (long)kAbsentRow)
     return set_error(CFSD_EINVAL, "dpre exceeds 32-bit buffer offsets");
-  return bf::launch_dx_flat_vm16(dpre, dpre_dt, inv_flat, flat_width, (const bf16_t*)w_bf16,
+  return bf::launch_dx_flat_vm16(dpre, dpre_dt, inv_flat, flat_width, (const bf16_t*)w,
                                  (const bf16_t*)elu_y, (bf16_t*)dx, vsrc, rows, batch, cin, cout,
                                  (hipStream_t)stream);
 }
@@ -2967,18 +3073,30 @@ extern "C" int cfsd_spiral_conv_bwd_weight_x(const void* x, int x_dt, const int3
   const int xvm = vm_of(x_dt), dpvm = vm_of(dpre_dt);
   x_dt = CFSD_DT_TYPE(x_dt);
   int n_slabs = 0;
+  if (mfma_shape(cin, cout) && x_dt == CFSD_DT_F32) {  // fp32: the fp32 kernels, x / dpre in any layout
+    if (CFSD_DT_TYPE(dpre_dt) != CFSD_DT_F32)
+      return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_x: fp32 x needs fp32 dpre");
+    return dw_f32((const float*)x, xvm, idx, (const float*)dpre, dpvm, dw, db, workspace, workspace_bytes, batch,
+                  vsrc, rows, cin, cout, st);
+  }
   if (mfma_shape(cin, cout) && x_dt == CFSD_DT_BF16) {
     rc = bf::launch_dw((const bf16_t*)x, xvm, idx, dpre, dpre_dt, workspace, vsrc, rows, M, cin, cout, st);
     n_slabs = bf::dw_slabs(batch, rows, cin, cout);
-  } else if (cin <= 3 && (cout == 32 || cout == 64) && x_dt == CFSD_DT_F32 &&
-             CFSD_DT_TYPE(dpre_dt) == CFSD_DT_BF16) {
+  } else if (cin <= 3 && (cout == 32 || cout == 64) && x_dt == CFSD_DT_F32) {
     const DwGeom g = dw_geom(batch, rows, cin, cout);
     if (g.kind != kDwInMfma) return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_x: geometry");
+    const bool dbf = CFSD_DT_TYPE(dpre_dt) == CFSD_DT_BF16;
 #define DWIB(CS_, CO_)                                                                             \
-  if (cin == CS_ && cout == CO_)                                                                   \
-    hipLaunchKernelGGL((conv_dw_in_mfma<CS_, CO_, bf16_t>), dim3(g.gx), dim3(256), 0, st,          \
-                       (const float*)x, idx, (const bf16_t*)dpre, workspace, vsrc, rows, M, batch,  \
-                       xvm, dpvm);
+  if (cin == CS_ && cout == CO_) {                                                                 \
+    if (dbf)                                                                                       \
+      hipLaunchKernelGGL((conv_dw_in_mfma<CS_, CO_, bf16_t>), dim3(g.gx), dim3(256), 0, st,        \
+                         (const float*)x, idx, (const bf16_t*)dpre, workspace, vsrc, rows, M, batch, \
+                         xvm, dpvm);                                                               \
+    else                                                                                           \
+      hipLaunchKernelGGL((conv_dw_in_mfma<CS_, CO_, float>), dim3(g.gx), dim3(256), 0, st,         \
+                         (const float*)x, idx, (const float*)dpre, workspace, vsrc, rows, M, batch,  \
+                         xvm, dpvm);                                                               \
+  }
     DWIB(1, 32) DWIB(2, 32) DWIB(3, 32) DWIB(1, 64) DWIB(2, 64) DWIB(3, 64)
 #undef DWIB
     rc = launch_status("spiral_conv_bwd_weight_in_bf16");
@@ -3000,7 +3118,8 @@ extern "C" int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* id
                                       int cin, int cout, void* stream) {
   int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
-  if (!dt_ok(x_dt) || CFSD_DT_TYPE(x_dt) != CFSD_DT_BF16) return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: x must be bf16");
+  if (!dt_ok(x_dt)) return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: bad x dtype");
+  const bool xbf = CFSD_DT_TYPE(x_dt) == CFSD_DT_BF16;  // x, elu_y and dx share x's storage
   if (!dt_ok(dpre_dt) || CFSD_DT_TYPE(dpre_dt) != CFSD_DT_F32)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: dpre must be fp32");
   if (!fused_small(cin, cout))
@@ -3018,10 +3137,16 @@ extern "C" int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* id
   const int n_el = cout * kSeq * cin + cout;
 #define BOSB(CIN_, CO_)                                                                          \
   if (cin == CIN_ && cout == CO_) {                                                              \
-    hipLaunchKernelGGL((conv_bwd_out_mfma<CIN_, CO_, bf16_t>), dim3(gx), dim3(256), 0, st, dpre, \
-                       inv_ptr, inv_row, (const int4*)inv_head, w, (const bf16_t*)elu_y,          \
-                       (const bf16_t*)x, (bf16_t*)dx, workspace, vsrc, rows, Ms, batch,           \
-                       vm_of(x_dt), vm_of(dpre_dt));                                              \
+    if (xbf)                                                                                     \
+      hipLaunchKernelGGL((conv_bwd_out_mfma<CIN_, CO_, bf16_t>), dim3(gx), dim3(256), 0, st, dpre, \
+                         inv_ptr, inv_row, (const int4*)inv_head, w, (const bf16_t*)elu_y,        \
+                         (const bf16_t*)x, (bf16_t*)dx, workspace, vsrc, rows, Ms, batch,         \
+                         vm_of(x_dt), vm_of(dpre_dt));                                            \
+    else                                                                                         \
+      hipLaunchKernelGGL((conv_bwd_out_mfma<CIN_, CO_, float>), dim3(gx), dim3(256), 0, st, dpre, \
+                         inv_ptr, inv_row, (const int4*)inv_head, w, (const float*)elu_y,         \
+                         (const float*)x, (float*)dx, workspace, vsrc, rows, Ms, batch,           \
+                         vm_of(x_dt), vm_of(dpre_dt));                                            \
     rc = launch_status("spiral_conv_bwd_small_bf16");                                            \
     if (rc || !dw) return rc;                                                                    \
     hipLaunchKernelGGL(slab_reduce, dim3((unsigned)((n_el + 63) / 64)), dim3(1024), 0, st,        \

@@ -845,7 +845,7 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
 
 using namespace cfsd;
 
-extern "C" int cfsd_version(void) { return (4 << 16) | 0; }  // 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments)
+extern "C" int cfsd_version(void) { return (4 << 16) | 1; }  // 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands
 extern "C" const char* cfsd_last_error_string(void) { return g_err; }
 
 extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {

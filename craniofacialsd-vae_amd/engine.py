@@ -133,7 +133,8 @@ class SDVAEEngine:
     topology and any number of batch sizes (buffers cached per batch)."""
 
     def __init__(self, topo, spec=None, lr=1e-4, weight_decay=0.0, w_kl=1e-4, w_lc=0.5,
-                 w_lap=0.1, eta1=0.5, eta2=0.5, swap_bs=4, seed=0, device="cuda", precision="fp32"):
+                 w_lap=0.1, eta1=0.5, eta2=0.5, swap_bs=4, seed=0, device="cuda", precision="fp32",
+                 vertex_major=True):
         """``precision``: "fp32" (the reference's arithmetic, the parity
         configuration) or "bf16" (configs C3/C5: the level-0/1 activations
         and gradients -- the large tensors -- stored in bf16 and VERTEX-MAJOR
@@ -141,7 +142,13 @@ class SDVAEEngine:
         block, so every spiral gather is a coalesced wave load), their convs
         on bf16 MFMA with the bf16 shadow of the fp32 master weights, fp32
         accumulation; the network input / output, coarse levels, bottleneck,
-        losses, gradients and Adam stay fp32 batch-major)."""
+        losses, gradients and Adam stay fp32 batch-major).
+
+        ``vertex_major`` (fp32): store the level-0/1 32-channel tensors
+        vertex-major too, for batches that are a multiple of 16 (the fp32
+        vertex-major kernels: same forward outputs bit for bit, the data
+        gradient through the flat inverse list); False keeps every fp32 tensor
+        batch-major (the reference's [B, V, C])."""
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
         self.precision = precision
@@ -168,6 +175,7 @@ class SDVAEEngine:
                 raise ValueError("bf16 precision needs 0/1 selection down-sampling and >= 3 levels")
             self.lp_levels = {0, 1}
             self.params.shadow = torch.zeros(self.params.numel, dtype=torch.bfloat16, device=self.device)
+        self.vertex_major = bool(vertex_major)
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -316,20 +324,44 @@ class SDVAEEngine:
         return int(last[-11:-3])
 
     # ----------------------------------------------------------- buffers
+    def vm_levels(self, bsz):
+        """Levels whose 32-channel tensors are stored vertex-major (and routed
+        through the mixed / vertex-major entry points) at batch ``bsz``: the
+        bf16 levels always; in fp32 levels 0 and 1 when the batch is a
+        multiple of 16, every down-sampling is a 0/1 selection, and the level's
+        convs fit the fp32 vertex-major kernels (32 -> 32/64 with flat
+        inverse lists)."""
+        if self.lp_levels:
+            return set(self.lp_levels)
+        T, S = self.topo, self.spec
+        if not (self.vertex_major and bsz % 16 == 0 and all(T.enc_select) and S.n >= 3):
+            return set()
+        for (cin, cout, lv, _) in S.dec_layers():
+            if lv in (0, 1) and not (cin == 32 and cout in (32, 64) and T.spiral_flat[lv] is not None):
+                return set()
+        for (cin, cout, lv) in S.enc_layers():
+            if lv == 1 and not (cin == 32 and cout in (32, 64) and T.enc_flat[1] is not None):
+                return set()
+        if S.enc_layers()[0][0] > 3 or S.out_ch[0] != 32:
+            return set()
+        return {0, 1}
+
     def buffers(self, bsz):
         if bsz in self._bufs:
             return self._bufs[bsz]
         T, S, dev = self.topo, self.spec, self.device
         f = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)  # noqa: E731
-        lp = self.lp_levels
+        lp = self.vm_levels(bsz)  # vertex-major levels (bf16 in bf16 mode)
+        ldt = torch.bfloat16 if self.lp_levels else torch.float32
 
         def fl(level, *shape):  # storage of a level's activation / gradient
-            if level in lp:  # bf16, vertex-major (ops.is_vm): a vertex's 16 mesh rows = one 1-KiB block
-                return ops.vm_empty(*shape, dtype=torch.bfloat16, device=dev)
+            if level in lp:  # vertex-major (ops.is_vm): a vertex's 16 mesh rows = one contiguous block
+                return ops.vm_empty(*shape, dtype=ldt, device=dev)
             return torch.empty(shape, dtype=torch.float32, device=dev)
 
         b = _Buffers()
         b.bsz = bsz
+        b.xl = lp
         nv = T.n_verts
         lat = S.latent
         last_enc = S.enc_layers()[-1][2]
@@ -412,7 +444,7 @@ class SDVAEEngine:
                 regions.append((key, rs))
                 return
             if low:
-                nb = ops.spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout)
+                nb = ops.spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout, ldt if cin > 3 else torch.float32)
             else:
                 nb = (ops.spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout) if b.paired[key]
                       else ops.spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout))
@@ -453,18 +485,29 @@ class SDVAEEngine:
         """bf16 shadow view of a conv weight (bf16 mode)."""
         return self.params.view(wname, self.params.shadow)
 
-    def _conv_fwd(self, b, x, idx, wname, act, out):
-        """SpiralConv forward on fp32 or mixed/bf16 operands."""
-        P = self.params
-        w, bias = P.view(wname + ".weight"), P.view(wname + ".bias")
-        if x.dtype == torch.float32 and out.dtype == torch.float32:
-            ops.spiral_conv_fwd(x, idx, w, bias, act, out=out, workspace=b.ws)
-        else:
-            ops.spiral_conv_fwd_x(x, idx, w, self._w16(wname + ".weight"), bias, act, out)
+    def _wx(self, wname):
+        """The weights the vertex-major kernels read: the bf16 shadow in bf16
+        mode, the fp32 master in fp32 mode."""
+        return self._w16(wname) if self.lp_levels else self.params.view(wname)
 
     @staticmethod
-    def _spmm(csr, x, m, out, elu_y=None, sched=None, uniform=0):
-        if x.dtype == torch.float32 and out.dtype == torch.float32:
+    def _plain(*ts):
+        """fp32 batch-major operands: the plain fp32 entry points apply."""
+        return all(t.dtype == torch.float32 and not ops.is_vm(t) for t in ts)
+
+    def _conv_fwd(self, b, x, idx, wname, act, out):
+        """SpiralConv forward on fp32, vertex-major or mixed/bf16 operands."""
+        P = self.params
+        w, bias = P.view(wname + ".weight"), P.view(wname + ".bias")
+        if self._plain(x, out):
+            ops.spiral_conv_fwd(x, idx, w, bias, act, out=out, workspace=b.ws)
+        else:
+            w16 = self._w16(wname + ".weight") if self.lp_levels else None
+            ops.spiral_conv_fwd_x(x, idx, w, w16, bias, act, out)
+
+    @classmethod
+    def _spmm(cls, csr, x, m, out, elu_y=None, sched=None, uniform=0):
+        if cls._plain(x, out):
             ops.spmm(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform)
         else:
             ops.spmm_x(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform)
@@ -599,7 +642,7 @@ class SDVAEEngine:
 
         weight_grad = ops.spiral_conv_bwd_weight
 
-        bwd_out = ops.spiral_conv_bwd_x if last_in.dtype == torch.bfloat16 else ops.spiral_conv_bwd
+        bwd_out = ops.spiral_conv_bwd_x if 0 in b.xl else ops.spiral_conv_bwd
         _, d = bwd_out(last_in, T.spiral[0], b.dout, T.spiral_inv[0],
                        P.view(f"de_layers.{n + 1}.layer.weight"), None, None,
                        dx=b.dpre_dec[-1], elu_y=last_in, workspace=b.ws_dw["out"])
@@ -608,10 +651,10 @@ class SDVAEEngine:
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]
             w, _ = self._dec_w(i)
-            if lv in self.lp_levels:  # bf16 operands: bf16 MFMA dW slabs + dx
+            if lv in b.xl:  # vertex-major (bf16 or fp32) operands: dW slabs + dx
                 defer(ops.spiral_conv_bwd_weight_x(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
                                                    b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
-                w16 = self._w16(f"de_layers.{i + 1}.conv.layer.weight")
+                w16 = self._wx(f"de_layers.{i + 1}.conv.layer.weight")
                 if self._flat_dx(b, lv, cin, cout):  # vertex-major, batch % 16: one MFMA per list entry
                     ops.spiral_conv_bwd_data_flat(b.dpre_dec[i], T.spiral_flat[lv], w16, T.n_verts[lv],
                                                   out=b.g_dec_up[i])
@@ -667,7 +710,7 @@ class SDVAEEngine:
     def _flat_dx(self, b, lv, cin, cout):
         """The flat-list bf16 data gradient applies (vertex-major level,
         batch a multiple of 16, 32 -> 32/64 channels, fan-in <= 20)."""
-        return (lv in self.lp_levels and b.bsz % 16 == 0 and cin == 32 and cout in (32, 64)
+        return (lv in b.xl and b.bsz % 16 == 0 and cin == 32 and cout in (32, 64)
                 and self.topo.spiral_flat[lv] is not None)
 
     def adam_args(self):
@@ -693,7 +736,7 @@ class SDVAEEngine:
             x_in = b.x if lv == 0 else b.enc_out[lv - 1]
             rows_tab = T.enc_rows[lv]
             prev = lv - 1
-            if lv in self.lp_levels:  # bf16 operands (selection down-sampling)
+            if lv in b.xl:  # vertex-major (bf16 or fp32) operands (selection down-sampling)
                 defer(ops.spiral_conv_bwd_weight_x(x_in, rows_tab, b.dpre_enc[lv], None, None,
                                                    b.ws_dw[("enc", lv)]), f"en_layers.{lv}.conv.layer")
                 if lv > 0 and b.dpre_enc[lv].dtype == torch.float32 and b.rowsub_x.get(lv):

@@ -734,28 +734,39 @@ def spiral_conv_bwd_data_x(dpre, inv, w_bf16, vsrc, elu_y=None, out=None):
     return out
 
 
-def spiral_conv_bwd_data_flat(dpre, flat, w_bf16, vsrc, elu_y=None, out=None):
-    """dx of a vertex-major bf16 layer through the flat inverse list
-    (``topology.spiral_flat``), batch a multiple of 16."""
+def spiral_conv_bwd_data_flat(dpre, flat, w, vsrc, elu_y=None, out=None):
+    """dx of a vertex-major layer through the flat inverse list
+    (``topology.spiral_flat``), batch a multiple of 16.  ``w`` bf16 (the
+    shadow; dx / elu_y bf16) or fp32 (dx, elu_y and dpre fp32: the fp32
+    step's vertex-major kernel)."""
     bsz, rows, cout = dpre.shape
     table, width = flat
     seq = 9
-    cin = w_bf16.shape[1] // seq
+    cin = w.shape[1] // seq
+    dt = w.dtype
+    if dt not in (torch.float32, torch.bfloat16):
+        raise ValueError(f"w must be fp32 or bf16, got {dt}")
     _needl(dpre, None, "dpre")
     _need(table, (vsrc, width), torch.int32, "inv_flat")
-    _need(w_bf16, (cout, seq * cin), torch.bfloat16, "w_bf16")
+    _need(w, (cout, seq * cin), dt, "w")
     if out is None:
-        out = vm_empty(bsz, vsrc, cin, dtype=torch.bfloat16, device=dpre.device)
-    _needl(out, (bsz, vsrc, cin), "dx", torch.bfloat16)
+        out = vm_empty(bsz, vsrc, cin, dtype=dt, device=dpre.device)
+    _needl(out, (bsz, vsrc, cin), "dx", dt)
+    if dt == torch.float32 and dpre.dtype != torch.float32:
+        raise ValueError("fp32 dx needs fp32 dpre")
     if elu_y is not None:
-        _needl(elu_y, (bsz, vsrc, cin), "elu_y", torch.bfloat16)
+        _needl(elu_y, (bsz, vsrc, cin), "elu_y", dt)
         _same_layout(out, elu_y, "dx and elu_y")
-    call("cfsd_spiral_conv_bwd_data_flat", ptr(dpre), _st(dpre), ptr(table), width, ptr(w_bf16), ptr(elu_y),
+    call("cfsd_spiral_conv_bwd_data_flat", ptr(dpre), _st(dpre), ptr(table), width, ptr(w), ptr(elu_y),
          ptr(out), _st(out), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
     return out
 
 
-def spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout):
+def spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout, x_dtype=torch.bfloat16):
+    """Workspace of :func:`spiral_conv_bwd_weight_x` (``x_dtype`` fp32: the
+    fp32 kernels' slab geometry, as :func:`spiral_conv_bwd_weight_workspace`)."""
+    if x_dtype == torch.float32:
+        return spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout)
     return int(_abi.lib().cfsd_spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout))
 
 
@@ -772,34 +783,38 @@ def spiral_conv_bwd_weight_x(x, idx, dpre, dw, db, workspace):
         _need(dw, (cout, seq * cin), name="dw")
         _need(db, (cout,), name="db")
     _need(workspace, None, name="workspace")
-    need = spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout)
+    need = spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout, x.dtype)
     nbytes = workspace.numel() * workspace.element_size()
     if nbytes < need:
         raise ValueError(f"workspace {nbytes} < {need} bytes")
     call("cfsd_spiral_conv_bwd_weight_x", ptr(x), _st(x), ptr(idx), ptr(dpre), _st(dpre), ptr(dw), ptr(db),
          ptr(workspace), ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
-    if dw is None:
-        mfma = cin in (32, 64) and cout in (32, 64)
+    if dw is None:  # bf16 32/64-channel slabs are plain (kind 2); fp32 x: the fp32 kernels' slabs
+        mfma = cin in (32, 64) and cout in (32, 64) and x.dtype == torch.bfloat16
         return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2 if mfma else 0)
     return None
 
 
 def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None):
-    """Fused dx + dW of the xyz output conv with bf16 x / elu_y / dx."""
+    """Fused dx + dW of the xyz output conv with bf16 (or fp32) x / elu_y /
+    dx in either layout."""
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape
     cout = dpre.shape[2]
     inv_ptr, inv_row, inv_head = inv
-    _needl(x, None, "x", torch.bfloat16)
+    xdt = x.dtype
+    if xdt not in (torch.float32, torch.bfloat16):
+        raise ValueError(f"x must be fp32 or bf16, got {xdt}")
+    _needl(x, None, "x", xdt)
     _need(idx, (rows, seq), torch.int32, "idx")
     _needl(dpre, (bsz, rows, cout), "dpre", torch.float32)
     _need(inv_head, (vsrc * seq, INV_HEAD), torch.int32, "inv_head")
     _need(w, (cout, seq * cin), name="w")
     if dx is not None:
-        _needl(dx, (bsz, vsrc, cin), "dx", torch.bfloat16)
+        _needl(dx, (bsz, vsrc, cin), "dx", xdt)
         _same_layout(x, dx, "x and dx")
     if elu_y is not None:
-        _needl(elu_y, (bsz, vsrc, cin), "elu_y", torch.bfloat16)
+        _needl(elu_y, (bsz, vsrc, cin), "elu_y", xdt)
         _same_layout(x, elu_y, "x and elu_y")
     if dw is not None or db is not None:
         _need(dw, (cout, seq * cin), name="dw")

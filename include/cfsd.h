@@ -374,7 +374,15 @@ int cfsd_scale(float* y, size_t n, float alpha, void* stream);
  * above (model.py:27-55 and autograd), products in bf16, sums in fp32.
  * 32/64-channel layers need x bf16 and the bf16 weight shadow `w_bf16`
  * ([cout, seq*cin], from cfsd_adam/cfsd_cast); the xyz layers use the fp32
- * `w` (input conv: x fp32 -> y bf16; output conv: x bf16 -> y fp32). */
+ * `w` (input conv: x fp32 -> y bf16; output conv: x bf16 -> y fp32).
+ *
+ * The same entry points take the fp32 step's VERTEX-MAJOR operands (ABI 4.1,
+ * the reference's fp32 arithmetic with the level-0/1 tensors stored
+ * [nv][batch][c], batch % 16 == 0): a 32 -> 32/64 layer with x_dt =
+ * CFSD_DT_F32 | CFSD_VM runs the fp32 vertex-major MFMA kernels with the fp32
+ * `w` (y fp32, either layout; same products in the same order as
+ * cfsd_spiral_conv_fwd, bit-identical outputs), and the xyz layers accept
+ * fp32 operands in either layout. */
 int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* idx, const float* w,
                            const uint16_t* w_bf16, const float* bias, void* y, int y_dt, int batch,
                            int vsrc, int rows, int seq, int cin, int cout, int act, void* stream);
@@ -389,25 +397,30 @@ int cfsd_spiral_conv_bwd_data_x(const void* dpre, int dpre_dt, const int32_t* in
  * source vertex the spiral positions p = r*seq + s naming it, ascending,
  * -1 padded to flat_width in {8, 12, 16, 20}): one MFMA per entry, exact
  * products (no bf16 rounding of per-slot row sums).  Vertex-major dpre / dx /
- * elu_y, batch % 16 == 0, 32 -> 32/64 channels (the bf16 step's level-0/1
- * Deblocks). */
+ * elu_y, batch % 16 == 0, 32 -> 32/64 channels (the level-0/1 Deblocks).
+ * dx_dt = CFSD_DT_BF16 | CFSD_VM: `w` is the bf16 shadow, elu_y bf16, dpre
+ * bf16 or fp32; dx_dt = CFSD_DT_F32 | CFSD_VM (ABI 4.1, the fp32 step): `w`,
+ * elu_y and dpre fp32 -- dx[u] = elu'(elu_y[u]) * sum over the list of
+ * W_s^T dpre[r] in list order (IndexSelectBackward's visiting order). */
 int cfsd_spiral_conv_bwd_data_flat(const void* dpre, int dpre_dt, const int32_t* inv_flat,
-                                   int flat_width, const uint16_t* w_bf16, const uint16_t* elu_y,
-                                   uint16_t* dx, int dx_dt, int batch, int vsrc, int rows, int seq,
-                                   int cin, int cout, void* stream);
-/* dW/db (fp32): 32/64-channel layers (x bf16, dpre bf16/fp32) and the xyz
- * input layer (x fp32, dpre bf16).  dw == db == NULL defers the reduction
- * (cfsd_dw_reduce_batch item with fused = 2 for the 32/64-channel kind, 0
- * for the input layer). */
+                                   int flat_width, const void* w, const void* elu_y, void* dx,
+                                   int dx_dt, int batch, int vsrc, int rows, int seq, int cin,
+                                   int cout, void* stream);
+/* dW/db (fp32): 32/64-channel layers (x bf16, dpre bf16/fp32; or x and dpre
+ * fp32, each batch-major or vertex-major) and the xyz input layer (x fp32,
+ * dpre bf16 or fp32).  dw == db == NULL defers the reduction
+ * (cfsd_dw_reduce_batch item with fused = 2 for the bf16 32/64-channel kind,
+ * 0 for fp32 x and for the input layer). */
 size_t cfsd_spiral_conv_bwd_weight_x_workspace(int batch, int rows, int seq, int cin, int cout);
 int cfsd_spiral_conv_bwd_weight_x(const void* x, int x_dt, const int32_t* idx, const void* dpre,
                                   int dpre_dt, float* dw, float* db, float* workspace,
                                   size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
                                   int cin, int cout, void* stream);
 /* Fused dx + dW of the xyz output layer (cout*seq <= 32) with x, elu_y, dx
- * bf16 and dpre fp32 (workspace: cfsd_spiral_conv_bwd_workspace; deferred
- * items use fused = 1).  x_dt's CFSD_VM flag is the layout of x, elu_y and
- * dx; dpre_dt = CFSD_DT_F32 [| CFSD_VM]. */
+ * bf16 (or all three fp32, ABI 4.1) and dpre fp32 (workspace:
+ * cfsd_spiral_conv_bwd_workspace; deferred items use fused = 1).  x_dt's
+ * storage type and CFSD_VM flag are those of x, elu_y and dx; dpre_dt =
+ * CFSD_DT_F32 [| CFSD_VM]. */
 int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* idx, const float* dpre,
                            int dpre_dt, const int32_t* inv_ptr, const int32_t* inv_row, const int32_t* inv_head,
                            const float* w, const void* elu_y, void* dx, float* dw, float* db,

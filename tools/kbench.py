@@ -76,7 +76,7 @@ def main():
         orders = locality_orders([npz[f"spiral_{l}"] for l in range(n)], int(npz[f"down_{n - 1}_shape"][0]))
         npz = relabel_npz(npz, orders)
     T = topology.DeviceTopology.from_npz(npz, device="cuda")
-    eng = E.SDVAEEngine(T, E.ModelSpec(), device="cuda")
+    eng = E.SDVAEEngine(T, E.ModelSpec(), device="cuda", vertex_major=False)
     b = eng.buffers(16)
     g = torch.Generator(device="cuda").manual_seed(0)
     for t in (b.x, b.dec_up[3], b.dec_out[3], b.dpre_dec[3], b.dout, b.dec_out[2], b.g_dec_up[3]):
@@ -230,6 +230,45 @@ def main():
                                         ops.spiral_conv_fwd_x(xin, T.spiral[0], w3h, w16, b3h, 1, yout))
     cases["fwd_d3_b16_self"] = lambda: ops.spiral_conv_fwd_x(c.dec_up[3], self_idx, w3h, w16, b3h, 1, c.dec_out[3])
     cases["fwd_d3_b16_shift"] = lambda: ops.spiral_conv_fwd_x(c.dec_up[3], shift_idx, w3h, w16, b3h, 1, c.dec_out[3])
+    # fp32 vertex-major kernels (the fp32 step's level-0/1 layers at batch 16)
+    ev = E.SDVAEEngine(T, E.ModelSpec(), device="cuda", vertex_major=True)
+    v = ev.buffers(16)
+    for t in (v.dec_up[3], v.dec_out[3], v.dpre_dec[3], v.dec_up[2], v.dpre_dec[2], v.enc_out[0],
+              v.dpre_enc[0]):
+        t.copy_(torch.randn(t.shape, device="cuda", generator=g))
+    v.dec_out[3].copy_(torch.nn.functional.elu(v.dec_out[3]))
+    w3v, b3v = ev._dec_w(3)
+    cases["fwd_d3_vm"] = lambda: ops.spiral_conv_fwd_x(v.dec_up[3], T.spiral[0], w3v, None, b3v, 1, v.dec_out[3])
+    cases["dxf_d3_vm"] = lambda: ops.spiral_conv_bwd_data_flat(v.dpre_dec[3], T.spiral_flat[0], w3v, T.n_verts[0],
+                                                               out=v.g_dec_up[3])
+    cases["dw_d3_vm"] = lambda: ops.spiral_conv_bwd_weight_x(v.dec_up[3], T.spiral[0], v.dpre_dec[3], None, None,
+                                                             v.ws_dw[("dec", 3)])
+    w2v, b2v = ev._dec_w(2)
+    cases["fwd_d2_vm"] = lambda: ops.spiral_conv_fwd_x(v.dec_up[2], T.spiral[1], w2v, None, b2v, 1, v.dec_out[2])
+    cases["dxf_d2_vm"] = lambda: ops.spiral_conv_bwd_data_flat(v.dpre_dec[2], T.spiral_flat[1], w2v, T.n_verts[1],
+                                                               out=v.g_dec_up[2])
+    cases["dw_d2_vm"] = lambda: ops.spiral_conv_bwd_weight_x(v.dec_up[2], T.spiral[1], v.dpre_dec[2], None, None,
+                                                             v.ws_dw[("dec", 2)])
+    wov, bov = ev.params.view("de_layers.5.layer.weight"), ev.params.view("de_layers.5.layer.bias")
+    cases["dout_fwd_vm"] = lambda: ops.spiral_conv_fwd_x(v.dec_out[3], T.spiral[0], wov, None, bov, 0, v.out)
+    cases["dout_bwd_vm"] = lambda: ops.spiral_conv_bwd_x(v.dec_out[3], T.spiral[0], v.dout, T.spiral_inv[0], wov,
+                                                         None, None, dx=v.dpre_dec[3], elu_y=v.dec_out[3],
+                                                         workspace=v.ws_dw["out"])
+    cases["e0_fwd_vm"] = lambda: ops.spiral_conv_fwd_x(v.x, T.enc_rows[0], *ev._enc_w(0)[:1], None, ev._enc_w(0)[1],
+                                                       1, v.enc_out[0])
+    cases["e0_dw_vm"] = lambda: ops.spiral_conv_bwd_weight_x(v.x, T.enc_rows[0], v.dpre_enc[0], None, None,
+                                                             v.ws_dw[("enc", 0)])
+    cases["fwd_e1_vm"] = lambda: ops.spiral_conv_fwd_x(v.enc_out[0], T.enc_rows[1], ev._enc_w(1)[0], None,
+                                                       ev._enc_w(1)[1], 1, v.enc_out[1])
+    cases["dw_e1_vm"] = lambda: ops.spiral_conv_bwd_weight_x(v.enc_out[0], T.enc_rows[1], v.dpre_enc[1], None, None,
+                                                             v.ws_dw[("enc", 1)])
+    cases["spmm_up0_vm"] = lambda: ops.spmm_x(T.up_csr[0], v.dec_out[2], T.n_verts[0], out=v.dec_up[3],
+                                              uniform=T.up_uniform[0])
+    cases["spmm_up0T_vm"] = lambda: ops.spmm_x(T.upT_csr[0], v.g_dec_up[3], T.n_verts[1], elu_y=v.dec_out[2],
+                                               out=v.dpre_dec[2], sched=T.upT_sched[0])
+    if "step_vm" in names:
+        ev.set_batch(b.x, key_index=3)
+        cases["step_vm"] = lambda: ev.train_step_on(v)
     if "step" in names:
         eng.set_batch(b.x, key_index=3)
         cases["step"] = lambda: eng.train_step_on(b)

@@ -13,3 +13,11 @@ for L in vm bm; do
   python tools/prof_summary.py $(find $O/prof_$L -name '*.db' | head -1) 45 > $O/kernel_stats_$L.txt
 done
 tail -48 $O/timeline_vm.txt
+# locality experiment: the same vertex-major kernels on an RCM-relabelled topology
+KBN="fwd_d3_vm dxf_d3_vm dw_d3_vm fwd_d2_vm dxf_d2_vm dw_d2_vm dout_fwd_vm dout_bwd_vm spmm_up0_vm spmm_up0T_vm fwd_d3 dx_d3 dw_d3"
+for R in 0 1; do
+  if [ $R = 1 ]; then export KB_REORDER=1; else unset KB_REORDER; fi
+  KB_ITERS=30 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kbprof_$R -o kb -- python3 tools/kbench.py $KBN > $O/kbprof_$R.log 2>&1 || { tail -20 $O/kbprof_$R.log; exit 1; }
+  python tools/prof_summary.py $(find $O/kbprof_$R -name '*.db' | head -1) 30 > $O/kb_stats_reorder$R.txt
+  echo "== reorder $R"; cat $O/kb_stats_reorder$R.txt
+done

@@ -229,13 +229,14 @@ def launch_cost(name, a):
         B, m, n, c = a[6:10]
         elu = a[4] is not None
         return 0.0, f4 * B * c * (n + m * (2 if elu else 1)), None
-    if name == "cfsd_swap_features":
-        bs, nv, c = a[5:8]
+    if name in ("cfsd_swap_features", "cfsd_swap_features_x"):
+        bs, nv, c = a[5:8] if name == "cfsd_swap_features" else a[6:9]
         return 0.0, f4 * (bs * nv * c + bs * bs * nv * c) + nv, None
-    if name == "cfsd_recon_lap_fwd":
+    if name in ("cfsd_recon_lap_fwd", "cfsd_recon_lap_fwd_x"):
         B, nv, c = a[7:10]
         return 0.0, f4 * 3 * B * nv * c, None
-    if name in ("cfsd_recon_lap_bwd", "cfsd_recon_lap_bwd_finalize"):
+    if name in ("cfsd_recon_lap_bwd", "cfsd_recon_lap_bwd_finalize", "cfsd_recon_lap_bwd_x",
+                "cfsd_recon_lap_bwd_finalize_x"):
         B, nv, c = a[7:10]
         return 0.0, f4 * 4 * B * nv * c, None
     if name == "cfsd_linear_fwd":

@@ -47,6 +47,7 @@ SIGNATURES = {
     "cfsd_spmm_csr_sched": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spmm_csr": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "cfsd_swap_features": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "cfsd_swap_features_x": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_normalize": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     "cfsd_spectral_blend": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "cfsd_linear_workspace": (_Z, [_I, _I, _I]),
@@ -57,6 +58,10 @@ SIGNATURES = {
     "cfsd_recon_lap_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P]),
     "cfsd_recon_lap_bwd_finalize": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P, _I, _P, _P,
                                          _P, _F, _F, _P]),
+    "cfsd_recon_lap_fwd_x": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "cfsd_recon_lap_bwd_x": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _I, _P]),
+    "cfsd_recon_lap_bwd_finalize_x": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P, _I, _P, _P,
+                                           _P, _F, _F, _I, _P]),
     "cfsd_latent_fwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F, _P]),
     "cfsd_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_loss_finalize": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P]),
@@ -68,6 +73,10 @@ SIGNATURES = {
     "cfsd_spiral_conv_bwd_weight_x": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_x": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I,
                                     _I, _I, _I, _P]),
+    "cfsd_spiral_conv_fwd_out_workspace": (_Z, [_I, _I, _I, _I, _I]),
+    "cfsd_spiral_conv_fwd_out": (_I, [_P, _I, _P, _P, _P, _P, _I, _P, _Z, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "cfsd_spiral_conv_bwd_out_flat": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I,
+                                           _I, _I, _I, _P]),
     "cfsd_spmm_csr_x": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spmm_uniform": (_I, [_I, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spmm_sched_csr": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),

@@ -19,12 +19,18 @@ int launch_fwd(const float* x, const int* idx, const float* w, const float* bias
 // spiral position p = 9r + s) of W_s^T dpre[r]; dpre, dx, elu_y vertex-major.
 int launch_dx_flat(const float* dpre, const int* flat, int width, const float* w, const float* elu_y,
                    float* dx, int vsrc, int rows, int batch, int cin, int cout, hipStream_t st);
-// dW / db partial slabs [n_slabs][cout*9*cin + cout] (plain layout, summed by
-// slab_reduce / dw_reduce_batch kind 2); x vertex-major, dpre vertex-major
-// (dpvm) or batch-major.
-int dw_slabs(int batch, int rows, int cin, int cout);
-int launch_dw(const float* x, const int* idx, const float* dpre, int dpvm, float* ws, int vsrc, int rows,
-              int batch, int cin, int cout, hipStream_t st);
+// dx (x's storage, times elu'(elu_y)) and the dW/db slab of one block per
+// n_slabs of the xyz output conv (32 -> 3); x / elu_y / dx / dout
+// vertex-major, flat = u's inverse list (topology.spiral_flat).
+int launch_bwd_out(const float* dout, const int* flat, int width, const float* w, const void* elu_y, const void* x,
+                   void* dx, int x_bf16, float* ws, int n_slabs, int vsrc, int rows, int batch, hipStream_t st);
+
+// Forward of the xyz output conv (32 -> 3) for a vertex-major x (fp32 or
+// bf16): Z = per-slot products of every source vertex into ws
+// (out_z_floats), then y = act(bias + sum_s Z[idx[v][s]][s]); y either layout.
+size_t out_z_floats(int batch, int vsrc);
+int launch_fwd_out(const void* x, int x_bf16, const int* idx, const float* w, const float* bias, float* y, int yvm,
+                   float* ws, int vsrc, int rows, int batch, int act, hipStream_t st);
 
 }  // namespace vm32
 }  // namespace cfsd

@@ -295,11 +295,11 @@ __global__ __launch_bounds__(256) void swap_k(const float* __restrict__ x,
                                               const unsigned char* __restrict__ mask,
                                               const int* __restrict__ key, float* __restrict__ out,
                                               int bs, int nv, int c, int n_meshes, int n_regions,
-                                              long total) {
+                                              long total, int yvm) {
   long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
-  int ob, v;
-  divmod32(t, nv, ob, v);
+  int ob, v;  // thread t = row t of the output storage (vertex-major: the bs^2 meshes of a vertex adjacent)
+  split_row(t, yvm, bs * bs, nv, ob, v);
   const int i = ob / bs, j = ob % bs;
   const int k = *key;
   const bool take = (i != j) && k >= 0 && k < n_regions && mask[(long)k * nv + v];
@@ -604,8 +604,24 @@ extern "C" int cfsd_swap_features(const float* x, const int32_t* batch_idx,
   if (total >= (1L << 31)) return set_error(CFSD_EINVAL, "swap_features: bs^2 x nv >= 2^31");
   hipLaunchKernelGGL(swap_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, x, batch_idx, region_mask, key, out, bs, nv, c, n_meshes,
-                     n_regions, total);
+                     n_regions, total, 0);
   return launch_status("swap_features");
+}
+
+extern "C" int cfsd_swap_features_x(const float* x, const int32_t* batch_idx, const uint8_t* region_mask,
+                                    const int32_t* key, float* out, int out_dt, int bs, int nv, int c,
+                                    int n_meshes, int n_regions, void* stream) {
+  if (!x || !batch_idx || !region_mask || !key || !out)
+    return set_error(CFSD_EINVAL, "swap_features_x: null pointer");
+  if (bs <= 0 || nv <= 0 || c <= 0 || n_meshes <= 0 || n_regions <= 0)
+    return set_error(CFSD_EINVAL, "swap_features_x: bad sizes");
+  if ((out_dt & ~CFSD_VM) != CFSD_DT_F32) return set_error(CFSD_EINVAL, "swap_features_x: bad dtype %d", out_dt);
+  const long total = (long)bs * bs * nv;
+  if (total >= (1L << 31)) return set_error(CFSD_EINVAL, "swap_features_x: bs^2 x nv >= 2^31");
+  hipLaunchKernelGGL(swap_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, batch_idx, region_mask, key, out, bs, nv, c, n_meshes,
+                     n_regions, total, (out_dt & CFSD_VM) != 0);
+  return launch_status("swap_features_x");
 }
 
 extern "C" int cfsd_spectral_blend(const float* s1, const float* s2, const float* values, float* s4,

@@ -3158,6 +3158,62 @@ extern "C" int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* id
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: unsupported channels %d -> %d", cin, cout);
 }
 
+// Forward of the xyz output conv for a vertex-major x in two passes through
+// a workspace (spiral_conv_vm32.hip conv_out_z_vm / conv_out_gather_vm).
+extern "C" size_t cfsd_spiral_conv_fwd_out_workspace(int batch, int vsrc, int seq, int cin, int cout) {
+  if (batch <= 0 || vsrc <= 0 || seq != kSeq || cin != 32 || cout != 3 || batch % 16) return 0;
+  return vm32::out_z_floats(batch, vsrc) * sizeof(float);
+}
+
+extern "C" int cfsd_spiral_conv_fwd_out(const void* x, int x_dt, const int32_t* idx, const float* w,
+                                        const float* bias, float* y, int y_dt, float* workspace,
+                                        size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
+                                        int cout, int act, void* stream) {
+  int rc = check_conv_args(x, idx, y, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!dt_ok(x_dt) || !vm_of(x_dt) || !dt_ok(y_dt) || CFSD_DT_TYPE(y_dt) != CFSD_DT_F32)
+    return set_error(CFSD_EINVAL, "spiral_conv_fwd_out: x must be vertex-major, y fp32");
+  if (cin != 32 || cout != 3) return set_error(CFSD_EINVAL, "spiral_conv_fwd_out: 32 -> 3 only (%d -> %d)", cin, cout);
+  if (!w || !workspace) return set_error(CFSD_EINVAL, "spiral_conv_fwd_out: null w / workspace");
+  if (act != CFSD_ACT_NONE && act != CFSD_ACT_ELU) return set_error(CFSD_EINVAL, "bad act %d", act);
+  const size_t need = cfsd_spiral_conv_fwd_out_workspace(batch, vsrc, seq, cin, cout);
+  if (need == 0 || workspace_bytes < need)
+    return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
+  return vm32::launch_fwd_out(x, CFSD_DT_TYPE(x_dt) == CFSD_DT_BF16, idx, w, bias, y, vm_of(y_dt), workspace, vsrc,
+                              rows, batch, act, (hipStream_t)stream);
+}
+
+// Fused dx + dW of the xyz output conv for vertex-major operands through the
+// flat inverse list (spiral_conv_vm32.hip conv_bwd_out_vm): same workspace
+// and slab layout as cfsd_spiral_conv_bwd_x (deferred items use fused = 1).
+extern "C" int cfsd_spiral_conv_bwd_out_flat(const void* x, int x_dt, const int32_t* idx, const float* dpre,
+                                             int dpre_dt, const int32_t* inv_flat, int flat_width, const float* w,
+                                             const void* elu_y, void* dx, float* dw, float* db, float* workspace,
+                                             size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
+                                             int cout, void* stream) {
+  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!dt_ok(x_dt) || !dt_ok(dpre_dt) || CFSD_DT_TYPE(dpre_dt) != CFSD_DT_F32 || !vm_of(x_dt) || !vm_of(dpre_dt))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_out_flat: x (and elu_y, dx) and fp32 dpre must be vertex-major");
+  if (cin != 32 || cout != 3 || vsrc != rows)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_out_flat: the 32 -> 3 output conv only (%d -> %d)", cin, cout);
+  if (!inv_flat || !w || !workspace) return set_error(CFSD_EINVAL, "spiral_conv_bwd_out_flat: null flat / w / workspace");
+  if ((uintptr_t)inv_flat & 15) return set_error(CFSD_EINVAL, "inv_flat must be 16-B aligned");
+  if ((dw == nullptr) != (db == nullptr))
+    return set_error(CFSD_EINVAL, "dw and db must both be set (or both NULL: deferred)");
+  const size_t need = cfsd_spiral_conv_bwd_workspace(batch, vsrc, rows, seq, cin, cout);
+  if (workspace_bytes < need) return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
+  const hipStream_t st = (hipStream_t)stream;
+  const int gx = fused_small_gx((long)batch * vsrc);
+  rc = vm32::launch_bwd_out(dpre, inv_flat, flat_width, w, elu_y, x, dx, CFSD_DT_TYPE(x_dt) == CFSD_DT_BF16,
+                            workspace, gx, vsrc, rows, batch, st);
+  if (rc || !dw) return rc;
+  const int n_el = cout * kSeq * cin + cout;
+  hipLaunchKernelGGL(slab_reduce, dim3((unsigned)((n_el + 63) / 64)), dim3(1024), 0, st, workspace, gx, n_el, dw,
+                     cout * kSeq * cin, db);
+  return launch_status("spiral_conv_bwd_out_flat_reduce");
+}
+
 static int dw_reduce_batch_launch(const cfsd_dw_slabs* items, int n, const DwAdam* adam, long n_params,
                                   void* stream) {
   if (n <= 0 && !adam) return CFSD_OK;

@@ -34,6 +34,11 @@ constexpr int kS = 9;
 constexpr int kAbsent = 0x7ffff000;  // out-of-range buffer offset: reads 0, no memory access
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// LDS written by a wave and read back by other lanes of the same wave
+__device__ __forceinline__ void wave_sync_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
 }
@@ -155,8 +160,14 @@ __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const fl
 // first), so the walk stops at the first -1 (uniform branch) and the
 // prefetches past the end are out-of-range loads (no memory access).  The
 // next tile's list is loaded at the start of this one.
+#ifndef CFSD_VM32_DX_PD
+#define CFSD_VM32_DX_PD 2  // list entries in flight ahead of the one being multiplied
+#endif
+#ifndef CFSD_VM32_DX_OCC
+#define CFSD_VM32_DX_OCC 1
+#endif
 template <int CIN, int COUT, int FW>
-__global__ __launch_bounds__(512) void conv_dx_flat_vm32(const float* __restrict__ dpre,
+__global__ __launch_bounds__(512, CFSD_VM32_DX_OCC) void conv_dx_flat_vm32(const float* __restrict__ dpre,
                                                          const int4* __restrict__ flat,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ elu_y,
@@ -204,16 +215,17 @@ __global__ __launch_bounds__(512) void conv_dx_flat_vm32(const float* __restrict
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    f32x4 buf[3][OC];
-    issue(0, buf[0]);
-    issue(1, buf[1]);
+    constexpr int PD = CFSD_VM32_DX_PD, NB = PD + 1;
+    f32x4 buf[NB][OC];
+#pragma unroll
+    for (int e = 0; e < PD; ++e) issue(e, buf[e]);
 #pragma unroll
     for (int e = 0; e < FW; ++e) {
-      if (e + 2 < FW) issue(e + 2, buf[(e + 2) % 3]);
+      if (e + PD < FW) issue(e + PD, buf[(e + PD) % NB]);
       if (pe[e] < 0) break;  // uniform: the rest of the list is padding
       const int s = pe[e] % kS;
       const float* wr = lwt + (s * CIN + j) * OP + 4 * g;
-      const f32x4(&cur)[OC] = buf[e % 3];
+      const f32x4(&cur)[OC] = buf[e % NB];
 #pragma unroll
       for (int c = 0; c < OC; ++c) {
         f32x4 a[NT];
@@ -248,6 +260,308 @@ __global__ __launch_bounds__(512) void conv_dx_flat_vm32(const float* __restrict
   }
 }
 
+
+// ------------------------------------------------------------------ output conv backward (32 -> 3)
+// dx and dW/db of the xyz output conv (model.py:172-173 and its autograd) for
+// vertex-major x / elu_y / dx and a vertex-major dout, batch % 16 == 0.
+// Wave = unit (source vertex u, mesh group mg):
+//  (1) T[s][m][o] = sum over u's flat inverse list (ascending p = 9r + s) of
+//      dout[r][m][o]: lane l < 48 owns (m = l / 3, o = l % 3), one dword of
+//      the 192-B dout block per entry, all FW entries in flight at once
+//      (absent entries out of range).  Per (s, m, o) the rows are added in
+//      list order, as the batch-major kernel adds its head rows;
+//  (2) dx^T[c][m] = sum_k W'[k][c] T[k][m] (k = 3s + o, 27 rows padded to 28):
+//      16x16x4 MFMAs, A = W' from LDS, B = T from a per-wave LDS image;
+//      elu'(elu_y) epilogue, 16-B stores;
+//  (3) dW'[k][c] += sum_m T[k][m] x[m][c] (K = the 16 meshes), kept in
+//      registers across the wave's units, summed over the block's waves in
+//      fixed order into one plain slab [3*288 + 3] (slab_reduce /
+//      dw_reduce_batch kind 1); db[o] = sum of T[0][m][o] (slot 0 of every
+//      spiral is the vertex itself: each output row is in exactly one slot-0
+//      list).
+// The batch-major kernel (conv_bwd_out_mfma) runs 32-row tiles at one wave
+// per SIMD with every memory latency exposed per tile; here a unit's
+// memory traffic is one flat list, 9 contiguous dout blocks and the 2-KiB x /
+// dx blocks.
+template <typename TX, int FW>
+__global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__ dout,
+                                                       const int4* __restrict__ flat,
+                                                       const float* __restrict__ w,
+                                                       const TX* __restrict__ elu_y,
+                                                       const TX* __restrict__ x, TX* __restrict__ dx,
+                                                       float* __restrict__ ws, int vsrc, int rows,
+                                                       int batch) {
+  constexpr int CIN = 32, CO = 3, KR = kS * CO, KP = 28, K = kS * CIN, NEL = CO * K + CO;
+  constexpr int WS = 48;  // W' row stride: conflict-free A reads (lane (c, g) -> bank 16g + c)
+  constexpr int TS = 17;  // T row stride: conflict-free A reads of the dW step
+  constexpr int FQ = FW / 4;
+  __shared__ float wl[KP * WS];
+  __shared__ float tl_all[4 * 32 * TS];
+  __shared__ float red[NEL];
+  __shared__ float dbl[4 * 48];
+  const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  // W'[k][c] = W[o][s*CIN + c], k = 3s + o; row 27 (padding) zero
+  for (int e = threadIdx.x; e < KP * CIN; e += blockDim.x) {
+    const int k = e / CIN, c = e % CIN;
+    wl[k * WS + c] = k < KR ? w[(k % CO) * K + (k / CO) * CIN + c] : 0.f;
+  }
+  float* tl = tl_all + wave * 32 * TS;
+  for (int e = lane; e < 32 * TS; e += 64) tl[e] = 0.f;  // rows 27..31 stay zero
+  __syncthreads();
+  const int G16 = batch >> 4;
+  const long n_units = (long)vsrc * G16;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dout), 0,
+                                                    (int)((long)rows * batch * CO * 4), 0x00020000);
+  const int rstride = batch * CO * 4;  // bytes between two vertices' dout blocks
+  const int m3 = lane / 3, o3 = lane - 3 * m3;
+  f32x4 dwacc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) dwacc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.f;
+  // software pipeline over the wave's units: the next unit's flat list and
+  // dout dwords are in flight while this unit runs its MFMAs; x / elu_y are
+  // issued at the top of the unit (independent of the dout chain)
+  const TileSweep sw = xcd_sweep(n_units, 4, wave);
+  const int voffl = lane < 48 ? lane * 4 : kAbsent;
+  auto load_list = [&](long unit, int (&pe)[FW]) {
+    const int u = uni((int)unit) / G16;
+#pragma unroll
+    for (int q = 0; q < FQ; ++q) {
+      const int4 f = flat[(long)u * FQ + q];
+      pe[4 * q] = uni(f.x);
+      pe[4 * q + 1] = uni(f.y);
+      pe[4 * q + 2] = uni(f.z);
+      pe[4 * q + 3] = uni(f.w);
+    }
+  };
+  auto load_dout = [&](long unit, const int (&pe)[FW], float (&v)[FW]) {
+    const int mg = uni((int)unit) % G16;
+    const int voff = voffl + mg * 48 * 4;
+#pragma unroll
+    for (int e = 0; e < FW; ++e)
+      v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                           rs, voff, pe[e] >= 0 ? (pe[e] / kS) * rstride : kAbsent, 0));
+  };
+  int pe[FW], pn[FW];
+  float v[FW], vn[FW];
+  if (sw.begin < sw.end) {
+    load_list(sw.begin, pe);
+    load_dout(sw.begin, pe, v);
+  }
+  for (long unit = sw.begin; unit < sw.end; unit += sw.step) {
+    const int un = uni((int)unit);
+    const int u = un / G16, mg = un - u * G16;
+    const long row = (long)u * batch + mg * 16 + i;
+    // x (dW operand, lane (g, c)) and elu_y (dx epilogue, lane (m, g)) early
+    const TX* xb = x + ((long)u * batch + mg * 16) * CIN + i;
+    float xv[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) xv[q][nt] = ldf(xb + (4 * q + g) * CIN + 16 * nt);
+    f32x4 ey[2];
+    if (elu_y) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) ey[ct] = ld4f(elu_y + row * CIN + 16 * ct + 4 * g);
+    }
+    const bool more = unit + sw.step < sw.end;  // uniform
+    if (more) load_list(unit + sw.step, pn);
+    float t[kS];
+#pragma unroll
+    for (int s = 0; s < kS; ++s) t[s] = 0.f;
+#pragma unroll
+    for (int e = 0; e < FW; ++e) {
+      if (pe[e] < 0) break;  // uniform: padding from here on
+      const int se = pe[e] % kS;
+#pragma unroll
+      for (int s = 0; s < kS; ++s) t[s] += se == s ? v[e] : 0.f;  // x + 0 == x: list order kept
+    }
+    dbs += t[0];
+    if (lane < 48) {
+#pragma unroll
+      for (int s = 0; s < kS; ++s) tl[(CO * s + o3) * TS + m3] = t[s];
+    }
+    if (more) load_dout(unit + sw.step, pn, vn);
+    wave_sync_lds();
+    // dx^T = W'^T . T  (2 column tiles x 7 k-steps)
+    f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int q = 0; q < KP / 4; ++q) {
+      const float b = tl[(4 * q + g) * TS + i];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) acc[ct] = mfma16(wl[(4 * q + g) * WS + 16 * ct + i], b, acc[ct]);
+    }
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      f32x4 vv = acc[ct];
+      if (elu_y) {
+        vv.x *= elu_grad_from_out(ey[ct].x);
+        vv.y *= elu_grad_from_out(ey[ct].y);
+        vv.z *= elu_grad_from_out(ey[ct].z);
+        vv.w *= elu_grad_from_out(ey[ct].w);
+      }
+      if (dx) st4f(dx + row * CIN + 16 * ct + 4 * g, vv);
+    }
+    // dW' += T . x  (K = meshes: 4 steps; 2 k-row tiles x 2 column tiles)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const float a = tl[(16 * mt + i) * TS + 4 * q + g];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) dwacc[mt][nt] = mfma16(a, xv[q][nt], dwacc[mt][nt]);
+      }
+    wave_sync_lds();  // T image free for the next unit
+    if (more) {
+#pragma unroll
+      for (int e = 0; e < FW; ++e) {
+        pe[e] = pn[e];
+        v[e] = vn[e];
+      }
+    }
+  }
+  // block combine in fixed wave order -> one slab
+  if (lane < 48) dbl[wave * 48 + lane] = dbs;
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int k = 16 * mt + 4 * g + rr, c = 16 * nt + i;
+            if (k < KR) {
+              const int e = (k % CO) * K + (k / CO) * CIN + c;
+              red[e] = wv == 0 ? dwacc[mt][nt][rr] : red[e] + dwacc[mt][nt][rr];
+            }
+          }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < CO) {
+    float sdb = 0.f;
+    for (int wv = 0; wv < 4; ++wv)
+      for (int m = 0; m < 16; ++m) sdb += dbl[wv * 48 + m * CO + threadIdx.x];
+    red[CO * K + threadIdx.x] = sdb;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NEL; e += 256) ws[(long)blockIdx.x * NEL + e] = red[e];
+}
+
+
+// ------------------------------------------------------------------ output conv forward (32 -> 3)
+// y[v][m][o] = act(bias[o] + sum_s sum_c W[o][s*32 + c] h[idx[v][s]][m][c])
+// (model.py:172-173) for a vertex-major h, batch % 16 == 0, in two passes
+// that move the spiral gather to the 3-wide side:
+//  (1) conv_out_z_vm: Z[u][s][m][o] = sum_c W[o][s*32 + c] h[u][m][c] for
+//      every source vertex u (dense: h read once; 27 of 32 rows of two
+//      16x16x4 MFMA tiles per unit), each unit's Z block written as nine
+//      contiguous 192-B rows (per s: 16 meshes x 3);
+//  (2) conv_out_gather_vm: y = act(bias + sum_s Z[idx[v][s]][s]) -- nine
+//      192-B gathers per output unit instead of nine 2-KiB h blocks.
+// The per-output sum runs s-major over per-slot dot products (the K = 288 dot
+// product reassociated): fp32 rounding differs from a single dot product.
+template <typename TX>
+__global__ __launch_bounds__(256) void conv_out_z_vm(const TX* __restrict__ h, const float* __restrict__ w,
+                                                     float* __restrict__ z, int vsrc, int batch) {
+  constexpr int CIN = 32, CO = 3, KR = kS * CO, K = kS * CIN, WS = 40;
+  __shared__ float wl[32 * WS];        // W'[k][c] = W[o][s*32 + c], k = 3s + o; rows 27..31 zero
+  __shared__ float zl_all[4 * kS * 48];
+  for (int e = threadIdx.x; e < 32 * CIN; e += blockDim.x) {
+    const int k = e / CIN, c = e % CIN;
+    wl[k * WS + c] = k < KR ? w[(k % CO) * K + (k / CO) * CIN + c] : 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  float* zl = zl_all + wave * kS * 48;
+  const int G16 = batch >> 4;
+  const long n_units = (long)vsrc * G16;
+  constexpr int UPW = 2;  // units per wave, their h loads in flight together
+  const long unit0 = ((long)xcd_block() * 4 + wave) * UPW;
+  if (unit0 >= n_units) return;
+  int uu[UPW], mgs[UPW];
+  f32x4 hv[UPW][2];
+#pragma unroll
+  for (int q = 0; q < UPW; ++q) {
+    const int un = uni((int)min(unit0 + q, n_units - 1));
+    uu[q] = un / G16;
+    mgs[q] = un - uu[q] * G16;
+    const TX* hb = h + ((long)uu[q] * batch + mgs[q] * 16 + j) * CIN + 4 * g;
+    hv[q][0] = ld4f(hb);
+    hv[q][1] = ld4f(hb + 16);
+  }
+#pragma unroll
+  for (int q = 0; q < UPW; ++q) {
+    if (unit0 + q >= n_units) break;  // uniform
+    f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        const f32x4 a = ld4(&wl[(16 * mt + j) * WS + 4 * g + 16 * cc]);
+        acc[mt] = mfma16(a.x, hv[q][cc].x, acc[mt]);
+        acc[mt] = mfma16(a.y, hv[q][cc].y, acc[mt]);
+        acc[mt] = mfma16(a.z, hv[q][cc].z, acc[mt]);
+        acc[mt] = mfma16(a.w, hv[q][cc].w, acc[mt]);
+      }
+    // D[k][m] (lane (m = j, g): k = 16mt + 4g + rr) -> Zl[s][m*3 + o]
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int k = 16 * mt + 4 * g + rr;
+        if (k < KR) zl[(k / CO) * 48 + j * CO + k % CO] = acc[mt][rr];
+      }
+    wave_sync_lds();
+    if (lane < 48) {
+#pragma unroll
+      for (int s = 0; s < kS; ++s)
+        z[(((long)uu[q] * kS + s) * batch + mgs[q] * 16) * CO + lane] = zl[s * 48 + lane];
+    }
+    wave_sync_lds();
+  }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(256) void conv_out_gather_vm(const float* __restrict__ z, const int* __restrict__ idx,
+                                                          const float* __restrict__ bias, float* __restrict__ y,
+                                                          int yvm, int rows, int batch) {
+  // lane = (unit q of the wave's 4, mesh m): one 12-B Z row per slot, the 16
+  // meshes of a unit one contiguous 192-B block
+  constexpr int CO = 3;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, m = lane & 15;
+  const int G16 = batch >> 4;
+  const long n_units = (long)rows * G16;
+  const long unit = ((long)xcd_block() * 4 + wave) * 4 + q;
+  if (unit >= n_units) return;
+  const int un = (int)unit;
+  const int v = un / G16, mg = un - v * G16;
+  int src[kS];
+#pragma unroll
+  for (int s = 0; s < kS; ++s) src[s] = idx[v * kS + s];
+  float zv[kS][CO];
+#pragma unroll
+  for (int s = 0; s < kS; ++s) ld_row<CO>(z + (((long)src[s] * kS + s) * batch + mg * 16 + m) * CO, zv[s]);
+  const int mesh = mg * 16 + m;
+  const long row = yvm ? (long)v * batch + mesh : (long)mesh * rows + v;
+  float r[CO];
+#pragma unroll
+  for (int o = 0; o < CO; ++o) {
+    float acc = zv[0][o];
+#pragma unroll
+    for (int s = 1; s < kS; ++s) acc += zv[s][o];
+    r[o] = (bias ? bias[o] : 0.f) + acc;
+    if (ACT == CFSD_ACT_ELU) r[o] = elu_f(r[o]);
+  }
+  st_row<CO>(y + row * CO, r);
+}
+
 // ------------------------------------------------------------------ launchers
 bool ok(int batch, int cin, int cout) { return batch % 16 == 0 && cin == 32 && (cout == 32 || cout == 64); }
 
@@ -274,13 +588,16 @@ static int fwd_t(const float* x, const int* idx, const float* w, const float* bi
 #ifndef CFSD_VM32_UPT1_UNITS
 #define CFSD_VM32_UPT1_UNITS 8192
 #endif
+#ifndef CFSD_VM32_PD2
+#define CFSD_VM32_PD2 1  // slots in flight ahead with two units per tile
+#endif
 
 template <int COUT, int ACT>
 static int fwd_pick(const float* x, const int* idx, const float* w, const float* bias, float* y, int yvm,
                     int vsrc, int rows, int batch, hipStream_t st) {
   if ((long)rows * (batch / 16) < CFSD_VM32_UPT1_UNITS)
     return fwd_t<32, COUT, ACT, 1, 2>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
-  return fwd_t<32, COUT, ACT, 2, 1>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
+  return fwd_t<32, COUT, ACT, 2, CFSD_VM32_PD2>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
 }
 
 int launch_fwd(const float* x, const int* idx, const float* w, const float* bias, float* y, int yvm, int vsrc,
@@ -320,6 +637,53 @@ int launch_dx_flat(const float* dpre, const int* flat, int width, const float* w
 #undef DF
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat (fp32): unsupported channels %d -> %d / width %d",
                    cin, cout, width);
+}
+
+
+template <typename TX, int FW>
+static int bwd_out_t(const float* dout, const int* flat, const float* w, const TX* elu_y, const TX* x, TX* dx,
+                     float* ws, int n_slabs, int vsrc, int rows, int batch, hipStream_t st) {
+  hipLaunchKernelGGL((conv_bwd_out_vm<TX, FW>), dim3(n_slabs), dim3(256), 0, st, dout, (const int4*)flat, w,
+                     elu_y, x, dx, ws, vsrc, rows, batch);
+  return launch_status("spiral_conv_bwd_out_vm");
+}
+
+int launch_bwd_out(const float* dout, const int* flat, int width, const float* w, const void* elu_y, const void* x,
+                   void* dx, int x_bf16, float* ws, int n_slabs, int vsrc, int rows, int batch, hipStream_t st) {
+  if (batch % 16) return set_error(CFSD_EINVAL, "spiral_conv_bwd (vertex-major output conv): batch %% 16 != 0");
+  if ((long)rows * batch * 12 >= (long)kAbsent)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd (vertex-major output conv): dout exceeds 32-bit offsets");
+#define BO(FW_)                                                                                           \
+  if (width == FW_)                                                                                       \
+    return x_bf16 ? bwd_out_t<bf16_t, FW_>(dout, flat, w, (const bf16_t*)elu_y, (const bf16_t*)x, (bf16_t*)dx, \
+                                           ws, n_slabs, vsrc, rows, batch, st)                            \
+                  : bwd_out_t<float, FW_>(dout, flat, w, (const float*)elu_y, (const float*)x, (float*)dx, ws, \
+                                          n_slabs, vsrc, rows, batch, st);
+  BO(8) BO(12) BO(16) BO(20)
+#undef BO
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd (vertex-major output conv): flat width %d", width);
+}
+
+
+size_t out_z_floats(int batch, int vsrc) { return (size_t)vsrc * kS * batch * 3; }
+
+int launch_fwd_out(const void* x, int x_bf16, const int* idx, const float* w, const float* bias, float* y, int yvm,
+                   float* ws, int vsrc, int rows, int batch, int act, hipStream_t st) {
+  if (batch % 16) return set_error(CFSD_EINVAL, "spiral_conv_fwd (vertex-major output conv): batch %% 16 != 0");
+  const long units_src = (long)vsrc * (batch / 16), units = (long)rows * (batch / 16);
+  const dim3 gz((unsigned)((units_src + 7) / 8)), gg((unsigned)((units + 15) / 16));
+  if (x_bf16)
+    hipLaunchKernelGGL((conv_out_z_vm<bf16_t>), gz, dim3(256), 0, st, (const bf16_t*)x, w, ws, vsrc, batch);
+  else
+    hipLaunchKernelGGL((conv_out_z_vm<float>), gz, dim3(256), 0, st, (const float*)x, w, ws, vsrc, batch);
+  int rc = launch_status("spiral_conv_fwd_out_z");
+  if (rc) return rc;
+  if (act == CFSD_ACT_ELU)
+    hipLaunchKernelGGL((conv_out_gather_vm<CFSD_ACT_ELU>), gg, dim3(256), 0, st, ws, idx, bias, y, yvm, rows, batch);
+  else
+    hipLaunchKernelGGL((conv_out_gather_vm<CFSD_ACT_NONE>), gg, dim3(256), 0, st, ws, idx, bias, y, yvm, rows,
+                       batch);
+  return launch_status("spiral_conv_fwd_out_gather");
 }
 
 }  // namespace vm32

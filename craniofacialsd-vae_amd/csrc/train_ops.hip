@@ -69,10 +69,12 @@ __device__ __forceinline__ float2 block_sum2(float a, float b, float2* sh) {
 }
 
 // ----------------------------------------------------------- recon + Laplacian
+// xb = the mesh's row of vertex 0, rs = floats between consecutive vertices'
+// rows of one mesh (C batch-major, batch*C vertex-major)
 template <int C>
 __device__ __forceinline__ void lap_row_dot(int beg, int end, const int* __restrict__ col,
                                             const float* __restrict__ val,
-                                            const float* __restrict__ xb, float (&acc)[C]) {
+                                            const float* __restrict__ xb, int rs, float (&acc)[C]) {
   constexpr int CK = 8;
   for (int e0 = beg; e0 < end; e0 += CK) {
     int cc[CK];
@@ -85,7 +87,7 @@ __device__ __forceinline__ void lap_row_dot(int beg, int end, const int* __restr
     }
     float xv[CK][C];
 #pragma unroll
-    for (int j = 0; j < CK; ++j) ld_row<C>(xb + (long)cc[j] * C, xv[j]);
+    for (int j = 0; j < CK; ++j) ld_row<C>(xb + (long)cc[j] * rs, xv[j]);
 #pragma unroll
     for (int j = 0; j < CK; ++j)
 #pragma unroll
@@ -99,17 +101,20 @@ template <int C>
 __global__ __launch_bounds__(kLapThreads) void recon_lap_fwd_k(
     const float* __restrict__ pred, const float* __restrict__ gt, const int* __restrict__ l_ptr,
     const int* __restrict__ l_col, const float* __restrict__ l_val, float* __restrict__ unit,
-    float* __restrict__ partials, int nv, long total) {
+    float* __restrict__ partials, int nv, long total, int batch, int vm) {
   __shared__ float2 sh[kLapThreads / 64];
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   float sq = 0.f, nrm = 0.f;
   if (t < total) {
+    // thread t = row t of the storage (vertex-major: the meshes of a vertex
+    // are adjacent threads, each Laplacian neighbour one contiguous block)
     int b, v;
-    divmod32(t, nv, b, v);
+    split_row(t, vm, batch, nv, b, v);
+    const Lay L = make_lay(vm, batch, nv);
     float lx[C];
 #pragma unroll
     for (int q = 0; q < C; ++q) lx[q] = 0.f;
-    lap_row_dot<C>(l_ptr[v], l_ptr[v + 1], l_col, l_val, pred + b * nv * C, lx);
+    lap_row_dot<C>(l_ptr[v], l_ptr[v + 1], l_col, l_val, pred + (long)b * L.bs * C, L.vs * C, lx);
     float n2 = 0.f, pv[C], gv[C];
     ld_row<C>(pred + t * C, pv);
     ld_row<C>(gt + t * C, gv);
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(256) void recon_lap_bwd_k(
     const float* __restrict__ pred, const float* __restrict__ gt, const float* __restrict__ unit,
     const int* __restrict__ lt_ptr, const int* __restrict__ lt_col,
     const float* __restrict__ lt_val, float* __restrict__ dpred, int nv, long total, float k_rec,
-    float k_lap, const LossFinalize fin) {
+    float k_lap, const LossFinalize fin, int batch, int vm) {
   if (fin.partials && blockIdx.x == gridDim.x - 1) {
     __shared__ float2 sh[4];
     loss_finalize_block(fin, sh);
@@ -180,11 +185,12 @@ __global__ __launch_bounds__(256) void recon_lap_bwd_k(
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   int b, u;
-  divmod32(t, nv, b, u);
+  split_row(t, vm, batch, nv, b, u);
+  const Lay L = make_lay(vm, batch, nv);
   float g[C];
 #pragma unroll
   for (int q = 0; q < C; ++q) g[q] = 0.f;
-  lap_row_dot<C>(lt_ptr[u], lt_ptr[u + 1], lt_col, lt_val, unit + b * nv * C, g);
+  lap_row_dot<C>(lt_ptr[u], lt_ptr[u + 1], lt_col, lt_val, unit + (long)b * L.bs * C, L.vs * C, g);
   float pv[C], gv[C], dv[C];
   ld_row<C>(pred + t * C, pv);
   ld_row<C>(gt + t * C, gv);
@@ -845,7 +851,7 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
 
 using namespace cfsd;
 
-extern "C" int cfsd_version(void) { return (4 << 16) | 1; }  // 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands
+extern "C" int cfsd_version(void) { return (4 << 16) | 2; }  // 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x)
 extern "C" const char* cfsd_last_error_string(void) { return g_err; }
 
 extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {
@@ -853,9 +859,9 @@ extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {
   return (int)((total + kLapThreads - 1) / kLapThreads);
 }
 
-extern "C" int cfsd_recon_lap_fwd(const float* pred, const float* gt, const int32_t* l_ptr,
-                                  const int32_t* l_col, const float* l_val, float* unit_lx,
-                                  float* partials, int batch, int nv, int c, void* stream) {
+static int recon_lap_fwd_launch(const float* pred, const float* gt, const int32_t* l_ptr,
+                                const int32_t* l_col, const float* l_val, float* unit_lx,
+                                float* partials, int batch, int nv, int c, int vm, void* stream) {
   if (!pred || !gt || !l_ptr || !l_col || !l_val || !unit_lx || !partials)
     return set_error(CFSD_EINVAL, "recon_lap_fwd: null pointer");
   if (batch <= 0 || nv <= 0 || c <= 0 || c > 4) return set_error(CFSD_EINVAL, "recon_lap_fwd: bad sizes");
@@ -866,17 +872,31 @@ extern "C" int cfsd_recon_lap_fwd(const float* pred, const float* gt, const int3
 #define RLF(C)                                                                                  \
   case C:                                                                                       \
     hipLaunchKernelGGL(recon_lap_fwd_k<C>, grid, dim3(kLapThreads), 0, st, pred, gt, l_ptr, l_col, \
-                       l_val, unit_lx, partials, nv, total);                                    \
+                       l_val, unit_lx, partials, nv, total, batch, vm);                         \
     break;
   switch (c) { RLF(1) RLF(2) RLF(3) RLF(4) }
 #undef RLF
   return launch_status("recon_lap_fwd");
 }
 
+extern "C" int cfsd_recon_lap_fwd(const float* pred, const float* gt, const int32_t* l_ptr,
+                                  const int32_t* l_col, const float* l_val, float* unit_lx,
+                                  float* partials, int batch, int nv, int c, void* stream) {
+  return recon_lap_fwd_launch(pred, gt, l_ptr, l_col, l_val, unit_lx, partials, batch, nv, c, 0, stream);
+}
+
+extern "C" int cfsd_recon_lap_fwd_x(const float* pred, const float* gt, const int32_t* l_ptr,
+                                    const int32_t* l_col, const float* l_val, float* unit_lx,
+                                    float* partials, int batch, int nv, int c, int dt, void* stream) {
+  if ((dt & ~CFSD_VM) != CFSD_DT_F32) return set_error(CFSD_EINVAL, "recon_lap_fwd_x: bad dtype %d", dt);
+  return recon_lap_fwd_launch(pred, gt, l_ptr, l_col, l_val, unit_lx, partials, batch, nv, c,
+                              (dt & CFSD_VM) != 0, stream);
+}
+
 static int recon_lap_bwd_launch(const float* pred, const float* gt, const float* unit_lx,
                                 const int32_t* lt_ptr, const int32_t* lt_col, const float* lt_val,
                                 float* dpred, int batch, int nv, int c, float w_rec, float w_lap,
-                                const LossFinalize& fin, void* stream) {
+                                const LossFinalize& fin, int vm, void* stream) {
   if (!pred || !gt || !unit_lx || !lt_ptr || !lt_col || !lt_val || !dpred)
     return set_error(CFSD_EINVAL, "recon_lap_bwd: null pointer");
   if (batch <= 0 || nv <= 0 || c <= 0 || c > 4) return set_error(CFSD_EINVAL, "recon_lap_bwd: bad sizes");
@@ -889,7 +909,7 @@ static int recon_lap_bwd_launch(const float* pred, const float* gt, const float*
 #define RLB(C)                                                                                   \
   case C:                                                                                        \
     hipLaunchKernelGGL(recon_lap_bwd_k<C>, grid, dim3(256), 0, st, pred, gt, unit_lx, lt_ptr,    \
-                       lt_col, lt_val, dpred, nv, total, k_rec, k_lap, fin);                     \
+                       lt_col, lt_val, dpred, nv, total, k_rec, k_lap, fin, batch, vm);         \
     break;
   switch (c) { RLB(1) RLB(2) RLB(3) RLB(4) }
 #undef RLB
@@ -902,7 +922,29 @@ extern "C" int cfsd_recon_lap_bwd(const float* pred, const float* gt, const floa
                                   float w_rec, float w_lap, void* stream) {
   const LossFinalize none{};  // losses finalised by cfsd_loss_finalize
   return recon_lap_bwd_launch(pred, gt, unit_lx, lt_ptr, lt_col, lt_val, dpred, batch, nv, c, w_rec,
-                              w_lap, none, stream);
+                              w_lap, none, 0, stream);
+}
+
+extern "C" int cfsd_recon_lap_bwd_x(const float* pred, const float* gt, const float* unit_lx,
+                                    const int32_t* lt_ptr, const int32_t* lt_col,
+                                    const float* lt_val, float* dpred, int batch, int nv, int c,
+                                    float w_rec, float w_lap, int dt, void* stream) {
+  if ((dt & ~CFSD_VM) != CFSD_DT_F32) return set_error(CFSD_EINVAL, "recon_lap_bwd_x: bad dtype %d", dt);
+  const LossFinalize none{};
+  return recon_lap_bwd_launch(pred, gt, unit_lx, lt_ptr, lt_col, lt_val, dpred, batch, nv, c, w_rec,
+                              w_lap, none, (dt & CFSD_VM) != 0, stream);
+}
+
+static int recon_lap_bwd_fin(const float* pred, const float* gt, const float* unit_lx, const int32_t* lt_ptr,
+                             const int32_t* lt_col, const float* lt_val, float* dpred, int batch, int nv, int c,
+                             float w_rec, float w_lap, const float* partials, int nblocks, const float* terms,
+                             float* out, float* acc, float w_kl, float w_lc, int vm, void* stream) {
+  if (!partials || !terms || !out) return set_error(CFSD_EINVAL, "recon_lap_bwd_finalize: null pointer");
+  if (batch <= 0 || nv <= 0 || c <= 0) return set_error(CFSD_EINVAL, "recon_lap_bwd_finalize: bad sizes");
+  const LossFinalize fin{partials, nblocks, terms, out, acc, 1.f / (float)((long)batch * nv * c),
+                         1.f / (float)((long)nv * batch), w_kl, w_lc, w_lap};
+  return recon_lap_bwd_launch(pred, gt, unit_lx, lt_ptr, lt_col, lt_val, dpred, batch, nv, c, w_rec,
+                              w_lap, fin, vm, stream);
 }
 
 extern "C" int cfsd_recon_lap_bwd_finalize(const float* pred, const float* gt, const float* unit_lx,
@@ -911,12 +953,20 @@ extern "C" int cfsd_recon_lap_bwd_finalize(const float* pred, const float* gt, c
                                            int c, float w_rec, float w_lap, const float* partials,
                                            int nblocks, const float* terms, float* out, float* acc,
                                            float w_kl, float w_lc, void* stream) {
-  if (!partials || !terms || !out) return set_error(CFSD_EINVAL, "recon_lap_bwd_finalize: null pointer");
-  if (batch <= 0 || nv <= 0 || c <= 0) return set_error(CFSD_EINVAL, "recon_lap_bwd_finalize: bad sizes");
-  const LossFinalize fin{partials, nblocks, terms, out, acc, 1.f / (float)((long)batch * nv * c),
-                         1.f / (float)((long)nv * batch), w_kl, w_lc, w_lap};
-  return recon_lap_bwd_launch(pred, gt, unit_lx, lt_ptr, lt_col, lt_val, dpred, batch, nv, c, w_rec,
-                              w_lap, fin, stream);
+  return recon_lap_bwd_fin(pred, gt, unit_lx, lt_ptr, lt_col, lt_val, dpred, batch, nv, c, w_rec, w_lap,
+                           partials, nblocks, terms, out, acc, w_kl, w_lc, 0, stream);
+}
+
+extern "C" int cfsd_recon_lap_bwd_finalize_x(const float* pred, const float* gt, const float* unit_lx,
+                                             const int32_t* lt_ptr, const int32_t* lt_col,
+                                             const float* lt_val, float* dpred, int batch, int nv,
+                                             int c, float w_rec, float w_lap, const float* partials,
+                                             int nblocks, const float* terms, float* out, float* acc,
+                                             float w_kl, float w_lc, int dt, void* stream) {
+  if ((dt & ~CFSD_VM) != CFSD_DT_F32)
+    return set_error(CFSD_EINVAL, "recon_lap_bwd_finalize_x: bad dtype %d", dt);
+  return recon_lap_bwd_fin(pred, gt, unit_lx, lt_ptr, lt_col, lt_val, dpred, batch, nv, c, w_rec, w_lap,
+                           partials, nblocks, terms, out, acc, w_kl, w_lc, (dt & CFSD_VM) != 0, stream);
 }
 
 extern "C" int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_t* key, float* z,

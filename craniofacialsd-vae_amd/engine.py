@@ -365,7 +365,10 @@ class SDVAEEngine:
         nv = T.n_verts
         lat = S.latent
         last_enc = S.enc_layers()[-1][2]
-        b.x = f(bsz, nv[0], S.in_ch)
+        # the xyz tensors of level 0 (input, output, Laplacian unit vectors,
+        # output gradient) share level 0's layout; fp32 always
+        f0 = ((lambda *shape: ops.vm_empty(*shape, dtype=torch.float32, device=dev)) if 0 in lp else f)
+        b.x = f0(bsz, nv[0], S.in_ch)
         b.enc_full = [None] * S.n     # full-resolution conv outputs (non-selection path)
         b.enc_out = []                # pooled Enblock outputs [B, V_{i+1}, C_i]
         for (cin, cout, lv) in S.enc_layers():
@@ -383,12 +386,12 @@ class SDVAEEngine:
         for (cin, cout, lv, ui) in S.dec_layers():
             b.dec_up.append(fl(lv, bsz, nv[lv], cin))
             b.dec_out.append(fl(lv, bsz, nv[lv], cout))
-        b.out = f(bsz, nv[0], S.in_ch)
-        b.unit = f(bsz, nv[0], S.in_ch)
+        b.out = f0(bsz, nv[0], S.in_ch)
+        b.unit = f0(bsz, nv[0], S.in_ch)
         b.partials = f(2 * ops.recon_lap_blocks(bsz, nv[0]))
         b.losses = f(5)
         # backward
-        b.dout = f(bsz, nv[0], S.in_ch)
+        b.dout = f0(bsz, nv[0], S.in_ch)
         b.g_dec_up = [fl(lv, bsz, nv[lv], cin) for (cin, cout, lv, ui) in S.dec_layers()]   # grad wrt dec_up
         b.dpre_dec = [fl(lv, bsz, nv[lv], cout) for (cin, cout, lv, ui) in S.dec_layers()]  # grad wrt pre-ELU
         b.dh = torch.empty_like(b.h)
@@ -417,6 +420,8 @@ class SDVAEEngine:
             ws = max(ws, ops.spiral_conv_workspace(bsz, nv[lv], nv[lv], T.seq[lv], cin, cout))
         ws = max(ws, ops.spiral_conv_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
         ws = max(ws, ops.spiral_conv_bwd_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
+        if 0 in lp:  # two-pass vertex-major output conv (per-slot products of every vertex)
+            ws = max(ws, ops.spiral_conv_fwd_out_workspace(bsz, nv[0], T.seq[0], S.out_ch[0], S.in_ch))
         # bf16 Enblocks whose dpre is fp32: dx by the row-subset dG + gather
         b.rowsub_x = {}
         for (cin, cout, lv) in S.enc_layers():
@@ -571,7 +576,12 @@ class SDVAEEngine:
                            b.dec_out[i])
             h = b.dec_out[i]
         n = S.n
-        self._conv_fwd(b, h, T.spiral[0], f"de_layers.{n + 1}.layer", ACT_NONE, b.out)
+        if self._flat_out(b):  # vertex-major: the spiral gather on the 3-wide side
+            P = self.params
+            ops.spiral_conv_fwd_out(h, T.spiral[0], P.view(f"de_layers.{n + 1}.layer.weight"),
+                                    P.view(f"de_layers.{n + 1}.layer.bias"), ACT_NONE, b.out, workspace=b.ws)
+        else:
+            self._conv_fwd(b, h, T.spiral[0], f"de_layers.{n + 1}.layer", ACT_NONE, b.out)
 
     def losses_fwd(self, b, acc=None, finalize=True):
         T = self.topo
@@ -642,10 +652,14 @@ class SDVAEEngine:
 
         weight_grad = ops.spiral_conv_bwd_weight
 
-        bwd_out = ops.spiral_conv_bwd_x if 0 in b.xl else ops.spiral_conv_bwd
-        _, d = bwd_out(last_in, T.spiral[0], b.dout, T.spiral_inv[0],
-                       P.view(f"de_layers.{n + 1}.layer.weight"), None, None,
-                       dx=b.dpre_dec[-1], elu_y=last_in, workspace=b.ws_dw["out"])
+        w_out = P.view(f"de_layers.{n + 1}.layer.weight")
+        if self._flat_out(b):  # vertex-major: one walk of each vertex's flat inverse list
+            _, d = ops.spiral_conv_bwd_out_flat(last_in, T.spiral[0], b.dout, T.spiral_flat[0], w_out, None, None,
+                                                dx=b.dpre_dec[-1], elu_y=last_in, workspace=b.ws_dw["out"])
+        else:
+            bwd_out = ops.spiral_conv_bwd_x if 0 in b.xl else ops.spiral_conv_bwd
+            _, d = bwd_out(last_in, T.spiral[0], b.dout, T.spiral_inv[0], w_out, None, None,
+                           dx=b.dpre_dec[-1], elu_y=last_in, workspace=b.ws_dw["out"])
         defer(d, f"de_layers.{n + 1}.layer")
         dec = S.dec_layers()
         for i in reversed(range(len(dec))):
@@ -706,6 +720,13 @@ class SDVAEEngine:
                            db=gB, workspace=b.lin_ws)
             ops.spmm(T.downT_csr[last], b.g_pooled[last], T.n_verts[last], elu_y=b.enc_full[last],
                      out=b.dpre_enc[last])
+
+    def _flat_out(self, b):
+        """The flat-list output-conv backward applies (vertex-major level 0,
+        batch % 16, the 32 -> 3 xyz conv)."""
+        S = self.spec
+        return (0 in b.xl and b.bsz % 16 == 0 and S.out_ch[0] == 32 and S.in_ch == 3
+                and self.topo.spiral_flat[0] is not None)
 
     def _flat_dx(self, b, lv, cin, cout):
         """The flat-list bf16 data gradient applies (vertex-major level,

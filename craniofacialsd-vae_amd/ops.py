@@ -401,6 +401,11 @@ def swap_features(x_all, batch_idx, region_mask, key, bs, out=None):
         raise ValueError("region_mask [n_regions, nv] is required")
     _need(region_mask, (region_mask.shape[0], nv), torch.uint8, "region_mask")
     _need(key, (1,), torch.int32, "key")
+    if out is not None and is_vm(out):  # vertex-major output (the fp32 step's level-0 input)
+        _needl(out, (bs * bs, nv, c), "out", torch.float32)
+        call("cfsd_swap_features_x", ptr(x_all), ptr(batch_idx), ptr(region_mask), ptr(key), ptr(out),
+             _st(out), bs, nv, c, n_meshes, int(region_mask.shape[0]), stream_ptr())
+        return out
     y = _out(out, (bs * bs, nv, c), x_all)
     call("cfsd_swap_features", ptr(x_all), ptr(batch_idx), ptr(region_mask), ptr(key), ptr(y), bs,
          nv, c, n_meshes, int(region_mask.shape[0]), stream_ptr())
@@ -501,23 +506,31 @@ def recon_lap_blocks(bsz, nv):
     return int(_abi.lib().cfsd_recon_lap_blocks(bsz, nv))
 
 
+def _loss_layout(*ts):
+    """Storage flag of the loss operands: all batch-major or all vertex-major."""
+    vm = [is_vm(t) for t in ts]
+    if any(vm) and not all(vm):
+        raise ValueError("loss operands must share one layout (batch-major or vertex-major)")
+    for t in ts:
+        _needl(t, tuple(ts[0].shape), "loss operand", torch.float32)
+    return VM if vm[0] else 0
+
+
 def recon_lap_fwd(pred, gt, lap_csr, unit, partials):
     bsz, nv, c = pred.shape
-    _need(pred, None, name="pred")
-    _need(gt, (bsz, nv, c), name="gt")
-    _need(unit, (bsz, nv, c), name="unit")
+    lay = _loss_layout(pred, gt, unit)
     _need(partials, (2 * recon_lap_blocks(bsz, nv),), name="partials")
     _need(lap_csr[0], (nv + 1,), torch.int32, "l_ptr")
-    call("cfsd_recon_lap_fwd", ptr(pred), ptr(gt), ptr(lap_csr[0]), ptr(lap_csr[1]),
-         ptr(lap_csr[2]), ptr(unit), ptr(partials), bsz, nv, c, stream_ptr())
+    call("cfsd_recon_lap_fwd_x", ptr(pred), ptr(gt), ptr(lap_csr[0]), ptr(lap_csr[1]),
+         ptr(lap_csr[2]), ptr(unit), ptr(partials), bsz, nv, c, lay, stream_ptr())
 
 
 def recon_lap_bwd(pred, gt, unit, lapT_csr, dpred, w_rec, w_lap):
     bsz, nv, c = pred.shape
-    _need(dpred, (bsz, nv, c), name="dpred")
+    lay = _loss_layout(pred, gt, unit, dpred)
     _need(lapT_csr[0], (nv + 1,), torch.int32, "lt_ptr")
-    call("cfsd_recon_lap_bwd", ptr(pred), ptr(gt), ptr(unit), ptr(lapT_csr[0]),
-         ptr(lapT_csr[1]), ptr(lapT_csr[2]), ptr(dpred), bsz, nv, c, float(w_rec), float(w_lap),
+    call("cfsd_recon_lap_bwd_x", ptr(pred), ptr(gt), ptr(unit), ptr(lapT_csr[0]),
+         ptr(lapT_csr[1]), ptr(lapT_csr[2]), ptr(dpred), bsz, nv, c, float(w_rec), float(w_lap), lay,
          stream_ptr())
 
 
@@ -526,15 +539,15 @@ def recon_lap_bwd_finalize(pred, gt, unit, lapT_csr, dpred, w_rec, w_lap, partia
     """recon_lap_bwd + loss_finalize in one launch (the last workgroup
     finalises the losses of the preceding recon_lap_fwd)."""
     bsz, nv, c = pred.shape
-    _need(dpred, (bsz, nv, c), name="dpred")
+    lay = _loss_layout(pred, gt, unit, dpred)
     _need(lapT_csr[0], (nv + 1,), torch.int32, "lt_ptr")
     _need(out, (5,), name="out")
     if acc is not None:
         _need(acc, (6,), name="acc")
-    call("cfsd_recon_lap_bwd_finalize", ptr(pred), ptr(gt), ptr(unit), ptr(lapT_csr[0]),
+    call("cfsd_recon_lap_bwd_finalize_x", ptr(pred), ptr(gt), ptr(unit), ptr(lapT_csr[0]),
          ptr(lapT_csr[1]), ptr(lapT_csr[2]), ptr(dpred), bsz, nv, c, float(w_rec), float(w_lap),
          ptr(partials), partials.numel() // 2, ptr(terms), ptr(out), ptr(acc), float(w_kl),
-         float(w_lc), stream_ptr())
+         float(w_lc), lay, stream_ptr())
 
 
 def latent_fwd(mulv, eps, key, z, dlat, terms, latent, region_size, train, is_vae, sigmoid,
@@ -823,6 +836,66 @@ def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspa
     call("cfsd_spiral_conv_bwd_x", ptr(x), _st(x), ptr(idx), ptr(dpre), _st(dpre), ptr(inv_ptr), ptr(inv_row),
          ptr(inv_head), ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb),
          bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    if dw is None:
+        return dx, DeferredDw(ws, bsz, vsrc, rows, cin, cout, 1)
+    return dx
+
+
+def spiral_conv_fwd_out_workspace(bsz, vsrc, seq, cin, cout):
+    return int(_abi.lib().cfsd_spiral_conv_fwd_out_workspace(bsz, vsrc, seq, cin, cout))
+
+
+def spiral_conv_fwd_out(x, idx, w, b, act, out, workspace=None):
+    """Forward of the xyz output conv (32 -> 3) for a vertex-major x (fp32 or
+    bf16), batch a multiple of 16: dense per-slot products of every source
+    vertex, then the spiral gather on the 3-wide side."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = w.shape[0]
+    if not is_vm(x):
+        raise ValueError("x must be vertex-major")
+    _needl(x, None, "x", x.dtype)
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(w, (cout, seq * cin), name="w")
+    if b is not None:
+        _need(b, (cout,), name="bias")
+    _needl(out, (bsz, rows, cout), "out", torch.float32)
+    need = spiral_conv_fwd_out_workspace(bsz, vsrc, seq, cin, cout)
+    if need == 0:
+        raise ValueError(f"no two-pass output conv for {cin} -> {cout} at batch {bsz}")
+    ws, nb = _conv_ws(workspace, x.device, need)
+    call("cfsd_spiral_conv_fwd_out", ptr(x), _st(x), ptr(idx), ptr(w), ptr(b), ptr(out), _st(out), ptr(ws),
+         ctypes.c_size_t(nb), bsz, vsrc, rows, seq, cin, cout, act, stream_ptr())
+    return out
+
+
+def spiral_conv_bwd_out_flat(x, idx, dpre, flat, w, dw, db, dx=None, elu_y=None, workspace=None):
+    """Fused dx + dW of the xyz output conv (32 -> 3) with vertex-major x /
+    elu_y / dx (fp32 or bf16) and dpre, through the flat inverse list
+    (``topology.spiral_flat``); batch a multiple of 16."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = dpre.shape[2]
+    table, width = flat
+    xdt = x.dtype
+    if not (is_vm(x) and is_vm(dpre)):
+        raise ValueError("x and dpre must be vertex-major")
+    _needl(x, None, "x", xdt)
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _needl(dpre, (bsz, rows, cout), "dpre", torch.float32)
+    _need(table, (vsrc, width), torch.int32, "inv_flat")
+    _need(w, (cout, seq * cin), name="w")
+    for t, nm in ((dx, "dx"), (elu_y, "elu_y")):
+        if t is not None:
+            _needl(t, (bsz, vsrc, cin), nm, xdt)
+            _same_layout(x, t, f"x and {nm}")
+    if dw is not None or db is not None:
+        _need(dw, (cout, seq * cin), name="dw")
+        _need(db, (cout,), name="db")
+    ws, nb = _conv_ws(workspace, x.device, spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout))
+    call("cfsd_spiral_conv_bwd_out_flat", ptr(x), _st(x), ptr(idx), ptr(dpre), _st(dpre), ptr(table), width,
+         ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, seq, cin,
+         cout, stream_ptr())
     if dw is None:
         return dx, DeferredDw(ws, bsz, vsrc, rows, cin, cout, 1)
     return dx

@@ -235,6 +235,11 @@ int cfsd_spmm_uniform(int k, const int32_t* col, const float* val, const void* x
 int cfsd_swap_features(const float* x, const int32_t* batch_idx, const uint8_t* region_mask,
                        const int32_t* key, float* out, int bs, int nv, int c, int n_meshes,
                        int n_regions, void* stream);
+/* The same with the output's layout: out_dt = CFSD_DT_F32 [| CFSD_VM] (ABI
+ * 4.2; x stays batch-major [n_meshes, nv, c]). */
+int cfsd_swap_features_x(const float* x, const int32_t* batch_idx, const uint8_t* region_mask,
+                         const int32_t* key, float* out, int out_dt, int bs, int nv, int c,
+                         int n_meshes, int n_regions, void* stream);
 
 /* Spectral augmentation blend (utils.py:244-267, data_loading.py:359-364):
  * with s1 = U^T x1, s2 = U^T x2 [pairs, k, c] (U: the k smallest Laplacian
@@ -298,6 +303,22 @@ int cfsd_recon_lap_bwd_finalize(const float* pred, const float* gt, const float*
                                 float* dpred, int batch, int nv, int c, float w_rec, float w_lap,
                                 const float* partials, int nblocks, const float* terms, float* out,
                                 float* acc, float w_kl, float w_lc, void* stream);
+/* The three loss passes with pred / gt / unit_lx / dpred in one layout, dt =
+ * CFSD_DT_F32 [| CFSD_VM] (ABI 4.2: the fp32 step's vertex-major level-0
+ * tensors).  Same values; the loss partial sums run over the storage order,
+ * so the reduced losses may differ in the last bits between layouts. */
+int cfsd_recon_lap_fwd_x(const float* pred, const float* gt, const int32_t* l_ptr,
+                         const int32_t* l_col, const float* l_val, float* unit_lx, float* partials,
+                         int batch, int nv, int c, int dt, void* stream);
+int cfsd_recon_lap_bwd_x(const float* pred, const float* gt, const float* unit_lx,
+                         const int32_t* lt_ptr, const int32_t* lt_col, const float* lt_val,
+                         float* dpred, int batch, int nv, int c, float w_rec, float w_lap, int dt,
+                         void* stream);
+int cfsd_recon_lap_bwd_finalize_x(const float* pred, const float* gt, const float* unit_lx,
+                                  const int32_t* lt_ptr, const int32_t* lt_col, const float* lt_val,
+                                  float* dpred, int batch, int nv, int c, float w_rec, float w_lap,
+                                  const float* partials, int nblocks, const float* terms, float* out,
+                                  float* acc, float w_kl, float w_lc, int dt, void* stream);
 
 /* Latent head, forward (model.py:146-160, 184-188; model_manager.py:352-393).
  * mulv [batch, 2*latent] = [logvar | mu] when is_vae (the two encoder Linears
@@ -426,6 +447,27 @@ int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* idx, const fl
                            const float* w, const void* elu_y, void* dx, float* dw, float* db,
                            float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows,
                            int seq, int cin, int cout, void* stream);
+/* The same fused backward of the xyz output conv (32 -> 3) for VERTEX-MAJOR
+ * x / elu_y / dx (fp32 or bf16) and fp32 dpre (ABI 4.2), batch % 16 == 0:
+ * per source vertex the spiral transpose is one walk of its flat inverse
+ * list (topology.inverse_flat, width 8/12/16/20), dx = W^T-products of the
+ * folded 3-wide dpre, dW = folded dpre (x) x.  Same workspace, slab layout
+ * and deferred kind (fused = 1) as cfsd_spiral_conv_bwd_x. */
+int cfsd_spiral_conv_bwd_out_flat(const void* x, int x_dt, const int32_t* idx, const float* dpre,
+                                  int dpre_dt, const int32_t* inv_flat, int flat_width, const float* w,
+                                  const void* elu_y, void* dx, float* dw, float* db, float* workspace,
+                                  size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
+                                  int cout, void* stream);
+/* Forward of the xyz output conv (32 -> 3, model.py:172-173) for a
+ * VERTEX-MAJOR x (fp32 or bf16, batch % 16 == 0; ABI 4.2) in two passes:
+ * Z[u][s][m][o] = sum_c w[o, s*32 + c] x[m, u, c] for every source vertex
+ * (dense), then y = act(bias + sum_s Z[idx[v, s]][s]) -- the gather moves to
+ * the 3-wide side.  y fp32 in either layout; workspace
+ * cfsd_spiral_conv_fwd_out_workspace() bytes (0: shape not supported). */
+size_t cfsd_spiral_conv_fwd_out_workspace(int batch, int vsrc, int seq, int cin, int cout);
+int cfsd_spiral_conv_fwd_out(const void* x, int x_dt, const int32_t* idx, const float* w, const float* bias,
+                             float* y, int y_dt, float* workspace, size_t workspace_bytes, int batch,
+                             int vsrc, int rows, int seq, int cin, int cout, int act, void* stream);
 /* cfsd_spmm_csr with per-operand storage types (elu_y has y's type). */
 int cfsd_spmm_csr_x(const int32_t* row_ptr, const int32_t* col, const float* val, const void* x,
                     int x_dt, const void* elu_y, void* y, int y_dt, int batch, int m, int n, int c,

@@ -207,9 +207,9 @@ def test_xyz_layers_vm32(mods, otopo, dtopo):
 
 def test_fp32_step_vertex_major_vs_batch_major(mods, dtopo):
     """Three C2 train steps (batch 16) in both fp32 layouts from the same
-    weights and batches: the forward is bit-identical, the gradients differ
-    only in fp32 summation order, so losses agree to 1e-5 relative and the
-    parameters after three Adam steps to 1e-5 of their magnitude."""
+    weights and batches: outputs and gradients differ only in fp32 summation
+    order, so outputs and losses agree to 1e-5 relative and the parameters
+    after three Adam steps to 1e-5 of their magnitude."""
     E, ops, _ = mods
     w = recipe.golden_weights()
     meshes = torch.from_numpy(recipe.normalized_meshes(12)).to(DEV)
@@ -232,7 +232,9 @@ def test_fp32_step_vertex_major_vs_batch_major(mods, dtopo):
             losses.append(b.losses.cpu().clone())
         res.append((out0, torch.stack(losses), eng.params.data.cpu().clone(), eng.params.grad.cpu().clone()))
     (o_bm, l_bm, p_bm, g_bm), (o_vm, l_vm, p_vm, g_vm) = res
-    assert torch.equal(o_bm, o_vm)
+    # every conv up to the output conv is bit-identical; the vertex-major
+    # output conv sums its K = 288 dot product per slot first (rel 1e-5)
+    assert err_rel_max(o_vm, o_bm) <= 1e-5
     assert float(((l_vm - l_bm).abs() / l_bm.abs().clamp_min(1e-12)).max()) <= 1e-5
     assert err_rel_max(p_vm, p_bm) <= 1e-5
     assert err_rel_max(g_vm, g_bm) <= 1e-4
@@ -268,3 +270,92 @@ def test_fp32_vm_graph_step_matches_eager(mods, dtopo):
         res.append((eng.params.data.cpu().clone(), b.losses.cpu().clone()))
         assert torch.isfinite(res[-1][1]).all()
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_swap_and_losses_vertex_major(mods, dtopo):
+    """Level-0 xyz tensors in the vertex-major layout: the feature swap
+    (swap_batch_transform.py:13-42) and the MSE + Laplacian passes
+    (model_manager.py:333-349) give the batch-major values element for
+    element (same per-row arithmetic); the reduced losses are sums in another
+    order (rel 1e-6)."""
+    _, ops, _ = mods
+    g = torch.Generator().manual_seed(3)
+    nv = dtopo.n_verts[0]
+    data = torch.randn(12, nv, 3, generator=g).to(DEV)
+    idx = torch.tensor([1, 5, 7, 9], dtype=torch.int32, device=DEV)
+    key = torch.tensor([2], dtype=torch.int32, device=DEV)
+    x_bm = ops.swap_features(data, idx, dtopo.region_mask, key, 4)
+    x_vm = ops.vm_empty(16, nv, 3, device=DEV)
+    ops.swap_features(data, idx, dtopo.region_mask, key, 4, out=x_vm)
+    assert ops.is_vm(x_vm) and torch.equal(x_vm.contiguous(), x_bm)
+    pred = torch.randn(16, nv, 3, generator=g).to(DEV)
+    res = []
+    for vm in (False, True):
+        mk = (lambda: ops.vm_empty(16, nv, 3, device=DEV)) if vm else (lambda: torch.empty(16, nv, 3, device=DEV))
+        p, x, unit, dout = mk(), mk(), mk(), mk()
+        p.copy_(pred)
+        x.copy_(x_bm)
+        parts = torch.empty(2 * ops.recon_lap_blocks(16, nv), device=DEV)
+        terms = torch.tensor([0.5, 0.25], device=DEV)
+        losses = torch.empty(5, device=DEV)
+        ops.recon_lap_fwd(p, x, dtopo.lap_csr, unit, parts)
+        ops.recon_lap_bwd_finalize(p, x, unit, dtopo.lapT_csr, dout, 1.0, 0.1, parts, terms, losses, None,
+                                   1e-4, 0.5)
+        torch.cuda.synchronize()
+        res.append((unit.contiguous().cpu(), dout.contiguous().cpu(), losses.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert err_rel_max(res[1][2], res[0][2]) <= 1e-6
+
+
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("bsz", [16, 32])
+def test_bwd_out_flat(mods, otopo, dtopo, xdt, bsz):
+    """Vertex-major fused backward of the xyz output conv (model.py:172-173
+    autograd) through the flat inverse list, against float64 autograd of
+    gather + Linear on the same (storage-rounded) operands: dx rel 1e-5 (+ one
+    bf16 rounding for bf16 storage), dW / db rel 1e-5; deferred slabs reduce
+    to the same values."""
+    _, ops, _ = mods
+    g = torch.Generator().manual_seed(bsz + (7 if xdt == torch.bfloat16 else 0))
+    sp = otopo.spirals[0]
+    v = sp.shape[0]
+    h = torch.nn.functional.elu(torch.randn(bsz, v, 32, generator=g)).to(xdt)
+    w = torch.randn(3, 288, generator=g) * 0.1
+    dout = torch.randn(bsz, v, 3, generator=g)
+    hl = h.double().requires_grad_()
+    wl = w.double().requires_grad_()
+    (gather(hl, sp) @ wl.T).backward(dout.double())
+    ref_dx = hl.grad * torch.where(h.double() > 0, 1.0, h.double() + 1.0)
+    hv = ops.to_vm(h.to(DEV))
+    dx = ops.vm_empty(bsz, v, 32, dtype=xdt, device=DEV)
+    dw, db = torch.empty(3, 288, device=DEV), torch.empty(3, device=DEV)
+    dv = ops.to_vm(dout.to(DEV))
+    ops.spiral_conv_bwd_out_flat(hv, dtopo.spiral[0], dv, dtopo.spiral_flat[0], w.to(DEV), dw, db, dx=dx, elu_y=hv)
+    tol = 1e-5 if xdt == torch.float32 else 2.0 ** -8
+    assert err_rel_max(dx.float(), ref_dx) <= tol
+    assert err_rel_max(dw, wl.grad) <= 1e-5
+    assert err_rel_max(db, dout.double().sum((0, 1))) <= 1e-5
+    dx2 = ops.vm_empty(bsz, v, 32, dtype=xdt, device=DEV)
+    _, d = ops.spiral_conv_bwd_out_flat(hv, dtopo.spiral[0], dv, dtopo.spiral_flat[0], w.to(DEV), None, None,
+                                        dx=dx2, elu_y=hv)
+    dw2, db2 = torch.empty_like(dw), torch.empty_like(db)
+    ops.dw_reduce_batch([(d, dw2, db2)])
+    assert torch.equal(dx2, dx) and torch.equal(dw2, dw) and torch.equal(db2, db)
+
+
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("bsz,yvm", [(16, True), (32, True), (16, False)])
+def test_fwd_out_two_pass(mods, otopo, dtopo, xdt, bsz, yvm):
+    """Two-pass vertex-major output conv (model.py:172-173) against float64
+    gather + Linear on the same (storage-rounded) x: rel 1e-5."""
+    _, ops, _ = mods
+    g = torch.Generator().manual_seed(bsz + yvm)
+    sp = otopo.spirals[0]
+    v = sp.shape[0]
+    h = torch.nn.functional.elu(torch.randn(bsz, v, 32, generator=g)).to(xdt)
+    w = torch.randn(3, 288, generator=g) * 0.1
+    bias = torch.randn(3, generator=g)
+    ref = gather(h.double(), sp) @ w.double().T + bias.double()
+    out = ops.vm_empty(bsz, v, 3, device=DEV) if yvm else torch.empty(bsz, v, 3, device=DEV)
+    ops.spiral_conv_fwd_out(ops.to_vm(h.to(DEV)), dtopo.spiral[0], w.to(DEV), bias.to(DEV), 0, out)
+    assert err_rel_max(out, ref) <= 1e-5

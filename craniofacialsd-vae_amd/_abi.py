@@ -73,8 +73,6 @@ SIGNATURES = {
     "cfsd_spiral_conv_bwd_weight_x": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_x": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I,
                                     _I, _I, _I, _P]),
-    "cfsd_spiral_conv_fwd_out_workspace": (_Z, [_I, _I, _I, _I, _I]),
-    "cfsd_spiral_conv_fwd_out": (_I, [_P, _I, _P, _P, _P, _P, _I, _P, _Z, _I, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_out_flat": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I,
                                            _I, _I, _I, _P]),
     "cfsd_spmm_csr_x": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),

@@ -25,12 +25,5 @@ int launch_dx_flat(const float* dpre, const int* flat, int width, const float* w
 int launch_bwd_out(const float* dout, const int* flat, int width, const float* w, const void* elu_y, const void* x,
                    void* dx, int x_bf16, float* ws, int n_slabs, int vsrc, int rows, int batch, hipStream_t st);
 
-// Forward of the xyz output conv (32 -> 3) for a vertex-major x (fp32 or
-// bf16): Z = per-slot products of every source vertex into ws
-// (out_z_floats), then y = act(bias + sum_s Z[idx[v][s]][s]); y either layout.
-size_t out_z_floats(int batch, int vsrc);
-int launch_fwd_out(const void* x, int x_bf16, const int* idx, const float* w, const float* bias, float* y, int yvm,
-                   float* ws, int vsrc, int rows, int batch, int act, hipStream_t st);
-
 }  // namespace vm32
 }  // namespace cfsd

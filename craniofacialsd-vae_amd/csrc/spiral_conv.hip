@@ -3158,31 +3158,6 @@ extern "C" int cfsd_spiral_conv_bwd_x(const void* x, int x_dt, const int32_t* id
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_x: unsupported channels %d -> %d", cin, cout);
 }
 
-// Forward of the xyz output conv for a vertex-major x in two passes through
-// a workspace (spiral_conv_vm32.hip conv_out_z_vm / conv_out_gather_vm).
-extern "C" size_t cfsd_spiral_conv_fwd_out_workspace(int batch, int vsrc, int seq, int cin, int cout) {
-  if (batch <= 0 || vsrc <= 0 || seq != kSeq || cin != 32 || cout != 3 || batch % 16) return 0;
-  return vm32::out_z_floats(batch, vsrc) * sizeof(float);
-}
-
-extern "C" int cfsd_spiral_conv_fwd_out(const void* x, int x_dt, const int32_t* idx, const float* w,
-                                        const float* bias, float* y, int y_dt, float* workspace,
-                                        size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
-                                        int cout, int act, void* stream) {
-  int rc = check_conv_args(x, idx, y, batch, vsrc, rows, seq, cin, cout);
-  if (rc) return rc;
-  if (!dt_ok(x_dt) || !vm_of(x_dt) || !dt_ok(y_dt) || CFSD_DT_TYPE(y_dt) != CFSD_DT_F32)
-    return set_error(CFSD_EINVAL, "spiral_conv_fwd_out: x must be vertex-major, y fp32");
-  if (cin != 32 || cout != 3) return set_error(CFSD_EINVAL, "spiral_conv_fwd_out: 32 -> 3 only (%d -> %d)", cin, cout);
-  if (!w || !workspace) return set_error(CFSD_EINVAL, "spiral_conv_fwd_out: null w / workspace");
-  if (act != CFSD_ACT_NONE && act != CFSD_ACT_ELU) return set_error(CFSD_EINVAL, "bad act %d", act);
-  const size_t need = cfsd_spiral_conv_fwd_out_workspace(batch, vsrc, seq, cin, cout);
-  if (need == 0 || workspace_bytes < need)
-    return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
-  return vm32::launch_fwd_out(x, CFSD_DT_TYPE(x_dt) == CFSD_DT_BF16, idx, w, bias, y, vm_of(y_dt), workspace, vsrc,
-                              rows, batch, act, (hipStream_t)stream);
-}
-
 // Fused dx + dW of the xyz output conv for vertex-major operands through the
 // flat inverse list (spiral_conv_vm32.hip conv_bwd_out_vm): same workspace
 // and slab layout as cfsd_spiral_conv_bwd_x (deferred items use fused = 1).

@@ -453,115 +453,6 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
 }
 
 
-// ------------------------------------------------------------------ output conv forward (32 -> 3)
-// y[v][m][o] = act(bias[o] + sum_s sum_c W[o][s*32 + c] h[idx[v][s]][m][c])
-// (model.py:172-173) for a vertex-major h, batch % 16 == 0, in two passes
-// that move the spiral gather to the 3-wide side:
-//  (1) conv_out_z_vm: Z[u][s][m][o] = sum_c W[o][s*32 + c] h[u][m][c] for
-//      every source vertex u (dense: h read once; 27 of 32 rows of two
-//      16x16x4 MFMA tiles per unit), each unit's Z block written as nine
-//      contiguous 192-B rows (per s: 16 meshes x 3);
-//  (2) conv_out_gather_vm: y = act(bias + sum_s Z[idx[v][s]][s]) -- nine
-//      192-B gathers per output unit instead of nine 2-KiB h blocks.
-// The per-output sum runs s-major over per-slot dot products (the K = 288 dot
-// product reassociated): fp32 rounding differs from a single dot product.
-template <typename TX>
-__global__ __launch_bounds__(256) void conv_out_z_vm(const TX* __restrict__ h, const float* __restrict__ w,
-                                                     float* __restrict__ z, int vsrc, int batch) {
-  constexpr int CIN = 32, CO = 3, KR = kS * CO, K = kS * CIN, WS = 40;
-  __shared__ float wl[32 * WS];        // W'[k][c] = W[o][s*32 + c], k = 3s + o; rows 27..31 zero
-  __shared__ float zl_all[4 * kS * 48];
-  for (int e = threadIdx.x; e < 32 * CIN; e += blockDim.x) {
-    const int k = e / CIN, c = e % CIN;
-    wl[k * WS + c] = k < KR ? w[(k % CO) * K + (k / CO) * CIN + c] : 0.f;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int j = lane & 15, g = lane >> 4;
-  float* zl = zl_all + wave * kS * 48;
-  const int G16 = batch >> 4;
-  const long n_units = (long)vsrc * G16;
-  constexpr int UPW = 2;  // units per wave, their h loads in flight together
-  const long unit0 = ((long)xcd_block() * 4 + wave) * UPW;
-  if (unit0 >= n_units) return;
-  int uu[UPW], mgs[UPW];
-  f32x4 hv[UPW][2];
-#pragma unroll
-  for (int q = 0; q < UPW; ++q) {
-    const int un = uni((int)min(unit0 + q, n_units - 1));
-    uu[q] = un / G16;
-    mgs[q] = un - uu[q] * G16;
-    const TX* hb = h + ((long)uu[q] * batch + mgs[q] * 16 + j) * CIN + 4 * g;
-    hv[q][0] = ld4f(hb);
-    hv[q][1] = ld4f(hb + 16);
-  }
-#pragma unroll
-  for (int q = 0; q < UPW; ++q) {
-    if (unit0 + q >= n_units) break;  // uniform
-    f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int cc = 0; cc < 2; ++cc) {
-        const f32x4 a = ld4(&wl[(16 * mt + j) * WS + 4 * g + 16 * cc]);
-        acc[mt] = mfma16(a.x, hv[q][cc].x, acc[mt]);
-        acc[mt] = mfma16(a.y, hv[q][cc].y, acc[mt]);
-        acc[mt] = mfma16(a.z, hv[q][cc].z, acc[mt]);
-        acc[mt] = mfma16(a.w, hv[q][cc].w, acc[mt]);
-      }
-    // D[k][m] (lane (m = j, g): k = 16mt + 4g + rr) -> Zl[s][m*3 + o]
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int k = 16 * mt + 4 * g + rr;
-        if (k < KR) zl[(k / CO) * 48 + j * CO + k % CO] = acc[mt][rr];
-      }
-    wave_sync_lds();
-    if (lane < 48) {
-#pragma unroll
-      for (int s = 0; s < kS; ++s)
-        z[(((long)uu[q] * kS + s) * batch + mgs[q] * 16) * CO + lane] = zl[s * 48 + lane];
-    }
-    wave_sync_lds();
-  }
-}
-
-template <int ACT>
-__global__ __launch_bounds__(256) void conv_out_gather_vm(const float* __restrict__ z, const int* __restrict__ idx,
-                                                          const float* __restrict__ bias, float* __restrict__ y,
-                                                          int yvm, int rows, int batch) {
-  // lane = (unit q of the wave's 4, mesh m): one 12-B Z row per slot, the 16
-  // meshes of a unit one contiguous 192-B block
-  constexpr int CO = 3;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int q = lane >> 4, m = lane & 15;
-  const int G16 = batch >> 4;
-  const long n_units = (long)rows * G16;
-  const long unit = ((long)xcd_block() * 4 + wave) * 4 + q;
-  if (unit >= n_units) return;
-  const int un = (int)unit;
-  const int v = un / G16, mg = un - v * G16;
-  int src[kS];
-#pragma unroll
-  for (int s = 0; s < kS; ++s) src[s] = idx[v * kS + s];
-  float zv[kS][CO];
-#pragma unroll
-  for (int s = 0; s < kS; ++s) ld_row<CO>(z + (((long)src[s] * kS + s) * batch + mg * 16 + m) * CO, zv[s]);
-  const int mesh = mg * 16 + m;
-  const long row = yvm ? (long)v * batch + mesh : (long)mesh * rows + v;
-  float r[CO];
-#pragma unroll
-  for (int o = 0; o < CO; ++o) {
-    float acc = zv[0][o];
-#pragma unroll
-    for (int s = 1; s < kS; ++s) acc += zv[s][o];
-    r[o] = (bias ? bias[o] : 0.f) + acc;
-    if (ACT == CFSD_ACT_ELU) r[o] = elu_f(r[o]);
-  }
-  st_row<CO>(y + row * CO, r);
-}
-
 // ------------------------------------------------------------------ launchers
 bool ok(int batch, int cin, int cout) { return batch % 16 == 0 && cin == 32 && (cout == 32 || cout == 64); }
 
@@ -664,27 +555,6 @@ int launch_bwd_out(const float* dout, const int* flat, int width, const float* w
   return set_error(CFSD_EINVAL, "spiral_conv_bwd (vertex-major output conv): flat width %d", width);
 }
 
-
-size_t out_z_floats(int batch, int vsrc) { return (size_t)vsrc * kS * batch * 3; }
-
-int launch_fwd_out(const void* x, int x_bf16, const int* idx, const float* w, const float* bias, float* y, int yvm,
-                   float* ws, int vsrc, int rows, int batch, int act, hipStream_t st) {
-  if (batch % 16) return set_error(CFSD_EINVAL, "spiral_conv_fwd (vertex-major output conv): batch %% 16 != 0");
-  const long units_src = (long)vsrc * (batch / 16), units = (long)rows * (batch / 16);
-  const dim3 gz((unsigned)((units_src + 7) / 8)), gg((unsigned)((units + 15) / 16));
-  if (x_bf16)
-    hipLaunchKernelGGL((conv_out_z_vm<bf16_t>), gz, dim3(256), 0, st, (const bf16_t*)x, w, ws, vsrc, batch);
-  else
-    hipLaunchKernelGGL((conv_out_z_vm<float>), gz, dim3(256), 0, st, (const float*)x, w, ws, vsrc, batch);
-  int rc = launch_status("spiral_conv_fwd_out_z");
-  if (rc) return rc;
-  if (act == CFSD_ACT_ELU)
-    hipLaunchKernelGGL((conv_out_gather_vm<CFSD_ACT_ELU>), gg, dim3(256), 0, st, ws, idx, bias, y, yvm, rows, batch);
-  else
-    hipLaunchKernelGGL((conv_out_gather_vm<CFSD_ACT_NONE>), gg, dim3(256), 0, st, ws, idx, bias, y, yvm, rows,
-                       batch);
-  return launch_status("spiral_conv_fwd_out_gather");
-}
 
 }  // namespace vm32
 }  // namespace cfsd

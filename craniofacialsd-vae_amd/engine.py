@@ -420,8 +420,6 @@ class SDVAEEngine:
             ws = max(ws, ops.spiral_conv_workspace(bsz, nv[lv], nv[lv], T.seq[lv], cin, cout))
         ws = max(ws, ops.spiral_conv_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
         ws = max(ws, ops.spiral_conv_bwd_workspace(bsz, nv[0], nv[0], T.seq[0], S.out_ch[0], S.in_ch))
-        if 0 in lp:  # two-pass vertex-major output conv (per-slot products of every vertex)
-            ws = max(ws, ops.spiral_conv_fwd_out_workspace(bsz, nv[0], T.seq[0], S.out_ch[0], S.in_ch))
         # bf16 Enblocks whose dpre is fp32: dx by the row-subset dG + gather
         b.rowsub_x = {}
         for (cin, cout, lv) in S.enc_layers():
@@ -576,12 +574,7 @@ class SDVAEEngine:
                            b.dec_out[i])
             h = b.dec_out[i]
         n = S.n
-        if self._flat_out(b):  # vertex-major: the spiral gather on the 3-wide side
-            P = self.params
-            ops.spiral_conv_fwd_out(h, T.spiral[0], P.view(f"de_layers.{n + 1}.layer.weight"),
-                                    P.view(f"de_layers.{n + 1}.layer.bias"), ACT_NONE, b.out, workspace=b.ws)
-        else:
-            self._conv_fwd(b, h, T.spiral[0], f"de_layers.{n + 1}.layer", ACT_NONE, b.out)
+        self._conv_fwd(b, h, T.spiral[0], f"de_layers.{n + 1}.layer", ACT_NONE, b.out)
 
     def losses_fwd(self, b, acc=None, finalize=True):
         T = self.topo

@@ -841,34 +841,6 @@ def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspa
     return dx
 
 
-def spiral_conv_fwd_out_workspace(bsz, vsrc, seq, cin, cout):
-    return int(_abi.lib().cfsd_spiral_conv_fwd_out_workspace(bsz, vsrc, seq, cin, cout))
-
-
-def spiral_conv_fwd_out(x, idx, w, b, act, out, workspace=None):
-    """Forward of the xyz output conv (32 -> 3) for a vertex-major x (fp32 or
-    bf16), batch a multiple of 16: dense per-slot products of every source
-    vertex, then the spiral gather on the 3-wide side."""
-    bsz, vsrc, cin = x.shape
-    rows, seq = idx.shape
-    cout = w.shape[0]
-    if not is_vm(x):
-        raise ValueError("x must be vertex-major")
-    _needl(x, None, "x", x.dtype)
-    _need(idx, (rows, seq), torch.int32, "idx")
-    _need(w, (cout, seq * cin), name="w")
-    if b is not None:
-        _need(b, (cout,), name="bias")
-    _needl(out, (bsz, rows, cout), "out", torch.float32)
-    need = spiral_conv_fwd_out_workspace(bsz, vsrc, seq, cin, cout)
-    if need == 0:
-        raise ValueError(f"no two-pass output conv for {cin} -> {cout} at batch {bsz}")
-    ws, nb = _conv_ws(workspace, x.device, need)
-    call("cfsd_spiral_conv_fwd_out", ptr(x), _st(x), ptr(idx), ptr(w), ptr(b), ptr(out), _st(out), ptr(ws),
-         ctypes.c_size_t(nb), bsz, vsrc, rows, seq, cin, cout, act, stream_ptr())
-    return out
-
-
 def spiral_conv_bwd_out_flat(x, idx, dpre, flat, w, dw, db, dx=None, elu_y=None, workspace=None):
     """Fused dx + dW of the xyz output conv (32 -> 3) with vertex-major x /
     elu_y / dx (fp32 or bf16) and dpre, through the flat inverse list

@@ -458,16 +458,6 @@ int cfsd_spiral_conv_bwd_out_flat(const void* x, int x_dt, const int32_t* idx, c
                                   const void* elu_y, void* dx, float* dw, float* db, float* workspace,
                                   size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
                                   int cout, void* stream);
-/* Forward of the xyz output conv (32 -> 3, model.py:172-173) for a
- * VERTEX-MAJOR x (fp32 or bf16, batch % 16 == 0; ABI 4.2) in two passes:
- * Z[u][s][m][o] = sum_c w[o, s*32 + c] x[m, u, c] for every source vertex
- * (dense), then y = act(bias + sum_s Z[idx[v, s]][s]) -- the gather moves to
- * the 3-wide side.  y fp32 in either layout; workspace
- * cfsd_spiral_conv_fwd_out_workspace() bytes (0: shape not supported). */
-size_t cfsd_spiral_conv_fwd_out_workspace(int batch, int vsrc, int seq, int cin, int cout);
-int cfsd_spiral_conv_fwd_out(const void* x, int x_dt, const int32_t* idx, const float* w, const float* bias,
-                             float* y, int y_dt, float* workspace, size_t workspace_bytes, int batch,
-                             int vsrc, int rows, int seq, int cin, int cout, int act, void* stream);
 /* cfsd_spmm_csr with per-operand storage types (elu_y has y's type). */
 int cfsd_spmm_csr_x(const int32_t* row_ptr, const int32_t* col, const float* val, const void* x,
                     int x_dt, const void* elu_y, void* y, int y_dt, int batch, int m, int n, int c,

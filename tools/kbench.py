@@ -254,6 +254,9 @@ def main():
     cases["dout_bwd_vm"] = lambda: ops.spiral_conv_bwd_x(v.dec_out[3], T.spiral[0], v.dout, T.spiral_inv[0], wov,
                                                          None, None, dx=v.dpre_dec[3], elu_y=v.dec_out[3],
                                                          workspace=v.ws_dw["out"])
+    cases["dout_bwd_flat"] = lambda: ops.spiral_conv_bwd_out_flat(v.dec_out[3], T.spiral[0], v.dout, T.spiral_flat[0],
+                                                                  wov, None, None, dx=v.dpre_dec[3],
+                                                                  elu_y=v.dec_out[3], workspace=v.ws_dw["out"])
     cases["e0_fwd_vm"] = lambda: ops.spiral_conv_fwd_x(v.x, T.enc_rows[0], *ev._enc_w(0)[:1], None, ev._enc_w(0)[1],
                                                        1, v.enc_out[0])
     cases["e0_dw_vm"] = lambda: ops.spiral_conv_bwd_weight_x(v.x, T.enc_rows[0], v.dpre_enc[0], None, None,

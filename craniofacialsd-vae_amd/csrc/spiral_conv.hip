@@ -882,8 +882,12 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
   // vertices x 16 meshes, so each slot's gathered rows are two contiguous
   // blocks); dpre rows are addressed in their own layout
   const Lay lx = make_lay(xvm, batch, vsrc), ldp = make_lay(dpvm, batch, rows);
+  // The gather addresses need the tile's spiral indices first: those are
+  // loaded one tile earlier than the x rows (xoff), so each tile's staging
+  // costs one memory latency, hidden behind the previous tile's MFMAs.
   f32x4 xs[C::XPT], ds[C::DPT];
-  auto load_tile = [&](long tile) {
+  int xoff[C::XPT];  // float offsets (x < 2^31 elements, checked by dw_f32)
+  auto load_idx = [&](long tile, int (&xo)[C::XPT]) {
     const long m0 = tile * 32;
 #pragma unroll
     for (int e = 0; e < C::XPT; ++e) {
@@ -897,8 +901,16 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
         int b, r;  // < 2^31 rows: 32-bit division
         split_row(m, xvm, batch, rows, b, r);
         const int src = idx[r * kSeq + s];
-        xs[e] = ld4(x + ((long)b * lx.bs + (long)src * lx.vs) * CIN + 4 * c4);
+        xo[e] = (b * lx.bs + src * lx.vs) * CIN + 4 * c4;
       }
+    }
+  };
+  auto load_tile = [&](long tile) {
+    const long m0 = tile * 32;
+#pragma unroll
+    for (int e = 0; e < C::XPT; ++e) {
+      const int f = tid + e * C::THREADS;
+      if (f < C::XF4) xs[e] = ld4(x + xoff[e]);
     }
 #pragma unroll
     for (int e = 0; e < C::DPT; ++e) {
@@ -920,7 +932,12 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
 
   const TileSweep sw = xcd_sweep(n_tiles, 1, 0);
   long tile = sw.begin;
-  if (tile < sw.end) load_tile(tile);
+  int xnext[C::XPT];
+  if (tile < sw.end) {
+    load_idx(tile, xoff);
+    load_tile(tile);
+    if (tile + sw.step < sw.end) load_idx(tile + sw.step, xnext);
+  }
   for (; tile < sw.end; tile += sw.step) {
 #pragma unroll
     for (int e = 0; e < C::XPT; ++e) {
@@ -934,7 +951,12 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
     }
     __syncthreads();
     const long next = tile + sw.step;
-    if (next < sw.end) load_tile(next);
+    if (next < sw.end) {
+#pragma unroll
+      for (int e = 0; e < C::XPT; ++e) xoff[e] = xnext[e];
+      load_tile(next);
+      if (next + sw.step < sw.end) load_idx(next + sw.step, xnext);
+    }
     if (tid < COUT) {
 #pragma unroll 8
       for (int row = 0; row < 32; ++row) db_acc += dp_lds[row * COUT + tid];
@@ -2521,6 +2543,8 @@ static int dw_f32(const float* x, int xvm, const int32_t* idx, const float* dpre
                      g.ws_floats * sizeof(float));
   if ((xvm || dpvm) && g.kind != kDwLat && g.kind != kDwMfma)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight: vertex-major operands need 32/64 channels");
+  if ((long)batch * vsrc * cin >= (1L << 31))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight: x has >= 2^31 elements (32-bit offsets)");
   const long M = (long)batch * rows;
   const int n_el = cout * kSeq * cin + cout;
   const dim3 rg((unsigned)((n_el + 63) / 64));

@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) void conv_dx_vm16(const TD* __restrict__ dpre,
 // of 3 head rows per slot, and the products are exact bf16 x bf16 in fp32
 // (no bf16 rounding of row sums).  One MFMA per entry and 16-column tile.
 template <int CIN, int COUT, typename TD, int FW>
-__global__ __launch_bounds__(256) void conv_dx_flat_vm16(const TD* __restrict__ dpre,
+__global__ __launch_bounds__(512) void conv_dx_flat_vm16(const TD* __restrict__ dpre,
                                                          const int4* __restrict__ flat,
                                                          const bf16_t* __restrict__ w,
                                                          const bf16_t* __restrict__ elu_y,
@@ -313,6 +313,7 @@ __global__ __launch_bounds__(256) void conv_dx_flat_vm16(const TD* __restrict__ 
   constexpr int K = kS * CIN, OP = COUT + 8, OC = COUT / 32, NT = CIN / 16, CPL = 4 * NT;
   constexpr int RB = COUT * (int)sizeof(TD);
   constexpr int NL = sizeof(TD) == 2 ? 1 : 2;
+  constexpr int FQ = FW / 4, PD = 2, NB = PD + 1;
   extern __shared__ bf16_t lwt[];  // as conv_dx_vm16
   coop_copy<12, bf16_t>(
       COUT * K, [&](int e) { return w[e]; },
@@ -329,42 +330,54 @@ __global__ __launch_bounds__(256) void conv_dx_flat_vm16(const TD* __restrict__ 
   const int nbytes = (int)((long)batch * rows * RB);
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<TD*>(dpre), 0, nbytes, 0x00020000);
   const int rstride = batch * RB;
-  const TileSweep sw = xcd_sweep(n_tiles, 4, wave, true);
-  for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
-    const int tl = uni((int)tile);
-    const int u = tl / G16, mg = tl - u * G16;
-    const int voff = (mg * 16 + j) * RB + 8 * g * (int)sizeof(TD);
-    int pe[FW];
+  const TileSweep sw = xcd_sweep(n_tiles, 8, wave, true);
+  // the walk stops at the list's first -1 (uniform branch), entries e + 1,
+  // e + 2 in flight while e runs its MFMAs, the next tile's list loaded at
+  // the start of this one (as the fp32 conv_dx_flat_vm32)
+  auto load_list = [&](long tile, int (&pe)[FW]) {
+    const int u = uni((int)tile) / G16;
 #pragma unroll
-    for (int q = 0; q < FW / 4; ++q) {
-      const int4 f = flat[u * (FW / 4) + q];
+    for (int q = 0; q < FQ; ++q) {
+      const int4 f = flat[(long)u * FQ + q];
       pe[4 * q] = uni(f.x);
       pe[4 * q + 1] = uni(f.y);
       pe[4 * q + 2] = uni(f.z);
       pe[4 * q + 3] = uni(f.w);
     }
-    u32x4 v[FW][OC][NL];
-#pragma unroll
-    for (int e = 0; e < FW; ++e) {
+  };
+  int pe[FW], pn[FW];
+  if (sw.begin < sw.end) load_list(sw.begin, pe);
+  for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
+    if (tile + sw.step < sw.end) load_list(tile + sw.step, pn);
+    const int tl = uni((int)tile);
+    const int u = tl / G16, mg = tl - u * G16;
+    const int voff = (mg * 16 + j) * RB + 8 * g * (int)sizeof(TD);
+    auto issue = [&](int e, u32x4(&d)[OC][NL]) {
       const int so = pe[e] >= 0 ? (pe[e] / kS) * rstride : kAbsent;
 #pragma unroll
       for (int oc = 0; oc < OC; ++oc)
 #pragma unroll
-        for (int l = 0; l < NL; ++l) v[e][oc][l] = bload16(rs, voff + 32 * oc * (int)sizeof(TD) + 16 * l, so);
-    }
+        for (int l = 0; l < NL; ++l) d[oc][l] = bload16(rs, voff + 32 * oc * (int)sizeof(TD) + 16 * l, so);
+    };
+    u32x4 v[NB][OC][NL];
+#pragma unroll
+    for (int e = 0; e < PD; ++e) issue(e, v[e]);
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int e = 0; e < FW; ++e) {
-      const int s = pe[e] >= 0 ? pe[e] % kS : 0;  // absent entries: B = 0, adds 0
+      if (e + PD < FW) issue(e + PD, v[(e + PD) % NB]);
+      if (pe[e] < 0) break;  // uniform: the rest of the list is padding
+      const int s = pe[e] % kS;
+      const u32x4(&cur)[OC][NL] = v[e % NB];
 #pragma unroll
       for (int oc = 0; oc < OC; ++oc) {
         u32x4 bt;
         if constexpr (sizeof(TD) == 2) {
-          bt = v[e][oc][0];
+          bt = cur[oc][0];
         } else {
-          const f32x4 a = __builtin_bit_cast(f32x4, v[e][oc][0]), b = __builtin_bit_cast(f32x4, v[e][oc][1]);
+          const f32x4 a = __builtin_bit_cast(f32x4, cur[oc][0]), b = __builtin_bit_cast(f32x4, cur[oc][1]);
           bt = (u32x4){pack_bf2(a.x, a.y), pack_bf2(a.z, a.w), pack_bf2(b.x, b.y), pack_bf2(b.z, b.w)};
         }
 #pragma unroll
@@ -398,6 +411,8 @@ __global__ __launch_bounds__(256) void conv_dx_flat_vm16(const TD* __restrict__ 
         vv[t][rr] = z;
       }
     store_row<NT>(dx + row * CIN + CPL * g, vv);
+#pragma unroll
+    for (int e = 0; e < FW; ++e) pe[e] = pn[e];
   }
 }
 
@@ -475,8 +490,9 @@ static int dxf16_t(const TD* dpre, const int* flat, const bf16_t* w, const bf16_
   constexpr size_t lds = (size_t)kS * CIN * (COUT + 8) * sizeof(bf16_t);
   auto kern = conv_dx_flat_vm16<CIN, COUT, TD, FW>;
   const long tiles = (long)vsrc * (batch / 16);
-  const unsigned grid = balanced_blocks(tiles, 4, resident(kern, lds));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows,
+  const int r = resident_blocks_of(kern, 512, lds);
+  const unsigned grid = balanced_blocks(tiles, 8, r > 0 ? r : 1);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows,
                      batch);
   return launch_status("spiral_conv_bwd_data_flat");
 }

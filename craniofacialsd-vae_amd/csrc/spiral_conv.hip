@@ -882,12 +882,10 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
   // vertices x 16 meshes, so each slot's gathered rows are two contiguous
   // blocks); dpre rows are addressed in their own layout
   const Lay lx = make_lay(xvm, batch, vsrc), ldp = make_lay(dpvm, batch, rows);
-  // The gather addresses need the tile's spiral indices first: those are
-  // loaded one tile earlier than the x rows (xoff), so each tile's staging
-  // costs one memory latency, hidden behind the previous tile's MFMAs.
+  // (loading the spiral indices one tile ahead of the gathers measured
+  // slower: D3 74 -> 91 us)
   f32x4 xs[C::XPT], ds[C::DPT];
-  int xoff[C::XPT];  // float offsets (x < 2^31 elements, checked by dw_f32)
-  auto load_idx = [&](long tile, int (&xo)[C::XPT]) {
+  auto load_tile = [&](long tile) {
     const long m0 = tile * 32;
 #pragma unroll
     for (int e = 0; e < C::XPT; ++e) {
@@ -901,16 +899,8 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
         int b, r;  // < 2^31 rows: 32-bit division
         split_row(m, xvm, batch, rows, b, r);
         const int src = idx[r * kSeq + s];
-        xo[e] = (b * lx.bs + src * lx.vs) * CIN + 4 * c4;
+        xs[e] = ld4(x + ((long)b * lx.bs + (long)src * lx.vs) * CIN + 4 * c4);
       }
-    }
-  };
-  auto load_tile = [&](long tile) {
-    const long m0 = tile * 32;
-#pragma unroll
-    for (int e = 0; e < C::XPT; ++e) {
-      const int f = tid + e * C::THREADS;
-      if (f < C::XF4) xs[e] = ld4(x + xoff[e]);
     }
 #pragma unroll
     for (int e = 0; e < C::DPT; ++e) {
@@ -932,12 +922,7 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
 
   const TileSweep sw = xcd_sweep(n_tiles, 1, 0);
   long tile = sw.begin;
-  int xnext[C::XPT];
-  if (tile < sw.end) {
-    load_idx(tile, xoff);
-    load_tile(tile);
-    if (tile + sw.step < sw.end) load_idx(tile + sw.step, xnext);
-  }
+  if (tile < sw.end) load_tile(tile);
   for (; tile < sw.end; tile += sw.step) {
 #pragma unroll
     for (int e = 0; e < C::XPT; ++e) {
@@ -951,12 +936,7 @@ __global__ __launch_bounds__(768) void conv_dw_mfma(
     }
     __syncthreads();
     const long next = tile + sw.step;
-    if (next < sw.end) {
-#pragma unroll
-      for (int e = 0; e < C::XPT; ++e) xoff[e] = xnext[e];
-      load_tile(next);
-      if (next + sw.step < sw.end) load_idx(next + sw.step, xnext);
-    }
+    if (next < sw.end) load_tile(next);
     if (tid < COUT) {
 #pragma unroll 8
       for (int row = 0; row < 32; ++row) db_acc += dp_lds[row * COUT + tid];

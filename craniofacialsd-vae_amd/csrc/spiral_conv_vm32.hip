@@ -151,6 +151,7 @@ __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const fl
   }
 }
 
+
 // ------------------------------------------------------------------ data gradient
 // Wave = tile (source vertex u, mesh group mg).  Entry e of u's flat list is
 // p_e = 9 r_e + s_e: B = dpre[r_e]^T (lane (j, g): mesh j, channels

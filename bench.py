@@ -593,7 +593,7 @@ def main():
             kern_names = {"conv_fwd_D3": "conv_fwd_vm32<32,32> (decoder level 0 forward, vertex-major)",
                           "conv_dx_D3": "conv_dx_flat_vm32<32,32> (decoder level 0 data gradient, vertex-major "
                                         "flat list)",
-                          "conv_dw_D3": "conv_dw_mfma<32,32> (decoder level 0 weight gradient, vertex-major)"}
+                          "conv_dw_D3": "conv_dw_vm32 (decoder level 0 weight gradient, vertex-major)"}
         else:
             kern_names = {"conv_fwd_D3": "conv_fwd_mfma<32,32> (decoder level 0 forward)",
                           "conv_dx_D3": "conv_dx_mfma<32,32> (decoder level 0 data gradient)",

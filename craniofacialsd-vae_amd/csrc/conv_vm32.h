@@ -19,6 +19,17 @@ int launch_fwd(const float* x, const int* idx, const float* w, const float* bias
 // spiral position p = 9r + s) of W_s^T dpre[r]; dpre, dx, elu_y vertex-major.
 int launch_dx_flat(const float* dpre, const int* flat, int width, const float* w, const float* elu_y,
                    float* dx, int vsrc, int rows, int batch, int cin, int cout, hipStream_t st);
+// dW/db slabs (conv_dw_mfma layout: [n_slabs][9][32][32], db [n_slabs][32] at
+// ws_db) of a 32 -> 32 conv, x and dpre vertex-major, batch % 16 == 0.
+// Workgroups (= slabs) launch_dw uses; max_slabs = the workspace's slab capacity.
+int dw_slabs(int batch, int rows, int max_slabs);
+int launch_dw(const float* x, const int* idx, const float* dpre, float* ws, float* ws_db, int n_slabs, int vsrc,
+              int rows, int batch, hipStream_t st);
+// The xyz output conv forward (32 -> cout <= 3), x vertex-major fp32 or bf16,
+// batch % 8 == 0, y vertex-major (yvm) or batch-major; the same bits as the
+// batch-major conv_fwd_out_small.
+int launch_fwd_out(const void* x, int x_bf16, const int* idx, const float* w, const float* bias, float* y, int yvm,
+                   int vsrc, int rows, int batch, int cout, int act, hipStream_t st);
 // dx (x's storage, times elu'(elu_y)) and the dW/db slab of one block per
 // n_slabs of the xyz output conv (32 -> 3); x / elu_y / dx / dout
 // vertex-major, flat = u's inverse list (topology.spiral_flat).

@@ -2505,6 +2505,13 @@ extern "C" size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int
   return dw_geom(batch, rows, cin, cout).ws_floats * sizeof(float);
 }
 
+#ifndef CFSD_DW_VM32
+#define CFSD_DW_VM32 1  // 32 -> 32 with vertex-major x and dpre: vm32::conv_dw_vm32
+#endif
+// The fp32 weight gradient takes vm32::conv_dw_vm32 (its slabs: cfsd_dw_slabs.fused == 3)
+static bool dw_vm32_path(int xvm, int dpvm, int cin, int cout, int batch) {
+  return CFSD_DW_VM32 && xvm && dpvm && cin == 32 && cout == 32 && batch % 16 == 0;
+}
 // dW / db of an fp32 conv, x and dpre each batch-major or vertex-major
 // (xvm / dpvm; the small-channel kernels are batch-major only).
 static int dw_f32(const float* x, int xvm, const int32_t* idx, const float* dpre, int dpvm, float* dw,
@@ -2552,10 +2559,15 @@ static int dw_f32(const float* x, int xvm, const int32_t* idx, const float* dpre
   if (cin == CIN_ && cout == COUT_) {                                                           \
     using C = DwCfg<CIN_, COUT_>;                                                               \
     auto k = conv_dw_mfma<CIN_, COUT_>;                                                         \
-    nslab = dw_mfma_slabs(cin, cout, g.gx);                                                     \
-    hipLaunchKernelGGL(k, dim3(nslab), dim3(C::THREADS), C::LDS_FLOATS * sizeof(float), st, x,  \
-                       idx, dpre, workspace, ws_db, vsrc, rows, M, batch, xvm, dpvm);           \
-    rc = launch_status("spiral_conv_bwd_weight");                                               \
+    if (dw_vm32_path(xvm, dpvm, cin, cout, batch)) {                                            \
+      nslab = vm32::dw_slabs(batch, rows, g.gx);                                                \
+      rc = vm32::launch_dw(x, idx, dpre, workspace, ws_db, nslab, vsrc, rows, batch, st);        \
+    } else {                                                                                    \
+      nslab = dw_mfma_slabs(cin, cout, g.gx);                                                   \
+      hipLaunchKernelGGL(k, dim3(nslab), dim3(C::THREADS), C::LDS_FLOATS * sizeof(float), st, x, \
+                         idx, dpre, workspace, ws_db, vsrc, rows, M, batch, xvm, dpvm);         \
+      rc = launch_status("spiral_conv_bwd_weight");                                             \
+    }                                                                                           \
     if (rc || deferred) return rc;                                                              \
     hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), rg, dim3(1024), 0, st, workspace, ws_db,  \
                        dw, db, nslab);                                                          \
@@ -2946,6 +2958,9 @@ extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* id
     FINF(1, 32) FINF(2, 32) FINF(3, 32) FINF(1, 64) FINF(2, 64) FINF(3, 64)
 #undef FINF
   }
+  if (cout <= 3 && cin == 32 && xvm && batch % 8 == 0 && y_dt == CFSD_DT_F32)  // xyz output conv, vertex-major x
+    return vm32::launch_fwd_out(x, x_dt == CFSD_DT_BF16, idx, w, bias, (float*)y, yvm, vsrc, rows, batch, cout, act,
+                                st);
   if (cout <= 3 && (cin == 16 || cin == 32 || cin == 64) && x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) {
 #define FOUTF(CI_, CO_)                                                                           \
   if (cin == CI_ && cout == CO_) {                                                                \
@@ -3229,7 +3244,10 @@ static int dw_reduce_batch_launch(const cfsd_dw_slabs* items, int n, const DwAda
       if (g.kind == kDwMfma || g.kind == kDwLat) {
         const int U = (int)dw_units(q.cin, q.cout);
         d.kind = 0;
-        d.n_slabs = g.kind == kDwLat ? g.gx : dw_mfma_slabs(q.cin, q.cout, g.gx);
+        const bool vm = q.fused == 3 && dw_vm32_path(1, 1, q.cin, q.cout, q.batch);  // as dw_f32 chose
+        d.n_slabs = g.kind == kDwLat ? g.gx
+                    : vm             ? vm32::dw_slabs(q.batch, q.rows, g.gx)
+                                     : dw_mfma_slabs(q.cin, q.cout, g.gx);
         d.n_el = U * 1024 + q.cout;
         d.ws_db = q.workspace + (size_t)g.gx * U * 1024;
       } else {

@@ -262,6 +262,127 @@ __global__ __launch_bounds__(512, CFSD_VM32_DX_OCC) void conv_dx_flat_vm32(const
 }
 
 
+// ------------------------------------------------------------------ weight gradient (32 -> 32)
+// dW_s[o][c] = sum over (vertex v, mesh m) of dpre[v][m][o] x[idx[v][s]][m][c]
+// (the Linear's weight gradient over the gathered rows, model.py:34, 40) for
+// vertex-major x and dpre, batch % 16 == 0.  No LDS staging: a unit
+// (vertex v, 16-mesh group) contributes K = 16 meshes to every slot, and in
+// the v_mfma_f32_32x32x2_f32 lane map (A[o][k]: lane (o, h) ~ mesh 2j + h)
+// both operands of step j are two consecutive 128-B rows of a contiguous
+// 2-KiB block -- ONE coalesced 256-B dword load each.  A wave keeps all nine
+// 32x32 slot accumulators (144 registers) for its whole contiguous unit
+// range, so the MFMA pipe always has nine independent chains; dpre is loaded
+// once per unit for the nine slots and the next unit's 80 loads are in
+// flight while this unit runs its 72 MFMAs (one wave per SIMD: a workgroup
+// of 4 waves per CU).  The 4 waves' accumulators are summed in LDS in fixed
+// order into one conv_dw_mfma-layout slab ([9][32][32] + db[32]) per
+// workgroup, reduced by conv_dw_reduce / dw_reduce_batch (kind 0).
+#ifndef CFSD_DWV_NS
+#define CFSD_DWV_NS 3  // slots per wave (3: a slot group of three, 9: all nine)
+#endif
+#ifndef CFSD_DWV_NR
+#define CFSD_DWV_NR 4  // unit ranges per workgroup (waves = NR * 9 / NS)
+#endif
+constexpr int DWV_NS = CFSD_DWV_NS, DWV_NR = CFSD_DWV_NR, DWV_WAVES = DWV_NR * (kS / DWV_NS);
+constexpr int DWV_THREADS = DWV_WAVES * 64;
+__global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restrict__ x,
+                                                            const int* __restrict__ idx,
+                                                            const float* __restrict__ dpre,
+                                                            float* __restrict__ ws, float* __restrict__ ws_db,
+                                                            int vsrc, int rows, int batch) {
+  constexpr int C = 32, NEL = kS * 1024, NS = DWV_NS, NG = kS / NS;
+  __shared__ float red[NEL];
+  __shared__ float dbl[DWV_NR * 64];
+  const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
+  const int sg = wave % NG, vg = wave / NG;  // slot group, unit range
+  const int G16 = batch >> 4;
+  const long n_units = (long)rows * G16;
+  // XCD-contiguous unit ranges: blocks b, b + 8, ... (one XCD) split one 1/8
+  const int nb = gridDim.x, G = nb < 8 ? nb : 8;
+  const int grp = blockIdx.x % G, lb = blockIdx.x / G, nb_g = (nb - grp + G - 1) / G;
+  const long per = (n_units + G - 1) / G;
+  const long g0 = grp * per, g1 = min(n_units, g0 + per);
+  const int nr = nb_g * DWV_NR, ri = lb * DWV_NR + vg;
+  const long u0 = g0 + (g1 - g0) * ri / nr, u1 = g0 + (g1 - g0) * (ri + 1) / nr;
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, (int)((long)vsrc * batch * C * 4),
+                                                    0x00020000);
+  const auto rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dpre), 0, (int)((long)rows * batch * C * 4),
+                                                    0x00020000);
+  const int voff = lane * 4;  // + 256 j: rows 2j, 2j + 1 of the 16-mesh block
+  f32x16 acc[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) acc[k] = (f32x16){0.f};
+  float dbs = 0.f;
+  float a[8], b[NS][8], an[8], bn[NS][8];
+  auto load_unit = [&](long un, float (&da)[8], float (&db)[NS][8]) {
+    const int uu = uni((int)un);
+    const int v = uu / G16, mg = uu - v * G16;
+    const int sd = (v * batch + mg * 16) * C * 4;
+#ifdef CFSD_DWV_NOLOAD
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      da[j] = (float)(sd + j + lane);
+#pragma unroll
+      for (int k = 0; k < NS; ++k) db[k][j] = (float)(uu + j + k);
+    }
+    return;
+#endif
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      da[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, voff + 256 * j, sd, 0));
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const int sx = (uni(idx[v * kS + NS * sg + k]) * batch + mg * 16) * C * 4;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        db[k][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff + 256 * j, sx, 0));
+    }
+  };
+  if (u0 < u1) load_unit(u0, a, b);
+  for (long un = u0; un < u1; ++un) {
+    const bool more = un + 1 < u1;  // uniform
+    if (more) load_unit(un + 1, an, bn);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int k = 0; k < NS; ++k) acc[k] = mfma32(a[j], b[k][j], acc[k]);
+    if (sg == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dbs += a[j];
+    }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[j] = an[j];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) b[k][j] = bn[k][j];
+      }
+    }
+  }
+  // block combine in fixed unit-range order -> one slab [9][32 o][32 c] + db
+  for (int g = 0; g < DWV_NR; ++g) {
+    if (vg == g) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int e = (NS * sg + k) * 1024 + acc_row(rr, lane) * 32 + (lane & 31);
+          red[e] = g == 0 ? acc[k][rr] : red[e] + acc[k][rr];
+        }
+      if (sg == 0) dbl[g * 64 + lane] = dbs;
+    }
+    __syncthreads();
+  }
+  float* slab = ws + (long)blockIdx.x * NEL;
+  for (int e = threadIdx.x; e < NEL / 4; e += DWV_THREADS) st4(slab + 4 * e, ld4(red + 4 * e));
+  if (threadIdx.x < C) {  // lanes o and o + 32 of each range hold meshes 2j and 2j + 1
+    float t = 0.f;
+    for (int g = 0; g < DWV_NR; ++g) t += dbl[g * 64 + threadIdx.x] + dbl[g * 64 + 32 + threadIdx.x];
+    ws_db[(long)blockIdx.x * C + threadIdx.x] = t;
+  }
+}
+
+
 // ------------------------------------------------------------------ output conv backward (32 -> 3)
 // dx and dW/db of the xyz output conv (model.py:172-173 and its autograd) for
 // vertex-major x / elu_y / dx and a vertex-major dout, batch % 16 == 0.
@@ -454,6 +575,107 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
 }
 
 
+// ------------------------------------------------------------------ output conv forward (32 -> CO <= 3)
+// The xyz output conv (model.py:172) for a vertex-major x, batch % 8 == 0.
+// Lane (r8, q): row r8 of an 8-row group (8 meshes of one vertex: each
+// neighbour load is ONE contiguous 1-KiB wave access), input channels
+// 4q .. 4q + 3.  A wave runs U groups per step: the U x 9 neighbour loads
+// are all in flight before the first FMA (spiral offsets wave-uniform, in
+// SGPRs), and every W fragment read from LDS serves all U groups (the
+// batch-major conv_fwd_out_small re-reads the 27 fragments per 8 rows).
+// Per output the products are accumulated in conv_fwd_out_small's order
+// (slot by slot, 4 channels by fmaf per lane, then the xor tree 4, 2, 1 over
+// the 8 lanes of the row, then the bias), so both layouts give the same bits.
+#ifndef CFSD_VM_OUT_U
+#define CFSD_VM_OUT_U 1
+#endif
+template <int CO, int ACT, int U, typename TX>
+__global__ __launch_bounds__(256) void conv_fwd_out_vm(const TX* __restrict__ x, const int* __restrict__ idx,
+                                                       const float* __restrict__ w, const float* __restrict__ bias,
+                                                       float* __restrict__ y, int vsrc, int rows, int batch,
+                                                       int yvm) {
+  constexpr int CIN = 32, K = kS * CIN, EB = (int)sizeof(TX);
+  __shared__ f32x4 lw[CO * K / 4];
+  for (int i = threadIdx.x; i < CO * K / 4; i += blockDim.x) lw[i] = ld4(w + 4 * i);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
+  const int q = lane & 7, r8 = lane >> 3;
+  float bo[CO];
+#pragma unroll
+  for (int o = 0; o < CO; ++o) bo[o] = bias ? bias[o] : 0.f;
+  const long n_grp = (long)rows * (batch >> 3);
+  const long n_it = (n_grp + U - 1) / U;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<TX*>(x), 0, (int)((long)vsrc * batch * CIN * EB),
+                                                    0x00020000);
+  const int vstride = batch * CIN * EB;  // bytes between two vertices' blocks
+  const TileSweep sw = xcd_sweep(n_it, 4, wave);
+  for (long it = sw.begin; it < sw.end; it += sw.step) {
+    int vv[U], bb[U], voff[U], soff[U][kS];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      long gl = it * U + u;
+      if (gl >= n_grp) gl = n_grp - 1;  // clamp loads, stores are skipped
+      const int m0 = uni((int)gl) * 8;
+      vv[u] = m0 / batch;
+      bb[u] = m0 - vv[u] * batch + r8;
+      voff[u] = (bb[u] * CIN + 4 * q) * EB;
+#pragma unroll
+      for (int s = 0; s < kS; ++s) soff[u][s] = uni(idx[vv[u] * kS + s]) * vstride;
+    }
+    f32x4 xv[U][kS];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int s = 0; s < kS; ++s) {
+        if constexpr (EB == 4) {
+          xv[u][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff[u], soff[u][s], 0));
+        } else {
+          const u32x2 h = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff[u], soff[u][s], 0));
+          xv[u][s] = (f32x4){__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xffff0000u),
+                             __uint_as_float(h.y << 16), __uint_as_float(h.y & 0xffff0000u)};
+        }
+      }
+    float acc[U][CO];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int o = 0; o < CO; ++o) acc[u][o] = 0.f;
+    int wq = q;
+    asm volatile("" : "+v"(wq));  // opaque: the W fragments stay LDS reads (not hoisted into VGPRs)
+#pragma unroll
+    for (int s = 0; s < kS; ++s)
+#pragma unroll
+      for (int o = 0; o < CO; ++o) {
+        const f32x4 wv = lw[(o * K + s * CIN) / 4 + wq];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          acc[u][o] = fmaf(xv[u][s].x, wv.x, acc[u][o]);
+          acc[u][o] = fmaf(xv[u][s].y, wv.y, acc[u][o]);
+          acc[u][o] = fmaf(xv[u][s].z, wv.z, acc[u][o]);
+          acc[u][o] = fmaf(xv[u][s].w, wv.w, acc[u][o]);
+        }
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int o = 0; o < CO; ++o)
+#pragma unroll
+        for (int d = 4; d >= 1; d >>= 1) acc[u][o] += __shfl_xor(acc[u][o], d);
+      if (it * U + u >= n_grp) break;  // uniform
+      if (q < CO) {  // lane q stores output channel q of its row: CO x 8 consecutive floats per group
+        float v = acc[u][0] + bo[0];
+#pragma unroll
+        for (int o = 1; o < CO; ++o)
+          if (q == o) v = acc[u][o] + bo[o];
+        if (ACT == CFSD_ACT_ELU) v = elu_f(v);
+        const long row = yvm ? (long)vv[u] * batch + bb[u] : (long)bb[u] * rows + vv[u];
+        y[row * CO + q] = v;
+      }
+    }
+  }
+}
+
+
 // ------------------------------------------------------------------ launchers
 bool ok(int batch, int cin, int cout) { return batch % 16 == 0 && cin == 32 && (cout == 32 || cout == 64); }
 
@@ -531,6 +753,55 @@ int launch_dx_flat(const float* dpre, const int* flat, int width, const float* w
                    cin, cout, width);
 }
 
+
+template <int CO, int ACT, typename TX>
+static int fwd_out_t(const TX* x, const int* idx, const float* w, const float* bias, float* y, int yvm, int vsrc,
+                     int rows, int batch, hipStream_t st) {
+  constexpr int U = CFSD_VM_OUT_U;
+  auto kern = conv_fwd_out_vm<CO, ACT, U, TX>;
+  const long its = ((long)rows * (batch / 8) + U - 1) / U;
+  const unsigned grid = balanced_blocks(its, 4, resident(kern, 256, 0));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
+  return launch_status("spiral_conv_fwd_out_vm");
+}
+
+int launch_fwd_out(const void* x, int x_bf16, const int* idx, const float* w, const float* bias, float* y, int yvm,
+                   int vsrc, int rows, int batch, int cout, int act, hipStream_t st) {
+  if (batch % 8 || cout < 1 || cout > 3)
+    return set_error(CFSD_EINVAL, "spiral_conv_fwd (vertex-major output conv): batch %% 8 == 0, 32 -> 1..3 only");
+  if ((long)vsrc * batch * 32 * 4 >= (long)kAbsent || (long)rows * batch * cout >= (1L << 31))
+    return set_error(CFSD_EINVAL, "spiral_conv_fwd (vertex-major output conv): x exceeds 32-bit buffer offsets");
+#define FO(CO_, TX)                                                                                          \
+  if (cout == CO_)                                                                                          \
+    return act == CFSD_ACT_ELU                                                                              \
+               ? fwd_out_t<CO_, CFSD_ACT_ELU, TX>((const TX*)x, idx, w, bias, y, yvm, vsrc, rows, batch, st) \
+               : fwd_out_t<CO_, CFSD_ACT_NONE, TX>((const TX*)x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
+  if (x_bf16) {
+    FO(1, bf16_t) FO(2, bf16_t) FO(3, bf16_t)
+  } else {
+    FO(1, float) FO(2, float) FO(3, float)
+  }
+#undef FO
+  return set_error(CFSD_EINVAL, "spiral_conv_fwd (vertex-major output conv): cout %d", cout);
+}
+
+int dw_slabs(int batch, int rows, int max_slabs) {
+  long n = resident(conv_dw_vm32, DWV_THREADS, 0);
+  const long units = (long)rows * (batch / 16);
+  if (n > (units + DWV_NR - 1) / DWV_NR) n = (units + DWV_NR - 1) / DWV_NR;  // >= 1 unit per range
+  if (n > max_slabs) n = max_slabs;
+  return n < 1 ? 1 : (int)n;
+}
+
+int launch_dw(const float* x, const int* idx, const float* dpre, float* ws, float* ws_db, int n_slabs, int vsrc,
+              int rows, int batch, hipStream_t st) {
+  if (batch % 16) return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight (fp32 vertex-major): batch %% 16 != 0");
+  if ((long)vsrc * batch * 128 >= (long)kAbsent || (long)rows * batch * 128 >= (long)kAbsent)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight (fp32 vertex-major): operands exceed 32-bit offsets");
+  hipLaunchKernelGGL(conv_dw_vm32, dim3(n_slabs), dim3(DWV_THREADS), 0, st, x, idx, dpre, ws, ws_db, vsrc, rows,
+                     batch);
+  return launch_status("spiral_conv_bwd_weight_vm32");
+}
 
 template <typename TX, int FW>
 static int bwd_out_t(const float* dout, const int* flat, const float* w, const TX* elu_y, const TX* x, TX* dx,

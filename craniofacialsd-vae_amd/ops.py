@@ -804,7 +804,10 @@ def spiral_conv_bwd_weight_x(x, idx, dpre, dw, db, workspace):
          ptr(workspace), ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
     if dw is None:  # bf16 32/64-channel slabs are plain (kind 2); fp32 x: the fp32 kernels' slabs
         mfma = cin in (32, 64) and cout in (32, 64) and x.dtype == torch.bfloat16
-        return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2 if mfma else 0)
+        # fp32 32 -> 32 with vertex-major x and dpre: conv_dw_vm32's slabs (3)
+        vm32 = (x.dtype == torch.float32 and is_vm(x) and is_vm(dpre) and cin == 32 and cout == 32
+                and bsz % 16 == 0)
+        return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2 if mfma else (3 if vm32 else 0))
     return None
 
 

@@ -108,7 +108,9 @@ size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int seq, int c
  * to 16 such layers (each with its own workspace) in ONE launch, with the
  * same fixed summation order (identical results).  `fused` = 1: the partials
  * came from cfsd_spiral_conv_bwd(_x) on a small-output layer (cout*seq <= 32);
- * 2: from cfsd_spiral_conv_bwd_weight_x on a 32/64-channel layer (bf16). */
+ * 2: from cfsd_spiral_conv_bwd_weight_x on a 32/64-channel layer (bf16); 3: from
+ * cfsd_spiral_conv_bwd_weight_x on a 32 -> 32 fp32 layer with vertex-major x
+ * and dpre, batch % 16 == 0 (ABI 4.3). */
 typedef struct {
   const float* workspace;
   float* dw;

@@ -13,5 +13,6 @@ for rep in 1 2; do
     CFSD_LIB_PATH=$PWD/$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/$name -o run \
       -- python3 tools/kbench.py ${KB:-step} > $OUT/$name.log 2>&1
     python3 tools/prof_summary.py $(find $OUT/$name -name '*.db' | head -1) 200 | grep -E "${PAT:-.}" | sed "s|^|$name |" || true
+    rm -rf $OUT/$name
   done
 done

@@ -156,6 +156,10 @@ def main():
                                                    P.gview("de_layers.2.conv.layer.weight"),
                                                    P.gview("de_layers.2.conv.layer.bias"), dx=b.g_dec_up[1],
                                                    workspace=b.ws_dw[("dec", 1)])
+    cases["dx_d1"] = lambda: ops.spiral_conv_bwd_data(b.dpre_dec[1], T.spiral_inv[2], w1, T.n_verts[2],
+                                                      out=b.g_dec_up[1], workspace=b.ws)
+    cases["dw_d1"] = lambda: ops.spiral_conv_bwd_weight(b.dec_up[1], T.spiral[2], b.dpre_dec[1], None, None,
+                                                       b.ws_dw[("dec", 1)])
     we1, be1 = eng._enc_w(1)
     cases["dw_e1"] = lambda: ops.spiral_conv_bwd_weight(b.enc_out[0], T.enc_rows[1], b.dpre_enc[1], None, None,
                                                        b.ws_dw[("enc", 1)])
@@ -269,6 +273,21 @@ def main():
                                               uniform=T.up_uniform[0])
     cases["spmm_up0T_vm"] = lambda: ops.spmm_x(T.upT_csr[0], v.g_dec_up[3], T.n_verts[1], elu_y=v.dec_out[2],
                                                out=v.dpre_dec[2], sched=T.upT_sched[0])
+    if "red_items" in names:  # the step's batched slab reduce, item by item (HIP events)
+        cap = []
+        orig = ops.dw_reduce_batch
+        ops.dw_reduce_batch = lambda items, adam=None: (cap.append((list(items), adam)), orig(items, adam=adam))[1]
+        ev.set_batch(b.x, key_index=3)
+        ev.train_step_on(v)
+        ops.dw_reduce_batch = orig
+        items, adam = cap[-1]
+        for i, it in enumerate(items):
+            cases[f"red_item{i}"] = (lambda it=it: orig([it]))
+            print(f"red_item{i}: sizes {it[0].sizes}", flush=True)
+        cases["red_all"] = lambda: orig(items)
+        cases["red_all_adam"] = lambda: orig(items, adam=adam)
+        names = [n for n in names if n != "red_items"] + [f"red_item{i}" for i in range(len(items))] + [
+            "red_all", "red_all_adam"]
     if "step_vm" in names:
         ev.set_batch(b.x, key_index=3)
         cases["step_vm"] = lambda: ev.train_step_on(v)

@@ -277,6 +277,9 @@ __global__ __launch_bounds__(512, CFSD_VM32_DX_OCC) void conv_dx_flat_vm32(const
 // of 4 waves per CU).  The 4 waves' accumulators are summed in LDS in fixed
 // order into one conv_dw_mfma-layout slab ([9][32][32] + db[32]) per
 // workgroup, reduced by conv_dw_reduce / dw_reduce_batch (kind 0).
+#ifndef CFSD_DWV_INTERLEAVE
+#define CFSD_DWV_INTERLEAVE 1
+#endif
 #ifndef CFSD_DWV_NS
 #define CFSD_DWV_NS 3  // slots per wave (3: a slot group of three, 9: all nine)
 #endif
@@ -303,7 +306,14 @@ __global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restr
   const long per = (n_units + G - 1) / G;
   const long g0 = grp * per, g1 = min(n_units, g0 + per);
   const int nr = nb_g * DWV_NR, ri = lb * DWV_NR + vg;
-  const long u0 = g0 + (g1 - g0) * ri / nr, u1 = g0 + (g1 - g0) * (ri + 1) / nr;
+#if CFSD_DWV_INTERLEAVE
+  // the XCD's unit ranges interleaved (unit g0 + ri + k nr): its waves sweep
+  // a narrow window of vertices together, so their neighbour blocks stay in
+  // the XCD's L2 (contiguous ranges gathered the whole eighth at once)
+  const long u0 = g0 + ri, u1 = g1, ustep = nr;
+#else
+  const long u0 = g0 + (g1 - g0) * ri / nr, u1 = g0 + (g1 - g0) * (ri + 1) / nr, ustep = 1;
+#endif
   const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, (int)((long)vsrc * batch * C * 4),
                                                     0x00020000);
   const auto rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dpre), 0, (int)((long)rows * batch * C * 4),
@@ -339,9 +349,9 @@ __global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restr
     }
   };
   if (u0 < u1) load_unit(u0, a, b);
-  for (long un = u0; un < u1; ++un) {
-    const bool more = un + 1 < u1;  // uniform
-    if (more) load_unit(un + 1, an, bn);
+  for (long un = u0; un < u1; un += ustep) {
+    const bool more = un + ustep < u1;  // uniform
+    if (more) load_unit(un + ustep, an, bn);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll

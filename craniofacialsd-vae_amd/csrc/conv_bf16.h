@@ -31,6 +31,14 @@ int launch_dw(const bf16_t* x, int xvm, const int* idx, const void* dpre, int dp
 // Vertex-major operands with batch % 16 == 0 (spiral_conv_vm16.hip): one
 // 16-row MFMA tile = one vertex x 16 meshes.
 bool vm16_ok(int batch, int cin, int cout);
+#ifndef CFSD_DW_VM16
+#define CFSD_DW_VM16 1
+#endif
+// bf16 32 -> 32 weight gradient with vertex-major x and dpre (both bf16): conv_dw_vm16,
+// n_slabs plain slabs (the conv_dw_b16 layout and count, dw_slabs())
+bool dw_vm16_ok(int batch, int cin, int cout, int xvm, int dpvm, int dpre_bf16);
+int launch_dw_vm16(const bf16_t* x, const int* idx, const bf16_t* dpre, float* ws, int n_slabs, int vsrc, int rows,
+                   int batch, hipStream_t st);
 int launch_fwd_vm16(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, void* y, int y_dt,
                     int vsrc, int rows, int batch, int cin, int cout, int act, hipStream_t st);
 int launch_dx_vm16(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_row, const int* inv_head,

@@ -452,6 +452,9 @@ static int dw_t(const bf16_t* x, const int* idx, const TD* dpre, float* ws, int 
 int launch_dw(const bf16_t* x, int xvm, const int* idx, const void* dpre, int dpre_dt, float* ws, int vsrc,
               int rows, long M, int cin, int cout, hipStream_t st) {
   const int dpvm = (dpre_dt & CFSD_VM) != 0;
+  const int batch = (int)(M / rows);
+  if (dw_vm16_ok(batch, cin, cout, xvm, dpvm, CFSD_DT_TYPE(dpre_dt) == DT_BF16))
+    return launch_dw_vm16(x, idx, (const bf16_t*)dpre, ws, dw_slabs(batch, rows, cin, cout), vsrc, rows, batch, st);
 #define W(CI, CO)                                                                                 \
   if (cin == CI && cout == CO)                                                                    \
     return CFSD_DT_TYPE(dpre_dt) == DT_BF16                                                       \

@@ -416,6 +416,131 @@ __global__ __launch_bounds__(512) void conv_dx_flat_vm16(const TD* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------ weight gradient (32 -> 32)
+// dW_s[o][c] = sum over (vertex v, mesh m) of dpre[v][m][o] x[idx[v][s]][m][c]
+// (model.py:34, 40) for vertex-major bf16 x and dpre, batch % 16 == 0.  A unit
+// (vertex v, 16-mesh group) is exactly the K = 16 of ONE
+// v_mfma_f32_32x32x16_bf16 per slot: A[o][k] = dpre[v][k][o], B[k][c] =
+// x_s[k][c].  Both operands are columns of the unit's contiguous 1-KiB
+// row-major blocks, so a wave writes its blocks to its OWN 1-KiB LDS slots
+// (one 16-B ds_write per lane each) and reads the fragments back with
+// ds_read_b64_tr_b16 (the hardware transpose): no workgroup barrier in the
+// sweep (the batch-major conv_dw_b16 stages 32-row tiles behind two barriers
+// per tile and runs 9 small MFMAs between them).  A wave owns 3 slots (slot
+// group) over an XCD-interleaved unit range; the next unit's blocks are in
+// flight in registers during this unit's MFMAs.  Workgroup = 4 ranges x 3
+// slot groups (12 waves, one per CU), summed in LDS in fixed order into one
+// plain slab [32 * 288 + 32] (the conv_dw_b16 layout, dw_reduce_batch kind 1).
+#ifndef CFSD_DW16_PD
+#define CFSD_DW16_PD 2
+#endif
+constexpr int DW16_NR = 4, DW16_WAVES = DW16_NR * 3, DW16_THREADS = DW16_WAVES * 64;
+typedef short s16x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4v lds_s16x4v;
+
+// 32x32x16 fragment of a [16 rows][32 cols] bf16 block in LDS (64-B rows):
+// lane l gets column 16(g & 1) + (l & 15) of rows 8(g >> 1) .. + 7, g = l >> 4
+__device__ __forceinline__ bf16x8 tr_frag32(const bf16_t* blk, int lane) {
+  const int li = lane & 15, g = lane >> 4, q = li >> 2, p = li & 3;
+  const bf16_t* a = blk + (8 * (g >> 1) + q) * 32 + 16 * (g & 1) + 4 * p;
+  const s16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4v*)a);
+  const s16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4v*)(a + 4 * 32));
+  const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+  return __builtin_bit_cast(bf16x8, (u32x4){l2.x, l2.y, h2.x, h2.y});
+}
+
+__global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __restrict__ x,
+                                                             const int* __restrict__ idx,
+                                                             const bf16_t* __restrict__ dpre,
+                                                             float* __restrict__ ws, int vsrc, int rows, int batch) {
+  constexpr int C = 32, K = kS * C, NEL = C * K + C, NS = 3;
+  constexpr int SLOT = 16 * C;  // bf16 elements of one 1-KiB block
+  __shared__ __attribute__((aligned(16))) bf16_t lds[DW16_WAVES * (1 + NS) * SLOT];  // 48 KiB, reused by red
+  const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
+  const int sg = wave % 3, vg = wave / 3;
+  bf16_t* my = lds + wave * (1 + NS) * SLOT;  // [dpre][x_0][x_1][x_2]
+  const int G16 = batch >> 4;
+  const long n_units = (long)rows * G16;
+  const int nb = gridDim.x, G = nb < 8 ? nb : 8;
+  const int grp = blockIdx.x % G, lb = blockIdx.x / G, nb_g = (nb - grp + G - 1) / G;
+  const long per = (n_units + G - 1) / G;
+  const long g0 = grp * per, g1 = min(n_units, g0 + per);
+  const int nr = nb_g * DW16_NR;
+  const long u0 = g0 + lb * DW16_NR + vg, u1 = g1, ustep = nr;  // XCD-interleaved unit range
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x), 0, (int)((long)vsrc * batch * C * 2),
+                                                    0x00020000);
+  const auto rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(dpre), 0, (int)((long)rows * batch * C * 2),
+                                                    0x00020000);
+  const int voff = lane * 16;
+  f32x16 acc[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) acc[k] = (f32x16){0.f};
+  float dbs = 0.f;
+  // DW16_PD units' blocks in flight (a unit is only 3 MFMAs: one unit ahead
+  // left every unit waiting out a memory latency)
+  constexpr int PD = CFSD_DW16_PD;
+  u32x4 ring[PD][1 + NS];
+  auto load_unit = [&](long un, u32x4 (&b)[1 + NS]) {
+    const int uu = uni((int)un);
+    const int v = uu / G16, mg = uu - v * G16;
+    b[0] = bload16(rd, voff, (v * batch + mg * 16) * C * 2);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) b[1 + k] = bload16(rx, voff, (uni(idx[v * kS + NS * sg + k]) * batch + mg * 16) * C * 2);
+  };
+#pragma unroll
+  for (int d = 0; d < PD - 1; ++d)
+    if (u0 + d * ustep < u1) load_unit(u0 + d * ustep, ring[d]);
+  for (long base = u0; base < u1; base += PD * ustep) {
+#pragma unroll
+    for (int d = 0; d < PD; ++d) {
+      const long un = base + d * ustep;
+      if (un >= u1) break;  // uniform
+      const long ahead = un + (PD - 1) * ustep;
+      if (ahead < u1) load_unit(ahead, ring[(d + PD - 1) % PD]);
+#pragma unroll
+      for (int k = 0; k < 1 + NS; ++k) *reinterpret_cast<u32x4*>(my + k * SLOT + 8 * lane) = ring[d][k];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const bf16x8 af = tr_frag32(my, lane);
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, tr_frag32(my + (1 + k) * SLOT, lane), acc[k], 0, 0, 0);
+      if (sg == 0) {
+        const u32x4 av = __builtin_bit_cast(u32x4, af);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dbs += bf2f(av[e] & 0xffffu) + bf2f(av[e] >> 16);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragments read before the slots are rewritten
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  // ranges summed in fixed order in LDS (reused) -> one plain slab per workgroup
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(lds);
+  __shared__ float dbl[DW16_NR * 64];
+  for (int g = 0; g < DW16_NR; ++g) {
+    if (vg == g) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int e = acc_row(rr, lane) * K + (NS * sg + k) * C + (lane & 31);
+          red[e] = g == 0 ? acc[k][rr] : red[e] + acc[k][rr];
+        }
+      if (sg == 0) dbl[g * 64 + lane] = dbs;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < C) {  // lane o + 32 h of a range summed meshes 8h .. 8h + 7 of column o
+    float t = 0.f;
+    for (int g = 0; g < DW16_NR; ++g) t += dbl[g * 64 + threadIdx.x] + dbl[g * 64 + 32 + threadIdx.x];
+    red[C * K + threadIdx.x] = t;
+  }
+  __syncthreads();
+  float* slab = ws + (long)blockIdx.x * NEL;
+  for (int e = threadIdx.x; e < NEL; e += DW16_THREADS) slab[e] = red[e];
+}
+
 // ------------------------------------------------------------------ launchers
 template <typename Kern>
 static int resident(Kern k, size_t lds) {
@@ -432,6 +557,18 @@ static int fwd16_t(const bf16_t* x, const int* idx, const bf16_t* w, const float
   const unsigned grid = balanced_blocks(tiles, 8, resident(kern, lds));  // >= 2 tiles per wave
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
   return launch_status("spiral_conv_fwd_vm16");
+}
+
+bool dw_vm16_ok(int batch, int cin, int cout, int xvm, int dpvm, int dpre_bf16) {
+  return CFSD_DW_VM16 && batch % 16 == 0 && cin == 32 && cout == 32 && xvm && dpvm && dpre_bf16;
+}
+
+int launch_dw_vm16(const bf16_t* x, const int* idx, const bf16_t* dpre, float* ws, int n_slabs, int vsrc, int rows,
+                   int batch, hipStream_t st) {
+  if ((long)vsrc * batch * 64 >= (long)kAbsent || (long)rows * batch * 64 >= (long)kAbsent)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_vm16: operands exceed 32-bit offsets");
+  hipLaunchKernelGGL(conv_dw_vm16, dim3(n_slabs), dim3(DW16_THREADS), 0, st, x, idx, dpre, ws, vsrc, rows, batch);
+  return launch_status("spiral_conv_bwd_weight_vm16");
 }
 
 bool vm16_ok(int batch, int cin, int cout) {

@@ -34,11 +34,15 @@ bool vm16_ok(int batch, int cin, int cout);
 #ifndef CFSD_DW_VM16
 #define CFSD_DW_VM16 1
 #endif
-// bf16 32 -> 32 weight gradient with vertex-major x and dpre (both bf16): conv_dw_vm16,
+#ifndef CFSD_DW_VM16_F32DP
+#define CFSD_DW_VM16_F32DP 1
+#endif
+// bf16 32 -> 32 weight gradient with vertex-major bf16 x and a vertex-major
+// bf16 (or batch-major fp32: an Enblock's kept rows) dpre: conv_dw_vm16,
 // n_slabs plain slabs (the conv_dw_b16 layout and count, dw_slabs())
 bool dw_vm16_ok(int batch, int cin, int cout, int xvm, int dpvm, int dpre_bf16);
-int launch_dw_vm16(const bf16_t* x, const int* idx, const bf16_t* dpre, float* ws, int n_slabs, int vsrc, int rows,
-                   int batch, hipStream_t st);
+int launch_dw_vm16(const bf16_t* x, const int* idx, const void* dpre, int dpre_bf16, float* ws, int n_slabs, int vsrc,
+                   int rows, int batch, hipStream_t st);
 int launch_fwd_vm16(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, void* y, int y_dt,
                     int vsrc, int rows, int batch, int cin, int cout, int act, hipStream_t st);
 int launch_dx_vm16(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_row, const int* inv_head,

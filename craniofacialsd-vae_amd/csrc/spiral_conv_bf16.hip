@@ -454,7 +454,8 @@ int launch_dw(const bf16_t* x, int xvm, const int* idx, const void* dpre, int dp
   const int dpvm = (dpre_dt & CFSD_VM) != 0;
   const int batch = (int)(M / rows);
   if (dw_vm16_ok(batch, cin, cout, xvm, dpvm, CFSD_DT_TYPE(dpre_dt) == DT_BF16))
-    return launch_dw_vm16(x, idx, (const bf16_t*)dpre, ws, dw_slabs(batch, rows, cin, cout), vsrc, rows, batch, st);
+    return launch_dw_vm16(x, idx, dpre, CFSD_DT_TYPE(dpre_dt) == DT_BF16, ws, dw_slabs(batch, rows, cin, cout), vsrc,
+                          rows, batch, st);
 #define W(CI, CO)                                                                                 \
   if (cin == CI && cout == CO)                                                                    \
     return CFSD_DT_TYPE(dpre_dt) == DT_BF16                                                       \

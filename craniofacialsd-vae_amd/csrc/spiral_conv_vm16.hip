@@ -449,9 +449,12 @@ __device__ __forceinline__ bf16x8 tr_frag32(const bf16_t* blk, int lane) {
   return __builtin_bit_cast(bf16x8, (u32x4){l2.x, l2.y, h2.x, h2.y});
 }
 
+// TD = float: an Enblock's dpre, fp32 batch-major at the kept rows (rounded to
+// bf16 when staged, as conv_dw_b16 rounds it).
+template <typename TD>
 __global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __restrict__ x,
                                                              const int* __restrict__ idx,
-                                                             const bf16_t* __restrict__ dpre,
+                                                             const TD* __restrict__ dpre,
                                                              float* __restrict__ ws, int vsrc, int rows, int batch) {
   constexpr int C = 32, K = kS * C, NEL = C * K + C, NS = 3;
   constexpr int SLOT = 16 * C;  // bf16 elements of one 1-KiB block
@@ -469,8 +472,8 @@ __global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __res
   const long u0 = g0 + lb * DW16_NR + vg, u1 = g1, ustep = nr;  // XCD-interleaved unit range
   const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x), 0, (int)((long)vsrc * batch * C * 2),
                                                     0x00020000);
-  const auto rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(dpre), 0, (int)((long)rows * batch * C * 2),
-                                                    0x00020000);
+  const auto rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<TD*>(dpre), 0,
+                                                    (int)((long)rows * batch * C * sizeof(TD)), 0x00020000);
   const int voff = lane * 16;
   f32x16 acc[NS];
 #pragma unroll
@@ -483,7 +486,14 @@ __global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __res
   auto load_unit = [&](long un, u32x4 (&b)[1 + NS]) {
     const int uu = uni((int)un);
     const int v = uu / G16, mg = uu - v * G16;
-    b[0] = bload16(rd, voff, (v * batch + mg * 16) * C * 2);
+    if constexpr (sizeof(TD) == 2) {
+      b[0] = bload16(rd, voff, (v * batch + mg * 16) * C * 2);
+    } else {  // fp32 batch-major: lane (mesh l / 4, channels 8 (l % 4) .. + 7) of row v
+      const int vo = ((mg * 16 + (lane >> 2)) * rows) * C * 4 + 32 * (lane & 3);
+      const f32x4 lo = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, vo, v * C * 4, 0));
+      const f32x4 hi = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, vo + 16, v * C * 4, 0));
+      b[0] = (u32x4){pack_bf2(lo.x, lo.y), pack_bf2(lo.z, lo.w), pack_bf2(hi.x, hi.y), pack_bf2(hi.z, hi.w)};
+    }
 #pragma unroll
     for (int k = 0; k < NS; ++k) b[1 + k] = bload16(rx, voff, (uni(idx[v * kS + NS * sg + k]) * batch + mg * 16) * C * 2);
   };
@@ -560,14 +570,20 @@ static int fwd16_t(const bf16_t* x, const int* idx, const bf16_t* w, const float
 }
 
 bool dw_vm16_ok(int batch, int cin, int cout, int xvm, int dpvm, int dpre_bf16) {
-  return CFSD_DW_VM16 && batch % 16 == 0 && cin == 32 && cout == 32 && xvm && dpvm && dpre_bf16;
+  return CFSD_DW_VM16 && batch % 16 == 0 && cin == 32 && cout == 32 && xvm &&
+         ((dpre_bf16 && dpvm) || (CFSD_DW_VM16_F32DP && !dpre_bf16 && !dpvm));
 }
 
-int launch_dw_vm16(const bf16_t* x, const int* idx, const bf16_t* dpre, float* ws, int n_slabs, int vsrc, int rows,
-                   int batch, hipStream_t st) {
-  if ((long)vsrc * batch * 64 >= (long)kAbsent || (long)rows * batch * 64 >= (long)kAbsent)
+int launch_dw_vm16(const bf16_t* x, const int* idx, const void* dpre, int dpre_bf16, float* ws, int n_slabs, int vsrc,
+                   int rows, int batch, hipStream_t st) {
+  if ((long)vsrc * batch * 64 >= (long)kAbsent || (long)rows * batch * 128 >= (long)kAbsent)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_vm16: operands exceed 32-bit offsets");
-  hipLaunchKernelGGL(conv_dw_vm16, dim3(n_slabs), dim3(DW16_THREADS), 0, st, x, idx, dpre, ws, vsrc, rows, batch);
+  if (dpre_bf16)
+    hipLaunchKernelGGL(conv_dw_vm16<bf16_t>, dim3(n_slabs), dim3(DW16_THREADS), 0, st, x, idx, (const bf16_t*)dpre, ws,
+                       vsrc, rows, batch);
+  else
+    hipLaunchKernelGGL(conv_dw_vm16<float>, dim3(n_slabs), dim3(DW16_THREADS), 0, st, x, idx, (const float*)dpre, ws,
+                       vsrc, rows, batch);
   return launch_status("spiral_conv_bwd_weight_vm16");
 }
 

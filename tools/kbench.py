@@ -221,6 +221,10 @@ def main():
                                                                 out=c.g_dec_up[3])
     cases["dw_d3_b16"] = lambda: ops.spiral_conv_bwd_weight_x(c.dec_up[3], T.spiral[0], c.dpre_dec[3], None, None,
                                                               c.ws_dw[("dec", 3)])
+    cases["dw_e1_b16"] = lambda: ops.spiral_conv_bwd_weight_x(c.enc_out[0], T.enc_rows[1], c.dpre_enc[1], None, None,
+                                                              c.ws_dw[("enc", 1)])
+    cases["dw_d2_b16"] = lambda: ops.spiral_conv_bwd_weight_x(c.dec_up[2], T.spiral[1], c.dpre_dec[2], None, None,
+                                                              c.ws_dw[("dec", 2)])
     bm_up, bm_out = c.dec_up[3].contiguous(), c.dec_out[3].contiguous()
     bm_dp, bm_g = c.dpre_dec[3].contiguous(), c.g_dec_up[3].contiguous()
     cases["fwd_d3_b16_bm"] = lambda: ops.spiral_conv_fwd_x(bm_up, T.spiral[0], w3h, w16, b3h, 1, bm_out)

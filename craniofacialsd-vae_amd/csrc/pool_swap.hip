@@ -159,6 +159,61 @@ __global__ __launch_bounds__(256) void spmm_uniform_k(const int* __restrict__ co
   }
 }
 
+// spmm_uniform_k for VERTEX-MAJOR x and y (the up-samplings of the
+// vertex-major levels): output row r is one contiguous block of batch x c
+// elements and a wave lies inside one row (batch * c / 4 % 64 == 0), so the
+// row's K columns / values are wave-uniform scalar loads and each tap is one
+// buffer load per lane with the source block's offset in an SGPR (the
+// batch-major kernel loads every column / value per lane).  A wave runs RW
+// rows (XCD-contiguous), all their tap loads issued before the first add;
+// the adds are spmm_uniform_k's (bit-identical).
+template <int K, int RW, typename TX, typename TY>
+__global__ __launch_bounds__(256) void spmm_uniform_vm_k(const int* __restrict__ col, const float* __restrict__ val,
+                                                         const TX* __restrict__ x, TY* __restrict__ y, int m, int n,
+                                                         int rowq) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int wpr = rowq / 64;  // waves per row
+  const long wg = (long)xcd_block() * 4 + (threadIdx.x >> 6);
+  const long row0 = (wg / wpr) * RW;
+  const int part = (int)(wg % wpr);
+  if (row0 >= m) return;
+  const int q = part * 64 + lane;  // 4-element chunk of the row block
+  const int eb = (int)sizeof(TX);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<TX*>(x), 0, (int)((long)n * rowq * 4 * eb), 0x00020000);
+  f32x4 xv[RW][K];
+  float vv[RW][K];
+#pragma unroll
+  for (int w = 0; w < RW; ++w) {
+    const int r = __builtin_amdgcn_readfirstlane((int)min(row0 + w, (long)m - 1));
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = col[r * K + k];
+      vv[w][k] = val[r * K + k];
+      if constexpr (sizeof(TX) == 4) {
+        xv[w][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, q * 16, c * rowq * 16, 0));
+      } else {
+        const u32x2 h = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, q * 8, c * rowq * 8, 0));
+        xv[w][k] = (f32x4){__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xffff0000u),
+                           __uint_as_float(h.y << 16), __uint_as_float(h.y & 0xffff0000u)};
+      }
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < RW; ++w) {
+    if (row0 + w >= m) break;  // uniform
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      acc.x = acc.x + xv[w][k].x * vv[w][k];
+      acc.y = acc.y + xv[w][k].y * vv[w][k];
+      acc.z = acc.z + xv[w][k].z * vv[w][k];
+      acc.w = acc.w + xv[w][k].w * vv[w][k];
+    }
+    st4f(y + ((row0 + w) * rowq + q) * 4, acc);
+  }
+}
+
 // The same SpMM for matrices with long, skewed rows (the transposes of the
 // up-sampling matrices: level 0 has 12 entries per row on average but up to
 // 96).  A row is a sequential fp32 fold in entry order (kept for
@@ -511,6 +566,12 @@ extern "C" int cfsd_spmm_csr_x(const int32_t* row_ptr, const int32_t* col, const
   return spmm_launch(row_ptr, col, val, nullptr, x, x_dt, elu_y, y, y_dt, batch, m, n, c, stream);
 }
 
+#ifndef CFSD_SPMM_UVM
+#define CFSD_SPMM_UVM 1
+#endif
+#ifndef CFSD_SPMM_UVM_RW
+#define CFSD_SPMM_UVM_RW 4
+#endif
 #ifndef CFSD_SPMM_URPT
 #define CFSD_SPMM_URPT 4
 #endif
@@ -526,6 +587,23 @@ extern "C" int cfsd_spmm_uniform(int k, const int32_t* col, const float* val, co
   const long total = (long)batch * m * (c / 4);
   if (total >= (1L << 31) || (long)batch * n >= (1L << 31) || (long)m * k >= (1L << 31))
     return set_error(CFSD_EINVAL, "spmm_uniform: sizes >= 2^31 (32-bit indices)");
+  if (CFSD_SPMM_UVM && xvm && yvm && !elu_y && k == 3 && (batch * (c / 4)) % 64 == 0 &&
+      (long)n * batch * c * 4 < 0x7ffff000L) {  // vertex-major: wave-uniform rows
+    constexpr int RW = CFSD_SPMM_UVM_RW;
+    const int rowq = batch * (c / 4), wpr = rowq / 64;
+    const long waves = (long)((m + RW - 1) / RW) * wpr;
+    const unsigned nb = (unsigned)((waves + 3) / 4);
+    const hipStream_t st = (hipStream_t)stream;
+#define SPUV(TX, TY)                                                                                \
+  hipLaunchKernelGGL((spmm_uniform_vm_k<3, RW, TX, TY>), dim3(nb), dim3(256), 0, st, col, val, (const TX*)x, \
+                     (TY*)y, m, n, rowq)
+    if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPUV(float, float);
+    else if (x_dt == CFSD_DT_F32) SPUV(float, bf16_t);
+    else if (y_dt == CFSD_DT_F32) SPUV(bf16_t, float);
+    else SPUV(bf16_t, bf16_t);
+#undef SPUV
+    return launch_status("spmm_uniform_vm");
+  }
   constexpr int RPT = CFSD_SPMM_URPT;
   const long per_grp = (total + 7) / 8;
   const unsigned nblk = (unsigned)(8 * ((per_grp + 256 * RPT - 1) / (256 * RPT)));

@@ -415,6 +415,9 @@ __global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restr
 // per SIMD with every memory latency exposed per tile; here a unit's
 // memory traffic is one flat list, 9 contiguous dout blocks and the 2-KiB x /
 // dx blocks.
+#ifndef CFSD_BO_SWITCH
+#define CFSD_BO_SWITCH 1
+#endif
 template <typename TX, int FW>
 __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__ dout,
                                                        const int4* __restrict__ flat,
@@ -508,8 +511,22 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
     for (int e = 0; e < FW; ++e) {
       if (pe[e] < 0) break;  // uniform: padding from here on
       const int se = pe[e] % kS;
+#if CFSD_BO_SWITCH
+      switch (se) {  // uniform: one add per entry instead of 9 selects + 9 adds (t is never -0: same bits)
+        case 0: t[0] += v[e]; break;
+        case 1: t[1] += v[e]; break;
+        case 2: t[2] += v[e]; break;
+        case 3: t[3] += v[e]; break;
+        case 4: t[4] += v[e]; break;
+        case 5: t[5] += v[e]; break;
+        case 6: t[6] += v[e]; break;
+        case 7: t[7] += v[e]; break;
+        default: t[8] += v[e]; break;
+      }
+#else
 #pragma unroll
       for (int s = 0; s < kS; ++s) t[s] += se == s ? v[e] : 0.f;  // x + 0 == x: list order kept
+#endif
     }
     dbs += t[0];
     if (lane < 48) {

@@ -221,6 +221,10 @@ def main():
                                                                 out=c.g_dec_up[3])
     cases["dw_d3_b16"] = lambda: ops.spiral_conv_bwd_weight_x(c.dec_up[3], T.spiral[0], c.dpre_dec[3], None, None,
                                                               c.ws_dw[("dec", 3)])
+    cases["spmm_up0_b16"] = lambda: ops.spmm_x(T.up_csr[0], c.dec_out[2], T.n_verts[0], out=c.dec_up[3],
+                                               uniform=T.up_uniform[0])
+    cases["spmm_up1_b16"] = lambda: ops.spmm_x(T.up_csr[1], c.dec_out[1], T.n_verts[1], out=c.dec_up[2],
+                                               uniform=T.up_uniform[1])
     cases["dw_e1_b16"] = lambda: ops.spiral_conv_bwd_weight_x(c.enc_out[0], T.enc_rows[1], c.dpre_enc[1], None, None,
                                                               c.ws_dw[("enc", 1)])
     cases["dw_d2_b16"] = lambda: ops.spiral_conv_bwd_weight_x(c.dec_up[2], T.spiral[1], c.dpre_dec[2], None, None,

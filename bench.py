@@ -358,6 +358,8 @@ def pmc_traffic(key="conv_fwd_d3"):
     for f in glob.glob(os.path.join(PROFILES, f"*_pmc_traffic_{key}.json")):
         with open(f) as fh:
             d = json.load(fh)
+        if not d.get("hbm_bytes_per_launch"):  # a pass that matched no launch
+            continue
         rank = (d.get("created", 0), os.path.getmtime(f))
         if best is None or rank > best[0]:
             best = (rank, d, f)
@@ -588,7 +590,7 @@ def main():
             kern_names = {"conv_fwd_D3": "conv_fwd_vm16<32,32> (decoder level 0 forward, bf16, vertex-major)",
                           "conv_dx_D3": "conv_dx_flat_vm16<32,32> (decoder level 0 data gradient, bf16, "
                                         "vertex-major flat list)",
-                          "conv_dw_D3": "conv_dw_b16<32,32> (decoder level 0 weight gradient, bf16, vertex-major)"}
+                          "conv_dw_D3": "conv_dw_vm16 (decoder level 0 weight gradient, bf16, vertex-major)"}
         elif vm0:
             kern_names = {"conv_fwd_D3": "conv_fwd_vm32<32,32> (decoder level 0 forward, vertex-major)",
                           "conv_dx_D3": "conv_dx_flat_vm32<32,32> (decoder level 0 data gradient, vertex-major "

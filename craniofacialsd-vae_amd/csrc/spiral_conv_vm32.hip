@@ -328,15 +328,6 @@ __global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restr
     const int uu = uni((int)un);
     const int v = uu / G16, mg = uu - v * G16;
     const int sd = (v * batch + mg * 16) * C * 4;
-#ifdef CFSD_DWV_NOLOAD
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      da[j] = (float)(sd + j + lane);
-#pragma unroll
-      for (int k = 0; k < NS; ++k) db[k][j] = (float)(uu + j + k);
-    }
-    return;
-#endif
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       da[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, voff + 256 * j, sd, 0));

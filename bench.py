@@ -125,7 +125,8 @@ class Runner:
         if meshes is None:
             gen = torch.Generator(device=device).manual_seed(1234 + rank)
             meshes = torch.randn(n_meshes, nv, 3, device=device, generator=gen)
-        self.data = E.ResidentData(meshes, bs=4, shuffle=True, norm=norm)
+        # the bench owns the set: normalised in place (one resident copy)
+        self.data = E.ResidentData(meshes, bs=4, shuffle=True, norm=norm, inplace=True)
         self.avg = cdist.GradientAverager(world)
         if world > 1:
             cdist.broadcast_parameters(self.eng.params.data, 0)
@@ -375,6 +376,47 @@ def pmc_traffic(key="conv_fwd_d3"):
     return best[1].get("hbm_bytes_per_launch"), os.path.relpath(best[2], ROOT)
 
 
+def _bits_checksum(t):
+    """Order-sensitive checksum of a float buffer's bit patterns (int64,
+    wrapping): equal on two ranks iff (up to a 2^-64 collision) the buffers
+    are bit-identical."""
+    bits = t.detach().contiguous().view(torch.int32).to(torch.int64)
+    w = torch.arange(bits.numel(), device=t.device, dtype=torch.int64) % 65521 + 1
+    return int((bits * w).sum().item())
+
+
+def dist_check(runner, el, steps, backend, shared_device):
+    """Self-verification of an N > 1 line (every rank calls it): the world
+    size and backend the process group really has, each rank's GPU (PCI
+    domain:bus:device, all-gathered; distinct unless the one-GPU rehearsal
+    CFSD_SHARE_DEVICE shares it on purpose), each rank's own ms per step, and
+    bit checksums of the parameters, the gradient and both Adam moments after
+    the timed steps, which data-parallel training keeps identical on every
+    rank (model_manager.py:360-393: each rank's swap groups are independent,
+    the averaged gradient and Adam are the same everywhere)."""
+    P = runner.eng.params
+    dev = P.data.device
+    props = torch.cuda.get_device_properties(dev)
+    mine = {"rank": dist.get_rank(), "device": str(dev),
+            "pci": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
+            "ms_per_step": el / steps * 1e3, "adam_t": int(P.step.item()),
+            "params": _bits_checksum(P.data), "grad": _bits_checksum(P.grad),
+            "exp_avg": _bits_checksum(P.exp_avg), "exp_avg_sq": _bits_checksum(P.exp_avg_sq)}
+    if P.shadow is not None:
+        mine["shadow"] = _bits_checksum(P.shadow.view(torch.int16).to(torch.int32).float())
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, mine)
+    keys = [k for k in ("params", "grad", "exp_avg", "exp_avg_sq", "shadow", "adam_t") if k in mine]
+    pcis = [r["pci"] for r in allr]
+    ms = [r["ms_per_step"] for r in allr]
+    return {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+            "shared_device_rehearsal": bool(shared_device),
+            "pci_bus_ids": pcis, "distinct_devices": len(set(pcis)) == len(pcis),
+            "ms_per_step_min": min(ms), "ms_per_step_max": max(ms),
+            "ranks_in_sync": all(r[k] == allr[0][k] for r in allr for k in keys),
+            "checksums_rank0": {k: allr[0][k] for k in keys}}
+
+
 def c1_parity(device):
     """The metric's second half: per-vertex L1 of C1 (encode + decode of the
     first 8 demo meshes, eval mode, golden weights) through the HIP path
@@ -541,8 +583,10 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
-    el = cdist.max_over_ranks(el, device)
+    el_rank = time.perf_counter() - t0
+    el = cdist.max_over_ranks(el_rank, device)
+    dcheck = dist_check(runner, el_rank, args.steps, backend, os.environ.get("CFSD_SHARE_DEVICE")) \
+        if world > 1 else None
     meshes = 16 * world * args.steps
     ms_per_step = el / args.steps * 1e3
     losses = runner.eng.loss_acc.cpu().numpy()
@@ -565,12 +609,9 @@ def main():
             except (ImportError, AttributeError) as e:  # precompute not available
                 s5k = {"error": str(e)}
         # the three D3 (decoder level 0, 32 -> 32) conv kernels, 5.02 GFLOP
-        # each; `roofline` is the dominant one (longest launch)
-        # the three D3 (decoder level 0, 32 -> 32) conv kernels, 5.02 GFLOP
         # each; `roofline` is the dominant one (longest launch).  fp32: MFMA
         # bound (AI 72 flop/B > ridge 19.7); bf16: HBM bound (AI ~140 flop/B
         # < ridge 312), priced on algorithmic bytes (input + output once).
-        bf = runner.precision == "bf16"
         s_act = 2 if bf else 4
         d3_bytes = {"conv_fwd_D3": s_act * 16 * nv * 64 + nv * 36,
                     "conv_dx_D3": s_act * 16 * nv * 64 + nv * 9 * 16,
@@ -634,6 +675,7 @@ def main():
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": gather_bytes / t_g / 1e9 / HBM_PEAK_GBS,
                                 "us_per_launch": t_g * 1e6},
+            "dist_check": dcheck,
             "synthetic_5k": s5k,
             "parity": parity,
             "cpu_baseline": cpu,

@@ -370,6 +370,29 @@ __global__ __launch_bounds__(256) void swap_k(const float* __restrict__ x,
   }
 }
 
+// The un-swapped batch (data config swap_features: False, data_loading.py:38
+// with no feature_swapper): out mesh b = x[batch_idx[b]], one thread per
+// (out mesh, vertex) row of out's storage; mesh indices clamped like swap_k.
+__global__ __launch_bounds__(256) void gather_meshes_k(const float* __restrict__ x,
+                                                       const int* __restrict__ batch_idx,
+                                                       float* __restrict__ out, int bs, int nv, int c,
+                                                       int n_meshes, long total, int yvm) {
+  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  int ob, v;
+  split_row(t, yvm, bs, nv, ob, v);
+  const long src_mesh = min(max(batch_idx[ob], 0), n_meshes - 1);
+  const float* src = x + (src_mesh * nv + v) * c;
+  float* dst = out + t * c;
+  if (c == 3) {
+    float v3[3];
+    ld_row<3>(src, v3);
+    st_row<3>(dst, v3);
+  } else {
+    for (int q = 0; q < c; ++q) dst[q] = src[q];
+  }
+}
+
 // Storage conversion fp32 <-> bf16 (round to nearest even), 4 elements per
 // thread (n % 4 tail by the last thread).
 template <typename TS, typename TD>
@@ -700,6 +723,18 @@ extern "C" int cfsd_swap_features_x(const float* x, const int32_t* batch_idx, co
                      (hipStream_t)stream, x, batch_idx, region_mask, key, out, bs, nv, c, n_meshes,
                      n_regions, total, (out_dt & CFSD_VM) != 0);
   return launch_status("swap_features_x");
+}
+
+extern "C" int cfsd_gather_meshes(const float* x, const int32_t* batch_idx, float* out, int out_dt, int bs,
+                                  int nv, int c, int n_meshes, void* stream) {
+  if (!x || !batch_idx || !out) return set_error(CFSD_EINVAL, "gather_meshes: null pointer");
+  if (bs <= 0 || nv <= 0 || c <= 0 || n_meshes <= 0) return set_error(CFSD_EINVAL, "gather_meshes: bad sizes");
+  if ((out_dt & ~CFSD_VM) != CFSD_DT_F32) return set_error(CFSD_EINVAL, "gather_meshes: bad dtype %d", out_dt);
+  const long total = (long)bs * nv;
+  if (total >= (1L << 31)) return set_error(CFSD_EINVAL, "gather_meshes: bs x nv >= 2^31");
+  hipLaunchKernelGGL(gather_meshes_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     batch_idx, out, bs, nv, c, n_meshes, total, (out_dt & CFSD_VM) != 0);
+  return launch_status("gather_meshes");
 }
 
 extern "C" int cfsd_spectral_blend(const float* s1, const float* s2, const float* values, float* s4,

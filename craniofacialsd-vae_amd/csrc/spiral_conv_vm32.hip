@@ -277,9 +277,6 @@ __global__ __launch_bounds__(512, CFSD_VM32_DX_OCC) void conv_dx_flat_vm32(const
 // of 4 waves per CU).  The 4 waves' accumulators are summed in LDS in fixed
 // order into one conv_dw_mfma-layout slab ([9][32][32] + db[32]) per
 // workgroup, reduced by conv_dw_reduce / dw_reduce_batch (kind 0).
-#ifndef CFSD_DWV_INTERLEAVE
-#define CFSD_DWV_INTERLEAVE 1
-#endif
 #ifndef CFSD_DWV_NS
 #define CFSD_DWV_NS 3  // slots per wave (3: a slot group of three, 9: all nine)
 #endif
@@ -306,14 +303,11 @@ __global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restr
   const long per = (n_units + G - 1) / G;
   const long g0 = grp * per, g1 = min(n_units, g0 + per);
   const int nr = nb_g * DWV_NR, ri = lb * DWV_NR + vg;
-#if CFSD_DWV_INTERLEAVE
   // the XCD's unit ranges interleaved (unit g0 + ri + k nr): its waves sweep
   // a narrow window of vertices together, so their neighbour blocks stay in
-  // the XCD's L2 (contiguous ranges gathered the whole eighth at once)
+  // the XCD's L2 (contiguous ranges gathered the whole eighth at once: HBM
+  // traffic 147 vs 93 MB per D3 launch at equal time)
   const long u0 = g0 + ri, u1 = g1, ustep = nr;
-#else
-  const long u0 = g0 + (g1 - g0) * ri / nr, u1 = g0 + (g1 - g0) * (ri + 1) / nr, ustep = 1;
-#endif
   const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, (int)((long)vsrc * batch * C * 4),
                                                     0x00020000);
   const auto rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dpre), 0, (int)((long)rows * batch * C * 4),
@@ -406,9 +400,6 @@ __global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restr
 // per SIMD with every memory latency exposed per tile; here a unit's
 // memory traffic is one flat list, 9 contiguous dout blocks and the 2-KiB x /
 // dx blocks.
-#ifndef CFSD_BO_SWITCH
-#define CFSD_BO_SWITCH 1
-#endif
 template <typename TX, int FW>
 __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__ dout,
                                                        const int4* __restrict__ flat,
@@ -502,7 +493,6 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
     for (int e = 0; e < FW; ++e) {
       if (pe[e] < 0) break;  // uniform: padding from here on
       const int se = pe[e] % kS;
-#if CFSD_BO_SWITCH
       switch (se) {  // uniform: one add per entry instead of 9 selects + 9 adds (t is never -0: same bits)
         case 0: t[0] += v[e]; break;
         case 1: t[1] += v[e]; break;
@@ -514,10 +504,6 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
         case 7: t[7] += v[e]; break;
         default: t[8] += v[e]; break;
       }
-#else
-#pragma unroll
-      for (int s = 0; s < kS; ++s) t[s] += se == s ? v[e] : 0.f;  // x + 0 == x: list order kept
-#endif
     }
     dbs += t[0];
     if (lane < 48) {

@@ -384,15 +384,17 @@ def load_mesh_dataset(data_config, batch_size, device="cuda", template=None, sha
             sets[kind] = None
             continue
         meshes = torch.stack([load_mesh(os.path.join(root, n)) for n in names]).to(device)
-        rows = None
+        rows, n_batches = None, None
         # (a shard smaller than one batch: every rank iterates the whole set;
         # the decision depends on the sizes only, so all ranks agree)
         if shard is not None and kind != "test" and shard[1] > 1 and len(names) // shard[1] >= batch_size:
-            from .dist import shard_range
+            from .dist import shard_range, steps_per_epoch
             lo, hi = shard_range(len(names), shard[0], shard[1])
             rows = torch.arange(lo, hi, dtype=torch.int32)
+            # shards differ by <= 1 mesh: every rank runs the smallest shard's count
+            n_batches = steps_per_epoch(len(names), shard[1], batch_size)
         rd = ResidentData(meshes, bs=batch_size, rows=rows, shuffle=shuffle,
-                          norm=norm if data_config.get("normalize_data", True) else None)
+                          norm=norm if data_config.get("normalize_data", True) else None, n_batches=n_batches)
         rd.names = list(names)
         rd.labels = [labels_of(n) for n in names]
         ag = [get_age_and_gender_from_summary(summary, n[:-4]) for n in names]

@@ -100,6 +100,16 @@ def shard_range(n_items, rank, world):
     return lo, lo + per + (1 if rank < rem else 0)
 
 
+def steps_per_epoch(n_items, world, bs):
+    """Train steps per epoch that EVERY rank runs over its :func:`shard_range`
+    shard: the smallest shard's ``len // bs`` (= (n_items // world) // bs).
+    Each step issues the gradient all-reduces, so ranks running different
+    counts would pair one rank's step collective with the other's end-of-epoch
+    loss all-reduce (RCCL hangs, gloo errors).  Depends on the sizes only, so
+    all ranks agree without communicating."""
+    return (n_items // world) // bs
+
+
 def max_over_ranks(value, device=None):
     """Max of a Python float over ranks (timing: the slowest rank defines the step)."""
     if not (dist.is_initialized() and dist.get_world_size() > 1):

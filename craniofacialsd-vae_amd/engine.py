@@ -134,7 +134,7 @@ class SDVAEEngine:
 
     def __init__(self, topo, spec=None, lr=1e-4, weight_decay=0.0, w_kl=1e-4, w_lc=0.5,
                  w_lap=0.1, eta1=0.5, eta2=0.5, swap_bs=4, seed=0, device="cuda", precision="fp32",
-                 vertex_major=True):
+                 vertex_major=True, swap_features=True):
         """``precision``: "fp32" (the reference's arithmetic, the parity
         configuration) or "bf16" (configs C3/C5: the level-0/1 activations
         and gradients -- the large tensors -- stored in bf16 and VERTEX-MAJOR
@@ -160,6 +160,10 @@ class SDVAEEngine:
         self.w_lc, self.w_lap = float(w_lc), float(w_lap)
         self.eta1, self.eta2 = float(eta1), float(eta2)
         self.swap_bs = int(swap_bs)
+        # data config swap_features (data_loading.py:38): a train step is the
+        # bs^2 swapped meshes of bs base meshes, or (False) the bs meshes
+        # themselves with the latent-consistency term 0 (model_manager.py:290-293)
+        self.swap = bool(swap_features)
         self.seed = int(seed)
         if topo.n_levels != self.spec.n:
             raise ValueError(f"topology has {topo.n_levels} levels, model {self.spec.n}")
@@ -549,9 +553,16 @@ class SDVAEEngine:
         W, B = self._enc_lin()
         ops.linear_fwd(h.view(b.bsz, -1), W, B, out=b.mulv, workspace=b.lin_ws)
 
+    @property
+    def step_rows(self):
+        """Meshes in one train step: bs^2 swapped meshes, or bs without the swap."""
+        return self.swap_bs ** 2 if self.swap else self.swap_bs
+
     def _lc_on(self, b):
-        """Latent consistency needs a swapped bs x bs group (model_manager.py:360-367)."""
-        return bool(self.region_size) and self.w_lc != 0.0 and b.bsz == self.swap_bs ** 2
+        """Latent consistency needs a swapped bs x bs group (model_manager.py:360-367);
+        without the swap it is 0 (model_manager.py:290-293)."""
+        return (self.swap and bool(self.region_size) and self.w_lc != 0.0
+                and b.bsz == self.swap_bs ** 2)
 
     def latent(self, b, train):
         S = self.spec
@@ -862,8 +873,16 @@ class SDVAEEngine:
                        n_regions=max(T.n_regions, 1), batch_idx=b.batch_idx, bs=self.swap_bs,
                        n_batches=data.n_batches, perm=data.rows, n_items=data.n_items,
                        shuffle=data.shuffle, adam_step=self.params.step)
-        ops.swap_features(data.meshes, b.batch_idx, T.region_mask, b.key, self.swap_bs, out=b.x)
+        self.load_batch(b, data)
         self.train_step_on(b, acc=acc, grad_hook=grad_hook, advance=False)
+
+    def load_batch(self, b, data):
+        """The step's input from the picked base meshes: the on-device feature
+        swap (bs -> bs^2) or, with ``swap_features`` False, the bs meshes."""
+        if self.swap:
+            ops.swap_features(data.meshes, b.batch_idx, self.topo.region_mask, b.key, self.swap_bs, out=b.x)
+        else:
+            ops.gather_meshes(data.meshes, b.batch_idx, self.swap_bs, out=b.x)
 
 
 class ResidentData:
@@ -874,16 +893,25 @@ class ResidentData:
     ``norm`` = {'mean', 'std'} [V, 3] when given, data_loading.py:259-260);
     ``rows`` optional int32 subset of mesh indices (e.g. this rank's shard);
     batches of ``bs`` base meshes with ``shuffle`` (a fresh device-drawn order
-    every epoch) and ``drop_last`` semantics (data_loading.py:40-48)."""
+    every epoch) and ``drop_last`` semantics (data_loading.py:40-48).
+    ``n_batches`` caps the steps per epoch (data-parallel shards whose sizes
+    differ by one must all run the same number of steps, each step issuing
+    the same gradient all-reduces: :func:`dist.steps_per_epoch`)."""
 
-    def __init__(self, meshes, bs, rows=None, shuffle=True, norm=None):
+    def __init__(self, meshes, bs, rows=None, shuffle=True, norm=None, n_batches=None, inplace=False):
         if not meshes.is_cuda or meshes.dim() != 3:
             raise ValueError("meshes must be a [N, V, C] device tensor")
-        if norm is not None:  # into a buffer of its own: the caller's tensor is left unchanged
+        if norm is not None:
+            # into a buffer of its own (the caller's tensor is left unchanged),
+            # or -- ``inplace``, for a caller that hands the set over (e.g. a
+            # 50k-mesh augmented set) -- over the caller's contiguous fp32
+            # tensor, so only one copy is resident
             mean = norm["mean"].to(meshes.device, torch.float32).contiguous()
             std = norm["std"].to(meshes.device, torch.float32).contiguous()
-            self.meshes = ops.normalize(meshes.contiguous(), mean, std,
-                                        out=torch.empty(meshes.shape, dtype=torch.float32, device=meshes.device))
+            if inplace and not (meshes.is_contiguous() and meshes.dtype == torch.float32):
+                raise ValueError("inplace normalisation needs a contiguous fp32 tensor")
+            dst = meshes if inplace else torch.empty(meshes.shape, dtype=torch.float32, device=meshes.device)
+            self.meshes = ops.normalize(meshes.contiguous(), mean, std, out=dst)
         else:
             self.meshes = meshes.contiguous()
         n = meshes.shape[0]
@@ -897,6 +925,10 @@ class ResidentData:
             self.rows, self.n_items = None, n
         self.bs = int(bs)
         self.n_batches = self.n_items // self.bs
+        if n_batches is not None:
+            if not 1 <= int(n_batches) <= self.n_batches:
+                raise ValueError(f"n_batches {n_batches} outside [1, {self.n_batches}]")
+            self.n_batches = int(n_batches)
         if self.n_batches < 1:
             raise ValueError(f"{self.n_items} meshes < one batch of {self.bs}")
         self.shuffle = bool(shuffle)

@@ -92,10 +92,7 @@ class ModelManager:
         self._normalized_data = configurations["data"].get("normalize_data", True)
         self.to_mm_const = configurations["data"].get("to_mm_constant", 1.0)
         self.device = torch.device(device)
-        self._swap_features = configurations["data"].get("swap_features", True)
-        if not self._swap_features:
-            raise NotImplementedError("swap_features: False is not supported (every reference "
-                                      "configuration swaps; the step's batch is bs^2 swapped meshes)")
+        self._swap_features = bool(configurations["data"].get("swap_features", True))
         self.template = precompute.load_template(configurations["data"]["template_path"])
         self.topology_arrays = load_or_build_topology(configurations, self.template, precomputed_storage_path)
         self.topology = topology.DeviceTopology.from_npz(self.topology_arrays, device=self.device)
@@ -110,7 +107,8 @@ class ModelManager:
             self.topology, spec, lr=float(op["lr"]), weight_decay=float(op["weight_decay"]),
             w_kl=self._w_kl_loss, w_lc=self._w_latent_cons_loss, w_lap=self._w_laplacian_loss,
             eta1=float(op.get("latent_consistency_eta1", 0.5)), eta2=float(op.get("latent_consistency_eta2", 0.5)),
-            swap_bs=self.bs, seed=seed, device=self.device, precision=precision)
+            swap_bs=self.bs, seed=seed, device=self.device, precision=precision,
+            swap_features=self._swap_features)
         self._latent_regions = self._compute_latent_regions()
         self._batch_diagonal_idx = [(self.bs + 1) * i for i in range(self.bs)]
         self._losses = None
@@ -174,7 +172,7 @@ class ModelManager:
         ops.step_begin(self.val_counter, eng.seed + 7919, key=b.key, n_regions=max(T.n_regions, 1),
                        batch_idx=b.batch_idx, bs=self.bs, n_batches=data.n_batches, perm=data.rows,
                        n_items=data.n_items, shuffle=data.shuffle)
-        ops.swap_features(data.meshes, b.batch_idx, T.region_mask, b.key, self.bs, out=b.x)
+        eng.load_batch(b, data)
         eng.forward(b, train=False, acc=self.val_acc, finalize=True)
 
     def run_epoch(self, data, train=True, record=None):
@@ -182,7 +180,7 @@ class ModelManager:
         of one (shuffled, drop_last) epoch; returns and stores the per-batch
         mean of the losses (``_reset/_add/_divide_losses``).  ``record`` (a
         list) receives (batch_idx, key, eps) of every step (parity tests)."""
-        b = self.engine.buffers(self.bs * self.bs)
+        b = self.engine.buffers(self.engine.step_rows)
         acc = self.engine.loss_acc if train else self.val_acc
         acc.zero_()
         steps_done = 0

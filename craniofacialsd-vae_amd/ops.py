@@ -412,6 +412,22 @@ def swap_features(x_all, batch_idx, region_mask, key, bs, out=None):
     return y
 
 
+def gather_meshes(x_all, batch_idx, bs, out=None):
+    """The un-swapped batch of a ``swap_features: False`` configuration
+    (``data_loading.py:38, 81-82``: MeshCollater without a feature swapper):
+    ``out[b] = x_all[batch_idx[b]]`` on device (``cfsd_gather_meshes``)."""
+    n_meshes, nv, c = x_all.shape
+    _need(x_all, None, name="x_all")
+    _need(batch_idx, (bs,), torch.int32, "batch_idx")
+    if out is not None and is_vm(out):
+        _needl(out, (bs, nv, c), "out", torch.float32)
+        y = out
+    else:
+        y = _out(out, (bs, nv, c), x_all)
+    call("cfsd_gather_meshes", ptr(x_all), ptr(batch_idx), ptr(y), _st(y), bs, nv, c, n_meshes, stream_ptr())
+    return y
+
+
 def spectral_blend(s1, s2, values, n_blend, out=None):
     """Augmentation coefficients s1 + v * (s2 - s1) on the first ``n_blend``
     spectral components (utils.py:256-267); s1/s2 [pairs, k, c], values [pairs, k]."""

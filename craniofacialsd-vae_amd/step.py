@@ -50,7 +50,7 @@ class TrainStep:
         self.eng = engine
         self.data = data
         self.avg = averager if (averager is not None and averager.world > 1) else None
-        self.b = engine.buffers(engine.swap_bs ** 2)
+        self.b = engine.buffers(engine.step_rows)
         self.acc = engine.loss_acc if acc is None else acc
         self.graphs = None
         self._split = engine.enc_conv_numel()
@@ -70,7 +70,7 @@ class TrainStep:
                        n_regions=max(T.n_regions, 1), batch_idx=b.batch_idx, bs=eng.swap_bs,
                        n_batches=d.n_batches, perm=d.rows, n_items=d.n_items, shuffle=d.shuffle,
                        adam_step=eng.params.step)
-        ops.swap_features(d.meshes, b.batch_idx, T.region_mask, b.key, eng.swap_bs, out=b.x)
+        eng.load_batch(b, d)
         eng.forward(b, train=True, acc=self.acc, finalize=False)
         eng.backward_head(b, split=self.avg is not None)
 

@@ -242,6 +242,12 @@ int cfsd_swap_features(const float* x, const int32_t* batch_idx, const uint8_t* 
 int cfsd_swap_features_x(const float* x, const int32_t* batch_idx, const uint8_t* region_mask,
                          const int32_t* key, float* out, int out_dt, int bs, int nv, int c,
                          int n_meshes, int n_regions, void* stream);
+/* The un-swapped batch of a swap_features: False configuration
+ * (data_loading.py:38, 81-82: MeshCollater without a feature_swapper):
+ * out[b] = x[batch_idx[b]], b < bs; out_dt = CFSD_DT_F32 [| CFSD_VM] (ABI 4.4).
+ * Bit-exact copy; mesh indices clamped into [0, n_meshes). */
+int cfsd_gather_meshes(const float* x, const int32_t* batch_idx, float* out, int out_dt, int bs, int nv,
+                       int c, int n_meshes, void* stream);
 
 /* Spectral augmentation blend (utils.py:244-267, data_loading.py:359-364):
  * with s1 = U^T x1, s2 = U^T x2 [pairs, k, c] (U: the k smallest Laplacian

@@ -301,10 +301,16 @@ class Adam:
             p.addcdiv_(self.m[k], denom, value=-self.lr / bc1)
 
 
-def train_step(P, opt, x4, topo, key_index, eps, w=LOSS_W, is_vae=True):
+def train_step(P, opt, x4, topo, key_index, eps, w=LOSS_W, is_vae=True, swap=True):
     """One ``_do_iteration(train=True)``: swap -> forward -> losses ->
-    backward -> Adam.  ``P`` holds leaf tensors (requires_grad)."""
-    x16 = torch.from_numpy(swap_features(x4, topo.region_features, key_index))
+    backward -> Adam.  ``P`` holds leaf tensors (requires_grad).  ``swap``
+    False: a ``swap_features: False`` configuration (no SwapFeatures in the
+    collater, data_loading.py:38, 81-82): the batch is ``x4`` itself and the
+    latent-consistency term is 0 (``model_manager.py:290-293``)."""
+    if not swap:
+        key_index = None
+    x16 = torch.from_numpy(swap_features(x4, topo.region_features, key_index) if swap
+                           else np.ascontiguousarray(x4, dtype=np.float32))
     for p in P.values():
         p.grad = None
     out = losses(P, x16, topo, key_index, None if eps is None else torch.as_tensor(eps),

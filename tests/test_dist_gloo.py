@@ -108,3 +108,50 @@ def test_shard_range_covers_everything():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def _epoch_worker(rank, world, port, n_items, bs, out_dir):
+    """One data-parallel epoch's collective sequence: per step one gradient
+    all-reduce (the step's bucket), then the end-of-epoch loss all-reduce of a
+    DIFFERENT size (manager.run_epoch).  Every rank runs
+    dist.steps_per_epoch steps over its own shard_range shard."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import cfsd_loader
+    cfsd_loader.load()
+    from craniofacialsd_vae_amd.dist import shard_range, steps_per_epoch
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_range(n_items, rank, world)
+    steps = steps_per_epoch(n_items, world, bs)
+    assert 1 <= steps <= (hi - lo) // bs
+    grad = torch.full((1000,), float(rank))
+    for _ in range(steps):
+        dist.all_reduce(grad)
+    acc = torch.tensor([float(steps), 1.0, 2.0, 3.0, 4.0, 5.0])
+    dist.all_reduce(acc)
+    torch.save({"steps": steps, "acc0": float(acc[0]), "grad0": float(grad[0])},
+               os.path.join(out_dir, f"e{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_unequal_shards_run_equal_steps(tmp_path):
+    """31 train meshes over 2 ranks = shards of 16 and 15,
+    i.e. 4 and 3 batches of 4.  Both ranks must run 3 steps, or rank 0's 4th
+    gradient all-reduce pairs with rank 1's 6-float loss all-reduce (gloo
+    errors, RCCL hangs).  Also: the count is the smallest shard's for every
+    size / world / bs."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import cfsd_loader
+    cfsd_loader.load()
+    from craniofacialsd_vae_amd.dist import shard_range, steps_per_epoch
+    for n in range(0, 200, 7):
+        for world in (1, 2, 3, 8):
+            for bs in (1, 4, 5):
+                spans = [shard_range(n, r, world) for r in range(world)]
+                assert steps_per_epoch(n, world, bs) == min((h - l) // bs for l, h in spans)
+    mp.spawn(_epoch_worker, args=(2, _free_port(), 31, 4, str(tmp_path)), nprocs=2, join=True)
+    r = [torch.load(tmp_path / f"e{i}.pt", weights_only=True) for i in range(2)]
+    assert r[0]["steps"] == r[1]["steps"] == 3
+    assert r[0]["acc0"] == r[1]["acc0"] == 6.0

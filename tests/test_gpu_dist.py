@@ -224,3 +224,27 @@ def test_dp2_graph_trainstep(tmp_path, precision):
         assert s["losses_finite"], (i, s)
         if precision == "bf16":
             assert s["shadow_equal_ranks"] and s["shadow_is_cast"], (i, s)
+
+
+def test_bench_line_self_verifies_at_world2(tmp_path):
+    """bench.py's N > 1 line carries its own evidence:
+    the process group's world size and backend, every rank's PCI id, per-rank
+    ms per step, and ``ranks_in_sync`` -- bit checksums of parameters,
+    gradient, Adam moments and t equal on every rank after the timed steps.
+    Rehearsed with 2 gloo ranks sharing the test GPU (the driver's 8-GPU run
+    uses RCCL, one GPU per rank: ``distinct_devices`` then holds)."""
+    env = dict(os.environ, CFSD_DIST_BACKEND="gloo", CFSD_SHARE_DEVICE="1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "4", "--warmup", "2", "--dataset", "32", "--no-cpu", "--no-extras"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    out = json.loads(lines[0])
+    dc = out["dist_check"]
+    assert out["n_gpus"] == 2 and dc["world_size"] == 2 and dc["backend"] == "gloo"
+    assert dc["shared_device_rehearsal"] and len(dc["pci_bus_ids"]) == 2
+    assert dc["ranks_in_sync"], dc
+    assert dc["checksums_rank0"]["adam_t"] == 1 + 2 + 4  # capture step + warmup + timed
+    assert 0 < dc["ms_per_step_min"] <= dc["ms_per_step_max"] <= out["ms_per_step"] * 1.0001

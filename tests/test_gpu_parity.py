@@ -384,6 +384,59 @@ def test_train_three_steps_golden(otopo, dtopo):
                                        atol=2e-5)
 
 
+@pytest.mark.parametrize("bs", [4, 1])
+def test_train_steps_without_swap(otopo, dtopo, bs):
+    """data config ``swap_features: False`` (data_loading.py:38, 81-82: no
+    SwapFeatures in the collater): the step's batch is the bs picked meshes
+    (cfsd_gather_meshes, bit-exact), latent consistency is 0
+    (model_manager.py:290-293) -- also at bs = 1, where a swapped group would
+    have bs^2 = bs rows -- and two steps (losses, every gradient, parameters
+    after Adam) match the oracle's un-swapped _do_iteration.  Through
+    step.TrainStep (the object the driver and the bench run)."""
+    from craniofacialsd_vae_amd.step import TrainStep
+    w = recipe.golden_weights()
+    eng = E.SDVAEEngine(dtopo, E.ModelSpec(), swap_bs=bs, device=DEV, swap_features=False)
+    eng.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
+    assert eng.step_rows == bs
+    meshes = recipe.normalized_meshes(12)
+    data = E.ResidentData(torch.from_numpy(meshes).to(DEV), bs=bs, shuffle=True)
+    ts = TrainStep(eng, data)
+    assert ts.b.bsz == bs
+    P = O.make_params(w)
+    opt = O.Adam(P)
+    for step in range(2):
+        ts.step()
+        torch.cuda.synchronize()
+        b = ts.b
+        picked = b.batch_idx.cpu().numpy()
+        assert len(set(picked.tolist())) == bs
+        np.testing.assert_array_equal(b.x.cpu().numpy(), meshes[picked])
+        out, grads, _ = O.train_step(P, opt, meshes[picked], otopo, None, b.eps.cpu().numpy(), swap=False)
+        got = b.losses.cpu().numpy()
+        assert got[2] == 0.0
+        np.testing.assert_allclose(got, [out[k].item() for k in ("rec", "kl", "lc", "lap", "tot")],
+                                   rtol=1e-4, atol=1e-7)
+        hip_grads = {k: v.cpu() for k, v in eng.grads().items()}
+        for name in w:
+            close(hip_grads[name], grads[name], 1e-4, f"step {step} grad {name}")
+        sd = eng.state_dict()
+        for name in w:
+            close(sd[name], P[name].detach(), 2e-5, f"step {step} param {name}")
+
+
+def test_gather_meshes_layouts(dtopo):
+    """cfsd_gather_meshes into either level-0 layout equals the host gather."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(7, dtopo.n_verts[0], 3, generator=g).to(DEV)
+    idx = torch.tensor([5, 0, 6, 2] * 4, dtype=torch.int32, device=DEV)
+    ref = x.cpu()[idx.cpu().long()]
+    y = ops.gather_meshes(x, idx, 16)
+    assert torch.equal(y.cpu(), ref)
+    yv = ops.vm_empty(16, dtopo.n_verts[0], 3, dtype=torch.float32, device=DEV)
+    ops.gather_meshes(x, idx, 16, out=yv)
+    assert torch.equal(yv.cpu(), ref)
+
+
 def test_train_step_deterministic(dtopo):
     w = recipe.golden_weights()
     outs = []

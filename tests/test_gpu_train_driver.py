@@ -42,8 +42,9 @@ def write_obj(path, v):
             f.write("v %.9g %.9g %.9g\n" % tuple(p))
 
 
-@pytest.fixture(scope="module")
-def workspace(tmp_path_factory, topo_npz):
+def make_workspace(tmp_path_factory, topo_npz, n_meshes=40, swap=True):
+    """Demo workspace of ``n_meshes`` OBJ files (split i % 100: 6 test, 5
+    validation, the rest train: 40 -> 29 train meshes, 42 -> 31)."""
     cfsd_loader.load()
     from craniofacialsd_vae_amd import precompute
     d = tmp_path_factory.mktemp("demo")
@@ -54,15 +55,20 @@ def workspace(tmp_path_factory, topo_npz):
     (d / "meshes").mkdir()
     m = recipe.load_meshes()
     rs = np.random.RandomState(3)
-    for i in range(40):
+    for i in range(n_meshes):
         v = m["verts"][i % 12] + (0 if i < 12 else rs.normal(0, 0.002, m["verts"][0].shape))
         write_obj(d / "meshes" / f"{'nacm'[i % 4]}_{i:03d}.obj", v.astype(np.float32))
     cfg = dict(CONFIG, data={"template_path": str(d / "template.ply"), "precomputed_path": str(d / "pre"),
                              "dataset_path": str(d / "meshes"), "normalize_data": True, "to_mm_constant": 89.11,
-                             "swap_features": True, "stratified_split": False})
+                             "swap_features": swap, "stratified_split": False})
     with open(d / "config.yaml", "w") as f:
         yaml.safe_dump(cfg, f)
     return d, cfg
+
+
+@pytest.fixture(scope="module")
+def workspace(tmp_path_factory, topo_npz):
+    return make_workspace(tmp_path_factory, topo_npz)
 
 
 def test_two_epochs_match_oracle(workspace, otopo):
@@ -106,6 +112,43 @@ def test_two_epochs_match_oracle(workspace, otopo):
         keys = ("reconstruction", "kl", "latent_consistency", "laplacian", "tot")
         np.testing.assert_allclose([got_t[k] for k in keys], ref_t, rtol=1e-4, err_msg=f"train epoch {epoch}")
         np.testing.assert_allclose([got_v[k] for k in keys], vs, rtol=1e-4, err_msg=f"val epoch {epoch}")
+
+
+def test_epoch_without_swap_matches_oracle(tmp_path_factory, topo_npz, otopo):
+    """``swap_features: False`` (the reference's _do_iteration with
+    loss_z_cons = 0, model_manager.py:290-293, batches of bs un-swapped
+    meshes): one train and one validation epoch of the driver match the oracle
+    replaying the recorded batches (rtol 1e-4); latent consistency is 0."""
+    from craniofacialsd_vae_amd import data as D
+    from craniofacialsd_vae_amd import manager as M
+    d, cfg = make_workspace(tmp_path_factory, topo_npz, swap=False)
+    torch.set_num_threads(4)
+    man = M.ModelManager(cfg, device="cuda", precomputed_storage_path=cfg["data"]["precomputed_path"],
+                         seed=13, use_graph=False)
+    assert man.engine.step_rows == 4
+    w = recipe.golden_weights()
+    man.engine.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
+    tr, va, te, norm = D.load_mesh_dataset(cfg["data"], 4, "cuda")
+    xs, xv = tr.meshes.cpu().numpy(), va.meshes.cpu().numpy()
+    P = O.make_params(w)
+    opt = O.Adam(P)
+    rec_t, rec_v = [], []
+    got_t = man.run_epoch(tr, train=True, record=rec_t)
+    got_v = man.run_epoch(va, train=False, record=rec_v)
+    assert len(rec_t) == 7 and len(rec_v) == 1
+    sums = np.zeros(5)
+    for bidx, _, eps in rec_t:
+        out, _, _ = O.train_step(P, opt, xs[bidx], otopo, None, eps, swap=False)
+        sums += [out[k].item() for k in ("rec", "kl", "lc", "lap", "tot")]
+    vs = np.zeros(5)
+    for bidx, _, _ in rec_v:
+        with torch.no_grad():
+            out = O.losses(P, torch.from_numpy(xv[bidx]), otopo, None, None, train=False)
+        vs += [out[k].item() for k in ("rec", "kl", "lc", "lap", "tot")]
+    keys = ("reconstruction", "kl", "latent_consistency", "laplacian", "tot")
+    assert got_t["latent_consistency"] == 0.0 and got_v["latent_consistency"] == 0.0
+    np.testing.assert_allclose([got_t[k] for k in keys], sums / 7, rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose([got_v[k] for k in keys], vs, rtol=1e-4, atol=1e-9)
 
 
 def test_cli_end_to_end_and_resume(workspace, tmp_path):
@@ -249,12 +292,17 @@ def test_bf16_epochs_on_augmented_set(aug_workspace):
     assert int(man.engine.params.step.item()) == 2 * tr.n_batches
 
 
-def test_cli_data_parallel_two_ranks(workspace, tmp_path):
+@pytest.mark.parametrize("n_meshes", [40, 42])
+def test_cli_data_parallel_two_ranks(tmp_path_factory, topo_npz, tmp_path, n_meshes):
     """train.py under torch.distributed.run with 2 ranks (C3's driver; here
     gloo with both ranks on the one test GPU): each rank trains its shard,
-    epoch losses are the all-reduced means, rank 0 logs and checkpoints."""
+    epoch losses are the all-reduced means, rank 0 logs and checkpoints.
+    42 meshes -> 31 train meshes: shards of 16 and 15 (4 and 3 batches of 4)
+    -- both ranks must run 3 steps per epoch (dist.steps_per_epoch), or the
+    extra step's gradient all-reduce meets the other rank's end-of-epoch loss
+    all-reduce."""
     import socket
-    d, cfg = workspace
+    d, cfg = make_workspace(tmp_path_factory, topo_npz, n_meshes)
     sock = socket.socket()
     sock.bind(("127.0.0.1", 0))
     port = sock.getsockname()[1]
@@ -267,6 +315,9 @@ def test_cli_data_parallel_two_ranks(workspace, tmp_path):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     od = out / "outputs" / "dp"
+    ck = torch.load(od / "checkpoints" / "optimizer.pt", weights_only=True)["optimizer"]
+    # 2 epochs x the smallest shard's batches, identical on both ranks
+    assert int(float(ck["state"][0]["step"])) == 2 * (((n_meshes - 11) // 2) // 4)
     assert sorted(os.listdir(od / "checkpoints")) == ["model_00000001.pt", "model_00000002.pt", "optimizer.pt"]
     logs = [json.loads(ln) for ln in open(od / "logs" / "scalars.jsonl")]
     assert len([x for x in logs if x["tag"] == "train/tot"]) == 2

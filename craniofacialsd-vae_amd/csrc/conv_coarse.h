@@ -1,0 +1,31 @@
+// Coarse-level SpiralConv launchers (spiral_conv_coarse.hip).
+#pragma once
+#include "cfsd_common.h"
+
+namespace cfsd {
+namespace coarse {
+
+// Layers below this many rows (batch x output vertices) take the slot-group
+// kernels: the coarse levels of the hierarchy, where one wave per tile and
+// all nine slots cannot fill the chip.
+constexpr long kMaxRows = 24576;
+
+struct FwdKsArgs {
+  const float* x;       // input rows; UP: the coarse tensor [batch, n_coarse, CIN] (batch-major)
+  const int* idx;       // spiral [rows][9] (indices into the input level)
+  const float* w;       // [COUT][9 CIN]
+  const float* bias;    // [COUT] or null
+  float* y;             // [batch, rows, COUT] in layout yvm
+  float* yup;           // UP: the up-sampled input [batch, rows, CIN] (written), or null
+  const int* up_col;    // UP: 3 columns per fine vertex (uniform-row up matrix), else null
+  const float* up_val;  // UP: 3 values per fine vertex
+  int vsrc, rows, batch, n_coarse;
+  long total_rows;      // batch * rows
+  int xvm, yvm, elu;
+};
+
+bool fwd_ks_enabled(long total_rows, int cin, int cout);
+int launch_fwd_ks(const FwdKsArgs& a, int cin, int cout, hipStream_t st);
+
+}  // namespace coarse
+}  // namespace cfsd

@@ -20,6 +20,7 @@
 #include "cfsd_common.h"
 #include "conv_bf16.h"
 #include "conv_vm32.h"
+#include "conv_coarse.h"
 
 namespace cfsd {
 
@@ -2213,10 +2214,32 @@ static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const
 #define CFSD_LAT_DW_MAX CFSD_LAT_MAX_ROWS
 #endif
 
+// coarse levels: slot groups in one workgroup, partials combined in LDS
+// (spiral_conv_coarse.hip)
+static int fwd_coarse(const float* x, int xvm, const int* idx, const float* w, const float* bias, float* y,
+                      int yvm, int vsrc, int rows, int batch, int cin, int cout, int act, hipStream_t st) {
+  coarse::FwdKsArgs a{};
+  a.x = x;
+  a.idx = idx;
+  a.w = w;
+  a.bias = bias;
+  a.y = y;
+  a.vsrc = vsrc;
+  a.rows = rows;
+  a.batch = batch;
+  a.total_rows = (long)batch * rows;
+  a.xvm = xvm;
+  a.yvm = yvm;
+  a.elu = act == CFSD_ACT_ELU;
+  return coarse::launch_fwd_ks(a, cin, cout, st);
+}
+
 template <int CIN, int COUT, int ACT>
 static int dispatch_fwd_mfma(const float* x, const int* idx, const float* w, const float* bias,
                              float* y, float* ws, size_t ws_floats, int vsrc, int rows, long M,
                              hipStream_t st) {
+  if (coarse::fwd_ks_enabled(M, CIN, COUT))
+    return fwd_coarse(x, 0, idx, w, bias, y, 0, vsrc, rows, (int)(M / rows), CIN, COUT, ACT, st);
   // (64 -> 32 excepted: measured slower there than slot groups + combine)
 #ifndef CFSD_FWD_LAT_6432
 #define CFSD_FWD_LAT_6432 0
@@ -2928,6 +2951,8 @@ extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* id
   if (!w) return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: w required");
   if (mfma_shape(cin, cout) && x_dt == CFSD_DT_F32 && xvm) {  // fp32 vertex-major
     if (y_dt != CFSD_DT_F32) return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: fp32 x needs fp32 y");
+    if (coarse::fwd_ks_enabled(M, cin, cout))
+      return fwd_coarse((const float*)x, xvm, idx, w, bias, (float*)y, yvm, vsrc, rows, batch, cin, cout, act, st);
     if (M < CFSD_LAT_FWD_MAX && cin == 32 && cout == 32) {  // few rows (an Enblock's kept rows): 16x16 tasks
       const long tasks = (M + 15) / 16 * 2;
       if (act == CFSD_ACT_ELU)

@@ -1,0 +1,253 @@
+// Coarse-level SpiralConv kernels (levels 2-4 of the craniofacial hierarchy:
+// 1065 / 267 / 67 vertices, i.e. 17k / 4.3k / 1.1k rows at batch 16).
+//
+// Why a separate family: at these sizes the whole layer is a few hundred
+// 16-row tiles, so a kernel that gives each wave a tile and ALL nine slots
+// (conv_fwd_lat) occupies ~500-2k waves on a 1024-SIMD chip and every wave
+// runs a 144-288 deep v_mfma_f32_16x16x4_f32 chain (32-cycle issue each):
+// the counters of round 3 (profiles/r04a_pmc_coarse_sq_summary.txt) show
+// those waves issue-stalled 65 % of their life with half the SIMDs idle.
+// Here the nine slots are split over the waves of a workgroup (slot groups),
+// each wave keeps ITS slots' weights in VGPRs and reuses them over RT row
+// tiles, and the slot-group partials are combined in LDS in a fixed order
+// (g = 0, 1, ..) by the same workgroup -- no workspace and no combine launch.
+//
+// The Deblock form (UP) also evaluates the Pool(up) of the input inside the
+// gather (model.py:80-82: Pool(x, up) then SpiralConv): the up-sampled row of
+// vertex v is sum_k val[3v+k] * xc[col[3v+k]] over its 3 barycentric taps,
+// computed with the SpMM's exact arithmetic ((0 + x0 v0) + x1 v1) + x2 v2
+// un-fused (bit-identical to spmm_uniform_k), so the separate up-sampling
+// launch disappears; the slot-0 wave (spiral slot 0 is the vertex itself,
+// checked on the host) stores the up-sampled rows of its tile, which the
+// weight gradient of the backward reads.
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "cfsd_common.h"
+#include "conv_coarse.h"
+
+namespace cfsd {
+namespace coarse {
+
+constexpr int kSeq = 9;
+
+// x_up chunk of fine vertex v for mesh b: the three taps of up row v
+// (spmm_uniform_k's order and rounding)
+__device__ __forceinline__ f32x4 up_row4(const f32x4 x0, const f32x4 x1, const f32x4 x2, float v0, float v1,
+                                         float v2) {
+#pragma clang fp contract(off)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc.x = acc.x + x0.x * v0;
+  acc.y = acc.y + x0.y * v0;
+  acc.z = acc.z + x0.z * v0;
+  acc.w = acc.w + x0.w * v0;
+  acc.x = acc.x + x1.x * v1;
+  acc.y = acc.y + x1.y * v1;
+  acc.z = acc.z + x1.z * v1;
+  acc.w = acc.w + x1.w * v1;
+  acc.x = acc.x + x2.x * v2;
+  acc.y = acc.y + x2.y * v2;
+  acc.z = acc.z + x2.z * v2;
+  acc.w = acc.w + x2.w * v2;
+  return acc;
+}
+
+// One workgroup = NSG waves (slot groups of kSeq / NSG slots) x RT 16-row
+// tiles x all COUT columns.  v_mfma_f32_16x16x4_f32 lane map as conv_fwd_lat:
+// lane (i = l & 15, kg = l >> 4) holds row i's 16-B chunks of channels
+// 16c + 4kg .. +3; B = W[o][s*CIN + 16c + 4kg + j] for the 4 MFMAs j of a chunk.
+template <int CIN, int COUT, int NSG, int RT, int UP>
+__global__ __launch_bounds__(64 * NSG) void conv_fwd_ks(const FwdKsArgs a) {
+  constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN, SPW = kSeq / NSG;
+  constexpr int LDC = COUT + 4;  // partial row stride (kg rows land on distinct banks)
+  static_assert(kSeq % NSG == 0, "slot groups");
+  __shared__ f32x4 part4[NSG * RT * 16 * LDC / 4];
+  float* part = reinterpret_cast<float*>(part4);
+  const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long rt0 = (long)xcd_block() * RT;
+  const long M = a.total_rows;
+  const int nv_x = UP ? a.n_coarse : a.vsrc;
+  const Lay lx = make_lay(a.xvm, a.batch, nv_x);
+  // this lane's row in each tile (x's layout), its mesh / vertex and spiral
+  int bq[RT], src[RT][SPW];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    long m = (rt0 + rt) * 16 + r16;
+    if (m >= M) m = M - 1;  // clamped rows: loads only, stores are masked
+    int r;
+    split_row(m, a.xvm, a.batch, a.rows, bq[rt], r);
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) src[rt][j] = a.idx[r * kSeq + g * SPW + j];
+  }
+  // this wave's weight slices (reused by all RT tiles)
+  f32x4 bw[SPW][CH][NCT];
+  const float* wb = a.w + (long)r16 * K + 4 * kg;
+#pragma unroll
+  for (int j = 0; j < SPW; ++j)
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) bw[j][c][t] = ld4(wb + (long)t * 16 * K + (g * SPW + j) * CIN + 16 * c);
+  f32x4 av[RT][SPW][CH];
+  if constexpr (UP) {
+    int cc[RT][SPW][3];
+    float vv[RT][SPW][3];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < SPW; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          cc[rt][j][k] = a.up_col[src[rt][j] * 3 + k];
+          vv[rt][j][k] = a.up_val[src[rt][j] * 3 + k];
+        }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const float* xb = a.x + (long)bq[rt] * lx.bs * CIN + 4 * kg;
+#pragma unroll
+      for (int j = 0; j < SPW; ++j)
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          const f32x4 x0 = ld4(xb + (long)cc[rt][j][0] * lx.vs * CIN + 16 * c);
+          const f32x4 x1 = ld4(xb + (long)cc[rt][j][1] * lx.vs * CIN + 16 * c);
+          const f32x4 x2 = ld4(xb + (long)cc[rt][j][2] * lx.vs * CIN + 16 * c);
+          av[rt][j][c] = up_row4(x0, x1, x2, vv[rt][j][0], vv[rt][j][1], vv[rt][j][2]);
+        }
+    }
+    // slot 0 of spiral row r is r itself: wave 0 holds the tile's up-sampled rows
+    if (g == 0 && a.yup) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const long m = (rt0 + rt) * 16 + r16;
+        if (m < M) {
+#pragma unroll
+          for (int c = 0; c < CH; ++c) st4(a.yup + m * CIN + 16 * c + 4 * kg, av[rt][0][c]);
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const float* xb = a.x + (long)bq[rt] * lx.bs * CIN + 4 * kg;
+#pragma unroll
+      for (int j = 0; j < SPW; ++j)
+#pragma unroll
+        for (int c = 0; c < CH; ++c) av[rt][j][c] = ld4(xb + (long)src[rt][j] * lx.vs * CIN + 16 * c);
+    }
+  }
+  f32x4 acc[RT][NCT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NCT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // consecutive MFMAs go to different (tile, column tile) accumulators
+#define KS_MF(Q)                        \
+  _Pragma("unroll") for (int rt = 0; rt < RT; ++rt) \
+  _Pragma("unroll") for (int t = 0; t < NCT; ++t) acc[rt][t] = mfma16(av[rt][j][c].Q, bw[j][c][t].Q, acc[rt][t]);
+#pragma unroll
+  for (int j = 0; j < SPW; ++j)
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      KS_MF(x) KS_MF(y) KS_MF(z) KS_MF(w)
+    }
+#undef KS_MF
+  // slot-group partials -> LDS, combined in fixed group order
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NCT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        part[((g * RT + rt) * 16 + 4 * kg + rr) * LDC + t * 16 + r16] = acc[rt][t][rr];
+  __syncthreads();
+  constexpr int N4 = RT * 16 * COUT / 4;
+  for (int q = threadIdx.x; q < N4; q += 64 * NSG) {
+    const int rt = q / (16 * COUT / 4), rem = q % (16 * COUT / 4);
+    const int row = rem / (COUT / 4), c4 = rem % (COUT / 4);
+    const long m = (rt0 + rt) * 16 + row;
+    if (m >= M) continue;
+    f32x4 v = part4[((0 * RT + rt) * 16 + row) * (LDC / 4) + c4];
+#pragma unroll
+    for (int gg = 1; gg < NSG; ++gg) v += part4[((gg * RT + rt) * 16 + row) * (LDC / 4) + c4];
+    if (a.bias) v += ld4(a.bias + 4 * c4);
+    if (a.elu) {
+      v.x = elu_f(v.x);
+      v.y = elu_f(v.y);
+      v.z = elu_f(v.z);
+      v.w = elu_f(v.w);
+    }
+    long yo = m;
+    if (a.xvm != a.yvm) {
+      int bo, ro;
+      split_row(m, a.xvm, a.batch, a.rows, bo, ro);
+      yo = row_of(make_lay(a.yvm, a.batch, a.rows), bo, ro);
+    }
+    st4(a.y + yo * COUT + 4 * c4, v);
+  }
+}
+
+// ------------------------------------------------------------------ host side
+// Geometry: slot groups and row tiles per workgroup.  More rows per
+// workgroup amortise the weight slices (each workgroup reads all of W once
+// from L2); more slot groups shorten each wave's MFMA chain.  Picked so the
+// grid holds >= ~2k waves (2 per SIMD) where the layer allows.
+static bool parse_override(int& nsg, int& rt) {
+  static int cached = -2, cn = 0, cr = 0;
+  if (cached == -2) {
+    const char* e = getenv("CFSD_KS");
+    cached = (e && sscanf(e, "%d:%d", &cn, &cr) == 2) ? 1 : (e && e[0] == '0' ? 0 : -1);
+  }
+  if (cached == 1) {
+    nsg = cn;
+    rt = cr;
+  }
+  return cached != 0;
+}
+
+bool fwd_ks_enabled(long total_rows, int cin, int cout) {
+  int n = 0, r = 0;
+  if (!parse_override(n, r)) return false;
+  return total_rows < kMaxRows && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
+}
+
+static void pick(long total_rows, int cin, int cout, int& nsg, int& rt) {
+  const long n_rt = (total_rows + 15) / 16;
+  nsg = (cin * cout >= 64 * 32 || n_rt < 2048) ? 9 : 3;
+  rt = 1;
+  while (rt < 4 && (n_rt + 2 * rt - 1) / (2 * rt) * nsg >= 2048) rt *= 2;
+  parse_override(nsg, rt);
+  if (nsg != 3 && nsg != 9) nsg = 9;
+  if (rt != 1 && rt != 2 && rt != 4) rt = 1;
+}
+
+template <int CIN, int COUT, int UP>
+static int launch_shape(const FwdKsArgs& a, int nsg, int rt, hipStream_t st) {
+  const long n_rt = (a.total_rows + 15) / 16;
+#define KS(NSG_, RT_)                                                                                 \
+  if (nsg == NSG_ && rt == RT_) {                                                                     \
+    hipLaunchKernelGGL((conv_fwd_ks<CIN, COUT, NSG_, RT_, UP>), dim3((unsigned)((n_rt + RT_ - 1) / RT_)), \
+                       dim3(64 * NSG_), 0, st, a);                                                    \
+    return launch_status("spiral_conv_fwd_ks");                                                       \
+  }
+  KS(3, 1) KS(3, 2) KS(3, 4) KS(9, 1) KS(9, 2) KS(9, 4)
+#undef KS
+  return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: bad geometry %d:%d", nsg, rt);
+}
+
+int launch_fwd_ks(const FwdKsArgs& a, int cin, int cout, hipStream_t st) {
+  if (a.total_rows <= 0 || a.total_rows >= kMaxRows) return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: rows");
+  const bool up = a.up_col != nullptr;
+  if (up && a.xvm) return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: fused up-sampling needs batch-major input");
+  int nsg, rt;
+  pick(a.total_rows, cin, cout, nsg, rt);
+#define SHAPE(CI_, CO_)                                                         \
+  if (cin == CI_ && cout == CO_)                                                \
+    return up ? launch_shape<CI_, CO_, 1>(a, nsg, rt, st) : launch_shape<CI_, CO_, 0>(a, nsg, rt, st);
+  SHAPE(32, 32) SHAPE(32, 64) SHAPE(64, 32) SHAPE(64, 64)
+#undef SHAPE
+  return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: unsupported channels %d -> %d", cin, cout);
+}
+
+}  // namespace coarse
+}  // namespace cfsd

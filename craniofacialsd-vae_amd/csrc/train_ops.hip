@@ -350,7 +350,7 @@ __global__ __launch_bounds__(CFSD_LAT_THREADS) void latent_fwd_k(const float* __
   float2 r = block_sum2(kl_part, lc_part, red);
   if (tid == 0) {
     terms[0] = is_vae ? -0.5f * r.x / (float)B : 0.f;
-    terms[1] = r.y * scale;
+    terms[1] = w_lc != 0.f ? r.y * scale : 0.f;  // (no LC: bs = 1 and scale = 1/0)
   }
 }
 

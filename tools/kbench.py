@@ -163,6 +163,9 @@ def main():
     we1, be1 = eng._enc_w(1)
     cases["dw_e1"] = lambda: ops.spiral_conv_bwd_weight(b.enc_out[0], T.enc_rows[1], b.dpre_enc[1], None, None,
                                                        b.ws_dw[("enc", 1)])
+    for lv in (2, 3):
+        cases[f"fwd_e{lv}"] = (lambda lv=lv: ops.spiral_conv_fwd(b.enc_out[lv - 1], T.enc_rows[lv], *eng._enc_w(lv), 1,
+                                                                 out=b.enc_out[lv], workspace=b.ws))
     cases["fwd_e1"] = lambda: ops.spiral_conv_fwd(b.enc_out[0], T.enc_rows[1], we1, be1, 1, out=b.enc_out[1], workspace=b.ws)
     cases["rowsub_e1"] = lambda: ops.spiral_conv_bwd_rowsub(b.enc_out[0], T.enc_rows[1], b.dpre_enc[1], T.enc_flat[1],
                                                             we1, None, None, dx=b.dpre_enc[0], elu_y=b.enc_out[0],

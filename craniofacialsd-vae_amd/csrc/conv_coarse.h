@@ -24,8 +24,22 @@ struct FwdKsArgs {
   int xvm, yvm, elu;
 };
 
+struct DxKsArgs {
+  const float* dpre;      // [batch, rows, COUT] batch-major
+  const int* inv_ptr;     // inverse spiral CSR (vsrc*9 + 1)
+  const int* inv_row;
+  const int4* inv_head;   // first four rows of every (u, s) list, -1 absent
+  const float* w;         // [COUT][9 CIN]
+  const float* elu_y;     // [batch, vsrc, CIN] ELU output (dx *= ELU'), or null
+  float* dx;              // [batch, vsrc, CIN]
+  int vsrc, rows, batch;
+  long total_rows;        // batch * vsrc (dx rows)
+};
+
 bool fwd_ks_enabled(long total_rows, int cin, int cout);
 int launch_fwd_ks(const FwdKsArgs& a, int cin, int cout, hipStream_t st);
+bool dx_ks_enabled(long total_src_rows, int cin, int cout);
+int launch_dx_ks(const DxKsArgs& a, int cin, int cout, hipStream_t st);
 
 }  // namespace coarse
 }  // namespace cfsd

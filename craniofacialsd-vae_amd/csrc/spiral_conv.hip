@@ -2386,6 +2386,11 @@ static int dispatch_dx_mfma(const float* dpre, const int* inv_ptr, const int* in
                             const int* inv_head, const float* w, const float* elu_y, float* dx,
                             float* ws, size_t ws_floats, int vsrc, int rows, long M,
                             hipStream_t st) {
+  if (coarse::dx_ks_enabled(M, CIN, COUT)) {
+    const coarse::DxKsArgs a{dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows,
+                             (int)(M / vsrc), M};
+    return coarse::launch_dx_ks(a, CIN, COUT, st);
+  }
   if (dx_is_lat(M, M / vsrc * rows)) {
     if (dx_lat_ctw(CIN, COUT, M) == 2) {
       constexpr int CTW2 = CIN / 16 >= 2 ? 2 : 1;
@@ -2648,6 +2653,7 @@ namespace {
 // E2 32->32 3-5 us faster).
 bool bwd_paired(int batch, int vsrc, int rows, int cin, int cout) {
   if (!((cin == 32 || cin == 64) && cout == 32)) return false;
+  if (coarse::dx_ks_enabled((long)batch * vsrc, cin, cout)) return false;  // the slot-group dx + dW
   return dx_is_lat((long)batch * vsrc, (long)batch * rows) &&
          dw_geom(batch, rows, cin, cout).kind == kDwLat;
 }

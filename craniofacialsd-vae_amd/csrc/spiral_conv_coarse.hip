@@ -187,6 +187,127 @@ __global__ __launch_bounds__(64 * NSG) void conv_fwd_ks(const FwdKsArgs a) {
   }
 }
 
+// Backward data, same geometry: a workgroup owns RT 16-row tiles of SOURCE
+// rows u (dx rows) x all CIN columns, wave g the slots of its group.  For slot
+// s the A operand is T_s[u, :] = sum_{r in inv(u,s)} dpre[r, :] (the inverse
+// spiral's head rows -- absent rows are out-of-range buffer loads that read 0
+// -- summed (r0 + r1) + r2, then r3 and the rare CSR tail: conv_dx_lat's
+// order), B = W_s^T (4 strided dwords per 4-chunk of o, kept in VGPRs over the
+// tiles); partials combined in LDS in group order, then ELU' and the store.
+constexpr int kInvHead = CFSD_INV_HEAD;
+constexpr int kAbsentRow = 0x7ffff000;
+__device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+template <int CIN, int COUT, int NSG, int RT>
+__global__ __launch_bounds__(64 * NSG) void conv_dx_ks(const DxKsArgs a) {
+  constexpr int CHO = COUT / 16, NCT = CIN / 16, K = kSeq * CIN, SPW = kSeq / NSG;
+  constexpr int LDC = CIN + 4, RB = COUT * (int)sizeof(float);
+  static_assert(kSeq % NSG == 0, "slot groups");
+  __shared__ f32x4 part4[NSG * RT * 16 * LDC / 4];
+  float* part = reinterpret_cast<float*>(part4);
+  const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long rt0 = (long)xcd_block() * RT;
+  const long M = a.total_rows;  // batch * vsrc
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.dpre), 0,
+                                                      (int)((long)a.batch * a.rows * RB), 0x00020000);
+  int base[RT];
+  int4 hd[RT][SPW];
+  int uq[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    long m = (rt0 + rt) * 16 + r16;
+    if (m >= M) m = M - 1;
+    int b, u;
+    divmod32(m, a.vsrc, b, u);
+    uq[rt] = u;
+    base[rt] = (b * a.rows * COUT + 4 * kg) * (int)sizeof(float);
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) hd[rt][j] = a.inv_head[(long)u * kSeq + g * SPW + j];
+  }
+  f32x4 bw[SPW][CHO][NCT];
+#pragma unroll
+  for (int j = 0; j < SPW; ++j)
+#pragma unroll
+    for (int ch = 0; ch < CHO; ++ch)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) {
+        const float* q = a.w + (long)(16 * ch + 4 * kg) * K + (g * SPW + j) * CIN + 16 * t + r16;
+        bw[j][ch][t] = f32x4{q[0], q[K], q[2 * K], q[3 * K]};
+      }
+  f32x4 av[RT][SPW][CHO];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) {
+      const int hr[4] = {hd[rt][j].x, hd[rt][j].y, hd[rt][j].z, hd[rt][j].w};
+      f32x4 r[4][CHO];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int ch = 0; ch < CHO; ++ch)
+          r[e][ch] = buf_ld4(rsrc, hr[e] >= 0 ? base[rt] + hr[e] * RB + 64 * ch : kAbsentRow);
+#pragma unroll
+      for (int ch = 0; ch < CHO; ++ch) av[rt][j][ch] = ((r[0][ch] + r[1][ch]) + r[2][ch]) + r[3][ch];
+    }
+  // list rows past the head (0.03 % of keys at level 0): exec branch, list order
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) {
+      if (hd[rt][j].w >= 0) {
+        const long key = (long)uq[rt] * kSeq + g * SPW + j;
+        for (int e = a.inv_ptr[key] + kInvHead; e < a.inv_ptr[key + 1]; ++e) {
+#pragma unroll
+          for (int ch = 0; ch < CHO; ++ch) av[rt][j][ch] += buf_ld4(rsrc, base[rt] + a.inv_row[e] * RB + 64 * ch);
+        }
+      }
+    }
+  f32x4 acc[RT][NCT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NCT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#define KS_MF(Q)                                        \
+  _Pragma("unroll") for (int rt = 0; rt < RT; ++rt)     \
+  _Pragma("unroll") for (int t = 0; t < NCT; ++t) acc[rt][t] = mfma16(av[rt][j][ch].Q, bw[j][ch][t].Q, acc[rt][t]);
+#pragma unroll
+  for (int j = 0; j < SPW; ++j)
+#pragma unroll
+    for (int ch = 0; ch < CHO; ++ch) {
+      KS_MF(x) KS_MF(y) KS_MF(z) KS_MF(w)
+    }
+#undef KS_MF
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NCT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        part[((g * RT + rt) * 16 + 4 * kg + rr) * LDC + t * 16 + r16] = acc[rt][t][rr];
+  __syncthreads();
+  constexpr int N4 = RT * 16 * CIN / 4;
+  for (int q = threadIdx.x; q < N4; q += 64 * NSG) {
+    const int rt = q / (16 * CIN / 4), rem = q % (16 * CIN / 4);
+    const int row = rem / (CIN / 4), c4 = rem % (CIN / 4);
+    const long m = (rt0 + rt) * 16 + row;
+    if (m >= M) continue;
+    f32x4 v = part4[((0 * RT + rt) * 16 + row) * (LDC / 4) + c4];
+#pragma unroll
+    for (int gg = 1; gg < NSG; ++gg) v += part4[((gg * RT + rt) * 16 + row) * (LDC / 4) + c4];
+    if (a.elu_y) {
+      const f32x4 y = ld4(a.elu_y + m * CIN + 4 * c4);
+      v.x *= elu_grad_from_out(y.x);
+      v.y *= elu_grad_from_out(y.y);
+      v.z *= elu_grad_from_out(y.z);
+      v.w *= elu_grad_from_out(y.w);
+    }
+    st4(a.dx + m * CIN + 4 * c4, v);
+  }
+}
+
 // ------------------------------------------------------------------ host side
 // Geometry: slot groups and row tiles per workgroup.  More rows per
 // workgroup amortise the weight slices (each workgroup reads all of W once
@@ -247,6 +368,37 @@ int launch_fwd_ks(const FwdKsArgs& a, int cin, int cout, hipStream_t st) {
   SHAPE(32, 32) SHAPE(32, 64) SHAPE(64, 32) SHAPE(64, 64)
 #undef SHAPE
   return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: unsupported channels %d -> %d", cin, cout);
+}
+
+bool dx_ks_enabled(long total_src_rows, int cin, int cout) {
+  int n = 0, r = 0;
+  if (!parse_override(n, r)) return false;
+  return total_src_rows < kMaxRows && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
+}
+
+template <int CIN, int COUT>
+static int launch_dx_shape(const DxKsArgs& a, int nsg, int rt, hipStream_t st) {
+  const long n_rt = (a.total_rows + 15) / 16;
+#define KS(NSG_, RT_)                                                                                       \
+  if (nsg == NSG_ && rt == RT_) {                                                                           \
+    hipLaunchKernelGGL((conv_dx_ks<CIN, COUT, NSG_, RT_>), dim3((unsigned)((n_rt + RT_ - 1) / RT_)),          \
+                       dim3(64 * NSG_), 0, st, a);                                                          \
+    return launch_status("spiral_conv_bwd_data_ks");                                                        \
+  }
+  KS(3, 1) KS(3, 2) KS(3, 4) KS(9, 1) KS(9, 2) KS(9, 4)
+#undef KS
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_ks: bad geometry %d:%d", nsg, rt);
+}
+
+int launch_dx_ks(const DxKsArgs& a, int cin, int cout, hipStream_t st) {
+  if (a.total_rows <= 0 || a.total_rows >= kMaxRows) return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_ks: rows");
+  int nsg, rt;
+  pick(a.total_rows, cout, cin, nsg, rt);
+#define SHAPE(CI_, CO_) \
+  if (cin == CI_ && cout == CO_) return launch_dx_shape<CI_, CO_>(a, nsg, rt, st);
+  SHAPE(32, 32) SHAPE(32, 64) SHAPE(64, 32) SHAPE(64, 64)
+#undef SHAPE
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_ks: unsupported channels %d -> %d", cin, cout);
 }
 
 }  // namespace coarse

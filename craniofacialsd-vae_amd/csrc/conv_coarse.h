@@ -22,6 +22,8 @@ struct FwdKsArgs {
   int vsrc, rows, batch, n_coarse;
   long total_rows;      // batch * rows
   int xvm, yvm, elu;
+  long long* stamps;    // timing experiment: per-wave s_memrealtime stamps, or null
+  int dbg;              // timing experiment: 1 no W loads, 2 no x loads, 4 stamp after idx+W
 };
 
 struct DxKsArgs {
@@ -37,6 +39,7 @@ struct DxKsArgs {
 };
 
 bool fwd_ks_enabled(long total_rows, int cin, int cout);
+bool fwd_up_supported(long total_rows, int cin, int cout);
 int launch_fwd_ks(const FwdKsArgs& a, int cin, int cout, hipStream_t st);
 bool dx_ks_enabled(long total_src_rows, int cin, int cout);
 int launch_dx_ks(const DxKsArgs& a, int cin, int cout, hipStream_t st);

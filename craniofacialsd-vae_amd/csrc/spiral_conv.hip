@@ -2214,6 +2214,14 @@ static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const
 #define CFSD_LAT_DW_MAX CFSD_LAT_MAX_ROWS
 #endif
 
+// timing experiment hook (tools/kb_stamps.py): device buffer for per-wave stamps
+static void* cfsd_debug_stamps = nullptr;
+static int cfsd_debug_flags = 0;
+extern "C" void cfsd_debug_set_stamps(void* p, int flags) {
+  cfsd_debug_stamps = p;
+  cfsd_debug_flags = flags;
+}
+
 // coarse levels: slot groups in one workgroup, partials combined in LDS
 // (spiral_conv_coarse.hip)
 static int fwd_coarse(const float* x, int xvm, const int* idx, const float* w, const float* bias, float* y,
@@ -2231,7 +2239,43 @@ static int fwd_coarse(const float* x, int xvm, const int* idx, const float* w, c
   a.xvm = xvm;
   a.yvm = yvm;
   a.elu = act == CFSD_ACT_ELU;
+  a.stamps = (long long*)cfsd_debug_stamps;
+  a.dbg = cfsd_debug_flags;
   return coarse::launch_fwd_ks(a, cin, cout, st);
+}
+
+extern "C" int cfsd_spiral_conv_fwd_up_supported(int batch, int rows, int seq, int cin, int cout) {
+  if (batch <= 0 || rows <= 0 || seq != kSeq) return 0;
+  return coarse::fwd_up_supported((long)batch * rows, cin, cout) ? 1 : 0;
+}
+
+extern "C" int cfsd_spiral_conv_fwd_up(const float* xc, const int32_t* comp_col, const float* comp_val,
+                                       const int32_t* idx, const float* w, const float* bias, float* y, float* y_up,
+                                       int batch, int n_coarse, int rows, int seq, int cin, int cout, int act,
+                                       void* stream) {
+  int rc = check_conv_args(xc, idx, w, batch, n_coarse, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!comp_col || !comp_val || !y) return set_error(CFSD_EINVAL, "spiral_conv_fwd_up: null pointer");
+  if (act != CFSD_ACT_NONE && act != CFSD_ACT_ELU) return set_error(CFSD_EINVAL, "bad act %d", act);
+  if (!coarse::fwd_up_supported((long)batch * rows, cin, cout))
+    return set_error(CFSD_EINVAL, "spiral_conv_fwd_up: unsupported layer (%d x %d rows, %d -> %d)", batch, rows,
+                     cin, cout);
+  coarse::FwdKsArgs a{};
+  a.x = xc;
+  a.idx = idx;
+  a.w = w;
+  a.bias = bias;
+  a.y = y;
+  a.yup = y_up;
+  a.up_col = comp_col;
+  a.up_val = comp_val;
+  a.vsrc = rows;
+  a.rows = rows;
+  a.batch = batch;
+  a.n_coarse = n_coarse;
+  a.total_rows = (long)batch * rows;
+  a.elu = act == CFSD_ACT_ELU;
+  return coarse::launch_fwd_ks(a, cin, cout, (hipStream_t)stream);
 }
 
 template <int CIN, int COUT, int ACT>

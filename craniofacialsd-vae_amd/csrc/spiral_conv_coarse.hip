@@ -56,8 +56,13 @@ __device__ __forceinline__ f32x4 up_row4(const f32x4 x0, const f32x4 x1, const f
 // tiles x all COUT columns.  v_mfma_f32_16x16x4_f32 lane map as conv_fwd_lat:
 // lane (i = l & 15, kg = l >> 4) holds row i's 16-B chunks of channels
 // 16c + 4kg .. +3; B = W[o][s*CIN + 16c + 4kg + j] for the 4 MFMAs j of a chunk.
+// 9-wave workgroups place 3 waves on one SIMD: two co-resident workgroups
+// need <= 85 VGPRs (6 waves x 85 <= 512), else every second workgroup of a
+// CU waits for the first to exit (measured: D0 forward 267 workgroups, 11 of
+// them a whole wave-life late)
+constexpr int ks_min_waves(int nsg) { return nsg == 9 ? 6 : 2; }
 template <int CIN, int COUT, int NSG, int RT, int UP>
-__global__ __launch_bounds__(64 * NSG) void conv_fwd_ks(const FwdKsArgs a) {
+__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_fwd_ks(const FwdKsArgs a) {
   constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN, SPW = kSeq / NSG;
   constexpr int LDC = COUT + 4;  // partial row stride (kg rows land on distinct banks)
   static_assert(kSeq % NSG == 0, "slot groups");
@@ -67,6 +72,8 @@ __global__ __launch_bounds__(64 * NSG) void conv_fwd_ks(const FwdKsArgs a) {
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const long rt0 = (long)xcd_block() * RT;
   const long M = a.total_rows;
+  long long st_[6];
+  if (a.stamps) st_[0] = __builtin_amdgcn_s_memrealtime();
   const int nv_x = UP ? a.n_coarse : a.vsrc;
   const Lay lx = make_lay(a.xvm, a.batch, nv_x);
   // this lane's row in each tile (x's layout), its mesh / vertex and spiral
@@ -88,7 +95,12 @@ __global__ __launch_bounds__(64 * NSG) void conv_fwd_ks(const FwdKsArgs a) {
 #pragma unroll
     for (int c = 0; c < CH; ++c)
 #pragma unroll
-      for (int t = 0; t < NCT; ++t) bw[j][c][t] = ld4(wb + (long)t * 16 * K + (g * SPW + j) * CIN + 16 * c);
+      for (int t = 0; t < NCT; ++t)
+        bw[j][c][t] = (a.dbg & 1) ? f32x4{1.f, 1.f, 1.f, 1.f} : ld4(wb + (long)t * 16 * K + (g * SPW + j) * CIN + 16 * c);
+  if ((a.dbg & 4) && a.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_[1] = __builtin_amdgcn_s_memrealtime();
+  }
   f32x4 av[RT][SPW][CH];
   if constexpr (UP) {
     int cc[RT][SPW][3];
@@ -133,8 +145,14 @@ __global__ __launch_bounds__(64 * NSG) void conv_fwd_ks(const FwdKsArgs a) {
 #pragma unroll
       for (int j = 0; j < SPW; ++j)
 #pragma unroll
-        for (int c = 0; c < CH; ++c) av[rt][j][c] = ld4(xb + (long)src[rt][j] * lx.vs * CIN + 16 * c);
+        for (int c = 0; c < CH; ++c)
+          av[rt][j][c] = (a.dbg & 2) ? f32x4{1.f, 1.f, 1.f, 1.f} : ld4(xb + (long)src[rt][j] * lx.vs * CIN + 16 * c);
     }
+  }
+  if (a.stamps) {
+    if (!(a.dbg & 4)) st_[1] = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_[2] = __builtin_amdgcn_s_memrealtime();
   }
   f32x4 acc[RT][NCT];
 #pragma unroll
@@ -160,7 +178,9 @@ __global__ __launch_bounds__(64 * NSG) void conv_fwd_ks(const FwdKsArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
         part[((g * RT + rt) * 16 + 4 * kg + rr) * LDC + t * 16 + r16] = acc[rt][t][rr];
+  if (a.stamps) st_[3] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
+  if (a.stamps) st_[4] = __builtin_amdgcn_s_memrealtime();
   constexpr int N4 = RT * 16 * COUT / 4;
   for (int q = threadIdx.x; q < N4; q += 64 * NSG) {
     const int rt = q / (16 * COUT / 4), rem = q % (16 * COUT / 4);
@@ -185,6 +205,146 @@ __global__ __launch_bounds__(64 * NSG) void conv_fwd_ks(const FwdKsArgs a) {
     }
     st4(a.y + yo * COUT + 4 * c4, v);
   }
+  if (a.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_[5] = __builtin_amdgcn_s_memrealtime();
+    if (lane < 6) {
+      long long v = st_[0];
+#pragma unroll
+      for (int k = 1; k < 6; ++k) v = lane == k ? st_[k] : v;
+      a.stamps[((long)blockIdx.x * NSG + g) * 8 + lane] = v;
+    }
+  }
+}
+
+// Persistent form for the layers with several tiles per CU (the 17k-row
+// layers: E1, D1): one 9-wave workgroup per CU, wave g = slot g, its weight
+// slice loaded ONCE into VGPRs, then the workgroup walks a contiguous range
+// of 16-row tiles: the next tile's spiral row (UP: its composite up-sampling
+// row -- the 3 coarse columns / values of every spiral neighbour, a static
+// table) is in flight during this tile's MFMAs and its gathers during this
+// tile's combine; partials double-buffered in LDS (one barrier per tile).
+template <int CIN, int COUT, int UP>
+__global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
+  constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN, LDC = COUT + 4;
+  constexpr int PB = 9 * 16 * LDC;  // floats per partial buffer
+  __shared__ f32x4 part4[2 * PB / 4];
+  float* part = reinterpret_cast<float*>(part4);
+  const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long M = a.total_rows, n_rt = (M + 15) / 16;
+  const int nb = gridDim.x, blk = xcd_block();
+  const long t0 = n_rt * blk / nb, t1 = n_rt * (blk + 1) / nb;
+  const int nv_x = UP ? a.n_coarse : a.vsrc;
+  const Lay lx = make_lay(a.xvm, a.batch, nv_x);
+  f32x4 bw[CH][NCT];
+  const float* wb = a.w + (long)r16 * K + g * CIN + 4 * kg;
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int t = 0; t < NCT; ++t) bw[c][t] = ld4(wb + (long)t * 16 * K + 16 * c);
+  // per tile: this lane's mesh b and spiral neighbour (UP: its 3 taps)
+  struct Src {
+    int b, v;
+    int cc[UP ? 3 : 1];
+    float vv[UP ? 3 : 1];
+  };
+  auto load_src = [&](long tile, Src& sr) {
+    long m = tile * 16 + r16;
+    if (m >= M) m = M - 1;
+    int r;
+    split_row(m, a.xvm, a.batch, a.rows, sr.b, r);
+    if constexpr (UP) {
+      const long e = ((long)r * kSeq + g) * 3;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        sr.cc[k] = a.up_col[e + k];
+        sr.vv[k] = a.up_val[e + k];
+      }
+    } else {
+      sr.v = a.idx[r * kSeq + g];
+    }
+  };
+  auto load_x = [&](const Src& sr, f32x4 (&av)[CH]) {
+    const float* xb = a.x + (long)sr.b * lx.bs * CIN + 4 * kg;
+    if constexpr (UP) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const f32x4 x0 = ld4(xb + (long)sr.cc[0] * lx.vs * CIN + 16 * c);
+        const f32x4 x1 = ld4(xb + (long)sr.cc[1] * lx.vs * CIN + 16 * c);
+        const f32x4 x2 = ld4(xb + (long)sr.cc[2] * lx.vs * CIN + 16 * c);
+        av[c] = up_row4(x0, x1, x2, sr.vv[0], sr.vv[1], sr.vv[2]);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) av[c] = ld4(xb + (long)sr.v * lx.vs * CIN + 16 * c);
+    }
+  };
+  if (t0 >= t1) return;  // (grid <= tiles: never taken)
+  Src cur;
+  load_src(t0, cur);
+  f32x4 av[CH];
+  load_x(cur, av);
+  for (long tile = t0; tile < t1; ++tile) {
+    const bool more = tile + 1 < t1;  // uniform
+    Src nxt;
+    if (more) load_src(tile + 1, nxt);
+    f32x4 acc[NCT];
+#pragma unroll
+    for (int t = 0; t < NCT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].x, bw[c][t].x, acc[t]);
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].y, bw[c][t].y, acc[t]);
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].z, bw[c][t].z, acc[t]);
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].w, bw[c][t].w, acc[t]);
+    }
+    if constexpr (UP) {  // slot 0 = the vertex itself: the tile's up-sampled rows
+      if (g == 0 && a.yup) {
+        const long m = tile * 16 + r16;
+        if (m < M) {
+#pragma unroll
+          for (int c = 0; c < CH; ++c) st4(a.yup + m * CIN + 16 * c + 4 * kg, av[c]);
+        }
+      }
+    }
+    float* pb = part + ((tile - t0) & 1) * PB;
+#pragma unroll
+    for (int t = 0; t < NCT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) pb[(g * 16 + 4 * kg + rr) * LDC + t * 16 + r16] = acc[t][rr];
+    if (more) load_x(nxt, av);  // next tile's gathers in flight during the combine
+    __syncthreads();
+    const f32x4* pb4 = reinterpret_cast<const f32x4*>(pb);
+    constexpr int N4 = 16 * COUT / 4;
+    for (int q = threadIdx.x; q < N4; q += 576) {
+      const int row = q / (COUT / 4), c4 = q % (COUT / 4);
+      const long m = tile * 16 + row;
+      if (m >= M) continue;
+      f32x4 v = pb4[row * (LDC / 4) + c4];
+#pragma unroll
+      for (int gg = 1; gg < 9; ++gg) v += pb4[(gg * 16 + row) * (LDC / 4) + c4];
+      if (a.bias) v += ld4(a.bias + 4 * c4);
+      if (a.elu) {
+        v.x = elu_f(v.x);
+        v.y = elu_f(v.y);
+        v.z = elu_f(v.z);
+        v.w = elu_f(v.w);
+      }
+      long yo = m;
+      if (a.xvm != a.yvm) {
+        int bo, ro;
+        split_row(m, a.xvm, a.batch, a.rows, bo, ro);
+        yo = row_of(make_lay(a.yvm, a.batch, a.rows), bo, ro);
+      }
+      st4(a.y + yo * COUT + 4 * c4, v);
+    }
+    cur = nxt;
+  }
 }
 
 // Backward data, same geometry: a workgroup owns RT 16-row tiles of SOURCE
@@ -201,7 +361,7 @@ __device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, int off) {
 }
 
 template <int CIN, int COUT, int NSG, int RT>
-__global__ __launch_bounds__(64 * NSG) void conv_dx_ks(const DxKsArgs a) {
+__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_dx_ks(const DxKsArgs a) {
   constexpr int CHO = COUT / 16, NCT = CIN / 16, K = kSeq * CIN, SPW = kSeq / NSG;
   constexpr int LDC = CIN + 4, RB = COUT * (int)sizeof(float);
   static_assert(kSeq % NSG == 0, "slot groups");
@@ -332,12 +492,22 @@ bool fwd_ks_enabled(long total_rows, int cin, int cout) {
   return total_rows < kMaxRows && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
 }
 
+bool fwd_up_supported(long total_rows, int cin, int cout) {
+  int n = 0, r = 0;
+  if (!parse_override(n, r)) return false;
+  return total_rows < kMaxRows && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
+}
+
 static void pick(long total_rows, int cin, int cout, int& nsg, int& rt) {
   const long n_rt = (total_rows + 15) / 16;
   nsg = (cin * cout >= 64 * 32 || n_rt < 2048) ? 9 : 3;
   rt = 1;
   while (rt < 4 && (n_rt + 2 * rt - 1) / (2 * rt) * nsg >= 2048) rt *= 2;
   parse_override(nsg, rt);
+  if (nsg == 0) {
+    rt = rt < 1 ? 1 : (rt > 2 ? 2 : rt);
+    return;
+  }
   if (nsg != 3 && nsg != 9) nsg = 9;
   if (rt != 1 && rt != 2 && rt != 4) rt = 1;
 }
@@ -345,6 +515,11 @@ static void pick(long total_rows, int cin, int cout, int& nsg, int& rt) {
 template <int CIN, int COUT, int UP>
 static int launch_shape(const FwdKsArgs& a, int nsg, int rt, hipStream_t st) {
   const long n_rt = (a.total_rows + 15) / 16;
+  if (nsg == 0) {  // persistent: rt workgroups per CU
+    const long grid = n_rt < 256L * rt ? n_rt : 256L * rt;
+    hipLaunchKernelGGL((conv_fwd_pt<CIN, COUT, UP>), dim3((unsigned)grid), dim3(576), 0, st, a);
+    return launch_status("spiral_conv_fwd_pt");
+  }
 #define KS(NSG_, RT_)                                                                                 \
   if (nsg == NSG_ && rt == RT_) {                                                                     \
     hipLaunchKernelGGL((conv_fwd_ks<CIN, COUT, NSG_, RT_, UP>), dim3((unsigned)((n_rt + RT_ - 1) / RT_)), \
@@ -362,6 +537,7 @@ int launch_fwd_ks(const FwdKsArgs& a, int cin, int cout, hipStream_t st) {
   if (up && a.xvm) return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: fused up-sampling needs batch-major input");
   int nsg, rt;
   pick(a.total_rows, cin, cout, nsg, rt);
+  if (up && nsg != 0) nsg = 0, rt = 1;  // (the fused up-sampling exists in the persistent form only)
 #define SHAPE(CI_, CO_)                                                         \
   if (cin == CI_ && cout == CO_)                                                \
     return up ? launch_shape<CI_, CO_, 1>(a, nsg, rt, st) : launch_shape<CI_, CO_, 0>(a, nsg, rt, st);

@@ -180,6 +180,7 @@ class SDVAEEngine:
             self.lp_levels = {0, 1}
             self.params.shadow = torch.zeros(self.params.numel, dtype=torch.bfloat16, device=self.device)
         self.vertex_major = bool(vertex_major)
+        self.fuse_up = True  # coarse Deblocks: Pool(up) fused into the conv gather (False: separate SpMM)
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -580,12 +581,27 @@ class SDVAEEngine:
                        workspace=b.lin_ws)
         h = b.h
         for i, (cin, cout, lv, ui) in enumerate(S.dec_layers()):
-            self._spmm(T.up_csr[ui], h, T.n_verts[lv], out=b.dec_up[i], uniform=T.up_uniform[ui])
-            self._conv_fwd(b, b.dec_up[i], T.spiral[lv], f"de_layers.{i + 1}.conv.layer", ACT_ELU,
-                           b.dec_out[i])
+            wname = f"de_layers.{i + 1}.conv.layer"
+            if self._fused_up(b, h, i, lv, ui, cin, cout):  # Pool(up) inside the conv gather
+                ops.spiral_conv_fwd_up(h, T.up_comp[ui], T.spiral[lv], self.params.view(wname + ".weight"),
+                                       self.params.view(wname + ".bias"), ACT_ELU, out=b.dec_out[i],
+                                       up_out=b.dec_up[i])
+            else:
+                self._spmm(T.up_csr[ui], h, T.n_verts[lv], out=b.dec_up[i], uniform=T.up_uniform[ui])
+                self._conv_fwd(b, b.dec_up[i], T.spiral[lv], wname, ACT_ELU, b.dec_out[i])
             h = b.dec_out[i]
         n = S.n
         self._conv_fwd(b, h, T.spiral[0], f"de_layers.{n + 1}.layer", ACT_NONE, b.out)
+
+    def _fused_up(self, b, h, i, lv, ui, cin, cout):
+        """The coarse Deblocks (fp32 batch-major, uniform 3-entry up rows,
+        spirals starting at their own vertex) fuse Pool(up) into the conv's
+        gather (cfsd_spiral_conv_fwd_up: bit-identical up-sampled rows, one
+        launch instead of two)."""
+        T = self.topo
+        return (self.fuse_up and lv not in b.xl and T.up_comp[ui] is not None
+                and self._plain(h, b.dec_up[i], b.dec_out[i])
+                and ops.spiral_conv_fwd_up_supported(b.bsz, T.n_verts[lv], T.seq[lv], cin, cout))
 
     def losses_fwd(self, b, acc=None, finalize=True):
         T = self.topo

@@ -412,6 +412,31 @@ def swap_features(x_all, batch_idx, region_mask, key, bs, out=None):
     return y
 
 
+def spiral_conv_fwd_up_supported(bsz, rows, seq, cin, cout):
+    return bool(_abi.lib().cfsd_spiral_conv_fwd_up_supported(bsz, rows, seq, cin, cout))
+
+
+def spiral_conv_fwd_up(xc, comp, idx, w, bias, act, out, up_out=None):
+    """SpiralDeblock forward (``model.py:80-82``) with Pool(up) fused into
+    the gather: ``comp`` = the level's composite up table
+    (``DeviceTopology.up_comp``); ``up_out`` receives Pool(xc, up) (the
+    input the weight gradient reads), bit-identical to :func:`spmm`."""
+    bsz, n_coarse, cin = xc.shape
+    rows, seq = idx.shape
+    cout = w.shape[0]
+    _need(xc, None, name="xc")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(comp[0], (rows, seq, 3), torch.int32, "comp_col")
+    _need(comp[1], (rows, seq, 3), torch.float32, "comp_val")
+    _need(w, (cout, seq * cin), name="w")
+    _need(out, (bsz, rows, cout), name="out")
+    if up_out is not None:
+        _need(up_out, (bsz, rows, cin), name="up_out")
+    call("cfsd_spiral_conv_fwd_up", ptr(xc), ptr(comp[0]), ptr(comp[1]), ptr(idx), ptr(w), ptr(bias), ptr(out),
+         ptr(up_out), bsz, n_coarse, rows, seq, cin, cout, int(act), stream_ptr())
+    return out
+
+
 def gather_meshes(x_all, batch_idx, bs, out=None):
     """The un-swapped batch of a ``swap_features: False`` configuration
     (``data_loading.py:38, 81-82``: MeshCollater without a feature swapper):

@@ -227,6 +227,24 @@ class DeviceTopology:
             self.upT_order.append(_dev(sched, self.device) if sched is not None else None)
             self.upT_sched.append(tuple(_dev(a, self.device) for a in scheduled_csr(*upT, sched))
                                   if sched is not None else None)
+        # composite up-sampling rows of every spiral position (the Deblock
+        # forward's fused Pool(up) gather, cfsd_spiral_conv_fwd_up): for up
+        # matrix ui (level ui+1 -> level ui, uniform 3-entry rows) and spiral
+        # position (r, s) of level ui, the 3 columns / values of up row
+        # spiral[r, s], in the row's CSR (file) order; None when the rows are
+        # not uniform or a spiral does not start at its own vertex
+        self.up_comp = []
+        for ui in range(self.n_levels):
+            sp = self.np_spirals[ui]
+            ok = (self.up_uniform[ui] == 3 and sp.shape[0] == self.up_csr[ui][0].numel() - 1
+                  and np.array_equal(sp[:, 0], np.arange(sp.shape[0])))
+            if not ok:
+                self.up_comp.append(None)
+                continue
+            ucol = self.up_csr[ui][1].cpu().numpy().reshape(-1, 3)
+            uval = self.up_csr[ui][2].cpu().numpy().reshape(-1, 3)
+            self.up_comp.append((_dev(_i32(ucol[sp]), self.device),
+                                 _dev(np.ascontiguousarray(uval[sp], np.float32), self.device)))
         self.lap_csr = self.lapT_csr = None
         if lap is not None:
             lr, lc, lv, lshape = lap

@@ -242,6 +242,20 @@ int cfsd_swap_features(const float* x, const int32_t* batch_idx, const uint8_t* 
 int cfsd_swap_features_x(const float* x, const int32_t* batch_idx, const uint8_t* region_mask,
                          const int32_t* key, float* out, int out_dt, int bs, int nv, int c,
                          int n_meshes, int n_regions, void* stream);
+/* SpiralDeblock forward with the Pool(up) fused into the gather (ABI 4.4;
+ * model.py:80-82: x_up = Pool(xc, up) then SpiralConv(x_up) + ELU): the input
+ * row of spiral position (r, s) is sum_k comp_val[(r*9+s)*3+k] *
+ * xc[b, comp_col[(r*9+s)*3+k], :] -- the composite table of a uniform
+ * 3-entry up matrix (topology.up_comp), summed ((0 + x0 v0) + x1 v1) + x2 v2
+ * exactly as cfsd_spmm_uniform (bit-identical up-sampled rows); idx [rows, 9]
+ * with idx[r][0] == r, and y_up (optional) receives the up-sampled input
+ * [batch, rows, cin] the weight gradient reads.  xc [batch, n_coarse, cin],
+ * y [batch, rows, cout], batch-major fp32.  Coarse layers only:
+ * cfsd_spiral_conv_fwd_up_supported() says which. */
+int cfsd_spiral_conv_fwd_up_supported(int batch, int rows, int seq, int cin, int cout);
+int cfsd_spiral_conv_fwd_up(const float* xc, const int32_t* comp_col, const float* comp_val, const int32_t* idx,
+                            const float* w, const float* bias, float* y, float* y_up, int batch, int n_coarse,
+                            int rows, int seq, int cin, int cout, int act, void* stream);
 /* The un-swapped batch of a swap_features: False configuration
  * (data_loading.py:38, 81-82: MeshCollater without a feature_swapper):
  * out[b] = x[batch_idx[b]], b < bs; out_dt = CFSD_DT_F32 [| CFSD_VM] (ABI 4.4).

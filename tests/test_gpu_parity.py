@@ -850,3 +850,47 @@ def test_rowsub_data_bf16_storage(dtopo, level, cout):
     ops.spiral_conv_bwd_rowsub(x, dtopo.enc_rows[level], dpre, dtopo.enc_flat[level], w, None, None, dxf,
                                elu_y=ey16.float())
     assert torch.equal(dxf, d32)
+
+
+@pytest.mark.parametrize("i", [0, 1])
+def test_deblock_fused_up_matches_spmm_then_conv(dtopo, i):
+    """cfsd_spiral_conv_fwd_up (coarse Deblock: Pool(up) inside the conv
+    gather, model.py:80-82) == cfsd_spmm_uniform then the conv: the
+    up-sampled input bit for bit, the ELU output within 1e-5 (same slot
+    partials, possibly another slot grouping)."""
+    eng = make_engine(dtopo, recipe.golden_weights(), bs=4)
+    cin, cout, lv, ui = eng.spec.dec_layers()[i]
+    assert dtopo.up_comp[ui] is not None
+    assert ops.spiral_conv_fwd_up_supported(16, dtopo.n_verts[lv], 9, cin, cout)
+    g = torch.Generator(device=DEV).manual_seed(i)
+    xc = torch.randn(16, dtopo.n_verts[lv + 1], cin, device=DEV, generator=g)
+    w, bias = eng._dec_w(i)
+    up = ops.spmm(dtopo.up_csr[ui], xc, dtopo.n_verts[lv], uniform=dtopo.up_uniform[ui])
+    ref = ops.spiral_conv_fwd(up, dtopo.spiral[lv], w, bias, 1)
+    y = torch.empty(16, dtopo.n_verts[lv], cout, device=DEV)
+    yup = torch.full((16, dtopo.n_verts[lv], cin), float("nan"), device=DEV)
+    ops.spiral_conv_fwd_up(xc, dtopo.up_comp[ui], dtopo.spiral[lv], w, bias, 1, out=y, up_out=yup)
+    assert torch.equal(yup, up)
+    close(y, ref, 1e-5, "fused Deblock forward")
+    # and against the oracle (float64 of the same up-sampled input)
+    sp = dtopo.spiral[lv].long().cpu()
+    r64 = O.spiral_conv(up.double().cpu(), sp, w.double().cpu(), bias.double().cpu())
+    close(y, torch.nn.functional.elu(r64), 1e-5, "fused Deblock forward vs float64")
+
+
+def test_engine_forward_fused_up_equals_unfused(dtopo):
+    """The step's forward with the fused coarse Deblocks equals the unfused
+    forward (reconstruction within 1e-5, the decoder's up-sampled inputs
+    bit-identical)."""
+    outs = []
+    x = torch.from_numpy(recipe.normalized_meshes(8)).to(DEV)
+    for fuse in (True, False):
+        eng = make_engine(dtopo, recipe.golden_weights())
+        eng.fuse_up = fuse
+        b = eng.set_batch(x)
+        eng.forward(b, train=False)
+        torch.cuda.synchronize()
+        outs.append((b.out.clone(), [u.clone() for u in b.dec_up[:2]]))
+    close(outs[0][0], outs[1][0], 1e-5, "reconstruction")
+    for a, c in zip(outs[0][1], outs[1][1]):
+        assert torch.equal(a, c)

@@ -66,10 +66,8 @@ def relabel_npz(npz, orders):
     return out
 
 
-def main():
-    names = sys.argv[1:] or ["fwd_d3", "dx_d3", "dw_d3", "dout_fwd", "dout_dx", "dout_dw", "spmm_up0",
-                             "spmm_up0T", "e0_fwd", "e0_dw"]
-    iters = int(os.environ.get("KB_ITERS", "50"))
+def build_cases(names=()):
+    names = list(names)
     npz = dict(np.load(os.path.join(ROOT, "tests", "golden", "topology_craniofacial.npz")))
     if os.environ.get("KB_REORDER"):  # locality (RCM) vertex order on every level
         n = int(npz["n_levels"])
@@ -305,6 +303,14 @@ def main():
     if "step" in names:
         eng.set_batch(b.x, key_index=3)
         cases["step"] = lambda: eng.train_step_on(b)
+    return cases, names, b
+
+
+def main():
+    names = sys.argv[1:] or ["fwd_d3", "dx_d3", "dw_d3", "dout_fwd", "dout_dx", "dout_dw", "spmm_up0",
+                             "spmm_up0T", "e0_fwd", "e0_dw"]
+    iters = int(os.environ.get("KB_ITERS", "50"))
+    cases, names, b = build_cases(names)
     if os.environ.get("KB_STAMPS"):
         for n in names:
             b.ws.zero_()

@@ -281,6 +281,8 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
     }
   };
   if (t0 >= t1) return;  // (grid <= tiles: never taken)
+  long long st_[6] = {0, 0, 0, 0, 0, 0};
+  if (a.stamps) st_[0] = __builtin_amdgcn_s_memrealtime();
   Src cur;
   load_src(t0, cur);
   f32x4 av[CH];
@@ -289,6 +291,12 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
     const bool more = tile + 1 < t1;  // uniform
     Src nxt;
     if (more) load_src(tile + 1, nxt);
+    long long ta = 0;
+    if (a.stamps) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ta = __builtin_amdgcn_s_memrealtime();
+      if (tile == t0) st_[1] = ta;
+    }
     f32x4 acc[NCT];
 #pragma unroll
     for (int t = 0; t < NCT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -318,7 +326,14 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) pb[(g * 16 + 4 * kg + rr) * LDC + t * 16 + r16] = acc[t][rr];
     if (more) load_x(nxt, av);  // next tile's gathers in flight during the combine
+    long long tb = 0;
+    if (a.stamps) tb = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
+    if (a.stamps) {
+      const long long tc = __builtin_amdgcn_s_memrealtime();
+      st_[2] += tb - ta;  // MFMA + partial store
+      st_[3] += tc - tb;  // barrier wait
+    }
     const f32x4* pb4 = reinterpret_cast<const f32x4*>(pb);
     constexpr int N4 = 16 * COUT / 4;
     for (int q = threadIdx.x; q < N4; q += 576) {
@@ -344,6 +359,17 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
       st4(a.y + yo * COUT + 4 * c4, v);
     }
     cur = nxt;
+  }
+  if (a.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_[4] = __builtin_amdgcn_s_memrealtime();
+    st_[5] = t1 - t0;
+    if (lane < 6) {
+      long long v = st_[0];
+#pragma unroll
+      for (int k = 1; k < 6; ++k) v = lane == k ? st_[k] : v;
+      a.stamps[((long)blockIdx.x * 9 + g) * 8 + lane] = v;
+    }
   }
 }
 
@@ -473,10 +499,11 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_dx_ks(const 
 // workgroup amortise the weight slices (each workgroup reads all of W once
 // from L2); more slot groups shorten each wave's MFMA chain.  Picked so the
 // grid holds >= ~2k waves (2 per SIMD) where the layer allows.
+template <int DX = 0>
 static bool parse_override(int& nsg, int& rt) {
   static int cached = -2, cn = 0, cr = 0;
   if (cached == -2) {
-    const char* e = getenv("CFSD_KS");
+    const char* e = getenv(DX ? "CFSD_KSDX" : "CFSD_KS");
     cached = (e && sscanf(e, "%d:%d", &cn, &cr) == 2) ? 1 : (e && e[0] == '0' ? 0 : -1);
   }
   if (cached == 1) {
@@ -498,12 +525,27 @@ bool fwd_up_supported(long total_rows, int cin, int cout) {
   return total_rows < kMaxRows && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
 }
 
+template <int DX = 0>
 static void pick(long total_rows, int cin, int cout, int& nsg, int& rt) {
+  // measured (kbench, rocprofv3 kernel trace, batch 16): the ~1k-tile layers
+  // (E1, D1) on the persistent form (E1 32->32 at 2 workgroups per CU 11.4 us
+  // vs 11.3-13.8 us slot-group grids and 16.6 us conv_fwd_lat; D1 64->32 at 1
+  // per CU 15.5 vs 18.5-22 and 22.2 us conv_fwd_mfma + combine), the <= 267-tile
+  // layers (E2, E3, D0) one 9-wave workgroup per tile (E2 6.8 / E3 6.6 vs 7.7 /
+  // 7.4 us); the data gradient: 9 slot groups, 2 tiles per workgroup at D0
+  // (13.7 vs 15.3 us), 3 slot groups at D1 (17.4 vs 19.9 us)
   const long n_rt = (total_rows + 15) / 16;
-  nsg = (cin * cout >= 64 * 32 || n_rt < 2048) ? 9 : 3;
-  rt = 1;
-  while (rt < 4 && (n_rt + 2 * rt - 1) / (2 * rt) * nsg >= 2048) rt *= 2;
-  parse_override(nsg, rt);
+  if (DX) {
+    nsg = n_rt >= 512 ? 3 : 9;
+    rt = n_rt >= 512 ? 1 : 2;
+  } else if (n_rt >= 512) {
+    nsg = 0;
+    rt = cin * cout >= 64 * 32 ? 1 : 2;
+  } else {
+    nsg = 9;
+    rt = 1;
+  }
+  parse_override<DX>(nsg, rt);
   if (nsg == 0) {
     rt = rt < 1 ? 1 : (rt > 2 ? 2 : rt);
     return;
@@ -548,7 +590,7 @@ int launch_fwd_ks(const FwdKsArgs& a, int cin, int cout, hipStream_t st) {
 
 bool dx_ks_enabled(long total_src_rows, int cin, int cout) {
   int n = 0, r = 0;
-  if (!parse_override(n, r)) return false;
+  if (!parse_override<1>(n, r)) return false;
   return total_src_rows < kMaxRows && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
 }
 
@@ -569,7 +611,8 @@ static int launch_dx_shape(const DxKsArgs& a, int nsg, int rt, hipStream_t st) {
 int launch_dx_ks(const DxKsArgs& a, int cin, int cout, hipStream_t st) {
   if (a.total_rows <= 0 || a.total_rows >= kMaxRows) return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_ks: rows");
   int nsg, rt;
-  pick(a.total_rows, cout, cin, nsg, rt);
+  pick<1>(a.total_rows, cout, cin, nsg, rt);
+  if (nsg == 0) nsg = 9, rt = 1;  // (no persistent data-gradient form yet)
 #define SHAPE(CI_, CO_) \
   if (cin == CI_ && cout == CO_) return launch_dx_shape<CI_, CO_>(a, nsg, rt, st);
   SHAPE(32, 32) SHAPE(32, 64) SHAPE(64, 32) SHAPE(64, 64)

@@ -152,7 +152,8 @@ def test_spiral_conv_bwd_paired_bit_exact(dtopo, table, level, cin, cout, bsz):
     idx = dtopo.spiral[level] if table == "dec" else dtopo.enc_rows[level]
     inv = dtopo.spiral_inv[level] if table == "dec" else dtopo.enc_inv[level]
     vsrc, rows = dtopo.n_verts[level], idx.shape[0]
-    assert ops.spiral_conv_bwd_paired(bsz, vsrc, rows, 9, cin, cout)
+    if not ops.spiral_conv_bwd_paired(bsz, vsrc, rows, 9, cin, cout):
+        pytest.skip("coarse layer: dx on the slot-group kernel (cfsd_spiral_conv_bwd does not pair)")
     g = torch.Generator(device=DEV).manual_seed(level * 10 + cin + cout + bsz)
     x = torch.randn(bsz, vsrc, cin, device=DEV, generator=g)
     y = torch.nn.functional.elu(x)

@@ -36,6 +36,15 @@ for name in sys.argv[1:]:
         torch.cuda.synchronize()
         lib.cfsd_debug_set_stamps(None, 0)
         st = buf.view(-1, 8).cpu().numpy()
+        if os.environ.get("KB_PT"):  # persistent kernel: start, first loads landed, sum mfma, sum barrier, end, tiles
+            st = st[st[:, 0] != 0][:, :6].astype(np.float64)
+            t0 = st[:, 0].min()
+            print(f"{name} rep{rep}: waves {len(st)} span {(st[:, 4].max() - t0) / 100:.2f} us | start spread "
+                  f"{(st[:, 0].max() - t0) / 100:.2f} | first loads {(st[:, 1] - st[:, 0]).mean() / 100:.2f} | tiles/wg "
+                  f"{st[:, 5].mean():.2f} | per tile: mfma+lds {(st[:, 2] / st[:, 5]).mean() / 100:.2f} barrier "
+                  f"{(st[:, 3] / st[:, 5]).mean() / 100:.2f} | loop total {(st[:, 4] - st[:, 1]).mean() / 100:.2f} "
+                  f"-> per tile {((st[:, 4] - st[:, 1]) / st[:, 5]).mean() / 100:.2f}", flush=True)
+            continue
         st = st[st[:, 0] != 0][:, :6].astype(np.float64) / 100.0  # us
         t0 = st[:, 0].min()
         st -= t0

@@ -10,6 +10,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace cfsd {
 
+constexpr int kSeq = 9;  // spiral length of every configuration (craniofacial/body/default.yaml)
+
 // XCD-aware persistent tile schedule.  Blocks b and b+8 share an XCD (and
 // its 4 MB L2) under the dispatcher's round-robin placement, so the blocks of
 // group g = b % G sweep ONE contiguous 1/G of the tile range: neighbouring

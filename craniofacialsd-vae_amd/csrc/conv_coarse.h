@@ -3,12 +3,16 @@
 #include "cfsd_common.h"
 
 namespace cfsd {
+struct DwLatArgs;  // conv_lat.h
 namespace coarse {
 
 // Layers below this many rows (batch x output vertices) take the slot-group
 // kernels: the coarse levels of the hierarchy, where one wave per tile and
 // all nine slots cannot fill the chip.
 constexpr long kMaxRows = 24576;
+// "few-tile" layers (<= ~2 16-row tiles per CU): the fused up-sampling and the
+// slot-group data gradient apply below this many tiles
+constexpr long kMaxTilesFew = 512;
 
 struct FwdKsArgs {
   const float* x;       // input rows; UP: the coarse tensor [batch, n_coarse, CIN] (batch-major)
@@ -43,6 +47,8 @@ bool fwd_up_supported(long total_rows, int cin, int cout);
 int launch_fwd_ks(const FwdKsArgs& a, int cin, int cout, hipStream_t st);
 bool dx_ks_enabled(long total_src_rows, int cin, int cout);
 int launch_dx_ks(const DxKsArgs& a, int cin, int cout, hipStream_t st);
+// dx (as launch_dx_ks) + dW slabs (conv_dw_lat_body, dw_tasks = chunks x units) in one launch
+int launch_bwd_ks_pair(const DxKsArgs& a, const DwLatArgs& d, long dw_tasks, int cin, int cout, hipStream_t st);
 
 }  // namespace coarse
 }  // namespace cfsd

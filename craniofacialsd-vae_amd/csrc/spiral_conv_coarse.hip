@@ -25,11 +25,10 @@
 
 #include "cfsd_common.h"
 #include "conv_coarse.h"
+#include "conv_lat.h"
 
 namespace cfsd {
 namespace coarse {
-
-constexpr int kSeq = 9;
 
 // x_up chunk of fine vertex v for mesh b: the three taps of up row v
 // (spmm_uniform_k's order and rounding)
@@ -387,7 +386,7 @@ __device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, int off) {
 }
 
 template <int CIN, int COUT, int NSG, int RT>
-__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_dx_ks(const DxKsArgs a) {
+__device__ __forceinline__ void conv_dx_ks_body(int vb, int vnb, const DxKsArgs& a) {
   constexpr int CHO = COUT / 16, NCT = CIN / 16, K = kSeq * CIN, SPW = kSeq / NSG;
   constexpr int LDC = CIN + 4, RB = COUT * (int)sizeof(float);
   static_assert(kSeq % NSG == 0, "slot groups");
@@ -395,7 +394,7 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_dx_ks(const 
   float* part = reinterpret_cast<float*>(part4);
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const long rt0 = (long)xcd_block() * RT;
+  const long rt0 = (long)xcd_block_of(vb, vnb) * RT;
   const long M = a.total_rows;  // batch * vsrc
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.dpre), 0,
                                                       (int)((long)a.batch * a.rows * RB), 0x00020000);
@@ -493,6 +492,34 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_dx_ks(const 
     st4(a.dx + m * CIN + 4 * c4, v);
   }
 }
+template <int CIN, int COUT, int NSG, int RT>
+__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_dx_ks(const DxKsArgs a) {
+  conv_dx_ks_body<CIN, COUT, NSG, RT>(blockIdx.x, gridDim.x, a);
+}
+
+// The data gradient and the weight-gradient slabs of one coarse conv in ONE
+// launch (they are independent and each alone leaves most of the chip idle):
+// workgroups alternate between the two halves while both last; the dW half
+// is conv_dw_lat_body with NSG waves per workgroup (same slabs, same values).
+template <int CIN, int COUT, int NSG, int RT>
+__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_bwd_ks_pair(const DxKsArgs a, const DwLatArgs d,
+                                                                              int nb_dx) {
+  const int bid = blockIdx.x, both = 2 * min(nb_dx, d.nb);
+  bool is_dx;
+  int vb;
+  if (bid < both) {
+    is_dx = (bid & 1) == 0;
+    vb = bid >> 1;
+  } else {
+    is_dx = nb_dx > d.nb;
+    vb = bid - both + both / 2;
+  }
+  if (is_dx)
+    conv_dx_ks_body<CIN, COUT, NSG, RT>(vb, nb_dx, a);
+  else
+    conv_dw_lat_body<CIN, COUT, NSG>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows, d.total_rows,
+                                     d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm);
+}
 
 // ------------------------------------------------------------------ host side
 // Geometry: slot groups and row tiles per workgroup.  More rows per
@@ -519,10 +546,12 @@ bool fwd_ks_enabled(long total_rows, int cin, int cout) {
   return total_rows < kMaxRows && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
 }
 
+// (fused only on the few-tile layers: D0 17.5 us fused vs 4.9 + 13.9 us; on D1
+// the three-tap gathers cost more than the launch they save, 24.6 vs 6.4 + 15.5 us)
 bool fwd_up_supported(long total_rows, int cin, int cout) {
   int n = 0, r = 0;
   if (!parse_override(n, r)) return false;
-  return total_rows < kMaxRows && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
+  return total_rows < kMaxTilesFew * 16 && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
 }
 
 template <int DX = 0>
@@ -588,10 +617,40 @@ int launch_fwd_ks(const FwdKsArgs& a, int cin, int cout, hipStream_t st) {
   return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: unsupported channels %d -> %d", cin, cout);
 }
 
+// (the ~1k-tile layers keep conv_bwd_lat_pair: D1 dx + dW 34.9 us paired vs
+// 17.2 + 19.6 us on the slot-group dx and a separate dW)
 bool dx_ks_enabled(long total_src_rows, int cin, int cout) {
   int n = 0, r = 0;
   if (!parse_override<1>(n, r)) return false;
-  return total_src_rows < kMaxRows && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
+  return total_src_rows < kMaxTilesFew * 16 && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
+}
+
+template <int CIN, int COUT>
+static int launch_pair_shape(const DxKsArgs& a, DwLatArgs d, long dw_tasks, int nsg, int rt, hipStream_t st) {
+  const long n_rt = (a.total_rows + 15) / 16;
+#define KS(NSG_, RT_)                                                                                     \
+  if (nsg == NSG_ && rt == RT_) {                                                                         \
+    const int nb_dx = (int)((n_rt + RT_ - 1) / RT_);                                                      \
+    d.nb = (int)((dw_tasks + NSG_ - 1) / NSG_);                                                           \
+    hipLaunchKernelGGL((conv_bwd_ks_pair<CIN, COUT, NSG_, RT_>), dim3((unsigned)(nb_dx + d.nb)), dim3(64 * NSG_), \
+                       0, st, a, d, nb_dx);                                                               \
+    return launch_status("spiral_conv_bwd_ks_pair");                                                      \
+  }
+  KS(3, 1) KS(3, 2) KS(9, 1) KS(9, 2)
+#undef KS
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_ks_pair: bad geometry %d:%d", nsg, rt);
+}
+
+int launch_bwd_ks_pair(const DxKsArgs& a, const DwLatArgs& d, long dw_tasks, int cin, int cout, hipStream_t st) {
+  if (a.total_rows <= 0 || a.total_rows >= kMaxRows) return set_error(CFSD_EINVAL, "spiral_conv_bwd_ks_pair: rows");
+  int nsg, rt;
+  pick<1>(a.total_rows, cout, cin, nsg, rt);
+  if (nsg == 0 || rt > 2) nsg = 9, rt = 1;
+#define SHAPE(CI_, CO_) \
+  if (cin == CI_ && cout == CO_) return launch_pair_shape<CI_, CO_>(a, d, dw_tasks, nsg, rt, st);
+  SHAPE(32, 32) SHAPE(32, 64) SHAPE(64, 32) SHAPE(64, 64)
+#undef SHAPE
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_ks_pair: unsupported channels %d -> %d", cin, cout);
 }
 
 template <int CIN, int COUT>

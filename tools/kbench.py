@@ -149,6 +149,8 @@ def build_cases(names=()):
     cases["dw_d0"] = lambda: ops.spiral_conv_bwd_weight(b.dec_up[0], T.spiral[3], b.dpre_dec[0],
                                                        P.gview("de_layers.1.conv.layer.weight"),
                                                        P.gview("de_layers.1.conv.layer.bias"), b.ws)
+    cases["pair_d0"] = lambda: ops.spiral_conv_bwd(b.dec_up[0], T.spiral[3], b.dpre_dec[0], T.spiral_inv[3], w0,
+                                                   None, None, dx=b.g_dec_up[0], workspace=b.ws_dw[("dec", 0)])
     cases["fwd_d1"] = lambda: ops.spiral_conv_fwd(b.dec_up[1], T.spiral[2], w1, b1, 1, out=b.dec_out[1], workspace=b.ws)
     cases["pair_d1"] = lambda: ops.spiral_conv_bwd(b.dec_up[1], T.spiral[2], b.dpre_dec[1], T.spiral_inv[2], w1,
                                                    P.gview("de_layers.2.conv.layer.weight"),

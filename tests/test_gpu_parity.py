@@ -853,8 +853,8 @@ def test_rowsub_data_bf16_storage(dtopo, level, cout):
     assert torch.equal(dxf, d32)
 
 
-@pytest.mark.parametrize("i", [0, 1])
-def test_deblock_fused_up_matches_spmm_then_conv(dtopo, i):
+@pytest.mark.parametrize("i,bsz", [(0, 16), (0, 3), (1, 4)])
+def test_deblock_fused_up_matches_spmm_then_conv(dtopo, i, bsz):
     """cfsd_spiral_conv_fwd_up (coarse Deblock: Pool(up) inside the conv
     gather, model.py:80-82) == cfsd_spmm_uniform then the conv: the
     up-sampled input bit for bit, the ELU output within 1e-5 (same slot
@@ -862,14 +862,16 @@ def test_deblock_fused_up_matches_spmm_then_conv(dtopo, i):
     eng = make_engine(dtopo, recipe.golden_weights(), bs=4)
     cin, cout, lv, ui = eng.spec.dec_layers()[i]
     assert dtopo.up_comp[ui] is not None
-    assert ops.spiral_conv_fwd_up_supported(16, dtopo.n_verts[lv], 9, cin, cout)
-    g = torch.Generator(device=DEV).manual_seed(i)
-    xc = torch.randn(16, dtopo.n_verts[lv + 1], cin, device=DEV, generator=g)
+    assert ops.spiral_conv_fwd_up_supported(bsz, dtopo.n_verts[lv], 9, cin, cout)
+    # (the fused form covers the few-tile layers only: D1 at batch 16 = 1065 tiles is not fused)
+    assert not ops.spiral_conv_fwd_up_supported(16, dtopo.n_verts[2], 9, 64, 32)
+    g = torch.Generator(device=DEV).manual_seed(i + bsz)
+    xc = torch.randn(bsz, dtopo.n_verts[lv + 1], cin, device=DEV, generator=g)
     w, bias = eng._dec_w(i)
     up = ops.spmm(dtopo.up_csr[ui], xc, dtopo.n_verts[lv], uniform=dtopo.up_uniform[ui])
     ref = ops.spiral_conv_fwd(up, dtopo.spiral[lv], w, bias, 1)
-    y = torch.empty(16, dtopo.n_verts[lv], cout, device=DEV)
-    yup = torch.full((16, dtopo.n_verts[lv], cin), float("nan"), device=DEV)
+    y = torch.empty(bsz, dtopo.n_verts[lv], cout, device=DEV)
+    yup = torch.full((bsz, dtopo.n_verts[lv], cin), float("nan"), device=DEV)
     ops.spiral_conv_fwd_up(xc, dtopo.up_comp[ui], dtopo.spiral[lv], w, bias, 1, out=y, up_out=yup)
     assert torch.equal(yup, up)
     close(y, ref, 1e-5, "fused Deblock forward")

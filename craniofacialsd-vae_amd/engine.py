@@ -181,12 +181,6 @@ class SDVAEEngine:
             self.params.shadow = torch.zeros(self.params.numel, dtype=torch.bfloat16, device=self.device)
         self.vertex_major = bool(vertex_major)
         self.fuse_up = True  # coarse Deblocks: Pool(up) fused into the conv gather (False: separate SpMM)
-        # coarse-level weight gradients (levels >= 2 and the Enblocks after
-        # level 0's) on a side stream: they feed nothing but the final
-        # reduce, so they overlap the latency-bound data-gradient chain
-        self.side_dw = True
-        self._side = None
-        self._side_pending = False
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -438,11 +432,6 @@ class SDVAEEngine:
                 need = ops.spiral_conv_bwd_data_rowsub_workspace(bsz, nv[lv + 1], T.seq[lv], cin)
                 b.rowsub_x[lv] = need > 0
                 ws = max(ws, need)
-        # side-stream weight gradients: the Enblock data gradient runs alone
-        # (dG at the kept rows in b.ws, then the flat gather)
-        for (cin, cout, lv) in S.enc_layers():
-            if lv > 0 and T.enc_select[lv]:
-                ws = max(ws, ops.spiral_conv_bwd_data_rowsub_workspace(bsz, nv[lv + 1], T.seq[lv], cin))
         b.ws = torch.empty(ws // 4 + 64, dtype=torch.float32, device=dev)
         # weight-gradient partials: one region per layer, all reduced by ONE
         # cfsd_dw_reduce_batch launch at the end of the backward
@@ -653,28 +642,6 @@ class SDVAEEngine:
         if bucket_hook is not None:
             bucket_hook(self.params.grad[:self.enc_conv_numel()])
 
-    def _coarse_side(self, b, lv):
-        """Weight gradient of a level-``lv`` conv goes to the side stream (fp32
-        batch-major coarse levels on a CUDA device)."""
-        return self.side_dw and lv not in b.xl and lv >= 1 and self.device.type == "cuda"
-
-    def _on_side(self, fn):
-        """Run ``fn``'s launches on the side stream, ordered after everything
-        already queued on the current stream (a fork edge in a captured graph)."""
-        main = torch.cuda.current_stream(self.device)
-        if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
-        self._side.wait_stream(main)
-        with torch.cuda.stream(self._side):
-            r = fn()
-        self._side_pending = True
-        return r
-
-    def _join_side(self):
-        if self._side_pending:
-            torch.cuda.current_stream(self.device).wait_stream(self._side)
-            self._side_pending = False
-
     def backward_head(self, b, split=False):
         """Losses -> decoder -> latent head -> encoder Linear.  ``split``:
         reduce the decoder conv weight gradients here (their bucket is then
@@ -728,12 +695,6 @@ class SDVAEEngine:
                 else:
                     ops.spiral_conv_bwd_data_x(b.dpre_dec[i], T.spiral_inv[lv], w16, T.n_verts[lv],
                                                out=b.g_dec_up[i])
-            elif self._coarse_side(b, lv):  # dW slabs on the side stream, dx on this one
-                defer(self._on_side(lambda i=i, lv=lv: weight_grad(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None,
-                                                                    None, b.ws_dw[("dec", i)])),
-                      f"de_layers.{i + 1}.conv.layer")
-                ops.spiral_conv_bwd_data(b.dpre_dec[i], T.spiral_inv[lv], w, T.n_verts[lv],
-                                         out=b.g_dec_up[i], workspace=b.ws)
             elif b.paired[("dec", i)]:  # dx + dW slabs in one launch
                 _, d = ops.spiral_conv_bwd(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_inv[lv],
                                            w, None, None, dx=b.g_dec_up[i], workspace=b.ws_dw[("dec", i)])
@@ -762,7 +723,6 @@ class SDVAEEngine:
             dz = b.dz
         ops.latent_bwd(b.mulv, b.eps, b.z, dz, b.dlat, b.dmulv, S.latent, True, S.is_vae, S.sigmoid)
         if split:
-            self._join_side()
             ops.dw_reduce_batch(deferred)
             deferred = []
         b.deferred = deferred
@@ -817,14 +777,9 @@ class SDVAEEngine:
             x_in = b.x if lv == 0 else b.enc_out[lv - 1]
             rows_tab = T.enc_rows[lv]
             prev = lv - 1
-            # the Enblock's conv reads level lv and writes level lv + 1: its
-            # weight gradient goes to the side stream when the level-(lv + 1)
-            # dpre is a coarse tensor
-            side = self._coarse_side(b, lv + 1) and lv > 0
             if lv in b.xl:  # vertex-major (bf16 or fp32) operands (selection down-sampling)
-                dwf = (lambda lv=lv, x_in=x_in, rows_tab=rows_tab: ops.spiral_conv_bwd_weight_x(
-                    x_in, rows_tab, b.dpre_enc[lv], None, None, b.ws_dw[("enc", lv)]))
-                defer(self._on_side(dwf) if side else dwf(), f"en_layers.{lv}.conv.layer")
+                defer(ops.spiral_conv_bwd_weight_x(x_in, rows_tab, b.dpre_enc[lv], None, None,
+                                                   b.ws_dw[("enc", lv)]), f"en_layers.{lv}.conv.layer")
                 if lv > 0 and b.dpre_enc[lv].dtype == torch.float32 and b.rowsub_x.get(lv):
                     # fp32 dpre: dG = dpre.W at the kept rows (fp32), then the
                     # flat gather rounded once to bf16
@@ -835,13 +790,6 @@ class SDVAEEngine:
                     ops.spiral_conv_bwd_data_x(b.dpre_enc[lv], T.enc_inv[lv],
                                                self._w16(f"en_layers.{lv}.conv.layer.weight"), T.n_verts[lv],
                                                elu_y=b.enc_out[prev], out=b.dpre_enc[prev])
-                continue
-            if side and b.rowsub[("enc", lv)] and T.enc_select[prev]:
-                # dW slabs on the side stream; dG at the kept rows + the flat gather here
-                defer(self._on_side(lambda lv=lv, x_in=x_in, rows_tab=rows_tab: weight_grad(
-                    x_in, rows_tab, b.dpre_enc[lv], None, None, b.ws_dw[("enc", lv)])), f"en_layers.{lv}.conv.layer")
-                ops.spiral_conv_bwd_data_rowsub(b.dpre_enc[lv], T.enc_flat[lv], w, T.n_verts[lv],
-                                                elu_y=b.enc_out[prev], out=b.dpre_enc[prev], workspace=b.ws)
                 continue
             if b.rowsub[("enc", lv)]:  # dG at the kept rows (+ dW slabs), then the flat gather
                 sel = T.enc_select[prev]
@@ -878,7 +826,6 @@ class SDVAEEngine:
                                          out=b.g_pooled[prev], workspace=b.ws)
                 ops.spmm(T.downT_csr[prev], b.g_pooled[prev], T.n_verts[prev], elu_y=b.enc_full[prev],
                          out=b.dpre_enc[prev])
-        self._join_side()
         ops.dw_reduce_batch(deferred, adam=self.adam_args() if fuse_adam else None)
 
     def adam_step(self):

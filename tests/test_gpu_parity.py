@@ -897,27 +897,3 @@ def test_engine_forward_fused_up_equals_unfused(dtopo):
     close(outs[0][0], outs[1][0], 1e-5, "reconstruction")
     for a, c in zip(outs[0][1], outs[1][1]):
         assert torch.equal(a, c)
-
-
-@pytest.mark.parametrize("vertex_major", [True, False])
-def test_side_stream_weight_grads_bit_identical(dtopo, vertex_major):
-    """Coarse weight gradients on the side stream (overlapping the data
-    gradient chain) give the same gradients and parameters, bit for bit, as
-    the single-stream step -- eager and graph-replayed (step.TrainStep)."""
-    from craniofacialsd_vae_amd.step import TrainStep
-    w = recipe.golden_weights()
-    meshes = torch.from_numpy(recipe.normalized_meshes(12)).to(DEV)
-    res = []
-    for side in (False, True):
-        eng = E.SDVAEEngine(dtopo, E.ModelSpec(), swap_bs=4, device=DEV, vertex_major=vertex_major)
-        eng.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
-        eng.side_dw = side
-        ts = TrainStep(eng, E.ResidentData(meshes, bs=4, shuffle=True))
-        ts.step()          # eager
-        ts.capture()       # one more eager step, then the graph
-        ts.step()
-        ts.step()
-        torch.cuda.synchronize()
-        res.append((eng.params.data.clone(), eng.params.grad.clone(), eng.params.exp_avg_sq.clone()))
-    for a, c in zip(*res):
-        assert torch.equal(a, c)

@@ -2720,12 +2720,36 @@ extern "C" size_t cfsd_spiral_conv_bwd_rowsub_workspace(int batch, int vsrc, int
          sizeof(float);
 }
 
+static int bwd_rowsub(const float* x, int xvm, const int32_t* idx, const float* dpre, const int32_t* inv_flat,
+                      int flat_width, const float* w, const float* elu_y, float* dx, float* dw, float* db,
+                      float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
+                      int cout, void* stream);
+
 extern "C" int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, const float* dpre,
                                            const int32_t* inv_flat, int flat_width,
                                            const float* w, const float* elu_y, float* dx,
                                            float* dw, float* db, float* workspace,
                                            size_t workspace_bytes, int batch, int vsrc, int rows,
                                            int seq, int cin, int cout, void* stream) {
+  return bwd_rowsub(x, 0, idx, dpre, inv_flat, flat_width, w, elu_y, dx, dw, db, workspace, workspace_bytes, batch,
+                    vsrc, rows, seq, cin, cout, stream);
+}
+
+extern "C" int cfsd_spiral_conv_bwd_rowsub_x(const float* x, int x_dt, const int32_t* idx, const float* dpre,
+                                             const int32_t* inv_flat, int flat_width, const float* w,
+                                             const float* elu_y, float* dx, float* dw, float* db, float* workspace,
+                                             size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
+                                             int cout, void* stream) {
+  if (CFSD_DT_TYPE(x_dt) != CFSD_DT_F32 || (x_dt & ~(CFSD_VM | 0xf)))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_x: x must be fp32 (either layout)");
+  return bwd_rowsub(x, (x_dt & CFSD_VM) != 0, idx, dpre, inv_flat, flat_width, w, elu_y, dx, dw, db, workspace,
+                    workspace_bytes, batch, vsrc, rows, seq, cin, cout, stream);
+}
+
+static int bwd_rowsub(const float* x, int xvm, const int32_t* idx, const float* dpre, const int32_t* inv_flat,
+                      int flat_width, const float* w, const float* elu_y, float* dx, float* dw, float* db,
+                      float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
+                      int cout, void* stream) {
   int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
   if (!inv_flat || !w || !dx || !workspace)
@@ -2753,8 +2777,9 @@ extern "C" int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, c
   a.nb = (int)(((total + 15) / 16 + 3) / 4) * a.n_groups;
   const bool lat = g.kind == kDwLat;
   float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
-  DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, total, g.rchunk, g.gx, 0, batch, 0, 0};
+  DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, total, g.rchunk, g.gx, 0, batch, xvm, 0};
   if (lat) d.nb = (int)(((long)g.gx * (long)dw_units(cin, cout) + 3) / 4);
+  if (xvm && !lat) return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_x: vertex-major x needs a few-row layer");
   const dim3 grid((unsigned)(a.nb + d.nb));
   const int n_el = cout * kSeq * cin + cout;
 #define RSP(CIN_, COUT_)                                                                          \
@@ -2780,7 +2805,7 @@ extern "C" int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, c
 #define RSG(CIN_, G_)                                                                             \
   if (cin == CIN_ && G == G_) {                                                                   \
     hipLaunchKernelGGL((conv_dx_rowsub_gather<CIN_, G_>), gg, dim3(256), 0, st, dg,               \
-                       (const int4*)inv_flat, elu_y, dx, vsrc, rows, M, (int)(dg_el * sizeof(float)), batch, 0); \
+                       (const int4*)inv_flat, elu_y, dx, vsrc, rows, M, (int)(dg_el * sizeof(float)), batch, xvm); \
     return launch_status("spiral_conv_bwd_rowsub_gather");                                       \
   }
   RSG(32, 1) RSG(32, 2) RSG(32, 3) RSG(32, 4)

@@ -442,12 +442,17 @@ class SDVAEEngine:
         b.paired = {}
 
         b.rowsub = {}
+        b.rowsub_vm = {}
 
         def dw_region(key, vsrc, rows, seq, cin, cout, has_dx, low, flat=None):
             b.paired[key] = (not low) and has_dx and ops.spiral_conv_bwd_paired(bsz, vsrc, rows, seq, cin, cout)
             # Enblock conv on a row subset: dG at the kept rows + flat-list gather
             rs = ops.spiral_conv_bwd_rowsub_workspace(bsz, vsrc, rows, seq, cin, cout)
-            b.rowsub[key] = (not low) and has_dx and flat is not None and rs > 0
+            # fp32 vertex-major input (E1 of the fp32 step): the same paired
+            # dG + dW-slab launch reading x vertex-major (few-row layers)
+            b.rowsub_vm[key] = (low and not self.lp_levels and has_dx and flat is not None and rs > 0
+                                and bsz * rows < 65536)
+            b.rowsub[key] = ((not low) or b.rowsub_vm[key]) and has_dx and flat is not None and rs > 0
             if b.rowsub[key]:
                 regions.append((key, rs))
                 return
@@ -777,7 +782,9 @@ class SDVAEEngine:
             x_in = b.x if lv == 0 else b.enc_out[lv - 1]
             rows_tab = T.enc_rows[lv]
             prev = lv - 1
-            if lv in b.xl:  # vertex-major (bf16 or fp32) operands (selection down-sampling)
+            if lv in b.xl and b.rowsub_vm.get(("enc", lv)) and T.enc_select[prev]:
+                pass  # fp32 vertex-major x / dx: the paired row-subset launch below
+            elif lv in b.xl:  # vertex-major (bf16 or fp32) operands (selection down-sampling)
                 defer(ops.spiral_conv_bwd_weight_x(x_in, rows_tab, b.dpre_enc[lv], None, None,
                                                    b.ws_dw[("enc", lv)]), f"en_layers.{lv}.conv.layer")
                 if lv > 0 and b.dpre_enc[lv].dtype == torch.float32 and b.rowsub_x.get(lv):

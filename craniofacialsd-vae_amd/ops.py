@@ -276,7 +276,10 @@ def spiral_conv_bwd_rowsub(x, idx, dpre, flat, w, dw, db, dx, elu_y=None, worksp
     rows, seq = idx.shape
     cout = dpre.shape[2]
     table, width = flat
-    _need(x, None, name="x")
+    if is_vm(x):  # vertex-major fp32 x (the fp32 step's E1): cfsd_spiral_conv_bwd_rowsub_x
+        _needl(x, (bsz, vsrc, cin), "x", torch.float32)
+    else:
+        _need(x, None, name="x")
     _need(idx, (rows, seq), torch.int32, "idx")
     _need(dpre, (bsz, rows, cout), name="dpre")
     _need(table, (vsrc, width), torch.int32, "inv_flat")
@@ -284,16 +287,28 @@ def spiral_conv_bwd_rowsub(x, idx, dpre, flat, w, dw, db, dx, elu_y=None, worksp
     if dw is not None or db is not None:
         _need(dw, (cout, seq * cin), name="dw")
         _need(db, (cout,), name="db")
-    _need(dx, (bsz, vsrc, cin), name="dx")
-    if elu_y is not None:
-        _need(elu_y, (bsz, vsrc, cin), name="elu_y")
+    if is_vm(x):  # x, dx and elu_y share the source level's layout
+        _needl(dx, (bsz, vsrc, cin), "dx", torch.float32)
+        _same_layout(x, dx, "x and dx")
+        if elu_y is not None:
+            _needl(elu_y, (bsz, vsrc, cin), "elu_y", torch.float32)
+            _same_layout(x, elu_y, "x and elu_y")
+    else:
+        _need(dx, (bsz, vsrc, cin), name="dx")
+        if elu_y is not None:
+            _need(elu_y, (bsz, vsrc, cin), name="elu_y")
     need = spiral_conv_bwd_rowsub_workspace(bsz, vsrc, rows, seq, cin, cout)
     if need == 0:
         raise ValueError(f"no row-subset backward for {cin} -> {cout} channels")
     ws, nb = _conv_ws(workspace, x.device, need)
-    call("cfsd_spiral_conv_bwd_rowsub", ptr(x), ptr(idx), ptr(dpre), ptr(table), width, ptr(w),
-         ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, seq,
-         cin, cout, stream_ptr())
+    if is_vm(x):
+        call("cfsd_spiral_conv_bwd_rowsub_x", ptr(x), _st(x), ptr(idx), ptr(dpre), ptr(table), width, ptr(w),
+             ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, seq,
+             cin, cout, stream_ptr())
+    else:
+        call("cfsd_spiral_conv_bwd_rowsub", ptr(x), ptr(idx), ptr(dpre), ptr(table), width, ptr(w),
+             ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, seq,
+             cin, cout, stream_ptr())
     if dw is None:  # deferred weight gradient (slabs at the workspace start)
         return dx, DeferredDw(ws, bsz, vsrc, rows, cin, cout, True)
     return dx

@@ -169,6 +169,14 @@ int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, const float*
                                 const float* elu_y, float* dx, float* dw, float* db,
                                 float* workspace, size_t workspace_bytes, int batch, int vsrc,
                                 int rows, int seq, int cin, int cout, void* stream);
+/* The same with the source level's layout (ABI 4.4): x_dt = CFSD_DT_F32
+ * [| CFSD_VM] describes x, dx and elu_y (the fp32 step's E1 reads and writes
+ * the vertex-major level-1 tensors); dpre stays batch-major fp32.  Few-row
+ * layers only (the dW slabs of conv_dw_lat). */
+int cfsd_spiral_conv_bwd_rowsub_x(const float* x, int x_dt, const int32_t* idx, const float* dpre,
+                                  const int32_t* inv_flat, int flat_width, const float* w, const float* elu_y,
+                                  float* dx, float* dw, float* db, float* workspace, size_t workspace_bytes,
+                                  int batch, int vsrc, int rows, int seq, int cin, int cout, void* stream);
 
 /* dx alone of the row-subset backward (as cfsd_spiral_conv_bwd_rowsub):
  * dG = dpre.W (fp32 dpre and W, fp32 MFMA) in `workspace`

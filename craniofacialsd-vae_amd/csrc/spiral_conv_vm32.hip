@@ -24,8 +24,6 @@
 // one 2-KiB dpre block and 16 MFMAs per entry (9 entries per vertex on
 // average).  The batch-major kernel instead sums each slot's list rows
 // (three unconditional head loads per slot, 27 per vertex) before its MFMAs.
-#include <stdlib.h>
-
 #include "conv_vm32.h"
 
 namespace cfsd {
@@ -56,8 +54,8 @@ __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t rs, int voff, int
 #ifndef CFSD_VM32_FWD_OCC
 #define CFSD_VM32_FWD_OCC 4  // waves per SIMD (VGPR budget 128)
 #endif
-template <int CIN, int COUT, int ACT, int UPT, int PD, int NT = 256>
-__global__ __launch_bounds__(NT, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const float* __restrict__ x,
+template <int CIN, int COUT, int ACT, int UPT, int PD>
+__global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const float* __restrict__ x,
                                                      const int* __restrict__ idx,
                                                      const float* __restrict__ w,
                                                      const float* __restrict__ bias,
@@ -82,7 +80,7 @@ __global__ __launch_bounds__(NT, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const flo
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0,
                                                     (int)((long)vsrc * batch * CIN * 4), 0x00020000);
   const int vstride = batch * CIN * 4;  // bytes between two vertices' blocks
-  const TileSweep sw = xcd_sweep(n_tiles, NT / 64, wave, n_tiles < kContigTiles);
+  const TileSweep sw = xcd_sweep(n_tiles, 4, wave, n_tiles < kContigTiles);
   for (long tile = sw.begin; tile < sw.end; tile += sw.step) {
     // compiler barrier: keeps the W fragments as per-MFMA-group LDS reads
     // (hipcc otherwise hoists the whole W slice out of the tile loop and spills)
@@ -691,34 +689,15 @@ static int resident(Kern k, int threads, size_t lds) {
   return r > 0 ? r : 1;
 }
 
-template <int CIN, int COUT, int ACT, int UPT, int PD, int NT>
-static int fwd_nt(const float* x, const int* idx, const float* w, const float* bias, float* y, int yvm,
-                  int vsrc, int rows, int batch, hipStream_t st) {
-  constexpr size_t lds = (size_t)COUT * (kS * CIN + 8) * sizeof(float);
-  auto kern = conv_fwd_vm32<CIN, COUT, ACT, UPT, PD, NT>;
-  const long tiles = ((long)rows * (batch / 16) + UPT - 1) / UPT;
-  const unsigned grid = balanced_blocks(tiles, NT / 64, resident(kern, NT, lds));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
-  return launch_status("spiral_conv_fwd_vm32");
-}
-// workgroup size: every workgroup stages the layer's W in LDS once, so
-// fewer, larger workgroups cut the L2 -> LDS weight traffic
-static int fwd_threads() {
-  static int nt = -1;
-  if (nt < 0) {
-    const char* e = getenv("CFSD_VM32_NT");
-    nt = e ? atoi(e) : 256;
-    if (nt != 256 && nt != 512 && nt != 1024) nt = 256;
-  }
-  return nt;
-}
 template <int CIN, int COUT, int ACT, int UPT, int PD>
 static int fwd_t(const float* x, const int* idx, const float* w, const float* bias, float* y, int yvm,
                  int vsrc, int rows, int batch, hipStream_t st) {
-  const int nt = fwd_threads();
-  if (nt == 1024) return fwd_nt<CIN, COUT, ACT, UPT, PD, 1024>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
-  if (nt == 512) return fwd_nt<CIN, COUT, ACT, UPT, PD, 512>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
-  return fwd_nt<CIN, COUT, ACT, UPT, PD, 256>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
+  constexpr size_t lds = (size_t)COUT * (kS * CIN + 8) * sizeof(float);
+  auto kern = conv_fwd_vm32<CIN, COUT, ACT, UPT, PD>;
+  const long tiles = ((long)rows * (batch / 16) + UPT - 1) / UPT;
+  const unsigned grid = balanced_blocks(tiles, 4, resident(kern, 256, lds));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
+  return launch_status("spiral_conv_fwd_vm32");
 }
 
 // Units (vertex x 16 meshes) below which a wave takes ONE unit with two slots

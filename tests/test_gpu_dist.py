@@ -172,7 +172,10 @@ for step in range(1, 4):
         eng_e.resident_step(b_e, data_e, acc=eng_e.loss_acc, grad_hook=avg_e)
         torch.cuda.synchronize()
     sg, se = state(eng_g), state(eng_e)
+    names = ["data", "grad", "exp_avg", "exp_avg_sq", "step", "counter", "shadow"]
     rec = {"graph_equals_eager": all(torch.equal(a, b) for a, b in zip(sg, se)),
+           "differs": [(n, float((a.double() - b.double()).abs().max()), int((a != b).sum()))
+                       for n, a, b in zip(names, sg, se) if not torch.equal(a, b)],
            "params_equal_ranks": gather_equal(eng_g.params.data.cpu()),
            "moments_equal_ranks": gather_equal(eng_g.params.exp_avg_sq.cpu()),
            "batch_idx": ts.b.batch_idx.cpu().tolist()}

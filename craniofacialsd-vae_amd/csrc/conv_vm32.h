@@ -11,7 +11,7 @@ namespace vm32 {
 
 bool ok(int batch, int cin, int cout);
 // The last Deblock (32 -> 32 + ELU, vertex-major) also writing the output
-// conv's per-slot partials z [9][rows][3][batch]; then the output conv from z.
+// conv's per-slot partials z [9][rows][batch][3]; then the output conv from z.
 int launch_fwd_zout(const float* x, const int* idx, const float* w, const float* bias, float* y, const float* w_out,
                     float* zbuf, int vsrc, int rows, int batch, hipStream_t st);
 int launch_out_from_z(const float* zbuf, const int* idx, const float* bias, float* out, int yvm, int rows, int batch,

@@ -56,10 +56,9 @@ __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t rs, int voff, int
 #endif
 // ZO (the last Deblock, 32 -> 32, followed by the 32 -> 3 output conv): the
 // epilogue also writes the output conv's per-slot partial products of its own
-// rows, z[s][v][c][mesh] = sum_k w_out[c][s*32 + k] y[v][mesh][k] (slot-major;
-// one vertex's 16 meshes contiguous per (slot, c)), computed on the MFMA from
-// the tile's outputs in registers, so the output conv gathers 3 x 64 B per
-// slot and unit (conv_out_from_z) instead of a 2-KiB neighbour block.
+// rows, z[s][v][mesh][c] = sum_k w_out[c][s*32 + k] y[v][mesh][k] (slot-major,
+// 3 floats per (slot, vertex, mesh)), so the output conv becomes a 12-B gather
+// per slot (conv_out_from_z) instead of nine 128-B neighbour rows.
 template <int CIN, int COUT, int ACT, int UPT, int PD, int ZO = 0>
 __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const float* __restrict__ x,
                                                      const int* __restrict__ idx,
@@ -70,10 +69,14 @@ __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const fl
                                                      float* __restrict__ zbuf = nullptr) {
   constexpr int CH = CIN / 16, NCT = COUT / 16, K = kS * CIN, KP = K + 8, NB = PD + 1;
   constexpr int KO = kS * COUT;  // w_out row length (ZO)
-  extern __shared__ float lds_w[];  // [COUT][KP]
+  extern __shared__ float lds_w[];  // [COUT][KP] (+ ZO: w_out [3][KO])
   coop_copy<8, f32x4>(
       COUT * (K / 4), [&](int e) { return ld4(&w[(long)(e / (K / 4)) * K + 4 * (e % (K / 4))]); },
       [&](int e, f32x4 v) { st4(&lds_w[(e / (K / 4)) * KP + 4 * (e % (K / 4))], v); });
+  float* lds_wo = lds_w + COUT * KP;
+  if constexpr (ZO) {
+    for (int e = threadIdx.x; e < 3 * KO / 4; e += blockDim.x) st4(&lds_wo[4 * e], ld4(&w_out[4 * e]));
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
@@ -82,19 +85,6 @@ __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const fl
   for (int t = 0; t < NCT; ++t)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) bn[t][rr] = bias ? bias[16 * t + 4 * g + rr] : 0.f;
-  // ZO: A fragments of Wo' [32 q][32 ch]: lane (m, g) holds Wo'[16 qt + m][16 t + 4 g + rr]
-  float wo[ZO ? 2 : 1][ZO ? NCT : 1][4];
-  if constexpr (ZO) {
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int t = 0; t < NCT; ++t)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int q = 16 * qt + j, sl = q / 3, c = q - 3 * sl;
-          wo[qt][t][rr] = q < 3 * kS ? w_out[c * KO + sl * COUT + 16 * t + 4 * g + rr] : 0.f;
-        }
-  }
   const int G16 = batch >> 4;
   const long n_units = (long)rows * G16;
   const long n_tiles = (n_units + UPT - 1) / UPT;
@@ -171,28 +161,26 @@ __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const fl
         st4(y + row * COUT + 16 * t + 4 * g, v);
       }
       if constexpr (ZO) {
-        // Z[q][mesh] = sum_ch Wo'[q][ch] Y[ch][mesh] (q = 3 s + c < 27, padded to
-        // 32) on the MFMA: B = this lane's outputs as they are (lane (mesh j,
-        // g) holds channels 16t + 4g + rr = the k-step (t, rr) B fragment), A =
-        // the w_out fragments kept in VGPRs; lane (j, g) gets q = 16 qt + 4g + i
-        f32x4 zq[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+        // lane (mesh j, g) holds channels 16t + 4g .. +3: partial dot products
+        // over them, summed over the four g lanes of the mesh (xor 16, 32)
+        float* zb = zbuf + ((long)vr[u] * batch + mesh) * 3;
+        const long zs = (long)rows * batch * 3;  // slot stride
+#pragma unroll 3
+        for (int sq = 0; sq < kS * 3; ++sq) {
+          const int sl = sq / 3, c = sq - 3 * sl;
+          float pz = 0.f;
 #pragma unroll
-        for (int t = 0; t < NCT; ++t)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-            for (int qt = 0; qt < 2; ++qt) zq[qt] = mfma16(wo[qt][t][rr], yv[t][rr], zq[qt]);
-        const long zbase = (long)vr[u] * 3 * batch + mesh;
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int q = 16 * qt + 4 * g + i;
-            if (q < 3 * kS) {
-              const int sl = q / 3, c = q - 3 * sl;
-              zbuf[((long)sl * rows * 3 + c) * batch + zbase + 0] = zq[qt][i];
-            }
+          for (int t = 0; t < NCT; ++t) {
+            const f32x4 wv = ld4(&lds_wo[c * KO + sl * COUT + 16 * t + 4 * g]);
+            pz = fmaf(yv[t].x, wv.x, pz);
+            pz = fmaf(yv[t].y, wv.y, pz);
+            pz = fmaf(yv[t].z, wv.z, pz);
+            pz = fmaf(yv[t].w, wv.w, pz);
           }
+          pz += __shfl_xor(pz, 16);
+          pz += __shfl_xor(pz, 32);
+          if (g == (sq & 3)) zb[sl * zs + c] = pz;
+        }
       }
     }
   }
@@ -201,7 +189,7 @@ __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const fl
 // The 32 -> 3 output conv from the Deblock's per-slot partials (ZO above):
 // out[v][mesh][c] = bias[c] + sum_s z[s][idx[v][s]][mesh][c], slots in order.
 // One thread per (vertex, mesh) row of the vertex-major output; a slot's 16
-// meshes of one neighbour and channel are one contiguous 64-B run of z.
+// meshes of one neighbour are one contiguous 192-B run of z.
 __global__ __launch_bounds__(256) void conv_out_from_z(const float* __restrict__ z, const int* __restrict__ idx,
                                                        const float* __restrict__ bias, float* __restrict__ out,
                                                        int rows, int batch, int yvm) {
@@ -215,10 +203,10 @@ __global__ __launch_bounds__(256) void conv_out_from_z(const float* __restrict__
   float zv[kS][3];
 #pragma unroll
   for (int s = 0; s < kS; ++s) {
-    const float* p = z + s * zs + (long)nb[s] * 3 * batch + mesh;
+    const float* p = z + s * zs + ((long)nb[s] * batch + mesh) * 3;
     zv[s][0] = p[0];
-    zv[s][1] = p[batch];
-    zv[s][2] = p[2 * batch];
+    zv[s][1] = p[1];
+    zv[s][2] = p[2];
   }
   float o[3];
 #pragma unroll
@@ -808,7 +796,7 @@ int launch_fwd_zout(const float* x, const int* idx, const float* w, const float*
   if ((long)vsrc * batch * 32 * 4 >= (long)kAbsent || (long)kS * rows * batch * 3 >= (1L << 31))
     return set_error(CFSD_EINVAL, "spiral_conv_fwd_zout: tensors exceed 32-bit offsets");
   constexpr int UPT = 2, PD = CFSD_VM32_PD2;
-  constexpr size_t lds = (size_t)32 * (kS * 32 + 8) * sizeof(float);
+  constexpr size_t lds = ((size_t)32 * (kS * 32 + 8) + 3 * kS * 32) * sizeof(float);
   auto kern = conv_fwd_vm32<32, 32, CFSD_ACT_ELU, UPT, PD, 1>;
   const long tiles = ((long)rows * (batch / 16) + UPT - 1) / UPT;
   const unsigned grid = balanced_blocks(tiles, 4, resident(kern, 256, lds));

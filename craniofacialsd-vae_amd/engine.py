@@ -394,7 +394,7 @@ class SDVAEEngine:
             b.dec_out.append(fl(lv, bsz, nv[lv], cout))
         b.out = f0(bsz, nv[0], S.in_ch)
         last = S.dec_layers()[-1]
-        b.zout = (torch.empty(T.seq[0], nv[0], S.in_ch, bsz, dtype=torch.float32, device=dev)
+        b.zout = (torch.empty(T.seq[0], nv[0], bsz, S.in_ch, dtype=torch.float32, device=dev)
                   if (0 in lp and not self.lp_levels and bsz % 16 == 0 and S.in_ch == 3 and last[0] == 32
                       and last[1] == 32 and last[2] == 0 and T.seq[0] == 9) else None)
         b.unit = f0(bsz, nv[0], S.in_ch)

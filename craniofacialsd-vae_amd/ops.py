@@ -454,7 +454,7 @@ def spiral_conv_fwd_up(xc, comp, idx, w, bias, act, out, up_out=None):
 
 def spiral_conv_fwd_zout(x, idx, w, bias, w_out, out, z):
     """The last Deblock's conv + ELU (vertex-major fp32, 32 -> 32) also writing
-    the output conv's per-slot partials ``z`` [9, rows, 3, batch]
+    the output conv's per-slot partials ``z`` [9, rows, batch, 3]
     (cfsd_spiral_conv_fwd_zout)."""
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape
@@ -466,7 +466,7 @@ def spiral_conv_fwd_zout(x, idx, w, bias, w_out, out, z):
     _need(idx, (rows, seq), torch.int32, "idx")
     _need(w, (cout, seq * cin), name="w")
     _need(w_out, (co, seq * cout), name="w_out")
-    _need(z, (seq, rows, co, bsz), name="z")
+    _need(z, (seq, rows, bsz, co), name="z")
     call("cfsd_spiral_conv_fwd_zout", ptr(x), ptr(idx), ptr(w), ptr(bias), ptr(out), ptr(w_out), ptr(z), bsz, vsrc,
          rows, seq, cin, cout, co, stream_ptr())
     return out
@@ -475,7 +475,7 @@ def spiral_conv_fwd_zout(x, idx, w, bias, w_out, out, z):
 def spiral_conv_out_from_z(z, idx, bias, out):
     """Output conv (model.py:172-173) from the partials of
     :func:`spiral_conv_fwd_zout`: out = bias + sum over slots of z."""
-    seq, rows, co, bsz = z.shape
+    seq, rows, bsz, co = z.shape
     _need(z, None, name="z")
     _need(idx, (rows, seq), torch.int32, "idx")
     _needl(out, (bsz, rows, co), "out", torch.float32)

@@ -268,8 +268,8 @@ int cfsd_spiral_conv_fwd_up(const float* xc, const int32_t* comp_col, const floa
  * (1) the 32 -> 32 SpiralConv + ELU of cfsd_spiral_conv_fwd_x (vertex-major
  * fp32 x and y, batch % 16 == 0) whose epilogue ALSO writes the output
  * conv's per-slot partial products of its own rows,
- *   z[s][v][c][b] = sum_k w_out[c, s*32 + k] * y[b, v, k]   (fp32, [9][rows][3][batch]),
- * and (2) out[b, v, c] = bias_out[c] + sum_{s = 0..8} z[s][idx[v, s]][c][b]
+ *   z[s][v][b][c] = sum_k w_out[c, s*32 + k] * y[b, v, k]   (fp32, [9][rows][batch][3]),
+ * and (2) out[b, v, c] = bias_out[c] + sum_{s = 0..8} z[s][idx[v, s]][b][c]
  * (out_dt = CFSD_DT_F32 [| CFSD_VM]).  The output conv then gathers 12 B per
  * spiral slot instead of a 128-B neighbour row (ABI 4.4). */
 int cfsd_spiral_conv_fwd_zout(const float* x, const int32_t* idx, const float* w, const float* bias, float* y,

@@ -361,7 +361,7 @@ def test_output_conv_from_slot_partials(mods, otopo, dtopo):
     bo = torch.randn(3, generator=g) * 0.1
     xv = ops.to_vm(x.to(DEV))
     y = ops.vm_empty(16, nv, 32, device=DEV)
-    z = torch.empty(9, nv, 3, 16, device=DEV)
+    z = torch.empty(9, nv, 16, 3, device=DEV)
     ops.spiral_conv_fwd_zout(xv, dtopo.spiral[0], w.to(DEV), b.to(DEV), wo.to(DEV), out=y, z=z)
     y_ref = ops.vm_empty(16, nv, 32, device=DEV)
     ops.spiral_conv_fwd_x(xv, dtopo.spiral[0], w.to(DEV), None, b.to(DEV), 1, y_ref)

@@ -52,8 +52,6 @@ SIGNATURES = {
     "cfsd_swap_features_x": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_conv_fwd_up_supported": (_I, [_I, _I, _I, _I, _I]),
     "cfsd_spiral_conv_fwd_up": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
-    "cfsd_spiral_conv_fwd_zout": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
-    "cfsd_spiral_conv_out_from_z": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_gather_meshes": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_normalize": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     "cfsd_spectral_blend": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),

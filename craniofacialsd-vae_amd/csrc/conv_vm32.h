@@ -10,12 +10,6 @@ namespace cfsd {
 namespace vm32 {
 
 bool ok(int batch, int cin, int cout);
-// The last Deblock (32 -> 32 + ELU, vertex-major) also writing the output
-// conv's per-slot partials z [9][rows][batch][3]; then the output conv from z.
-int launch_fwd_zout(const float* x, const int* idx, const float* w, const float* bias, float* y, const float* w_out,
-                    float* zbuf, int vsrc, int rows, int batch, hipStream_t st);
-int launch_out_from_z(const float* zbuf, const int* idx, const float* bias, float* out, int yvm, int rows, int batch,
-                      hipStream_t st);
 // y[(b, r), :] = act(bias + W . gather(x)); x vertex-major [vsrc][batch][cin],
 // y vertex-major (yvm) or batch-major [batch][rows][cout].  Same products in
 // the same order as conv_fwd_mfma (bit-identical results).

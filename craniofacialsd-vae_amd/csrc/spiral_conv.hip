@@ -2121,26 +2121,6 @@ static int fwd_coarse(const float* x, int xvm, const int* idx, const float* w, c
   return coarse::launch_fwd_ks(a, cin, cout, st);
 }
 
-extern "C" int cfsd_spiral_conv_fwd_zout(const float* x, const int32_t* idx, const float* w, const float* bias,
-                                         float* y, const float* w_out, float* z, int batch, int vsrc, int rows,
-                                         int seq, int cin, int cout, int cout_out, void* stream) {
-  int rc = check_conv_args(x, idx, w, batch, vsrc, rows, seq, cin, cout);
-  if (rc) return rc;
-  if (!y || !w_out || !z) return set_error(CFSD_EINVAL, "spiral_conv_fwd_zout: null pointer");
-  if (cin != 32 || cout != 32 || cout_out != 3 || batch % 16)
-    return set_error(CFSD_EINVAL, "spiral_conv_fwd_zout: 32 -> 32 then 32 -> 3, batch %% 16 == 0 only");
-  return vm32::launch_fwd_zout(x, idx, w, bias, y, w_out, z, vsrc, rows, batch, (hipStream_t)stream);
-}
-
-extern "C" int cfsd_spiral_conv_out_from_z(const float* z, const int32_t* idx, const float* bias, float* out,
-                                           int out_dt, int batch, int rows, int seq, int cout_out, void* stream) {
-  if (!z || !idx || !out) return set_error(CFSD_EINVAL, "spiral_conv_out_from_z: null pointer");
-  if (batch <= 0 || rows <= 0 || seq != kSeq || cout_out != 3 || CFSD_DT_TYPE(out_dt) != CFSD_DT_F32)
-    return set_error(CFSD_EINVAL, "spiral_conv_out_from_z: bad arguments");
-  if ((long)kSeq * rows * batch * 3 >= (1L << 31)) return set_error(CFSD_EINVAL, "spiral_conv_out_from_z: too large");
-  return vm32::launch_out_from_z(z, idx, bias, out, (out_dt & CFSD_VM) != 0, rows, batch, (hipStream_t)stream);
-}
-
 extern "C" int cfsd_spiral_conv_fwd_up_supported(int batch, int rows, int seq, int cin, int cout) {
   if (batch <= 0 || rows <= 0 || seq != kSeq) return 0;
   return coarse::fwd_up_supported((long)batch * rows, cin, cout) ? 1 : 0;

@@ -54,29 +54,18 @@ __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t rs, int voff, int
 #ifndef CFSD_VM32_FWD_OCC
 #define CFSD_VM32_FWD_OCC 4  // waves per SIMD (VGPR budget 128)
 #endif
-// ZO (the last Deblock, 32 -> 32, followed by the 32 -> 3 output conv): the
-// epilogue also writes the output conv's per-slot partial products of its own
-// rows, z[s][v][mesh][c] = sum_k w_out[c][s*32 + k] y[v][mesh][k] (slot-major,
-// 3 floats per (slot, vertex, mesh)), so the output conv becomes a 12-B gather
-// per slot (conv_out_from_z) instead of nine 128-B neighbour rows.
-template <int CIN, int COUT, int ACT, int UPT, int PD, int ZO = 0>
+template <int CIN, int COUT, int ACT, int UPT, int PD>
 __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const float* __restrict__ x,
                                                      const int* __restrict__ idx,
                                                      const float* __restrict__ w,
                                                      const float* __restrict__ bias,
                                                      float* __restrict__ y, int vsrc, int rows,
-                                                     int batch, int yvm, const float* __restrict__ w_out = nullptr,
-                                                     float* __restrict__ zbuf = nullptr) {
+                                                     int batch, int yvm) {
   constexpr int CH = CIN / 16, NCT = COUT / 16, K = kS * CIN, KP = K + 8, NB = PD + 1;
-  constexpr int KO = kS * COUT;  // w_out row length (ZO)
-  extern __shared__ float lds_w[];  // [COUT][KP] (+ ZO: w_out [3][KO])
+  extern __shared__ float lds_w[];  // [COUT][KP]
   coop_copy<8, f32x4>(
       COUT * (K / 4), [&](int e) { return ld4(&w[(long)(e / (K / 4)) * K + 4 * (e % (K / 4))]); },
       [&](int e, f32x4 v) { st4(&lds_w[(e / (K / 4)) * KP + 4 * (e % (K / 4))], v); });
-  float* lds_wo = lds_w + COUT * KP;
-  if constexpr (ZO) {
-    for (int e = threadIdx.x; e < 3 * KO / 4; e += blockDim.x) st4(&lds_wo[4 * e], ld4(&w_out[4 * e]));
-  }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
@@ -147,7 +136,6 @@ __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const fl
       if (tile * UPT + u >= n_units) break;  // uniform
       const int mesh = mgr[u] * 16 + j;
       const long row = yvm ? (long)vr[u] * batch + mesh : (long)mesh * rows + vr[u];
-      f32x4 yv[NCT];
 #pragma unroll
       for (int t = 0; t < NCT; ++t) {
         f32x4 v;
@@ -157,69 +145,10 @@ __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const fl
           if (ACT == CFSD_ACT_ELU) z = elu_f(z);
           v[rr] = z;
         }
-        yv[t] = v;
         st4(y + row * COUT + 16 * t + 4 * g, v);
-      }
-      if constexpr (ZO) {
-        // lane (mesh j, g) holds channels 16t + 4g .. +3: partial dot products
-        // over them, summed over the four g lanes of the mesh (xor 16, 32)
-        float* zb = zbuf + ((long)vr[u] * batch + mesh) * 3;
-        const long zs = (long)rows * batch * 3;  // slot stride
-#pragma unroll 3
-        for (int sq = 0; sq < kS * 3; ++sq) {
-          const int sl = sq / 3, c = sq - 3 * sl;
-          float pz = 0.f;
-#pragma unroll
-          for (int t = 0; t < NCT; ++t) {
-            const f32x4 wv = ld4(&lds_wo[c * KO + sl * COUT + 16 * t + 4 * g]);
-            pz = fmaf(yv[t].x, wv.x, pz);
-            pz = fmaf(yv[t].y, wv.y, pz);
-            pz = fmaf(yv[t].z, wv.z, pz);
-            pz = fmaf(yv[t].w, wv.w, pz);
-          }
-          pz += __shfl_xor(pz, 16);
-          pz += __shfl_xor(pz, 32);
-          if (g == (sq & 3)) zb[sl * zs + c] = pz;
-        }
       }
     }
   }
-}
-
-// The 32 -> 3 output conv from the Deblock's per-slot partials (ZO above):
-// out[v][mesh][c] = bias[c] + sum_s z[s][idx[v][s]][mesh][c], slots in order.
-// One thread per (vertex, mesh) row of the vertex-major output; a slot's 16
-// meshes of one neighbour are one contiguous 192-B run of z.
-__global__ __launch_bounds__(256) void conv_out_from_z(const float* __restrict__ z, const int* __restrict__ idx,
-                                                       const float* __restrict__ bias, float* __restrict__ out,
-                                                       int rows, int batch, int yvm) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long)rows * batch) return;
-  const int v = (int)(t / batch), mesh = (int)(t - (long)v * batch);
-  const long zs = (long)rows * batch * 3;
-  int nb[kS];
-#pragma unroll
-  for (int s = 0; s < kS; ++s) nb[s] = idx[v * kS + s];
-  float zv[kS][3];
-#pragma unroll
-  for (int s = 0; s < kS; ++s) {
-    const float* p = z + s * zs + ((long)nb[s] * batch + mesh) * 3;
-    zv[s][0] = p[0];
-    zv[s][1] = p[1];
-    zv[s][2] = p[2];
-  }
-  float o[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    float a = zv[0][c];
-#pragma unroll
-    for (int s = 1; s < kS; ++s) a += zv[s][c];
-    o[c] = a + (bias ? bias[c] : 0.f);
-  }
-  const long row = yvm ? t : (long)mesh * rows + v;
-  out[row * 3 + 0] = o[0];
-  out[row * 3 + 1] = o[1];
-  out[row * 3 + 2] = o[2];
 }
 
 
@@ -767,8 +696,7 @@ static int fwd_t(const float* x, const int* idx, const float* w, const float* bi
   auto kern = conv_fwd_vm32<CIN, COUT, ACT, UPT, PD>;
   const long tiles = ((long)rows * (batch / 16) + UPT - 1) / UPT;
   const unsigned grid = balanced_blocks(tiles, 4, resident(kern, 256, lds));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, batch, yvm,
-                     (const float*)nullptr, (float*)nullptr);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
   return launch_status("spiral_conv_fwd_vm32");
 }
 
@@ -788,28 +716,6 @@ static int fwd_pick(const float* x, const int* idx, const float* w, const float*
   if ((long)rows * (batch / 16) < CFSD_VM32_UPT1_UNITS)
     return fwd_t<32, COUT, ACT, 1, 2>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
   return fwd_t<32, COUT, ACT, 2, CFSD_VM32_PD2>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
-}
-
-int launch_fwd_zout(const float* x, const int* idx, const float* w, const float* bias, float* y, const float* w_out,
-                    float* zbuf, int vsrc, int rows, int batch, hipStream_t st) {
-  if (batch % 16) return set_error(CFSD_EINVAL, "spiral_conv_fwd_zout: batch %% 16 != 0");
-  if ((long)vsrc * batch * 32 * 4 >= (long)kAbsent || (long)kS * rows * batch * 3 >= (1L << 31))
-    return set_error(CFSD_EINVAL, "spiral_conv_fwd_zout: tensors exceed 32-bit offsets");
-  constexpr int UPT = 2, PD = CFSD_VM32_PD2;
-  constexpr size_t lds = ((size_t)32 * (kS * 32 + 8) + 3 * kS * 32) * sizeof(float);
-  auto kern = conv_fwd_vm32<32, 32, CFSD_ACT_ELU, UPT, PD, 1>;
-  const long tiles = ((long)rows * (batch / 16) + UPT - 1) / UPT;
-  const unsigned grid = balanced_blocks(tiles, 4, resident(kern, 256, lds));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, batch, 1, w_out, zbuf);
-  return launch_status("spiral_conv_fwd_zout");
-}
-
-int launch_out_from_z(const float* zbuf, const int* idx, const float* bias, float* out, int yvm, int rows, int batch,
-                      hipStream_t st) {
-  const long n = (long)rows * batch;
-  hipLaunchKernelGGL(conv_out_from_z, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, zbuf, idx, bias, out, rows,
-                     batch, yvm);
-  return launch_status("spiral_conv_out_from_z");
 }
 
 int launch_fwd(const float* x, const int* idx, const float* w, const float* bias, float* y, int yvm, int vsrc,

@@ -181,7 +181,6 @@ class SDVAEEngine:
             self.params.shadow = torch.zeros(self.params.numel, dtype=torch.bfloat16, device=self.device)
         self.vertex_major = bool(vertex_major)
         self.fuse_up = True  # coarse Deblocks: Pool(up) fused into the conv gather (False: separate SpMM)
-        self.zout_on = True  # fp32 vertex-major: output conv from the last Deblock's slot partials
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -393,10 +392,6 @@ class SDVAEEngine:
             b.dec_up.append(fl(lv, bsz, nv[lv], cin))
             b.dec_out.append(fl(lv, bsz, nv[lv], cout))
         b.out = f0(bsz, nv[0], S.in_ch)
-        last = S.dec_layers()[-1]
-        b.zout = (torch.empty(T.seq[0], nv[0], bsz, S.in_ch, dtype=torch.float32, device=dev)
-                  if (0 in lp and not self.lp_levels and bsz % 16 == 0 and S.in_ch == 3 and last[0] == 32
-                      and last[1] == 32 and last[2] == 0 and T.seq[0] == 9) else None)
         b.unit = f0(bsz, nv[0], S.in_ch)
         b.partials = f(2 * ops.recon_lap_blocks(bsz, nv[0]))
         b.losses = f(5)
@@ -598,27 +593,10 @@ class SDVAEEngine:
                                        up_out=b.dec_up[i])
             else:
                 self._spmm(T.up_csr[ui], h, T.n_verts[lv], out=b.dec_up[i], uniform=T.up_uniform[ui])
-                if i == len(S.dec_layers()) - 1 and self._zout(b):
-                    # + the output conv's per-slot partials of these rows
-                    ops.spiral_conv_fwd_zout(b.dec_up[i], T.spiral[lv], self.params.view(wname + ".weight"),
-                                             self.params.view(wname + ".bias"),
-                                             self.params.view(f"de_layers.{S.n + 1}.layer.weight"),
-                                             out=b.dec_out[i], z=b.zout)
-                else:
-                    self._conv_fwd(b, b.dec_up[i], T.spiral[lv], wname, ACT_ELU, b.dec_out[i])
+                self._conv_fwd(b, b.dec_up[i], T.spiral[lv], wname, ACT_ELU, b.dec_out[i])
             h = b.dec_out[i]
         n = S.n
-        if self._zout(b):  # output conv = sum of the slot partials the last Deblock wrote
-            ops.spiral_conv_out_from_z(b.zout, T.spiral[0], self.params.view(f"de_layers.{n + 1}.layer.bias"),
-                                       out=b.out)
-        else:
-            self._conv_fwd(b, h, T.spiral[0], f"de_layers.{n + 1}.layer", ACT_NONE, b.out)
-
-    def _zout(self, b):
-        """The fp32 vertex-major step computes the output conv from per-slot
-        partials written by the last Deblock's epilogue
-        (cfsd_spiral_conv_fwd_zout / cfsd_spiral_conv_out_from_z)."""
-        return getattr(b, "zout", None) is not None and self.zout_on
+        self._conv_fwd(b, h, T.spiral[0], f"de_layers.{n + 1}.layer", ACT_NONE, b.out)
 
     def _fused_up(self, b, h, i, lv, ui, cin, cout):
         """The coarse Deblocks (fp32 batch-major, uniform 3-entry up rows,

@@ -452,38 +452,6 @@ def spiral_conv_fwd_up(xc, comp, idx, w, bias, act, out, up_out=None):
     return out
 
 
-def spiral_conv_fwd_zout(x, idx, w, bias, w_out, out, z):
-    """The last Deblock's conv + ELU (vertex-major fp32, 32 -> 32) also writing
-    the output conv's per-slot partials ``z`` [9, rows, batch, 3]
-    (cfsd_spiral_conv_fwd_zout)."""
-    bsz, vsrc, cin = x.shape
-    rows, seq = idx.shape
-    cout, co = w.shape[0], w_out.shape[0]
-    _needl(x, (bsz, vsrc, cin), "x", torch.float32)
-    _needl(out, (bsz, rows, cout), "out", torch.float32)
-    if not (is_vm(x) and is_vm(out)):
-        raise ValueError("spiral_conv_fwd_zout: x and out must be vertex-major")
-    _need(idx, (rows, seq), torch.int32, "idx")
-    _need(w, (cout, seq * cin), name="w")
-    _need(w_out, (co, seq * cout), name="w_out")
-    _need(z, (seq, rows, bsz, co), name="z")
-    call("cfsd_spiral_conv_fwd_zout", ptr(x), ptr(idx), ptr(w), ptr(bias), ptr(out), ptr(w_out), ptr(z), bsz, vsrc,
-         rows, seq, cin, cout, co, stream_ptr())
-    return out
-
-
-def spiral_conv_out_from_z(z, idx, bias, out):
-    """Output conv (model.py:172-173) from the partials of
-    :func:`spiral_conv_fwd_zout`: out = bias + sum over slots of z."""
-    seq, rows, bsz, co = z.shape
-    _need(z, None, name="z")
-    _need(idx, (rows, seq), torch.int32, "idx")
-    _needl(out, (bsz, rows, co), "out", torch.float32)
-    call("cfsd_spiral_conv_out_from_z", ptr(z), ptr(idx), ptr(bias), ptr(out), _st(out), bsz, rows, seq, co,
-         stream_ptr())
-    return out
-
-
 def gather_meshes(x_all, batch_idx, bs, out=None):
     """The un-swapped batch of a ``swap_features: False`` configuration
     (``data_loading.py:38, 81-82``: MeshCollater without a feature swapper):

@@ -264,19 +264,6 @@ int cfsd_spiral_conv_fwd_up_supported(int batch, int rows, int seq, int cin, int
 int cfsd_spiral_conv_fwd_up(const float* xc, const int32_t* comp_col, const float* comp_val, const int32_t* idx,
                             const float* w, const float* bias, float* y, float* y_up, int batch, int n_coarse,
                             int rows, int seq, int cin, int cout, int act, void* stream);
-/* The last Deblock and the output conv (model.py:83-84, 172-173) as
- * (1) the 32 -> 32 SpiralConv + ELU of cfsd_spiral_conv_fwd_x (vertex-major
- * fp32 x and y, batch % 16 == 0) whose epilogue ALSO writes the output
- * conv's per-slot partial products of its own rows,
- *   z[s][v][b][c] = sum_k w_out[c, s*32 + k] * y[b, v, k]   (fp32, [9][rows][batch][3]),
- * and (2) out[b, v, c] = bias_out[c] + sum_{s = 0..8} z[s][idx[v, s]][b][c]
- * (out_dt = CFSD_DT_F32 [| CFSD_VM]).  The output conv then gathers 12 B per
- * spiral slot instead of a 128-B neighbour row (ABI 4.4). */
-int cfsd_spiral_conv_fwd_zout(const float* x, const int32_t* idx, const float* w, const float* bias, float* y,
-                              const float* w_out, float* z, int batch, int vsrc, int rows, int seq, int cin, int cout,
-                              int cout_out, void* stream);
-int cfsd_spiral_conv_out_from_z(const float* z, const int32_t* idx, const float* bias, float* out, int out_dt,
-                                int batch, int rows, int seq, int cout_out, void* stream);
 /* The un-swapped batch of a swap_features: False configuration
  * (data_loading.py:38, 81-82: MeshCollater without a feature_swapper):
  * out[b] = x[batch_idx[b]], b < bs; out_dt = CFSD_DT_F32 [| CFSD_VM] (ABI 4.4).

@@ -224,18 +224,15 @@ def test_fp32_step_vertex_major_vs_batch_major(mods, dtopo):
             eng.inject(b, recipe.train_key_index(step), torch.from_numpy(recipe.train_eps(step)))
             b.batch_idx.copy_(torch.arange(4 * step, 4 * step + 4, dtype=torch.int32))
             ops.swap_features(meshes, b.batch_idx, dtopo.region_mask, b.key, 4, out=b.x)
-            if step == 0:  # forward only: bit-identical layer outputs
+            if step == 0:  # forward only: bit-identical outputs
                 eng.forward(b, train=True)
-                out0 = (b.out.clone(), b.dec_out[-1].clone())
+                out0 = b.out.clone()
             eng.train_step_on(b)
             torch.cuda.synchronize()
             losses.append(b.losses.cpu().clone())
         res.append((out0, torch.stack(losses), eng.params.data.cpu().clone(), eng.params.grad.cpu().clone()))
     (o_bm, l_bm, p_bm, g_bm), (o_vm, l_vm, p_vm, g_vm) = res
-    assert torch.equal(o_bm[1], o_vm[1])  # every conv kernel: same products in the same order
-    # (the vertex-major output conv sums the last Deblock's per-slot partials:
-    # same products, slot sums in another order)
-    assert err_rel_max(o_vm[0], o_bm[0]) <= 1e-6
+    assert torch.equal(o_bm, o_vm)  # every forward kernel: same products in the same order
     assert float(((l_vm - l_bm).abs() / l_bm.abs().clamp_min(1e-12)).max()) <= 1e-5
     assert err_rel_max(p_vm, p_bm) <= 1e-5
     assert err_rel_max(g_vm, g_bm) <= 1e-4
@@ -343,34 +340,3 @@ def test_bwd_out_flat(mods, otopo, dtopo, xdt, bsz):
     ops.dw_reduce_batch([(d, dw2, db2)])
     assert torch.equal(dx2, dx) and torch.equal(dw2, dw) and torch.equal(db2, db)
 
-
-
-def test_output_conv_from_slot_partials(mods, otopo, dtopo):
-    """cfsd_spiral_conv_fwd_zout + cfsd_spiral_conv_out_from_z (the fp32
-    vertex-major step's last Deblock + output conv, model.py:83-84, 172-173):
-    the Deblock output is bit-identical to the plain vertex-major forward, the
-    reconstruction within 1e-5 of the float64 oracle and 1e-6 of the one-pass
-    output conv."""
-    _, ops, _ = mods
-    g = torch.Generator().manual_seed(21)
-    nv = dtopo.n_verts[0]
-    x = torch.randn(16, nv, 32, generator=g)
-    w = torch.randn(32, 288, generator=g) * 0.1
-    b = torch.randn(32, generator=g) * 0.1
-    wo = torch.randn(3, 288, generator=g) * 0.1
-    bo = torch.randn(3, generator=g) * 0.1
-    xv = ops.to_vm(x.to(DEV))
-    y = ops.vm_empty(16, nv, 32, device=DEV)
-    z = torch.empty(9, nv, 16, 3, device=DEV)
-    ops.spiral_conv_fwd_zout(xv, dtopo.spiral[0], w.to(DEV), b.to(DEV), wo.to(DEV), out=y, z=z)
-    y_ref = ops.vm_empty(16, nv, 32, device=DEV)
-    ops.spiral_conv_fwd_x(xv, dtopo.spiral[0], w.to(DEV), None, b.to(DEV), 1, y_ref)
-    assert torch.equal(y, y_ref)
-    out = ops.vm_empty(16, nv, 3, device=DEV)
-    ops.spiral_conv_out_from_z(z, dtopo.spiral[0], bo.to(DEV), out)
-    one = ops.vm_empty(16, nv, 3, device=DEV)
-    ops.spiral_conv_fwd_x(y_ref, dtopo.spiral[0], wo.to(DEV), None, bo.to(DEV), 0, one)
-    assert err_rel_max(out, one) <= 1e-6
-    sp = otopo.spirals[0]
-    ref = O.spiral_conv(y.double().cpu(), sp, wo.double(), bo.double())
-    assert err_rel_max(out, ref) <= 1e-5

@@ -26,8 +26,6 @@ struct FwdKsArgs {
   int vsrc, rows, batch, n_coarse;
   long total_rows;      // batch * rows
   int xvm, yvm, elu;
-  long long* stamps;    // timing experiment: per-wave s_memrealtime stamps, or null
-  int dbg;              // timing experiment: 1 no W loads, 2 no x loads, 4 stamp after idx+W
 };
 
 struct DxKsArgs {

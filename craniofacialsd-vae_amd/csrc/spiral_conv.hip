@@ -2091,13 +2091,6 @@ static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const
 #define CFSD_LAT_DW_MAX CFSD_LAT_MAX_ROWS
 #endif
 
-// timing experiment hook (tools/kb_stamps.py): device buffer for per-wave stamps
-static void* cfsd_debug_stamps = nullptr;
-static int cfsd_debug_flags = 0;
-extern "C" void cfsd_debug_set_stamps(void* p, int flags) {
-  cfsd_debug_stamps = p;
-  cfsd_debug_flags = flags;
-}
 
 // coarse levels: slot groups in one workgroup, partials combined in LDS
 // (spiral_conv_coarse.hip)
@@ -2116,8 +2109,6 @@ static int fwd_coarse(const float* x, int xvm, const int* idx, const float* w, c
   a.xvm = xvm;
   a.yvm = yvm;
   a.elu = act == CFSD_ACT_ELU;
-  a.stamps = (long long*)cfsd_debug_stamps;
-  a.dbg = cfsd_debug_flags;
   return coarse::launch_fwd_ks(a, cin, cout, st);
 }
 

@@ -20,9 +20,6 @@
 // launch disappears; the slot-0 wave (spiral slot 0 is the vertex itself,
 // checked on the host) stores the up-sampled rows of its tile, which the
 // weight gradient of the backward reads.
-#include <stdio.h>
-#include <stdlib.h>
-
 #include "cfsd_common.h"
 #include "conv_coarse.h"
 #include "conv_lat.h"
@@ -59,9 +56,10 @@ __device__ __forceinline__ f32x4 up_row4(const f32x4 x0, const f32x4 x1, const f
 // need <= 85 VGPRs (6 waves x 85 <= 512), else every second workgroup of a
 // CU waits for the first to exit (measured: D0 forward 267 workgroups, 11 of
 // them a whole wave-life late)
-constexpr int ks_min_waves(int nsg) { return nsg == 9 ? 6 : 2; }
+// (two-tile workgroups: 78 KB of partials in LDS, one workgroup per CU)
+constexpr int ks_min_waves(int nsg, int rt) { return nsg == 9 ? (rt == 1 ? 6 : 3) : 2; }
 template <int CIN, int COUT, int NSG, int RT, int UP>
-__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_fwd_ks(const FwdKsArgs a) {
+__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_fwd_ks(const FwdKsArgs a) {
   constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN, SPW = kSeq / NSG;
   constexpr int LDC = COUT + 4;  // partial row stride (kg rows land on distinct banks)
   static_assert(kSeq % NSG == 0, "slot groups");
@@ -71,8 +69,6 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_fwd_ks(const
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const long rt0 = (long)xcd_block() * RT;
   const long M = a.total_rows;
-  long long st_[6];
-  if (a.stamps) st_[0] = __builtin_amdgcn_s_memrealtime();
   const int nv_x = UP ? a.n_coarse : a.vsrc;
   const Lay lx = make_lay(a.xvm, a.batch, nv_x);
   // this lane's row in each tile (x's layout), its mesh / vertex and spiral
@@ -94,12 +90,7 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_fwd_ks(const
 #pragma unroll
     for (int c = 0; c < CH; ++c)
 #pragma unroll
-      for (int t = 0; t < NCT; ++t)
-        bw[j][c][t] = (a.dbg & 1) ? f32x4{1.f, 1.f, 1.f, 1.f} : ld4(wb + (long)t * 16 * K + (g * SPW + j) * CIN + 16 * c);
-  if ((a.dbg & 4) && a.stamps) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_[1] = __builtin_amdgcn_s_memrealtime();
-  }
+      for (int t = 0; t < NCT; ++t) bw[j][c][t] = ld4(wb + (long)t * 16 * K + (g * SPW + j) * CIN + 16 * c);
   f32x4 av[RT][SPW][CH];
   if constexpr (UP) {
     int cc[RT][SPW][3];
@@ -144,14 +135,8 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_fwd_ks(const
 #pragma unroll
       for (int j = 0; j < SPW; ++j)
 #pragma unroll
-        for (int c = 0; c < CH; ++c)
-          av[rt][j][c] = (a.dbg & 2) ? f32x4{1.f, 1.f, 1.f, 1.f} : ld4(xb + (long)src[rt][j] * lx.vs * CIN + 16 * c);
+        for (int c = 0; c < CH; ++c) av[rt][j][c] = ld4(xb + (long)src[rt][j] * lx.vs * CIN + 16 * c);
     }
-  }
-  if (a.stamps) {
-    if (!(a.dbg & 4)) st_[1] = __builtin_amdgcn_s_memrealtime();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_[2] = __builtin_amdgcn_s_memrealtime();
   }
   f32x4 acc[RT][NCT];
 #pragma unroll
@@ -177,9 +162,7 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_fwd_ks(const
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
         part[((g * RT + rt) * 16 + 4 * kg + rr) * LDC + t * 16 + r16] = acc[rt][t][rr];
-  if (a.stamps) st_[3] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
-  if (a.stamps) st_[4] = __builtin_amdgcn_s_memrealtime();
   constexpr int N4 = RT * 16 * COUT / 4;
   for (int q = threadIdx.x; q < N4; q += 64 * NSG) {
     const int rt = q / (16 * COUT / 4), rem = q % (16 * COUT / 4);
@@ -203,16 +186,6 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_fwd_ks(const
       yo = row_of(make_lay(a.yvm, a.batch, a.rows), bo, ro);
     }
     st4(a.y + yo * COUT + 4 * c4, v);
-  }
-  if (a.stamps) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_[5] = __builtin_amdgcn_s_memrealtime();
-    if (lane < 6) {
-      long long v = st_[0];
-#pragma unroll
-      for (int k = 1; k < 6; ++k) v = lane == k ? st_[k] : v;
-      a.stamps[((long)blockIdx.x * NSG + g) * 8 + lane] = v;
-    }
   }
 }
 
@@ -280,8 +253,6 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
     }
   };
   if (t0 >= t1) return;  // (grid <= tiles: never taken)
-  long long st_[6] = {0, 0, 0, 0, 0, 0};
-  if (a.stamps) st_[0] = __builtin_amdgcn_s_memrealtime();
   Src cur;
   load_src(t0, cur);
   f32x4 av[CH];
@@ -290,12 +261,6 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
     const bool more = tile + 1 < t1;  // uniform
     Src nxt;
     if (more) load_src(tile + 1, nxt);
-    long long ta = 0;
-    if (a.stamps) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      ta = __builtin_amdgcn_s_memrealtime();
-      if (tile == t0) st_[1] = ta;
-    }
     f32x4 acc[NCT];
 #pragma unroll
     for (int t = 0; t < NCT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -325,14 +290,7 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) pb[(g * 16 + 4 * kg + rr) * LDC + t * 16 + r16] = acc[t][rr];
     if (more) load_x(nxt, av);  // next tile's gathers in flight during the combine
-    long long tb = 0;
-    if (a.stamps) tb = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
-    if (a.stamps) {
-      const long long tc = __builtin_amdgcn_s_memrealtime();
-      st_[2] += tb - ta;  // MFMA + partial store
-      st_[3] += tc - tb;  // barrier wait
-    }
     const f32x4* pb4 = reinterpret_cast<const f32x4*>(pb);
     constexpr int N4 = 16 * COUT / 4;
     for (int q = threadIdx.x; q < N4; q += 576) {
@@ -358,17 +316,6 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
       st4(a.y + yo * COUT + 4 * c4, v);
     }
     cur = nxt;
-  }
-  if (a.stamps) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_[4] = __builtin_amdgcn_s_memrealtime();
-    st_[5] = t1 - t0;
-    if (lane < 6) {
-      long long v = st_[0];
-#pragma unroll
-      for (int k = 1; k < 6; ++k) v = lane == k ? st_[k] : v;
-      a.stamps[((long)blockIdx.x * 9 + g) * 8 + lane] = v;
-    }
   }
 }
 
@@ -493,7 +440,7 @@ __device__ __forceinline__ void conv_dx_ks_body(int vb, int vnb, const DxKsArgs&
   }
 }
 template <int CIN, int COUT, int NSG, int RT>
-__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_dx_ks(const DxKsArgs a) {
+__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_dx_ks(const DxKsArgs a) {
   conv_dx_ks_body<CIN, COUT, NSG, RT>(blockIdx.x, gridDim.x, a);
 }
 
@@ -502,7 +449,7 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_dx_ks(const 
 // workgroups alternate between the two halves while both last; the dW half
 // is conv_dw_lat_body with NSG waves per workgroup (same slabs, same values).
 template <int CIN, int COUT, int NSG, int RT>
-__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_bwd_ks_pair(const DxKsArgs a, const DwLatArgs d,
+__global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_bwd_ks_pair(const DxKsArgs a, const DwLatArgs d,
                                                                               int nb_dx) {
   const int bid = blockIdx.x, both = 2 * min(nb_dx, d.nb);
   bool is_dx;
@@ -522,158 +469,87 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG)) void conv_bwd_ks_pair(
 }
 
 // ------------------------------------------------------------------ host side
-// Geometry: slot groups and row tiles per workgroup.  More rows per
-// workgroup amortise the weight slices (each workgroup reads all of W once
-// from L2); more slot groups shorten each wave's MFMA chain.  Picked so the
-// grid holds >= ~2k waves (2 per SIMD) where the layer allows.
-template <int DX = 0>
-static bool parse_override(int& nsg, int& rt) {
-  static int cached = -2, cn = 0, cr = 0;
-  if (cached == -2) {
-    const char* e = getenv(DX ? "CFSD_KSDX" : "CFSD_KS");
-    cached = (e && sscanf(e, "%d:%d", &cn, &cr) == 2) ? 1 : (e && e[0] == '0' ? 0 : -1);
-  }
-  if (cached == 1) {
-    nsg = cn;
-    rt = cr;
-  }
-  return cached != 0;
-}
-
+// Geometry, measured (kbench under rocprofv3 kernel trace, batch 16; same-box
+// A/B of the slot-group / row-tile grids, profiles/r04*):
+//  * the ~1k-tile layers (E1, D1: 17k rows) take the persistent form -- E1
+//    32 -> 32 at 2 workgroups per CU 11.4 us (slot-group grids 11.3-13.8 us,
+//    conv_fwd_lat 16.6 us), D1 64 -> 32 at 1 per CU 15.5 us (slot-group grids
+//    18.5-22 us, conv_fwd_mfma + combine 22.2 us);
+//  * the <= 267-tile layers (E2, E3, D0) one 9-wave workgroup per tile (E2
+//    6.8, E3 6.6 us vs 7.7, 7.4 us); the fused up-sampling Deblock (D0) the
+//    persistent form;
+//  * the data gradient of the few-tile layers (D0) 9 slot groups x 2 tiles
+//    per workgroup, paired with the dW slabs (26 us vs 14.7 + 14.6 us).
 bool fwd_ks_enabled(long total_rows, int cin, int cout) {
-  int n = 0, r = 0;
-  if (!parse_override(n, r)) return false;
   return total_rows < kMaxRows && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
 }
 
 // (fused only on the few-tile layers: D0 17.5 us fused vs 4.9 + 13.9 us; on D1
 // the three-tap gathers cost more than the launch they save, 24.6 vs 6.4 + 15.5 us)
 bool fwd_up_supported(long total_rows, int cin, int cout) {
-  int n = 0, r = 0;
-  if (!parse_override(n, r)) return false;
   return total_rows < kMaxTilesFew * 16 && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
 }
 
-template <int DX = 0>
-static void pick(long total_rows, int cin, int cout, int& nsg, int& rt) {
-  // measured (kbench, rocprofv3 kernel trace, batch 16): the ~1k-tile layers
-  // (E1, D1) on the persistent form (E1 32->32 at 2 workgroups per CU 11.4 us
-  // vs 11.3-13.8 us slot-group grids and 16.6 us conv_fwd_lat; D1 64->32 at 1
-  // per CU 15.5 vs 18.5-22 and 22.2 us conv_fwd_mfma + combine), the <= 267-tile
-  // layers (E2, E3, D0) one 9-wave workgroup per tile (E2 6.8 / E3 6.6 vs 7.7 /
-  // 7.4 us); the data gradient: 9 slot groups, 2 tiles per workgroup at D0
-  // (13.7 vs 15.3 us), 3 slot groups at D1 (17.4 vs 19.9 us)
-  const long n_rt = (total_rows + 15) / 16;
-  if (DX) {
-    nsg = n_rt >= 512 ? 3 : 9;
-    rt = n_rt >= 512 ? 1 : 2;
-  } else if (n_rt >= 512) {
-    nsg = 0;
-    rt = cin * cout >= 64 * 32 ? 1 : 2;
-  } else {
-    nsg = 9;
-    rt = 1;
-  }
-  parse_override<DX>(nsg, rt);
-  if (nsg == 0) {
-    rt = rt < 1 ? 1 : (rt > 2 ? 2 : rt);
-    return;
-  }
-  if (nsg != 3 && nsg != 9) nsg = 9;
-  if (rt != 1 && rt != 2 && rt != 4) rt = 1;
+// (the ~1k-tile layers keep conv_bwd_lat_pair: D1 dx + dW 34.9 us paired vs
+// 17.2 + 19.6 us on the slot-group dx and a separate dW)
+bool dx_ks_enabled(long total_src_rows, int cin, int cout) {
+  return total_src_rows < kMaxTilesFew * 16 && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
 }
 
 template <int CIN, int COUT, int UP>
-static int launch_shape(const FwdKsArgs& a, int nsg, int rt, hipStream_t st) {
+static int launch_shape(const FwdKsArgs& a, hipStream_t st) {
   const long n_rt = (a.total_rows + 15) / 16;
-  if (nsg == 0) {  // persistent: rt workgroups per CU
-    const long grid = n_rt < 256L * rt ? n_rt : 256L * rt;
+  if (UP || n_rt >= kMaxTilesFew) {  // persistent: 1 (64-channel layers) or 2 workgroups per CU
+    const long per_cu = (UP || CIN * COUT >= 64 * 32) ? 1 : 2;
+    const long grid = n_rt < 256 * per_cu ? n_rt : 256 * per_cu;
     hipLaunchKernelGGL((conv_fwd_pt<CIN, COUT, UP>), dim3((unsigned)grid), dim3(576), 0, st, a);
     return launch_status("spiral_conv_fwd_pt");
   }
-#define KS(NSG_, RT_)                                                                                 \
-  if (nsg == NSG_ && rt == RT_) {                                                                     \
-    hipLaunchKernelGGL((conv_fwd_ks<CIN, COUT, NSG_, RT_, UP>), dim3((unsigned)((n_rt + RT_ - 1) / RT_)), \
-                       dim3(64 * NSG_), 0, st, a);                                                    \
-    return launch_status("spiral_conv_fwd_ks");                                                       \
+  if constexpr (!UP) {
+    hipLaunchKernelGGL((conv_fwd_ks<CIN, COUT, 9, 1, 0>), dim3((unsigned)n_rt), dim3(576), 0, st, a);
+    return launch_status("spiral_conv_fwd_ks");
   }
-  KS(3, 1) KS(3, 2) KS(3, 4) KS(9, 1) KS(9, 2) KS(9, 4)
-#undef KS
-  return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: bad geometry %d:%d", nsg, rt);
+  return CFSD_OK;
 }
 
 int launch_fwd_ks(const FwdKsArgs& a, int cin, int cout, hipStream_t st) {
   if (a.total_rows <= 0 || a.total_rows >= kMaxRows) return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: rows");
   const bool up = a.up_col != nullptr;
   if (up && a.xvm) return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: fused up-sampling needs batch-major input");
-  int nsg, rt;
-  pick(a.total_rows, cin, cout, nsg, rt);
-  if (up && nsg != 0) nsg = 0, rt = 1;  // (the fused up-sampling exists in the persistent form only)
 #define SHAPE(CI_, CO_)                                                         \
-  if (cin == CI_ && cout == CO_)                                                \
-    return up ? launch_shape<CI_, CO_, 1>(a, nsg, rt, st) : launch_shape<CI_, CO_, 0>(a, nsg, rt, st);
+  if (cin == CI_ && cout == CO_) return up ? launch_shape<CI_, CO_, 1>(a, st) : launch_shape<CI_, CO_, 0>(a, st);
   SHAPE(32, 32) SHAPE(32, 64) SHAPE(64, 32) SHAPE(64, 64)
 #undef SHAPE
   return set_error(CFSD_EINVAL, "spiral_conv_fwd_ks: unsupported channels %d -> %d", cin, cout);
 }
 
-// (the ~1k-tile layers keep conv_bwd_lat_pair: D1 dx + dW 34.9 us paired vs
-// 17.2 + 19.6 us on the slot-group dx and a separate dW)
-bool dx_ks_enabled(long total_src_rows, int cin, int cout) {
-  int n = 0, r = 0;
-  if (!parse_override<1>(n, r)) return false;
-  return total_src_rows < kMaxTilesFew * 16 && (cin == 32 || cin == 64) && (cout == 32 || cout == 64);
-}
-
-template <int CIN, int COUT>
-static int launch_pair_shape(const DxKsArgs& a, DwLatArgs d, long dw_tasks, int nsg, int rt, hipStream_t st) {
+int launch_bwd_ks_pair(const DxKsArgs& a, const DwLatArgs& d0, long dw_tasks, int cin, int cout, hipStream_t st) {
+  if (a.total_rows <= 0 || a.total_rows >= kMaxTilesFew * 16)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_ks_pair: rows");
   const long n_rt = (a.total_rows + 15) / 16;
-#define KS(NSG_, RT_)                                                                                     \
-  if (nsg == NSG_ && rt == RT_) {                                                                         \
-    const int nb_dx = (int)((n_rt + RT_ - 1) / RT_);                                                      \
-    d.nb = (int)((dw_tasks + NSG_ - 1) / NSG_);                                                           \
-    hipLaunchKernelGGL((conv_bwd_ks_pair<CIN, COUT, NSG_, RT_>), dim3((unsigned)(nb_dx + d.nb)), dim3(64 * NSG_), \
-                       0, st, a, d, nb_dx);                                                               \
+  const int nb_dx = (int)((n_rt + 1) / 2);
+  DwLatArgs d = d0;
+  d.nb = (int)((dw_tasks + 8) / 9);
+#define SHAPE(CI_, CO_)                                                                                   \
+  if (cin == CI_ && cout == CO_) {                                                                        \
+    hipLaunchKernelGGL((conv_bwd_ks_pair<CI_, CO_, 9, 2>), dim3((unsigned)(nb_dx + d.nb)), dim3(576), 0, st, a, \
+                       d, nb_dx);                                                                         \
     return launch_status("spiral_conv_bwd_ks_pair");                                                      \
   }
-  KS(3, 1) KS(3, 2) KS(9, 1) KS(9, 2)
-#undef KS
-  return set_error(CFSD_EINVAL, "spiral_conv_bwd_ks_pair: bad geometry %d:%d", nsg, rt);
-}
-
-int launch_bwd_ks_pair(const DxKsArgs& a, const DwLatArgs& d, long dw_tasks, int cin, int cout, hipStream_t st) {
-  if (a.total_rows <= 0 || a.total_rows >= kMaxRows) return set_error(CFSD_EINVAL, "spiral_conv_bwd_ks_pair: rows");
-  int nsg, rt;
-  pick<1>(a.total_rows, cout, cin, nsg, rt);
-  if (nsg == 0 || rt > 2) nsg = 9, rt = 1;
-#define SHAPE(CI_, CO_) \
-  if (cin == CI_ && cout == CO_) return launch_pair_shape<CI_, CO_>(a, d, dw_tasks, nsg, rt, st);
   SHAPE(32, 32) SHAPE(32, 64) SHAPE(64, 32) SHAPE(64, 64)
 #undef SHAPE
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_ks_pair: unsupported channels %d -> %d", cin, cout);
 }
 
-template <int CIN, int COUT>
-static int launch_dx_shape(const DxKsArgs& a, int nsg, int rt, hipStream_t st) {
-  const long n_rt = (a.total_rows + 15) / 16;
-#define KS(NSG_, RT_)                                                                                       \
-  if (nsg == NSG_ && rt == RT_) {                                                                           \
-    hipLaunchKernelGGL((conv_dx_ks<CIN, COUT, NSG_, RT_>), dim3((unsigned)((n_rt + RT_ - 1) / RT_)),          \
-                       dim3(64 * NSG_), 0, st, a);                                                          \
-    return launch_status("spiral_conv_bwd_data_ks");                                                        \
-  }
-  KS(3, 1) KS(3, 2) KS(3, 4) KS(9, 1) KS(9, 2) KS(9, 4)
-#undef KS
-  return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_ks: bad geometry %d:%d", nsg, rt);
-}
-
 int launch_dx_ks(const DxKsArgs& a, int cin, int cout, hipStream_t st) {
-  if (a.total_rows <= 0 || a.total_rows >= kMaxRows) return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_ks: rows");
-  int nsg, rt;
-  pick<1>(a.total_rows, cout, cin, nsg, rt);
-  if (nsg == 0) nsg = 9, rt = 1;  // (no persistent data-gradient form yet)
-#define SHAPE(CI_, CO_) \
-  if (cin == CI_ && cout == CO_) return launch_dx_shape<CI_, CO_>(a, nsg, rt, st);
+  if (a.total_rows <= 0 || a.total_rows >= kMaxTilesFew * 16)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_ks: rows");
+  const long n_rt = (a.total_rows + 15) / 16;
+#define SHAPE(CI_, CO_)                                                                                          \
+  if (cin == CI_ && cout == CO_) {                                                                               \
+    hipLaunchKernelGGL((conv_dx_ks<CI_, CO_, 9, 2>), dim3((unsigned)((n_rt + 1) / 2)), dim3(576), 0, st, a);    \
+    return launch_status("spiral_conv_bwd_data_ks");                                                             \
+  }
   SHAPE(32, 32) SHAPE(32, 64) SHAPE(64, 32) SHAPE(64, 64)
 #undef SHAPE
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_ks: unsupported channels %d -> %d", cin, cout);

@@ -31,12 +31,8 @@ int launch_dw(const bf16_t* x, int xvm, const int* idx, const void* dpre, int dp
 // Vertex-major operands with batch % 16 == 0 (spiral_conv_vm16.hip): one
 // 16-row MFMA tile = one vertex x 16 meshes.
 bool vm16_ok(int batch, int cin, int cout);
-#ifndef CFSD_DW_VM16
-#define CFSD_DW_VM16 1
-#endif
-#ifndef CFSD_DW_VM16_F32DP
-#define CFSD_DW_VM16_F32DP 1
-#endif
+constexpr int kDwVm16 = 1;
+constexpr int kDwVm16F32dp = 1;
 // bf16 32 -> 32 weight gradient with vertex-major bf16 x and a vertex-major
 // bf16 (or batch-major fp32: an Enblock's kept rows) dpre: conv_dw_vm16,
 // n_slabs plain slabs (the conv_dw_b16 layout and count, dw_slabs())

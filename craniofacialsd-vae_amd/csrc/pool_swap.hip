@@ -589,15 +589,9 @@ extern "C" int cfsd_spmm_csr_x(const int32_t* row_ptr, const int32_t* col, const
   return spmm_launch(row_ptr, col, val, nullptr, x, x_dt, elu_y, y, y_dt, batch, m, n, c, stream);
 }
 
-#ifndef CFSD_SPMM_UVM
-#define CFSD_SPMM_UVM 1
-#endif
-#ifndef CFSD_SPMM_UVM_RW
-#define CFSD_SPMM_UVM_RW 4
-#endif
-#ifndef CFSD_SPMM_URPT
-#define CFSD_SPMM_URPT 4
-#endif
+constexpr int kSpmmUvm = 1;
+constexpr int kSpmmUvmRw = 4;
+constexpr int kSpmmUrpt = 4;
 extern "C" int cfsd_spmm_uniform(int k, const int32_t* col, const float* val, const void* x,
                                  int x_dt, const void* elu_y, void* y, int y_dt, int batch, int m,
                                  int n, int c, void* stream) {
@@ -610,9 +604,9 @@ extern "C" int cfsd_spmm_uniform(int k, const int32_t* col, const float* val, co
   const long total = (long)batch * m * (c / 4);
   if (total >= (1L << 31) || (long)batch * n >= (1L << 31) || (long)m * k >= (1L << 31))
     return set_error(CFSD_EINVAL, "spmm_uniform: sizes >= 2^31 (32-bit indices)");
-  if (CFSD_SPMM_UVM && xvm && yvm && !elu_y && k == 3 && (batch * (c / 4)) % 64 == 0 &&
+  if (kSpmmUvm && xvm && yvm && !elu_y && k == 3 && (batch * (c / 4)) % 64 == 0 &&
       (long)n * batch * c * 4 < 0x7ffff000L) {  // vertex-major: wave-uniform rows
-    constexpr int RW = CFSD_SPMM_UVM_RW;
+    constexpr int RW = kSpmmUvmRw;
     const int rowq = batch * (c / 4), wpr = rowq / 64;
     const long waves = (long)((m + RW - 1) / RW) * wpr;
     const unsigned nb = (unsigned)((waves + 3) / 4);
@@ -627,7 +621,7 @@ extern "C" int cfsd_spmm_uniform(int k, const int32_t* col, const float* val, co
 #undef SPUV
     return launch_status("spmm_uniform_vm");
   }
-  constexpr int RPT = CFSD_SPMM_URPT;
+  constexpr int RPT = kSpmmUrpt;
   const long per_grp = (total + 7) / 8;
   const unsigned nblk = (unsigned)(8 * ((per_grp + 256 * RPT - 1) / (256 * RPT)));
   const hipStream_t st = (hipStream_t)stream;

@@ -425,10 +425,8 @@ __device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
-#ifndef CFSD_DX_OCC
-#define CFSD_DX_OCC 3
-#endif
-constexpr int dx_occ(int cin, int cout) { return (cin == 32 && cout == 32) ? CFSD_DX_OCC : 2; }
+constexpr int kDxOcc = 3;
+constexpr int dx_occ(int cin, int cout) { return (cin == 32 && cout == 32) ? kDxOcc : 2; }
 
 template <int CIN, int COUT, int SPG>
 __global__ __launch_bounds__(256, dx_occ(CIN, COUT)) void conv_dx_mfma(
@@ -556,12 +554,8 @@ __global__ __launch_bounds__(256, dx_occ(CIN, COUT)) void conv_dx_mfma(
 // two accumulators (even / odd chunk) halve the dependent-MFMA chain.
 // Tasks are numbered column-tile fastest, so the waves of a workgroup
 // gather the same rows (L1 hits).
-#ifndef CFSD_FWD_LAT_SB
-#define CFSD_FWD_LAT_SB 3
-#endif
-#ifndef CFSD_DX_LAT_SB
-#define CFSD_DX_LAT_SB 3
-#endif
+constexpr int kFwdLatSb = 3;
+constexpr int kDxLatSb = 3;
 template <int CIN, int COUT, int ACT, int CTW>
 __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
                                                     const int* __restrict__ idx,
@@ -571,7 +565,7 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
                                                     long total_rows, int batch, int xvm, int yvm) {
   // CTW column tiles per wave share the wave's A gathers
   constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN, NTW = NCT / CTW;
-  constexpr int FSB = CFSD_FWD_LAT_SB;
+  constexpr int FSB = kFwdLatSb;
   static_assert(kSeq % FSB == 0, "slot batches");
   static_assert(NCT % CTW == 0, "column tiles per wave");
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
@@ -664,7 +658,7 @@ __device__ __forceinline__ void conv_dx_lat_body(int vb, int vnb, const float* _
                                                  float* __restrict__ dx, int vsrc, int rows,
                                                  long total_rows) {
   constexpr int CH = COUT / 16, NCT = CIN / 16, K = kSeq * CIN, NTW = NCT / CTW;
-  constexpr int DSB = CFSD_DX_LAT_SB;
+  constexpr int DSB = kDxLatSb;
   static_assert(kSeq % DSB == 0, "slot batches");
   static_assert(NCT % CTW == 0, "column tiles per wave");
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
@@ -1771,11 +1765,9 @@ __device__ __forceinline__ void load_row(__amdgpu_buffer_rsrc_t rsrc, int off, f
   }
 }
 constexpr int kAtS = 36;  // At row stride: conflict-free ds_read_b128 of the dW A operand
-#ifndef CFSD_BWD_OUT_OCC
-#define CFSD_BWD_OUT_OCC 1
-#endif
+constexpr int kBwdOutOcc = 1;
 template <int CIN, int CO, typename TX = float>
-__global__ __launch_bounds__(256, CFSD_BWD_OUT_OCC) void conv_bwd_out_mfma(
+__global__ __launch_bounds__(256, kBwdOutOcc) void conv_bwd_out_mfma(
     const float* __restrict__ dpre, const int* __restrict__ inv_ptr,
     const int* __restrict__ inv_row, const int4* __restrict__ inv_head,
     const float* __restrict__ w, const TX* __restrict__ elu_y, const TX* __restrict__ x,
@@ -2081,15 +2073,9 @@ static int launch_fwd_mfma(const float* x, const int* idx, const float* w, const
 
 // Rows below which the latency-shaped kernels (conv_fwd_lat / conv_dx_lat)
 // beat the persistent ones (fewer 32-row tiles than ~8 per CU).
-#ifndef CFSD_LAT_MAX_ROWS
-#define CFSD_LAT_MAX_ROWS 65536
-#endif
-#ifndef CFSD_LAT_FWD_MAX
-#define CFSD_LAT_FWD_MAX CFSD_LAT_MAX_ROWS
-#endif
-#ifndef CFSD_LAT_DW_MAX
-#define CFSD_LAT_DW_MAX CFSD_LAT_MAX_ROWS
-#endif
+constexpr int kLatMaxRows = 65536;
+constexpr int kLatFwdMax = kLatMaxRows;
+constexpr int kLatDwMax = kLatMaxRows;
 
 
 // coarse levels: slot groups in one workgroup, partials combined in LDS
@@ -2153,19 +2139,15 @@ static int dispatch_fwd_mfma(const float* x, const int* idx, const float* w, con
   if (coarse::fwd_ks_enabled(M, CIN, COUT))
     return fwd_coarse(x, 0, idx, w, bias, y, 0, vsrc, rows, (int)(M / rows), CIN, COUT, ACT, st);
   // (64 -> 32 excepted: measured slower there than slot groups + combine)
-#ifndef CFSD_FWD_LAT_6432
-#define CFSD_FWD_LAT_6432 0
-#endif
-  if (M < CFSD_LAT_FWD_MAX && (CFSD_FWD_LAT_6432 || !(CIN == 64 && COUT == 32))) {
-#ifndef CFSD_FWD_LAT_CTW
-#define CFSD_FWD_LAT_CTW 1
-#endif
+constexpr int kFwdLat6432 = 0;
+  if (M < kLatFwdMax && (kFwdLat6432 || !(CIN == 64 && COUT == 32))) {
+constexpr int kFwdLatCtw = 1;
     // one wave per column tile: sharing the A gathers across both 32 -> 32
     // column tiles (CTW 2) measured slower here (E1 16.8 vs 16.1 us, E2 11.0
     // vs 7.8 us, same-box A/B) -- unlike the dx, whose A is a list gather-sum
     // 64 -> 64 (the level-3 Deblock): two column tiles per wave, each A
     // gather feeding twice the MFMAs (D0 forward 19.1 -> 16.3 us)
-    constexpr int ctw = (CIN == 32 && COUT == 32) ? CFSD_FWD_LAT_CTW : (CIN == 64 ? 2 : 1);
+    constexpr int ctw = (CIN == 32 && COUT == 32) ? kFwdLatCtw : (CIN == 64 ? 2 : 1);
     const long tasks = (M + 15) / 16 * (COUT / 16 / ctw);
     hipLaunchKernelGGL((conv_fwd_lat<CIN, COUT, ACT, ctw>), dim3((unsigned)((tasks + 3) / 4)),
                        dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, M, (int)(M / rows), 0, 0);
@@ -2274,22 +2256,18 @@ static int launch_dx_mfma(const float* dpre, const int* inv_ptr, const int* inv_
 // of 9; each persistent block would stage W for ~2 tiles) -- measured on the
 // 68k-row E1 dx: 33.8 us latency-shaped vs 38.8 us persistent
 static bool dx_is_lat(long m_dx, long dpre_rows) {
-  return m_dx < CFSD_LAT_MAX_ROWS || (m_dx < 80000 && 2 * dpre_rows <= m_dx);
+  return m_dx < kLatMaxRows || (m_dx < 80000 && 2 * dpre_rows <= m_dx);
 }
 // 32 -> 32 with >= 32k rows: one wave covers both 16-column tiles (the list
 // gathers are shared instead of repeated per column tile; measured E1 dx
 // 33 -> 29 us; the fewer, fatter waves lose on the smaller levels)
-#ifndef CFSD_DX_LAT_CTW64
-#define CFSD_DX_LAT_CTW64 2
-#endif
-#ifndef CFSD_DX_LAT_CTW6432
-#define CFSD_DX_LAT_CTW6432 2
-#endif
+constexpr int kDxLatCtw64 = 2;
+constexpr int kDxLatCtw6432 = 2;
 static int dx_lat_ctw(int cin, int cout, long m_dx) {
   // 64-wide inputs: two column tiles per wave share the list gather-sums
   // (D0 dx 18.6 -> 15.2 us; the D1 paired backward 40.7 -> 36.9 us)
-  if (cin == 64 && cout == 64) return CFSD_DX_LAT_CTW64;
-  if (cin == 64 && cout == 32) return CFSD_DX_LAT_CTW6432;
+  if (cin == 64 && cout == 64) return kDxLatCtw64;
+  if (cin == 64 && cout == 32) return kDxLatCtw6432;
   return (cin == 32 && cout == 32 && m_dx >= 32768) ? 2 : 1;
 }
 
@@ -2389,16 +2367,14 @@ int dw_mfma_slabs(int cin, int cout, int gx) {
   return gx < cap ? gx : cap;
 }
 
-#ifndef CFSD_DW_LAT_WAVES
-#define CFSD_DW_LAT_WAVES 2048
-#endif
+constexpr int kDwLatWaves = 2048;
 DwGeom dw_geom(int batch, int rows, int cin, int cout) {
   DwGeom g{kDwNone, 0, 0, 0};
   const long M = (long)batch * rows;
-  if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64) && M < CFSD_LAT_DW_MAX) {
+  if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64) && M < kLatDwMax) {
     // few rows: one wave per (dW unit, row chunk); ~2k waves
     const long U = (long)dw_units(cin, cout);
-    long R = (M * U / CFSD_DW_LAT_WAVES + 15) / 16 * 16;
+    long R = (M * U / kDwLatWaves + 15) / 16 * 16;
     R = R < 32 ? 32 : (R > 512 ? 512 : R);
     g.kind = kDwLat;
     g.rchunk = (int)R;
@@ -2407,14 +2383,10 @@ DwGeom dw_geom(int batch, int rows, int cin, int cout) {
   } else if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64)) {
     g.kind = kDwMfma;
     const long n_tiles = (M + 31) / 32;
-#ifndef CFSD_DW_TPB
-#define CFSD_DW_TPB 4
-#endif
-    long gx = (n_tiles + CFSD_DW_TPB - 1) / CFSD_DW_TPB;  // >= 4 tiles per block keeps the slab traffic bounded
-#ifndef CFSD_DW_MAX_WG
-#define CFSD_DW_MAX_WG 512  // (768: same time, 1.5x the slab traffic)
-#endif
-    if (gx > CFSD_DW_MAX_WG) gx = CFSD_DW_MAX_WG;  // 2 blocks of 9 waves per CU
+constexpr int kDwTpb = 4;
+    long gx = (n_tiles + kDwTpb - 1) / kDwTpb;  // >= 4 tiles per block keeps the slab traffic bounded
+constexpr int kDwMaxWg = 512;  // (768: same time, 1.5x the slab traffic)
+    if (gx > kDwMaxWg) gx = kDwMaxWg;  // 2 blocks of 9 waves per CU
     g.gx = (int)(gx > 0 ? gx : 1);
     g.ws_floats = (size_t)g.gx * dw_units(cin, cout) * 1024 + (size_t)g.gx * cout;
   } else if (cin <= 3 && (cout == 32 || cout == 64)) {
@@ -2445,12 +2417,10 @@ extern "C" size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int
   return dw_geom(batch, rows, cin, cout).ws_floats * sizeof(float);
 }
 
-#ifndef CFSD_DW_VM32
-#define CFSD_DW_VM32 1  // 32 -> 32 with vertex-major x and dpre: vm32::conv_dw_vm32
-#endif
+constexpr int kDwVm32 = 1;  // 32 -> 32 with vertex-major x and dpre: vm32::conv_dw_vm32
 // The fp32 weight gradient takes vm32::conv_dw_vm32 (its slabs: cfsd_dw_slabs.fused == 3)
 static bool dw_vm32_path(int xvm, int dpvm, int cin, int cout, int batch) {
-  return CFSD_DW_VM32 && xvm && dpvm && cin == 32 && cout == 32 && batch % 16 == 0;
+  return kDwVm32 && xvm && dpvm && cin == 32 && cout == 32 && batch % 16 == 0;
 }
 // dW / db of an fp32 conv, x and dpre each batch-major or vertex-major
 // (xvm / dpvm; the small-channel kernels are batch-major only).
@@ -2920,7 +2890,7 @@ extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* id
     if (y_dt != CFSD_DT_F32) return set_error(CFSD_EINVAL, "spiral_conv_fwd_x: fp32 x needs fp32 y");
     if (coarse::fwd_ks_enabled(M, cin, cout))
       return fwd_coarse((const float*)x, xvm, idx, w, bias, (float*)y, yvm, vsrc, rows, batch, cin, cout, act, st);
-    if (M < CFSD_LAT_FWD_MAX && cin == 32 && cout == 32) {  // few rows (an Enblock's kept rows): 16x16 tasks
+    if (M < kLatFwdMax && cin == 32 && cout == 32) {  // few rows (an Enblock's kept rows): 16x16 tasks
       const long tasks = (M + 15) / 16 * 2;
       if (act == CFSD_ACT_ELU)
         hipLaunchKernelGGL((conv_fwd_lat<32, 32, CFSD_ACT_ELU, 1>), dim3((unsigned)((tasks + 3) / 4)), dim3(256),

@@ -431,15 +431,13 @@ int launch_dx(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_data (bf16): unsupported channels %d -> %d", cin, cout);
 }
 
-#ifndef CFSD_DW16_UPB
-#define CFSD_DW16_UPB 8
-#endif
+constexpr int kDw16Upb = 8;
 int dw_slabs(int batch, int rows, int cin, int cout) {
   const long tiles = ((long)batch * rows + 31) / 32;
   const int G = 16 / ((cout / 16) * (cin / 16)) > 0 ? 16 / ((cout / 16) * (cin / 16)) : 1;
   // >= ~4 tiles per group (conv_dw_b16); conv_dw_vm16 (cin = cout = 32):
-  // >= CFSD_DW16_UPB 16-row units per workgroup
-  long gx = (CFSD_DW16_UPB > 0 && cin == 32 && cout == 32) ? (2 * tiles + CFSD_DW16_UPB - 1) / CFSD_DW16_UPB
+  // >= kDw16Upb 16-row units per workgroup
+  long gx = (kDw16Upb > 0 && cin == 32 && cout == 32) ? (2 * tiles + kDw16Upb - 1) / kDw16Upb
                                                            : (tiles + 4 * G - 1) / (4 * G);
   if (gx > 256) gx = 256;                   // one workgroup per CU: bounded slab traffic
   return (int)(gx < 1 ? 1 : gx);

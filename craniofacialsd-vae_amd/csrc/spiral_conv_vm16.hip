@@ -431,9 +431,7 @@ __global__ __launch_bounds__(512) void conv_dx_flat_vm16(const TD* __restrict__ 
 // flight in registers during this unit's MFMAs.  Workgroup = 4 ranges x 3
 // slot groups (12 waves, one per CU), summed in LDS in fixed order into one
 // plain slab [32 * 288 + 32] (the conv_dw_b16 layout, dw_reduce_batch kind 1).
-#ifndef CFSD_DW16_PD
-#define CFSD_DW16_PD 2
-#endif
+constexpr int kDw16Pd = 2;
 constexpr int DW16_NR = 4, DW16_WAVES = DW16_NR * 3, DW16_THREADS = DW16_WAVES * 64;
 typedef short s16x4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4v lds_s16x4v;
@@ -481,7 +479,7 @@ __global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __res
   float dbs = 0.f;
   // DW16_PD units' blocks in flight (a unit is only 3 MFMAs: one unit ahead
   // left every unit waiting out a memory latency)
-  constexpr int PD = CFSD_DW16_PD;
+  constexpr int PD = kDw16Pd;
   u32x4 ring[PD][1 + NS];
   auto load_unit = [&](long un, u32x4 (&b)[1 + NS]) {
     const int uu = uni((int)un);
@@ -570,8 +568,8 @@ static int fwd16_t(const bf16_t* x, const int* idx, const bf16_t* w, const float
 }
 
 bool dw_vm16_ok(int batch, int cin, int cout, int xvm, int dpvm, int dpre_bf16) {
-  return CFSD_DW_VM16 && batch % 16 == 0 && cin == 32 && cout == 32 && xvm &&
-         ((dpre_bf16 && dpvm) || (CFSD_DW_VM16_F32DP && !dpre_bf16 && !dpvm));
+  return kDwVm16 && batch % 16 == 0 && cin == 32 && cout == 32 && xvm &&
+         ((dpre_bf16 && dpvm) || (kDwVm16F32dp && !dpre_bf16 && !dpvm));
 }
 
 int launch_dw_vm16(const bf16_t* x, const int* idx, const void* dpre, int dpre_bf16, float* ws, int n_slabs, int vsrc,

@@ -51,11 +51,9 @@ __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t rs, int voff, int
 // kernel's B fragment, unchanged).  Slot s + PD's gathers are in flight while
 // slot s runs its MFMAs.  y vertex-major (yvm) or batch-major (the Enblock
 // evaluated at the kept rows writes the coarser, batch-major level).
-#ifndef CFSD_VM32_FWD_OCC
-#define CFSD_VM32_FWD_OCC 4  // waves per SIMD (VGPR budget 128)
-#endif
+constexpr int kVm32FwdOcc = 4;  // waves per SIMD (VGPR budget 128)
 template <int CIN, int COUT, int ACT, int UPT, int PD>
-__global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const float* __restrict__ x,
+__global__ __launch_bounds__(256, kVm32FwdOcc) void conv_fwd_vm32(const float* __restrict__ x,
                                                      const int* __restrict__ idx,
                                                      const float* __restrict__ w,
                                                      const float* __restrict__ bias,
@@ -161,14 +159,10 @@ __global__ __launch_bounds__(256, CFSD_VM32_FWD_OCC) void conv_fwd_vm32(const fl
 // first), so the walk stops at the first -1 (uniform branch) and the
 // prefetches past the end are out-of-range loads (no memory access).  The
 // next tile's list is loaded at the start of this one.
-#ifndef CFSD_VM32_DX_PD
-#define CFSD_VM32_DX_PD 2  // list entries in flight ahead of the one being multiplied
-#endif
-#ifndef CFSD_VM32_DX_OCC
-#define CFSD_VM32_DX_OCC 1
-#endif
+constexpr int kVm32DxPd = 2;  // list entries in flight ahead of the one being multiplied
+constexpr int kVm32DxOcc = 1;
 template <int CIN, int COUT, int FW>
-__global__ __launch_bounds__(512, CFSD_VM32_DX_OCC) void conv_dx_flat_vm32(const float* __restrict__ dpre,
+__global__ __launch_bounds__(512, kVm32DxOcc) void conv_dx_flat_vm32(const float* __restrict__ dpre,
                                                          const int4* __restrict__ flat,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ elu_y,
@@ -216,7 +210,7 @@ __global__ __launch_bounds__(512, CFSD_VM32_DX_OCC) void conv_dx_flat_vm32(const
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    constexpr int PD = CFSD_VM32_DX_PD, NB = PD + 1;
+    constexpr int PD = kVm32DxPd, NB = PD + 1;
     f32x4 buf[NB][OC];
 #pragma unroll
     for (int e = 0; e < PD; ++e) issue(e, buf[e]);
@@ -277,13 +271,9 @@ __global__ __launch_bounds__(512, CFSD_VM32_DX_OCC) void conv_dx_flat_vm32(const
 // of 4 waves per CU).  The 4 waves' accumulators are summed in LDS in fixed
 // order into one conv_dw_mfma-layout slab ([9][32][32] + db[32]) per
 // workgroup, reduced by conv_dw_reduce / dw_reduce_batch (kind 0).
-#ifndef CFSD_DWV_NS
-#define CFSD_DWV_NS 3  // slots per wave (3: a slot group of three, 9: all nine)
-#endif
-#ifndef CFSD_DWV_NR
-#define CFSD_DWV_NR 4  // unit ranges per workgroup (waves = NR * 9 / NS)
-#endif
-constexpr int DWV_NS = CFSD_DWV_NS, DWV_NR = CFSD_DWV_NR, DWV_WAVES = DWV_NR * (kS / DWV_NS);
+constexpr int kDwvNs = 3;  // slots per wave (3: a slot group of three, 9: all nine)
+constexpr int kDwvNr = 4;  // unit ranges per workgroup (waves = NR * 9 / NS)
+constexpr int DWV_NS = kDwvNs, DWV_NR = kDwvNr, DWV_WAVES = DWV_NR * (kS / DWV_NS);
 constexpr int DWV_THREADS = DWV_WAVES * 64;
 __global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restrict__ x,
                                                             const int* __restrict__ idx,
@@ -590,9 +580,7 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
 // Per output the products are accumulated in conv_fwd_out_small's order
 // (slot by slot, 4 channels by fmaf per lane, then the xor tree 4, 2, 1 over
 // the 8 lanes of the row, then the bias), so both layouts give the same bits.
-#ifndef CFSD_VM_OUT_U
-#define CFSD_VM_OUT_U 1
-#endif
+constexpr int kVmOutU = 1;
 template <int CO, int ACT, int U, typename TX>
 __global__ __launch_bounds__(256) void conv_fwd_out_vm(const TX* __restrict__ x, const int* __restrict__ idx,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
@@ -703,19 +691,15 @@ static int fwd_t(const float* x, const int* idx, const float* w, const float* bi
 // Units (vertex x 16 meshes) below which a wave takes ONE unit with two slots
 // in flight (the level-1 row subset of an Enblock: ~1k units), else two units
 // (more MFMA work per gathered slot) with one slot in flight.
-#ifndef CFSD_VM32_UPT1_UNITS
-#define CFSD_VM32_UPT1_UNITS 8192
-#endif
-#ifndef CFSD_VM32_PD2
-#define CFSD_VM32_PD2 1  // slots in flight ahead with two units per tile
-#endif
+constexpr int kVm32Upt1Units = 8192;
+constexpr int kVm32Pd2 = 1;  // slots in flight ahead with two units per tile
 
 template <int COUT, int ACT>
 static int fwd_pick(const float* x, const int* idx, const float* w, const float* bias, float* y, int yvm,
                     int vsrc, int rows, int batch, hipStream_t st) {
-  if ((long)rows * (batch / 16) < CFSD_VM32_UPT1_UNITS)
+  if ((long)rows * (batch / 16) < kVm32Upt1Units)
     return fwd_t<32, COUT, ACT, 1, 2>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
-  return fwd_t<32, COUT, ACT, 2, CFSD_VM32_PD2>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
+  return fwd_t<32, COUT, ACT, 2, kVm32Pd2>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
 }
 
 int launch_fwd(const float* x, const int* idx, const float* w, const float* bias, float* y, int yvm, int vsrc,
@@ -761,7 +745,7 @@ int launch_dx_flat(const float* dpre, const int* flat, int width, const float* w
 template <int CO, int ACT, typename TX>
 static int fwd_out_t(const TX* x, const int* idx, const float* w, const float* bias, float* y, int yvm, int vsrc,
                      int rows, int batch, hipStream_t st) {
-  constexpr int U = CFSD_VM_OUT_U;
+  constexpr int U = kVmOutU;
   auto kern = conv_fwd_out_vm<CO, ACT, U, TX>;
   const long its = ((long)rows * (batch / 8) + U - 1) / U;
   const unsigned grid = balanced_blocks(its, 4, resident(kern, 256, 0));

@@ -206,10 +206,8 @@ __global__ __launch_bounds__(256) void recon_lap_bwd_k(
 // 16 waves: the LC distance and gradient phases are chains of dependent LDS
 // reads that one wave per SIMD cannot hide (256: 16.0 us, 512: 11.4,
 // 1024: 9.8, same-box A/B in the step).
-#ifndef CFSD_LAT_THREADS
-#define CFSD_LAT_THREADS 1024
-#endif
-__global__ __launch_bounds__(CFSD_LAT_THREADS) void latent_fwd_k(const float* __restrict__ mulv,
+constexpr int kLatThreads = 1024;
+__global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const float* __restrict__ mulv,
                                                     const float* __restrict__ eps,
                                                     const int* __restrict__ key,
                                                     float* __restrict__ z,
@@ -222,7 +220,7 @@ __global__ __launch_bounds__(CFSD_LAT_THREADS) void latent_fwd_k(const float* __
   extern __shared__ float lat_lds[];
   float* zs = lat_lds;
   float* dist = lat_lds + B * L;
-  __shared__ float2 red[CFSD_LAT_THREADS / 64];
+  __shared__ float2 red[kLatThreads / 64];
   const int tid = threadIdx.x;
   const int ldm = is_vae ? 2 * L : L;
   const int mu_off = is_vae ? L : 0;
@@ -991,7 +989,7 @@ extern "C" int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_
       hipFuncSetAttribute((const void*)latent_fwd_k, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)kLatLdsMax) != hipSuccess)
     return set_error(CFSD_EINVAL, "latent_fwd: cannot raise the dynamic LDS limit");
-  hipLaunchKernelGGL(latent_fwd_k, dim3(1), dim3(CFSD_LAT_THREADS), lds, (hipStream_t)stream, mulv, eps, key, z,
+  hipLaunchKernelGGL(latent_fwd_k, dim3(1), dim3(kLatThreads), lds, (hipStream_t)stream, mulv, eps, key, z,
                      dlat, terms, batch, latent, region_size, train, is_vae, sigmoid, w_kl, w_lc,
                      eta1, eta2, bs);
   return launch_status("latent_fwd");

@@ -1,17 +1,18 @@
 #!/bin/bash
-# Experimental timing variants of libcfsd.so (macro switches), into variants/ (git-ignored).
+# A/B libraries: builds libcfsd.so as of other git revisions into variants/
+# (git-ignored), for ab_kernel.sh / kb_variants.sh / bench_variants.sh.
+# usage: bash tools/build_variants.sh name:rev [name:rev ...]
+#   e.g. bash tools/build_variants.sh prev:HEAD~1 r03:r03-tag
+# (Kernel geometry is compiled in as constants; variants are revisions, not -D switches.)
 set -e
-cd "$(dirname "$0")/../craniofacialsd-vae_amd/csrc"
-mkdir -p ../../variants
-H=/opt/rocm/bin/hipcc
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950"
+cd "$(dirname "$0")/.."
+mkdir -p variants
 for v in "$@"; do
-  name=${v%%:*}; defs=${v#*:}
-  mkdir -p /tmp/var_$name
-  for f in spiral_conv spiral_conv_bf16 spiral_conv_vm16 spiral_conv_vm32 pool_swap train_ops; do
-    $H $F $defs -c $f.hip -o /tmp/var_$name/$f.o &
-  done
-  wait
-  $H -shared --offload-arch=gfx950 -o ../../variants/libcfsd_$name.so /tmp/var_$name/*.o
-  echo built $name
+  name=${v%%:*}; rev=${v#*:}
+  tmp=/tmp/var_$name
+  rm -rf $tmp && mkdir -p $tmp
+  git archive "$rev" craniofacialsd-vae_amd/csrc include | tar -x -C $tmp
+  make -C $tmp/craniofacialsd-vae_amd/csrc -j8 > $tmp/build.log 2>&1
+  cp $tmp/craniofacialsd-vae_amd/libcfsd.so variants/libcfsd_$name.so
+  echo built $name from $rev
 done

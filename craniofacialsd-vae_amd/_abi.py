@@ -68,6 +68,9 @@ SIGNATURES = {
     "cfsd_recon_lap_bwd_finalize_x": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P, _I, _P, _P,
                                            _P, _F, _F, _I, _P]),
     "cfsd_latent_fwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F, _P]),
+    "cfsd_latent_linear_fwd_supported": (_I, [_I, _I, _I]),
+    "cfsd_latent_linear_fwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _F, _F,
+                                    _P, _P, _P, _I, _P]),
     "cfsd_latent_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_loss_finalize": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P]),
     "cfsd_adam": (_I, [_P, _P, _P, _P, _P, _Z, _F, _F, _F, _F, _F, _P, _P]),

@@ -207,23 +207,30 @@ __global__ __launch_bounds__(256) void recon_lap_bwd_k(
 // reads that one wave per SIMD cannot hide (256: 16.0 us, 512: 11.4,
 // 1024: 9.8, same-box A/B in the step).
 constexpr int kLatThreads = 1024;
-__global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const float* __restrict__ mulv,
-                                                    const float* __restrict__ eps,
-                                                    const int* __restrict__ key,
-                                                    float* __restrict__ z,
-                                                    float* __restrict__ dlat,
-                                                    float* __restrict__ terms, int B, int L,
-                                                    int region_size, int train, int is_vae,
-                                                    int sigmoid, float w_kl, float w_lc,
-                                                    float eta1, float eta2, int bs) {
-  // dynamic LDS: z [B][L], then the distances [kind][pair][t] (4 npairs bs)
-  extern __shared__ float lat_lds[];
-  float* zs = lat_lds;
-  float* dist = lat_lds + B * L;
-  __shared__ float2 red[kLatThreads / 64];
+struct LatentArgs {
+  const float* mulv;
+  const float* eps;
+  const int* key;
+  float* z;
+  float* dlat;
+  float* terms;
+  int B, L, region_size, train, is_vae, sigmoid;
+  float w_kl, w_lc, eta1, eta2;
+  int bs;
+};
+
+// The latent head on one workgroup's LDS (zs [B][L], dist [4 npairs bs]).
+// Every workgroup that runs it holds all of z and the LC distances; the
+// `lead` one also writes z, the KL gradient pieces and terms[], and each
+// writes the LC gradient elements [g0, g1) (one workgroup: [0, B L)).
+// Each output element is the same expression whichever workgroup computes it.
+__device__ __forceinline__ void latent_body(const LatentArgs& a, float* zs, float* dist, float2* red,
+                                            bool lead, int g0, int g1) {
+  const int B = a.B, L = a.L, bs = a.bs;
+  const float w_lc = a.w_lc;
   const int tid = threadIdx.x;
-  const int ldm = is_vae ? 2 * L : L;
-  const int mu_off = is_vae ? L : 0;
+  const int ldm = a.is_vae ? 2 * L : L;
+  const int mu_off = a.is_vae ? L : 0;
   // z and KL pieces.  The inputs of up to 8 elements per thread are loaded
   // before any is used (mulv was just written by the encoder Linear, possibly
   // on another XCD: each dependent load round trip is ~1-2 us here).
@@ -236,9 +243,9 @@ __global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const float* __restr
       const int e = e0 + k * blockDim.x;
       const int ec = e < B * L ? e : B * L - 1;
       const int i = ec / L, l = ec % L;
-      mu_r[k] = mulv[i * ldm + mu_off + l];
-      lv_r[k] = is_vae ? mulv[i * ldm + l] : 0.f;
-      ep_r[k] = (is_vae && train) ? eps[ec] : 0.f;
+      mu_r[k] = a.mulv[i * ldm + mu_off + l];
+      lv_r[k] = a.is_vae ? a.mulv[i * ldm + l] : 0.f;
+      ep_r[k] = (a.is_vae && a.train) ? a.eps[ec] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
@@ -247,19 +254,23 @@ __global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const float* __restr
       const int i = e / L, l = e % L;
       const float mu = mu_r[k];
       float zz = mu;
-      if (is_vae) {
+      if (a.is_vae) {
         const float lv = lv_r[k];
         const float ex = expf(lv);
-        if (train) zz = mu + ep_r[k] * expf(0.5f * lv);
+        if (a.train) zz = mu + ep_r[k] * expf(0.5f * lv);
         kl_part += 1.f + lv - mu * mu - ex;
-        dlat[i * 3 * L + L + l] = w_kl * mu / (float)B;
-        dlat[i * 3 * L + 2 * L + l] = w_kl * (-0.5f) * (1.f - ex) / (float)B;
+        if (lead) {
+          a.dlat[i * 3 * L + L + l] = a.w_kl * mu / (float)B;
+          a.dlat[i * 3 * L + 2 * L + l] = a.w_kl * (-0.5f) * (1.f - ex) / (float)B;
+        }
       } else {
-        if (sigmoid) zz = 1.f / (1.f + expf(-mu));
-        dlat[i * 3 * L + L + l] = 0.f;
-        dlat[i * 3 * L + 2 * L + l] = 0.f;
+        if (a.sigmoid) zz = 1.f / (1.f + expf(-mu));
+        if (lead) {
+          a.dlat[i * 3 * L + L + l] = 0.f;
+          a.dlat[i * 3 * L + 2 * L + l] = 0.f;
+        }
       }
-      z[e] = zz;
+      if (lead) a.z[e] = zz;
       zs[e] = zz;
     }
   }
@@ -269,8 +280,8 @@ __global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const float* __restr
   // and a 3-step shuffle tree (fixed order): 75-long serial loops were the
   // latency of this single-workgroup kernel.
   const int npairs = bs * (bs - 1) / 2;
-  const int lo = region_size > 0 ? (*key) * region_size : 0;
-  const int hi = lo + region_size;
+  const int lo = a.region_size > 0 ? (*a.key) * a.region_size : 0;
+  const int hi = lo + a.region_size;
   const int nd = 4 * npairs * bs;
   for (int e0 = 0; e0 < nd && w_lc != 0.f; e0 += blockDim.x / 8) {
     const int e = e0 + tid / 8, j = tid % 8;
@@ -300,17 +311,17 @@ __global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const float* __restr
   __syncthreads();
   const float scale = 1.f / (float)(bs * bs * bs - bs * bs);
   float lc_part = 0.f;
-  for (int e = tid; e < npairs * bs && w_lc != 0.f; e += blockDim.x) {
+  for (int e = tid; lead && e < npairs * bs && w_lc != 0.f; e += blockDim.x) {
     const float lg = dist[0 * npairs * bs + e], dg = dist[1 * npairs * bs + e];
     const float dr = dist[2 * npairs * bs + e], lr = dist[3 * npairs * bs + e];
-    lc_part += fmaxf(0.f, lr - dr + eta2) + fmaxf(0.f, lg - dg + eta1);
+    lc_part += fmaxf(0.f, lr - dr + a.eta2) + fmaxf(0.f, lg - dg + a.eta1);
   }
   // gradient of LC w.r.t. z: one thread per (row i, dim l).  Row i = (ii, jj)
   // (base ii, donor jj) appears in the hinge terms of the pairs that contain
   // ii (same-donor distances, t = jj) and of those that contain jj
   // (same-base distances, t = ii); the terms are added in a fixed order.
   const float k2 = 2.f * scale * w_lc;
-  for (int e = tid; e < B * L; e += blockDim.x) {
+  for (int e = g0 + tid; e < g1; e += blockDim.x) {
     const int i = e / L, l = e % L;
     float g = 0.f;
     if (w_lc != 0.f) {
@@ -324,8 +335,8 @@ __global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const float* __restr
         // same-donor term (t = jj): rows a1 = q*bs + t, b1 = p*bs + t
         if (ii == q || ii == p) {
           const int de = pr * bs + jj;
-          const bool act = inr ? (dist[0 * npairs * bs + de] - dist[1 * npairs * bs + de] + eta1) > 0.f
-                               : (dist[3 * npairs * bs + de] - dist[2 * npairs * bs + de] + eta2) > 0.f;
+          const bool act = inr ? (dist[0 * npairs * bs + de] - dist[1 * npairs * bs + de] + a.eta1) > 0.f
+                               : (dist[3 * npairs * bs + de] - dist[2 * npairs * bs + de] + a.eta2) > 0.f;
           if (act) {
             const float d1 = zs[(q * bs + jj) * L + l] - zs[(p * bs + jj) * L + l];
             g += (ii == q ? 1.f : -1.f) * s1 * k2 * d1;
@@ -334,8 +345,8 @@ __global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const float* __restr
         // same-base term (t = ii): rows a2 = t*bs + q, b2 = t*bs + p
         if (jj == q || jj == p) {
           const int de = pr * bs + ii;
-          const bool act = inr ? (dist[0 * npairs * bs + de] - dist[1 * npairs * bs + de] + eta1) > 0.f
-                               : (dist[3 * npairs * bs + de] - dist[2 * npairs * bs + de] + eta2) > 0.f;
+          const bool act = inr ? (dist[0 * npairs * bs + de] - dist[1 * npairs * bs + de] + a.eta1) > 0.f
+                               : (dist[3 * npairs * bs + de] - dist[2 * npairs * bs + de] + a.eta2) > 0.f;
           if (act) {
             const float d2 = zs[(ii * bs + q) * L + l] - zs[(ii * bs + p) * L + l];
             g -= (jj == q ? 1.f : -1.f) * s1 * k2 * d2;
@@ -343,12 +354,91 @@ __global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const float* __restr
         }
       }
     }
-    dlat[i * 3 * L + l] = g;
+    a.dlat[i * 3 * L + l] = g;
   }
-  float2 r = block_sum2(kl_part, lc_part, red);
-  if (tid == 0) {
-    terms[0] = is_vae ? -0.5f * r.x / (float)B : 0.f;
-    terms[1] = w_lc != 0.f ? r.y * scale : 0.f;  // (no LC: bs = 1 and scale = 1/0)
+  if (lead) {
+    float2 r = block_sum2(kl_part, lc_part, red);
+    if (tid == 0) {
+      a.terms[0] = a.is_vae ? -0.5f * r.x / (float)B : 0.f;
+      a.terms[1] = w_lc != 0.f ? r.y * scale : 0.f;  // (no LC: bs = 1 and scale = 1/0)
+    }
+  }
+}
+
+// Single workgroup.  mulv [B, 2L] = [logvar | mu] (rows of the stacked
+// encoder Linear), z [B, L].  dlat [B, 3L] = {w_lc*dLC/dz | w_kl*dKL/dmu | w_kl*dKL/dlogvar}.
+// terms[2] = {kl, lc}.
+// 16 waves: the LC distance and gradient phases are chains of dependent LDS
+// reads that one wave per SIMD cannot hide (256: 16.0 us, 512: 11.4,
+// 1024: 9.8, same-box A/B in the step).
+__global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const LatentArgs a) {
+  // dynamic LDS: z [B][L], then the distances [kind][pair][t] (4 npairs bs)
+  extern __shared__ float lat_lds[];
+  __shared__ float2 red[kLatThreads / 64];
+  latent_body(a, lat_lds, lat_lds + a.B * a.L, red, true, 0, a.B * a.L);
+}
+
+// Latent head + decoder Linear (model.py:184-188 then :167-168) in ONE
+// launch: the Linear's input z is made in each workgroup's own LDS, so the
+// kernel boundary between them (and the z round trip through memory) is gone.
+// Workgroup g owns 256 columns of y = z W^T + b: its W slice ([256][k],
+// contiguous) is loaded coalesced into registers before the latent phases
+// and parked in LDS after them (lane stride k floats: k odd or 2 mod 4 keeps
+// the reads conflict-free), then thread (column, row quad) runs the same fmaf
+// chain per output as linear_fwd_nred (bit-identical y).  Every workgroup
+// holds all of z and the LC distances in LDS and writes the LC gradient
+// elements of its 1/grid slice; workgroup 0 also the KL pieces, z and terms
+// (its KL / LC sums run over 512 threads: terms may differ from
+// latent_fwd_k's 1024-thread sum in the last bit).
+constexpr int kLatLinThreads = 512;
+constexpr int kLatLinCols = 256;
+constexpr int kLatLinMaxK = 80;  // latent width (configs: 75, 33)
+constexpr int kLatLinWPer = (kLatLinCols * kLatLinMaxK + kLatLinThreads - 1) / kLatLinThreads;
+__global__ __launch_bounds__(kLatLinThreads) void latent_linear_fwd_k(const LatentArgs a,
+                                                                      const float* __restrict__ w,
+                                                                      const float* __restrict__ bias,
+                                                                      float* __restrict__ y, int n,
+                                                                      int lat_floats) {
+  extern __shared__ float lat_lds[];
+  __shared__ float2 red[kLatLinThreads / 64];
+  const int m = a.B, k = a.L;
+  const int c0 = blockIdx.x * kLatLinCols, nc = min(kLatLinCols, n - c0);
+  const int nw = nc * k;
+  const float* ws = w + (long)c0 * k;
+  float wv[kLatLinWPer];
+#pragma unroll
+  for (int j = 0; j < kLatLinWPer; ++j) {
+    const int e = j * kLatLinThreads + threadIdx.x;
+    wv[j] = e < nw ? ws[e] : 0.f;
+  }
+  const int col = c0 + (threadIdx.x & (kLatLinCols - 1));
+  const float bv = (bias && col < n) ? bias[col] : 0.f;
+  const int per = (m * k + gridDim.x - 1) / gridDim.x;
+  const int g0 = min(m * k, (int)blockIdx.x * per), g1 = min(m * k, g0 + per);
+  float* zs = lat_lds;
+  float* wl = lat_lds + lat_floats;
+  latent_body(a, zs, lat_lds + m * k, red, blockIdx.x == 0, g0, g1);
+#pragma unroll
+  for (int j = 0; j < kLatLinWPer; ++j) {
+    const int e = j * kLatLinThreads + threadIdx.x;
+    if (e < nw) wl[e] = wv[j];
+  }
+  __syncthreads();
+  if (col >= n) return;
+  const float* wr = wl + (col - c0) * k;
+  for (int i0 = (threadIdx.x / kLatLinCols) * 4; i0 < m; i0 += 4 * (kLatLinThreads / kLatLinCols)) {
+    const int mr = min(4, m - i0);
+    const float* zr = zs + i0 * k;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 5
+    for (int kk = 0; kk < k; ++kk) {
+      const float wk = wr[kk];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = fmaf(zr[min(i, mr - 1) * k + kk], wk, acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < mr) y[(long)(i0 + i) * n + col] = acc[i] + bv;
   }
 }
 
@@ -849,7 +939,7 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
 
 using namespace cfsd;
 
-extern "C" int cfsd_version(void) { return (4 << 16) | 4; }  // 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
+extern "C" int cfsd_version(void) { return (4 << 16) | 5; }  // 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
 extern "C" const char* cfsd_last_error_string(void) { return g_err; }
 
 extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {
@@ -967,32 +1057,79 @@ extern "C" int cfsd_recon_lap_bwd_finalize_x(const float* pred, const float* gt,
                            partials, nblocks, terms, out, acc, w_kl, w_lc, (dt & CFSD_VM) != 0, stream);
 }
 
+// LDS floats of the latent head (z + pair distances) for one workgroup
+static size_t latent_lds_floats(int batch, int latent, int bs) {
+  return (size_t)batch * latent + (size_t)4 * (bs * (bs - 1) / 2) * bs;
+}
+constexpr size_t kLatLdsMax = 160 * 1024 - 1024;  // minus the static reduction array
+
+// Checks the latent head's arguments and sizes its dynamic LDS (z and the
+// pair distances of one workgroup, up to 160 KB: e.g. batch 256 = 16^2 at
+// latent 75 takes 105 KB); raises the kernel's dynamic-LDS limit when needed.
+static int latent_prepare(const char* name, const void* kernel, const float* mulv, const float* eps,
+                          const int32_t* key, float* z, float* dlat, float* terms, int batch,
+                          int latent, int region_size, int train, int is_vae, float w_lc,
+                          size_t extra_lds, int& bs, size_t& lds) {
+  if (!mulv || !z || !dlat || !terms) return set_error(CFSD_EINVAL, "%s: null pointer", name);
+  if (is_vae && train && !eps) return set_error(CFSD_EINVAL, "%s: eps required", name);
+  if (w_lc != 0.f && (!key || region_size <= 0)) return set_error(CFSD_EINVAL, "%s: key/region required", name);
+  bs = (int)lrint(sqrt((double)batch));
+  if (w_lc != 0.f && bs * bs != batch) return set_error(CFSD_EINVAL, "%s: batch %d is not bs^2", name, batch);
+  if (w_lc == 0.f) bs = 1;
+  if (batch <= 0 || latent <= 0) return set_error(CFSD_EINVAL, "%s: bad sizes", name);
+  lds = latent_lds_floats(batch, latent, bs) * sizeof(float) + extra_lds;
+  if (lds > kLatLdsMax)
+    return set_error(CFSD_EINVAL, "%s: batch %d x latent %d needs %zu B of LDS (> %zu)", name, batch,
+                     latent, lds, kLatLdsMax);
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLatLdsMax) != hipSuccess)
+    return set_error(CFSD_EINVAL, "%s: cannot raise the dynamic LDS limit", name);
+  return CFSD_OK;
+}
+
 extern "C" int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_t* key, float* z,
                                float* dlat, float* terms, int batch, int latent, int region_size,
                                int train, int is_vae, int sigmoid, float w_kl, float w_lc,
                                float eta1, float eta2, void* stream) {
-  if (!mulv || !z || !dlat || !terms) return set_error(CFSD_EINVAL, "latent_fwd: null pointer");
-  if (is_vae && train && !eps) return set_error(CFSD_EINVAL, "latent_fwd: eps required");
-  if (w_lc != 0.f && (!key || region_size <= 0)) return set_error(CFSD_EINVAL, "latent_fwd: key/region required");
-  int bs = (int)lrint(sqrt((double)batch));
-  if (w_lc != 0.f && bs * bs != batch) return set_error(CFSD_EINVAL, "latent_fwd: batch %d is not bs^2", batch);
-  if (w_lc == 0.f) bs = 1;
-  if (batch <= 0 || latent <= 0) return set_error(CFSD_EINVAL, "latent_fwd: bad sizes");
-  // one workgroup holds z and the pair distances in LDS (up to 160 KB:
-  // e.g. batch 256 = 16^2 at latent 75 takes 105 KB)
-  const size_t lds = ((size_t)batch * latent + (size_t)4 * (bs * (bs - 1) / 2) * bs) * sizeof(float);
-  constexpr size_t kLatLdsMax = 160 * 1024 - 1024;  // minus the static reduction array
-  if (lds > kLatLdsMax)
-    return set_error(CFSD_EINVAL, "latent_fwd: batch %d x latent %d needs %zu B of LDS (> %zu)", batch,
-                     latent, lds, kLatLdsMax);
-  if (lds > 64 * 1024 &&
-      hipFuncSetAttribute((const void*)latent_fwd_k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)kLatLdsMax) != hipSuccess)
-    return set_error(CFSD_EINVAL, "latent_fwd: cannot raise the dynamic LDS limit");
-  hipLaunchKernelGGL(latent_fwd_k, dim3(1), dim3(kLatThreads), lds, (hipStream_t)stream, mulv, eps, key, z,
-                     dlat, terms, batch, latent, region_size, train, is_vae, sigmoid, w_kl, w_lc,
-                     eta1, eta2, bs);
+  int bs = 1;
+  size_t lds = 0;
+  const int rc = latent_prepare("latent_fwd", (const void*)latent_fwd_k, mulv, eps, key, z, dlat, terms,
+                                batch, latent, region_size, train, is_vae, w_lc, 0, bs, lds);
+  if (rc != CFSD_OK) return rc;
+  const LatentArgs a{mulv, eps, key, z, dlat, terms, batch, latent, region_size, train, is_vae,
+                     sigmoid, w_kl, w_lc, eta1, eta2, bs};
+  hipLaunchKernelGGL(latent_fwd_k, dim3(1), dim3(kLatThreads), lds, (hipStream_t)stream, a);
   return launch_status("latent_fwd");
+}
+
+extern "C" int cfsd_latent_linear_fwd_supported(int batch, int latent, int n) {
+  if (batch <= 0 || latent <= 0 || latent > kLatLinMaxK || n <= 0) return 0;
+  const int bs = (int)lrint(sqrt((double)batch));  // LC sizing (the larger case)
+  const size_t f = latent_lds_floats(batch, latent, bs * bs == batch ? bs : 1);
+  return (f + (size_t)kLatLinCols * latent) * sizeof(float) <= kLatLdsMax;
+}
+
+extern "C" int cfsd_latent_linear_fwd(const float* mulv, const float* eps, const int32_t* key, float* z,
+                                      float* dlat, float* terms, int batch, int latent,
+                                      int region_size, int train, int is_vae, int sigmoid,
+                                      float w_kl, float w_lc, float eta1, float eta2,
+                                      const float* w, const float* bias, float* y, int n,
+                                      void* stream) {
+  if (!w || !y) return set_error(CFSD_EINVAL, "latent_linear_fwd: null pointer");
+  if (!cfsd_latent_linear_fwd_supported(batch, latent, n))
+    return set_error(CFSD_EINVAL, "latent_linear_fwd: latent %d (max %d) / n %d unsupported", latent,
+                     kLatLinMaxK, n);
+  int bs = 1;
+  size_t lds = 0;
+  const int rc = latent_prepare("latent_linear_fwd", (const void*)latent_linear_fwd_k, mulv, eps, key, z,
+                                dlat, terms, batch, latent, region_size, train, is_vae, w_lc,
+                                (size_t)kLatLinCols * latent * sizeof(float), bs, lds);
+  if (rc != CFSD_OK) return rc;
+  const LatentArgs a{mulv, eps, key, z, dlat, terms, batch, latent, region_size, train, is_vae,
+                     sigmoid, w_kl, w_lc, eta1, eta2, bs};
+  hipLaunchKernelGGL(latent_linear_fwd_k, dim3((n + kLatLinCols - 1) / kLatLinCols), dim3(kLatLinThreads),
+                     lds, (hipStream_t)stream, a, w, bias, y, n, (int)latent_lds_floats(batch, latent, bs));
+  return launch_status("latent_linear_fwd");
 }
 
 extern "C" int cfsd_latent_bwd(const float* mulv, const float* eps, const float* z,

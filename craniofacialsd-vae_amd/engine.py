@@ -181,6 +181,7 @@ class SDVAEEngine:
             self.params.shadow = torch.zeros(self.params.numel, dtype=torch.bfloat16, device=self.device)
         self.vertex_major = bool(vertex_major)
         self.fuse_up = True  # coarse Deblocks: Pool(up) fused into the conv gather (False: separate SpMM)
+        self.fuse_latent = True  # latent head + decoder Linear in one launch (False: two)
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -570,20 +571,34 @@ class SDVAEEngine:
         return (self.swap and bool(self.region_size) and self.w_lc != 0.0
                 and b.bsz == self.swap_bs ** 2)
 
-    def latent(self, b, train):
+    def latent(self, b, train, dec_linear=False):
+        """Latent head (model.py:184-188 + the KL / LC terms); with
+        ``dec_linear`` also the decoder Linear in the same launch
+        (cfsd_latent_linear_fwd; decode() then starts at the first Deblock)."""
         S = self.spec
         lc = self._lc_on(b)
-        ops.latent_fwd(b.mulv, b.eps if (train and S.is_vae) else None,
-                       b.key if lc else None, b.z, b.dlat, b.terms, S.latent,
-                       self.region_size if lc else 0, train, S.is_vae, S.sigmoid, self.w_kl,
-                       self.w_lc if lc else 0.0, self.eta1, self.eta2)
+        args = (b.mulv, b.eps if (train and S.is_vae) else None,
+                b.key if lc else None, b.z, b.dlat, b.terms, S.latent,
+                self.region_size if lc else 0, train, S.is_vae, S.sigmoid, self.w_kl,
+                self.w_lc if lc else 0.0, self.eta1, self.eta2)
+        if dec_linear:
+            ops.latent_linear_fwd(*args, self.params.view("de_layers.0.weight"),
+                                  self.params.view("de_layers.0.bias"), out=b.h.view(b.bsz, -1))
+        else:
+            ops.latent_fwd(*args)
 
-    def decode(self, b, z=None):
-        """de_layers: Linear -> 4x (Pool up -> conv -> ELU) -> conv (model.py:162-173)."""
+    def _fused_latent(self, b):
+        return self.fuse_latent and ops.latent_linear_fwd_supported(
+            b.bsz, self.spec.latent, self.params.view("de_layers.0.weight").shape[0])
+
+    def decode(self, b, z=None, linear=True):
+        """de_layers: Linear -> 4x (Pool up -> conv -> ELU) -> conv (model.py:162-173).
+        ``linear=False``: b.h already holds the Linear's output."""
         T, S = self.topo, self.spec
-        ops.linear_fwd(b.z if z is None else z, self.params.view("de_layers.0.weight"),
-                       self.params.view("de_layers.0.bias"), out=b.h.view(b.bsz, -1),
-                       workspace=b.lin_ws)
+        if linear:
+            ops.linear_fwd(b.z if z is None else z, self.params.view("de_layers.0.weight"),
+                           self.params.view("de_layers.0.bias"), out=b.h.view(b.bsz, -1),
+                           workspace=b.lin_ws)
         h = b.h
         for i, (cin, cout, lv, ui) in enumerate(S.dec_layers()):
             wname = f"de_layers.{i + 1}.conv.layer"
@@ -619,8 +634,9 @@ class SDVAEEngine:
         """``finalize=False``: the loss reduction is left to backward(), whose
         first launch finalises it (one launch less per train step)."""
         self.encode(b)
-        self.latent(b, train)
-        self.decode(b)
+        fused = self._fused_latent(b)
+        self.latent(b, train, dec_linear=fused)
+        self.decode(b, linear=not fused)
         if self.topo.lap_csr is not None:
             self.losses_fwd(b, acc, finalize)
         b.pending_finalize = (not finalize, acc)

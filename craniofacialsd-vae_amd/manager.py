@@ -59,8 +59,8 @@ def load_or_build_topology(config, template, precomputed_path):
         h = precompute.build_hierarchy(template.pos, template.faces, template.colors,
                                        mp["sampling"]["sampling_factors"], mp["spirals"]["length"],
                                        mp["spirals"].get("dilation"), mp["sampling"].get("type", "basic"))
-    if template.feat_and_cont is not None:
-        keys = list(template.feat_and_cont.keys())
+    if template.feat_and_cont is not None and "region_keys" not in h:  # (a fresh build wrote its own,
+        keys = list(template.feat_and_cont.keys())                   # r_weighted-extended ones)
         h["region_keys"] = np.asarray(keys)
         for i, k in enumerate(keys):
             h[f"region_{i}_feature"] = np.asarray(template.feat_and_cont[k]["feature"], np.int32)

@@ -622,6 +622,33 @@ def latent_fwd(mulv, eps, key, z, dlat, terms, latent, region_size, train, is_va
          float(eta1), float(eta2), stream_ptr())
 
 
+def latent_linear_fwd_supported(batch, latent, n):
+    return bool(_abi.lib().cfsd_latent_linear_fwd_supported(int(batch), int(latent), int(n)))
+
+
+def latent_linear_fwd(mulv, eps, key, z, dlat, terms, latent, region_size, train, is_vae, sigmoid,
+                      w_kl, w_lc, eta1, eta2, w, bias, out):
+    """latent_fwd, then the decoder Linear out = z w^T + bias, in one launch
+    (cfsd_latent_linear_fwd: z, dlat, out bit-identical to the two calls)."""
+    bsz = z.shape[0]
+    n = w.shape[0]
+    _need(mulv, (bsz, 2 * latent if is_vae else latent), name="mulv")
+    _need(z, (bsz, latent), name="z")
+    _need(dlat, (bsz, 3 * latent), name="dlat")
+    _need(terms, (2,), name="terms")
+    _need(w, (n, latent), name="w")
+    _need(out, (bsz, n), name="out")
+    if bias is not None:
+        _need(bias, (n,), name="bias")
+    if eps is not None:
+        _need(eps, (bsz, latent), name="eps")
+    if key is not None:
+        _need(key, (1,), torch.int32, "key")
+    call("cfsd_latent_linear_fwd", ptr(mulv), ptr(eps), ptr(key), ptr(z), ptr(dlat), ptr(terms), bsz,
+         latent, region_size, int(train), int(is_vae), int(sigmoid), float(w_kl), float(w_lc),
+         float(eta1), float(eta2), ptr(w), ptr(bias), ptr(out), n, stream_ptr())
+
+
 def latent_bwd(mulv, eps, z, dz_dec, dlat, dmulv, latent, train, is_vae, sigmoid):
     """``dz_dec`` [B, latent], or [parts, B, latent] partial products (summed
     in part order: cfsd_latent_bwd_parts)."""

@@ -417,12 +417,15 @@ def vertex_quadrics(pos, faces):
     return q
 
 
-def quadric_edge_collapse(pos, faces, sampling_factor, region_weights=None):
+def quadric_edge_collapse(pos, faces, sampling_factor, region_weights=None, edge_length_weighted=False):
     """``MeshSimplifier.quadric_edge_collapse`` with ``_quadric_edge_collapse``
     and ``_edge_collapse_cost`` (mesh_simplification.py:43-167): greedy
     lowest-cost edge collapse (lazy heap, stale costs re-pushed) down to
-    ceil(V / factor) vertices.  Returns (new_faces [F',3], kept vertex
-    indices ascending = the 0/1 down matrix's columns)."""
+    ceil(V / factor) vertices.  ``edge_length_weighted`` adds the edge's fp32
+    length to the collapse cost before the region weighting (:157-160; an
+    option of MeshSimplifier that ModelManager never sets).  Returns
+    (new_faces [F',3], kept vertex indices ascending = the 0/1 down matrix's
+    columns)."""
     pos = np.asarray(pos, np.float32)
     n = len(pos)
     desired = math.ceil(n / sampling_factor)
@@ -439,6 +442,8 @@ def quadric_edge_collapse(pos, faces, sampling_factor, region_weights=None):
         d0 = p0.T.dot(qs).dot(p0).item()
         d1 = p1.T.dot(qs).dot(p1).item()
         c = min([d0, d1])
+        if edge_length_weighted:
+            c += np.linalg.norm(pos[e0] - pos[e1])
         if region_weights is not None:
             c *= (region_weights[e0] + region_weights[e1]) / 2
         return c, d0, d1, qs
@@ -575,7 +580,7 @@ def upsampling_matrix(fine_pos, coarse_pos, coarse_faces):
 
 # ============================================================== hierarchy
 def build_hierarchy(pos, faces, colors=None, sampling_factors=(4, 4, 4, 4), seq_lengths=(9, 9, 9, 9),
-                    dilations=None, sampling_type="basic"):
+                    dilations=None, sampling_type="basic", edge_length_weighted=False):
     """The reference's precompute chain (``ModelManager._precompute_transformations``
     + ``_precompute_spirals``, model_manager.py:176-230) from a template:
     per sampling factor one quadric-edge-collapse level (0/1 down matrix) and
@@ -585,10 +590,13 @@ def build_hierarchy(pos, faces, colors=None, sampling_factors=(4, 4, 4, 4), seq_
     ``region_*``, ``lap_*``) that ``DeviceTopology.from_npz`` consumes.
 
     ``sampling_type='r_weighted'`` weights the collapse costs by 1/|region|
-    (mesh_simplification.py:50-59).  (The reference also appends each
-    region's contour to its feature list in place there, changing the swap
-    regions of a freshly precomputed template; that side effect is not
-    reproduced.)"""
+    (mesh_simplification.py:50-59, model_manager.py:191).  The reference's
+    weighting loop also extends each region's feature list by its contour in
+    place (``feat_and_cont.extend``, :56-58) on the template object the
+    ModelManager keeps, so after a fresh r_weighted precompute the swap
+    regions (``region_i_feature``) are feature + contour; that is reproduced
+    here (a run that loads a cached ``transforms.pkl`` has no such effect).
+    ``edge_length_weighted`` is MeshSimplifier's length term (:157-158)."""
     n_lv = len(sampling_factors)
     dilations = dilations or [1] * n_lv
     tpl = Template(pos, faces, colors)
@@ -598,7 +606,10 @@ def build_hierarchy(pos, faces, colors=None, sampling_factors=(4, 4, 4, 4), seq_
         keys = list(tpl.feat_and_cont.keys())
         out["region_keys"] = np.asarray(keys)
         for i, k in enumerate(keys):
-            out[f"region_{i}_feature"] = np.asarray(tpl.feat_and_cont[k]["feature"], np.int32)
+            feat = list(tpl.feat_and_cont[k]["feature"])
+            if sampling_type != "basic":  # the in-place extend of mesh_simplification.py:56-58
+                feat = feat + list(tpl.feat_and_cont[k]["contour"])
+            out[f"region_{i}_feature"] = np.asarray(feat, np.int32)
             out[f"region_{i}_contour"] = np.asarray(tpl.feat_and_cont[k]["contour"], np.int32)
     out["lap_row"], out["lap_col"], out["lap_val"] = tpl.laplacian
     cur_pos, cur_faces, cur_col = tpl.pos, tpl.faces, tpl.colors
@@ -611,7 +622,8 @@ def build_hierarchy(pos, faces, colors=None, sampling_factors=(4, 4, 4, 4), seq_
             rw = np.ones(len(cur_pos))
             for k, f in fc.items():
                 rw[f["feature"] + f["contour"]] = 1 / (len(f["feature"]) + len(f["contour"]))
-        new_faces, kept = quadric_edge_collapse(cur_pos, cur_faces, factor, region_weights=rw)
+        new_faces, kept = quadric_edge_collapse(cur_pos, cur_faces, factor, region_weights=rw,
+                                                edge_length_weighted=edge_length_weighted)
         m = len(kept)
         out[f"down_{l}_row"] = np.arange(m, dtype=np.int32)
         out[f"down_{l}_col"] = kept.astype(np.int32)

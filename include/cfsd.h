@@ -365,6 +365,17 @@ int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_t* key, flo
                     float* dlat, float* terms, int batch, int latent, int region_size, int train,
                     int is_vae, int sigmoid, float w_kl, float w_lc, float eta1, float eta2,
                     void* stream);
+/* (ABI 4.5) cfsd_latent_fwd followed by the decoder Linear (model.py:167-168)
+ * y [batch, n] = z w^T + bias, w [n, latent], in ONE launch: z, dlat and y are
+ * bit-identical to cfsd_latent_fwd + cfsd_linear_fwd(z, w, bias, y, batch,
+ * latent, n); terms[] equal up to the order of the KL / LC sums (512- instead
+ * of 1024-thread tree).  _supported: latent <= 80. */
+int cfsd_latent_linear_fwd_supported(int batch, int latent, int n);
+int cfsd_latent_linear_fwd(const float* mulv, const float* eps, const int32_t* key, float* z,
+                           float* dlat, float* terms, int batch, int latent, int region_size,
+                           int train, int is_vae, int sigmoid, float w_kl, float w_lc, float eta1,
+                           float eta2, const float* w, const float* bias, float* y, int n,
+                           void* stream);
 /* Latent head, backward: dmulv (same layout as mulv) from dz_dec (gradient of
  * the decoder input) + dlat.  z is only read for the sigmoid AE variant. */
 int cfsd_latent_bwd(const float* mulv, const float* eps, const float* z, const float* dz_dec,

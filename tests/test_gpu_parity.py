@@ -897,3 +897,56 @@ def test_engine_forward_fused_up_equals_unfused(dtopo):
     close(outs[0][0], outs[1][0], 1e-5, "reconstruction")
     for a, c in zip(outs[0][1], outs[1][1]):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("bs,vae,train,n", [(4, True, True, 4288), (3, True, True, 300), (9, True, True, 4288),
+                                            (4, True, False, 4288), (4, False, True, 1000)])
+def test_latent_linear_fused_equals_two_launches(bs, vae, train, n):
+    """cfsd_latent_linear_fwd (latent head + decoder Linear in one launch):
+    z, dlat and the Linear output bit-identical to cfsd_latent_fwd followed by
+    cfsd_linear_fwd; terms within 1e-6 (sum-tree order)."""
+    g = torch.Generator().manual_seed(bs * 7 + n)
+    L, B = 75, bs * bs
+    mulv = torch.randn(B, (2 if vae else 1) * L, generator=g).to(DEV) * 0.5
+    eps = torch.randn(B, L, generator=g).to(DEV)
+    w = torch.randn(n, L, generator=g).to(DEV) * 0.1
+    bias = torch.randn(n, generator=g).to(DEV)
+    keyt = torch.full((1,), 2, dtype=torch.int32, device=DEV)
+    res = []
+    for fused in (True, False):
+        zz, dlat = torch.full((B, L), 7.0, device=DEV), torch.full((B, 3 * L), 7.0, device=DEV)
+        terms, h = torch.full((2,), 7.0, device=DEV), torch.full((B, n), 7.0, device=DEV)
+        args = (mulv, eps if (vae and train) else None, keyt, zz, dlat, terms, L, 5, train, vae, False,
+                1e-4, 0.5, 0.5, 0.5)
+        if fused:
+            assert ops.latent_linear_fwd_supported(B, L, n)
+            ops.latent_linear_fwd(*args, w, bias, out=h)
+        else:
+            ops.latent_fwd(*args)
+            ops.linear_fwd(zz, w, bias, out=h, workspace=None)
+        torch.cuda.synchronize()
+        res.append((zz, dlat, terms, h))
+    for name, a, c in zip(("z", "dlat", "terms", "h"), res[0], res[1]):
+        if name == "terms":
+            close(a, c, 1e-6, name)
+        else:
+            assert torch.equal(a, c), name
+
+
+def test_engine_forward_fused_latent_equals_unfused(dtopo):
+    """The step's forward with the latent head and decoder Linear in one launch
+    equals the two-launch forward bit for bit (z, decoder input, output)."""
+    outs = []
+    x = torch.from_numpy(recipe.normalized_meshes(12)).to(DEV)
+    x = torch.cat([x, x[:4]])  # 16 = bs^2: latent consistency on
+    for fuse in (True, False):
+        eng = make_engine(dtopo, recipe.golden_weights())
+        eng.fuse_latent = fuse
+        assert eng._lc_on(eng.buffers(16))
+        eps = torch.randn(16, eng.spec.latent, generator=torch.Generator().manual_seed(5)).to(DEV)
+        b = eng.set_batch(x, key_index=3, eps=eps)
+        eng.forward(b, train=True)
+        torch.cuda.synchronize()
+        outs.append((b.z.clone(), b.h.clone(), b.out.clone(), b.dlat.clone()))
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)

@@ -109,3 +109,27 @@ def test_synthetic_hierarchy_builds():
         u = sp.csr_matrix((h[f"up_{l}_val"], (h[f"up_{l}_row"], h[f"up_{l}_col"])),
                           shape=tuple(h[f"up_{l}_shape"]))
         assert np.abs(np.asarray(u.sum(1)).ravel() - 1).max() < 1e-5
+
+
+def test_sampling_variants_r_weighted_and_edge_length():
+    """f2 sampling variants (parity unpinned: trimesh/torch_geometric absent,
+    no reference cache for these modes).  ``r_weighted`` (model_manager.py:191,
+    mesh_simplification.py:50-59): region-weighted collapse costs, and the
+    template's swap regions become feature + contour (the reference's in-place
+    ``extend``); ``edge_length_weighted`` (:157-158) adds the edge length to
+    each cost.  Both keep the level sizes and change which vertices survive."""
+    pos, faces, col = PC.torus(n_major=40, n_minor=32)
+    kw = dict(sampling_factors=(4, 4), seq_lengths=(9, 9))
+    base = PC.build_hierarchy(pos, faces, col, **kw)
+    rw = PC.build_hierarchy(pos, faces, col, sampling_type="r_weighted", **kw)
+    el = PC.build_hierarchy(pos, faces, col, edge_length_weighted=True, **kw)
+    tpl = PC.Template(pos, faces, col)
+    for i, k in enumerate(base["region_keys"]):
+        fc = tpl.feat_and_cont[k]
+        assert list(base[f"region_{i}_feature"]) == list(fc["feature"])
+        assert list(rw[f"region_{i}_feature"]) == list(fc["feature"]) + list(fc["contour"])
+        assert list(rw[f"region_{i}_contour"]) == list(fc["contour"])
+    for h in (rw, el):
+        assert [h[f"pos_{l}"].shape[0] for l in range(3)] == [1280, 320, 80]
+    assert not np.array_equal(rw["down_0_col"], base["down_0_col"])
+    assert not np.array_equal(el["down_0_col"], base["down_0_col"])

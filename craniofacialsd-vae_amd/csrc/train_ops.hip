@@ -381,17 +381,22 @@ __global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const LatentArgs a) 
 // Latent head + decoder Linear (model.py:184-188 then :167-168) in ONE
 // launch: the Linear's input z is made in each workgroup's own LDS, so the
 // kernel boundary between them (and the z round trip through memory) is gone.
-// Workgroup g owns 256 columns of y = z W^T + b: its W slice ([256][k],
+// Workgroup g owns 64 columns of y = z W^T + b: its W slice ([64][k],
 // contiguous) is loaded coalesced into registers before the latent phases
 // and parked in LDS after them (lane stride k floats: k odd or 2 mod 4 keeps
-// the reads conflict-free), then thread (column, row quad) runs the same fmaf
-// chain per output as linear_fwd_nred (bit-identical y).  Every workgroup
-// holds all of z and the LC distances in LDS and writes the LC gradient
-// elements of its 1/grid slice; workgroup 0 also the KL pieces, z and terms
-// (its KL / LC sums run over 512 threads: terms may differ from
-// latent_fwd_k's 1024-thread sum in the last bit).
-constexpr int kLatLinThreads = 512;
-constexpr int kLatLinCols = 256;
+// the reads conflict-free); thread (column, row pair) then runs the same
+// fmaf chain per output as linear_fwd_nred (bit-identical y), z rows read as
+// wave-uniform LDS broadcasts.  64-column slices: 67 workgroups at n = 4288
+// (256-column slices with 8 outputs per thread left the Linear's chain of
+// LDS reads as long as the latent head: 18.6 us vs 6.6 + 9.8 + 7.9 for the
+// separate launches; 64 columns: 11.3-11.7 us at 512 or 1024 threads).
+// Every workgroup holds all of z and the LC distances in LDS and writes the
+// LC gradient elements of its 1/grid slice; workgroup 0 also the KL pieces,
+// z and terms with latent_fwd_k's thread mapping and sum tree (1024
+// threads): z, dlat, terms and y all bit-identical to the two launches.
+constexpr int kLatLinThreads = 1024;
+constexpr int kLatLinCols = 64;
+constexpr int kLatLinRows = kLatLinThreads / kLatLinCols;  // row groups (waves) of 2 rows
 constexpr int kLatLinMaxK = 80;  // latent width (configs: 75, 33)
 constexpr int kLatLinWPer = (kLatLinCols * kLatLinMaxK + kLatLinThreads - 1) / kLatLinThreads;
 __global__ __launch_bounds__(kLatLinThreads) void latent_linear_fwd_k(const LatentArgs a,
@@ -411,7 +416,7 @@ __global__ __launch_bounds__(kLatLinThreads) void latent_linear_fwd_k(const Late
     const int e = j * kLatLinThreads + threadIdx.x;
     wv[j] = e < nw ? ws[e] : 0.f;
   }
-  const int col = c0 + (threadIdx.x & (kLatLinCols - 1));
+  const int col = c0 + (int)(threadIdx.x % kLatLinCols);
   const float bv = (bias && col < n) ? bias[col] : 0.f;
   const int per = (m * k + gridDim.x - 1) / gridDim.x;
   const int g0 = min(m * k, (int)blockIdx.x * per), g1 = min(m * k, g0 + per);
@@ -426,19 +431,19 @@ __global__ __launch_bounds__(kLatLinThreads) void latent_linear_fwd_k(const Late
   __syncthreads();
   if (col >= n) return;
   const float* wr = wl + (col - c0) * k;
-  for (int i0 = (threadIdx.x / kLatLinCols) * 4; i0 < m; i0 += 4 * (kLatLinThreads / kLatLinCols)) {
-    const int mr = min(4, m - i0);
-    const float* zr = zs + i0 * k;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int i0 = (threadIdx.x / kLatLinCols) * 2; i0 < m; i0 += 2 * kLatLinRows) {
+    const int mr = min(2, m - i0);
+    const float* z0 = zs + i0 * k;
+    const float* z1 = zs + (i0 + mr - 1) * k;
+    float a0 = 0.f, a1 = 0.f;
 #pragma unroll 5
     for (int kk = 0; kk < k; ++kk) {
       const float wk = wr[kk];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = fmaf(zr[min(i, mr - 1) * k + kk], wk, acc[i]);
+      a0 = fmaf(z0[kk], wk, a0);
+      a1 = fmaf(z1[kk], wk, a1);
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (i < mr) y[(long)(i0 + i) * n + col] = acc[i] + bv;
+    y[(long)i0 * n + col] = a0 + bv;
+    if (mr > 1) y[(long)(i0 + 1) * n + col] = a1 + bv;
   }
 }
 

@@ -25,11 +25,12 @@ struct TileSweep {
 // tiles instead of the interleaved sweep (measured: level-1 32 -> 32 forward
 // 27.8 -> 24.4 us and data gradient 35.4 -> 30.5 us; no gain at level 0,
 // where a wave has ~2 tiles, and a loss for the dW slabs).
-__device__ __forceinline__ TileSweep xcd_sweep(long n_tiles, int lanes_per_block, int lane_id,
-                                               bool contig = false) {
-  const int nb = gridDim.x;
+// (vb, nb: the block's index and count among the blocks sharing the sweep;
+// a launch that pairs two bodies passes its virtual block numbering)
+__device__ __forceinline__ TileSweep xcd_sweep_v(long n_tiles, int lanes_per_block, int lane_id, bool contig,
+                                                 int vb, int nb) {
   const int G = nb < 8 ? nb : 8;
-  const int grp = blockIdx.x % G, lb = blockIdx.x / G;
+  const int grp = vb % G, lb = vb / G;
   const int nb_g = (nb - grp + G - 1) / G;  // blocks in this group
   const long per = (n_tiles + G - 1) / G;
   TileSweep t;
@@ -44,6 +45,10 @@ __device__ __forceinline__ TileSweep xcd_sweep(long n_tiles, int lanes_per_block
   t.end = min(n_tiles, (grp + 1) * per);
   t.step = (long)nb_g * lanes_per_block;
   return t;
+}
+__device__ __forceinline__ TileSweep xcd_sweep(long n_tiles, int lanes_per_block, int lane_id,
+                                               bool contig = false) {
+  return xcd_sweep_v(n_tiles, lanes_per_block, lane_id, contig, blockIdx.x, gridDim.x);
 }
 
 // Non-persistent grids: renumber workgroups so that XCD x (hardware

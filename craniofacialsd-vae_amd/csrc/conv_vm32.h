@@ -5,6 +5,7 @@
 // neighbour is one contiguous 2-KiB block (16 meshes x 32 fp32 channels).
 #pragma once
 #include "cfsd_common.h"
+#include "conv_lat.h"
 
 namespace cfsd {
 namespace vm32 {
@@ -16,9 +17,17 @@ bool ok(int batch, int cin, int cout);
 int launch_fwd(const float* x, const int* idx, const float* w, const float* bias, float* y, int yvm,
                int vsrc, int rows, int batch, int cin, int cout, int act, hipStream_t st);
 // dx[u] = elu'(elu_y[u]) * sum over the flat inverse list of u (ascending
-// spiral position p = 9r + s) of W_s^T dpre[r]; dpre, dx, elu_y vertex-major.
-int launch_dx_flat(const float* dpre, const int* flat, int width, const float* w, const float* elu_y,
-                   float* dx, int vsrc, int rows, int batch, int cin, int cout, hipStream_t st);
+// spiral position p = 9r + s) of W_s^T dpre[r]; dpre, dx (and elu_y, in dx's
+// layout) vertex-major (dpvm / dxvm) or batch-major; 32 -> 32/64.
+int launch_dx_flat(const float* dpre, int dpvm, int dxvm, const int* flat, int width, const float* w,
+                   const float* elu_y, float* dx, int vsrc, int rows, int batch, int cin, int cout, hipStream_t st);
+// The row-subset (Enblock) backward, 32 -> 32, batch-major dpre at the kept rows:
+// launch_dx_flat's data gradient (dx / elu_y vertex-major when dxvm, else
+// batch-major) and the dW slabs described by `d` (its nb is set here;
+// dw_tasks = chunks x units) in one launch.
+int launch_bwd_flat_pair(const float* dpre, const int* flat, int width, const float* w, const float* elu_y,
+                         float* dx, int dxvm, int vsrc, int rows, int batch, int cin, int cout, const DwLatArgs& d,
+                         long dw_tasks, hipStream_t st);
 // dW/db slabs (conv_dw_mfma layout: [n_slabs][9][32][32], db [n_slabs][32] at
 // ws_db) of a 32 -> 32 conv, x and dpre vertex-major, batch % 16 == 0.
 // Workgroups (= slabs) launch_dw uses; max_slabs = the workspace's slab capacity.

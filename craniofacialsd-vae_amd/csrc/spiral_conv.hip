@@ -2741,8 +2741,27 @@ static int bwd_rowsub(const float* x, int xvm, const int32_t* idx, const float* 
   DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, total, g.rchunk, g.gx, 0, batch, xvm, 0};
   if (lat) d.nb = (int)(((long)g.gx * (long)dw_units(cin, cout) + 3) / 4);
   if (xvm && !lat) return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_x: vertex-major x needs a few-row layer");
-  const dim3 grid((unsigned)(a.nb + d.nb));
   const int n_el = cout * kSeq * cin + cout;
+  if (lat && batch % 16 == 0 && cin == 32 && cout == 32 && (flat_width == 8 || flat_width == 12 || flat_width == 16)) {
+    // 16-mesh batches, 32 -> 32: dx straight from dpre by the flat-list MFMA
+    // kernel (one 16-mesh MFMA tile per list entry; dx in x's layout) paired
+    // with the dW slabs in one launch -- no dG round trip, no gather launch
+    // (the fp32 step's E1: 22.1 + 8.2 -> 22.0 us, E2: 8.5 + 5.1 -> 11.9 us;
+    // E3, 32 -> 64 on 267 vertices: 14.9 vs 7.0 + 4.8 us, keeps the dG path).
+    // dx sums each entry's MFMA products into one accumulator (the dG path
+    // rounds every dG element first): equal to fp32 rounding, not bit for bit.
+    rc = vm32::launch_bwd_flat_pair(dpre, inv_flat, flat_width, w, elu_y, dx, xvm, vsrc, rows, batch, cin, cout,
+                                    d, (long)g.gx * (long)dw_units(cin, cout), st);
+    if (rc || !dw) return rc;
+#define RSR(CIN_, COUT_)                                                                          \
+    if (cin == CIN_ && cout == COUT_)                                                             \
+      hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), dim3((unsigned)((n_el + 63) / 64)),       \
+                         dim3(1024), 0, st, workspace, ws_db, dw, db, g.gx);
+    RSR(32, 32) RSR(32, 64)
+#undef RSR
+    return launch_status("spiral_conv_bwd_rowsub_reduce");
+  }
+  const dim3 grid((unsigned)(a.nb + d.nb));
 #define RSP(CIN_, COUT_)                                                                          \
   if (cin == CIN_ && cout == COUT_) {                                                             \
     hipLaunchKernelGGL((conv_bwd_rowsub_pair<CIN_, COUT_>), grid, dim3(256),                      \
@@ -3012,7 +3031,7 @@ extern "C" int cfsd_spiral_conv_bwd_data_flat(const void* dpre, int dpre_dt, con
     if (CFSD_DT_TYPE(dpre_dt) != CFSD_DT_F32)
       return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat: fp32 dx needs fp32 dpre");
     if ((uintptr_t)inv_flat & 15) return set_error(CFSD_EINVAL, "inv_flat must be 16-B aligned");
-    return vm32::launch_dx_flat((const float*)dpre, inv_flat, flat_width, (const float*)w, (const float*)elu_y,
+    return vm32::launch_dx_flat((const float*)dpre, 1, 1, inv_flat, flat_width, (const float*)w, (const float*)elu_y,
                                 (float*)dx, vsrc, rows, batch, cin, cout, (hipStream_t)stream);
   }
   if (!bf::vm16_ok(batch, cin, cout))

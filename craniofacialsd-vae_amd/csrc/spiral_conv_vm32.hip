@@ -162,16 +162,13 @@ __global__ __launch_bounds__(256, kVm32FwdOcc) void conv_fwd_vm32(const float* _
 constexpr int kVm32DxPd = 2;  // list entries in flight ahead of the one being multiplied
 constexpr int kVm32DxOcc = 1;
 template <int CIN, int COUT, int FW>
-__global__ __launch_bounds__(512, kVm32DxOcc) void conv_dx_flat_vm32(const float* __restrict__ dpre,
-                                                         const int4* __restrict__ flat,
-                                                         const float* __restrict__ w,
-                                                         const float* __restrict__ elu_y,
-                                                         float* __restrict__ dx, int vsrc, int rows,
-                                                         int batch) {
+__device__ __forceinline__ void dx_flat_body(const float* __restrict__ dpre, const int4* __restrict__ flat,
+                                             const float* __restrict__ w, const float* __restrict__ elu_y,
+                                             float* __restrict__ dx, int vsrc, int rows, int batch, int dpvm,
+                                             int dxvm, int vb, int nvb, float* lwt) {
   constexpr int K = kS * CIN, OP = COUT + 8, NT = CIN / 16, OC = COUT / 16, FQ = FW / 4;
   constexpr int RB = COUT * 4;  // dpre row bytes
   // lwt[(s*CIN + ci)*OP + o] = W[o][s*CIN + ci]  (16-B reads conflict-free: OP = 40 / 72)
-  extern __shared__ float lwt[];
   coop_copy<12, float>(
       COUT * K, [&](int e) { return w[e]; }, [&](int e, float v) { lwt[(e % K) * OP + e / K] = v; });
   __syncthreads();
@@ -181,8 +178,12 @@ __global__ __launch_bounds__(512, kVm32DxOcc) void conv_dx_flat_vm32(const float
   const long n_tiles = (long)vsrc * G16;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dpre), 0,
                                                     (int)((long)batch * rows * RB), 0x00020000);
-  const int rstride = batch * RB;  // bytes between two rows' blocks
-  const TileSweep sw = xcd_sweep(n_tiles, 8, wave, true);
+  // dpre vertex-major (dpvm: a row's 16-mesh block contiguous) or batch-major
+  // (the Enblock E1: dpre at the kept rows of the coarser, batch-major level):
+  // mesh part per lane, row part as the entry's SGPR offset either way
+  const int rstride = dpvm ? batch * RB : RB;  // bytes between two rows of one mesh
+  const int mstride = dpvm ? RB : rows * RB;   // bytes between two meshes of one row
+  const TileSweep sw = xcd_sweep_v(n_tiles, 8, wave, true, vb, nvb);
 
   auto load_list = [&](long tile, int (&pe)[FW]) {
     const int u = uni((int)tile) / G16;
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(512, kVm32DxOcc) void conv_dx_flat_vm32(const float
     if (tile + sw.step < sw.end) load_list(tile + sw.step, pn);
     const int tl = uni((int)tile);
     const int u = tl / G16, mg = tl - u * G16;
-    const int voff = (mg * 16 + j) * RB + 16 * g;
+    const int voff = (mg * 16 + j) * mstride + 16 * g;
     auto issue = [&](int e, f32x4(&d)[OC]) {
       const int so = pe[e] >= 0 ? (pe[e] / kS) * rstride : kAbsent;
 #pragma unroll
@@ -237,7 +238,8 @@ __global__ __launch_bounds__(512, kVm32DxOcc) void conv_dx_flat_vm32(const float
         for (int t = 0; t < NT; ++t) acc[t] = mfma16(a[t].w, bv.w, acc[t]);
       }
     }
-    const long row = (long)u * batch + mg * 16 + j;
+    // dx / elu_y row of (mesh, u): vertex-major, or batch-major (E2, E3)
+    const long row = dxvm ? (long)u * batch + mg * 16 + j : (long)(mg * 16 + j) * vsrc + u;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       f32x4 v = acc[t];
@@ -253,6 +255,51 @@ __global__ __launch_bounds__(512, kVm32DxOcc) void conv_dx_flat_vm32(const float
 #pragma unroll
     for (int e = 0; e < FW; ++e) pe[e] = pn[e];
   }
+}
+template <int CIN, int COUT, int FW>
+__global__ __launch_bounds__(512, kVm32DxOcc) void conv_dx_flat_vm32(const float* __restrict__ dpre,
+                                                         const int4* __restrict__ flat,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ elu_y,
+                                                         float* __restrict__ dx, int vsrc, int rows,
+                                                         int batch, int dpvm, int dxvm) {
+  extern __shared__ float lwt[];
+  dx_flat_body<CIN, COUT, FW>(dpre, flat, w, elu_y, dx, vsrc, rows, batch, dpvm, dxvm, blockIdx.x, gridDim.x,
+                              lwt);
+}
+
+// The row-subset Enblock backward with vertex-major x / dx (the fp32 step's
+// E1): the flat-list data gradient above (dpre batch-major) and the dW slabs
+// of conv_dw_lat_body (eight waves per workgroup, one (unit, row chunk) task
+// each) as the two halves of ONE launch, workgroups interleaved (no dG round
+// trip, no gather launch, one kernel boundary).
+struct DxFlatArgs {
+  const float* dpre;
+  const int4* flat;
+  const float* w;
+  const float* elu_y;
+  float* dx;
+  int vsrc, rows, batch, dpvm, dxvm, nb;
+};
+template <int CIN, int COUT, int FW>
+__global__ __launch_bounds__(512) void conv_bwd_flat_pair(const DxFlatArgs a, const DwLatArgs d) {
+  extern __shared__ float lwt[];
+  const int bid = blockIdx.x, both = 2 * min(a.nb, d.nb);
+  bool is_dx;
+  int vb;
+  if (bid < both) {
+    is_dx = (bid & 1) == 0;
+    vb = bid >> 1;
+  } else {
+    is_dx = a.nb > d.nb;
+    vb = bid - both + both / 2;
+  }
+  if (is_dx)
+    dx_flat_body<CIN, COUT, FW>(a.dpre, a.flat, a.w, a.elu_y, a.dx, a.vsrc, a.rows, a.batch, a.dpvm, a.dxvm, vb,
+                                a.nb, lwt);
+  else
+    conv_dw_lat_body<CIN, COUT, 8>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows, d.total_rows,
+                                   d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm);
 }
 
 
@@ -716,26 +763,58 @@ int launch_fwd(const float* x, const int* idx, const float* w, const float* bias
 }
 
 template <int CIN, int COUT, int FW>
-static int dxf_t(const float* dpre, const int* flat, const float* w, const float* elu_y, float* dx, int vsrc,
-                 int rows, int batch, hipStream_t st) {
+static int dxf_t(const float* dpre, int dpvm, int dxvm, const int* flat, const float* w, const float* elu_y,
+                 float* dx, int vsrc, int rows, int batch, hipStream_t st) {
   constexpr size_t lds = (size_t)kS * CIN * (COUT + 8) * sizeof(float);
   auto kern = conv_dx_flat_vm32<CIN, COUT, FW>;
   const long tiles = (long)vsrc * (batch / 16);
   const unsigned grid = balanced_blocks(tiles, 8, resident(kern, 512, lds));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows,
-                     batch);
+                     batch, dpvm, dxvm);
   return launch_status("spiral_conv_bwd_data_flat_vm32");
 }
 
-int launch_dx_flat(const float* dpre, const int* flat, int width, const float* w, const float* elu_y, float* dx,
-                   int vsrc, int rows, int batch, int cin, int cout, hipStream_t st) {
+template <int CIN, int COUT, int FW>
+static int pair_t(const float* dpre, const int* flat, const float* w, const float* elu_y, float* dx, int dxvm,
+                  int vsrc, int rows, int batch, DwLatArgs d, long dw_tasks, hipStream_t st) {
+  constexpr size_t lds = (size_t)kS * CIN * (COUT + 8) * sizeof(float);
+  auto kern = conv_bwd_flat_pair<CIN, COUT, FW>;
+  const long tiles = (long)vsrc * (batch / 16);
+  d.nb = (int)((dw_tasks + 7) / 8);
+  const int res = resident(kern, 512, lds);
+  const DxFlatArgs a{dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows, batch, 0, dxvm,
+                     (int)balanced_blocks(tiles, 8, res > d.nb ? res - d.nb : 8)};
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.nb + d.nb)), dim3(512), lds, st, a, d);
+  return launch_status("spiral_conv_bwd_flat_pair");
+}
+
+int launch_bwd_flat_pair(const float* dpre, const int* flat, int width, const float* w, const float* elu_y,
+                         float* dx, int dxvm, int vsrc, int rows, int batch, int cin, int cout, const DwLatArgs& d,
+                         long dw_tasks, hipStream_t st) {
+  if (!ok(batch, cin, cout))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub (vertex-major): batch %% 16 == 0 and 32 -> 32/64 only");
+  if ((long)batch * rows * cout * 4 >= (long)kAbsent)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub (vertex-major): dpre exceeds 32-bit buffer offsets");
+#define BP(CO, FW_)                                                                                         \
+  if (cout == CO && width == FW_)                                                                           \
+    return pair_t<32, CO, FW_>(dpre, flat, w, elu_y, dx, dxvm, vsrc, rows, batch, d, dw_tasks, st);
+  BP(32, 8) BP(32, 12) BP(32, 16)
+#undef BP
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub (vertex-major): unsupported channels %d -> %d / width %d",
+                   cin, cout, width);
+}
+
+int launch_dx_flat(const float* dpre, int dpvm, int dxvm, const int* flat, int width, const float* w,
+                   const float* elu_y, float* dx, int vsrc, int rows, int batch, int cin, int cout, hipStream_t st) {
   if (!ok(batch, cin, cout))
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat (fp32): batch %% 16 == 0 and 32 -> 32/64 only");
   if ((long)batch * rows * cout * 4 >= (long)kAbsent)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat (fp32): dpre exceeds 32-bit buffer offsets");
-#define DF(CO, FW_)                                                                                     \
-  if (cout == CO && width == FW_) return dxf_t<32, CO, FW_>(dpre, flat, w, elu_y, dx, vsrc, rows, batch, st);
-  DF(32, 8) DF(32, 12) DF(32, 16) DF(32, 20) DF(64, 8) DF(64, 12) DF(64, 16) DF(64, 20)
+#define DF(CI, CO, FW_)                                                                                 \
+  if (cin == CI && cout == CO && width == FW_)                                                          \
+    return dxf_t<CI, CO, FW_>(dpre, dpvm, dxvm, flat, w, elu_y, dx, vsrc, rows, batch, st);
+  DF(32, 32, 8) DF(32, 32, 12) DF(32, 32, 16) DF(32, 32, 20) DF(32, 64, 8) DF(32, 64, 12) DF(32, 64, 16)
+  DF(32, 64, 20)
 #undef DF
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat (fp32): unsupported channels %d -> %d / width %d",
                    cin, cout, width);

@@ -827,6 +827,47 @@ def test_rowsub_backward(otopo, dtopo, level, cout, bsz, elu, deferred):
 
 
 @pytest.mark.parametrize("level,cout", [(1, 32), (2, 32), (3, 64)])
+@pytest.mark.parametrize("deferred", [False, True])
+def test_rowsub_backward_vertex_major(otopo, dtopo, level, cout, deferred):
+    """Row-subset backward with vertex-major x / dx / elu_y (the fp32 step's
+    E1 layout; batch-major dpre): dx by the flat-list MFMA kernel straight from
+    dpre, dW slabs by the lat body -- vs autograd of conv -> row subset."""
+    bsz = 16
+    g = torch.Generator().manual_seed(level * 100 + cout)
+    sp = otopo.spirals[level]
+    sel = torch.from_numpy(otopo.down[level][1])
+    v = sp.shape[0]
+    x = torch.randn(bsz, v, 32, generator=g).requires_grad_()
+    w = (torch.randn(cout, 288, generator=g) * 0.1).requires_grad_()
+    b = (torch.randn(cout, generator=g) * 0.1).requires_grad_()
+    y = O.spiral_conv(x, sp, w, b)[:, sel]
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy)
+    ey = O.elu(torch.randn(bsz, v, 32, generator=g))
+    ref_dx = x.grad * torch.where(ey > 0, torch.ones_like(ey), ey + 1)
+    rows = sel.numel()
+    ws = torch.empty(ops.spiral_conv_bwd_rowsub_workspace(bsz, v, rows, 9, 32, cout) // 4 + 1, device=DEV)
+    xv = ops.to_vm(x.detach().to(DEV))
+    eyv = ops.to_vm(ey.to(DEV))
+    dx = ops.vm_empty(bsz, v, 32, device=DEV)
+    dw = torch.empty(cout, 288, device=DEV)
+    db = torch.empty(cout, device=DEV)
+    args = (xv, dtopo.enc_rows[level], dy.to(DEV), dtopo.enc_flat[level], w.detach().to(DEV))
+    if deferred:
+        _, d = ops.spiral_conv_bwd_rowsub(*args, None, None, dx, elu_y=eyv, workspace=ws)
+        ops.dw_reduce_batch([(d, dw, db)])
+    else:
+        ops.spiral_conv_bwd_rowsub(*args, dw, db, dx, elu_y=eyv, workspace=ws)
+    assert ops.is_vm(dx)
+    close(dx, ref_dx, 1e-5, f"rowsub vm dx L{level}")
+    close(dw, w.grad, 1e-5, f"rowsub vm dw L{level}")
+    close(db, b.grad, 1e-5, f"rowsub vm db L{level}")
+    dx2 = ops.vm_empty(bsz, v, 32, device=DEV)
+    ops.spiral_conv_bwd_rowsub(*args, dw, db, dx2, elu_y=eyv, workspace=ws)
+    assert torch.equal(dx, dx2)
+
+
+@pytest.mark.parametrize("level,cout", [(1, 32), (2, 32), (3, 64)])
 def test_rowsub_data_bf16_storage(dtopo, level, cout):
     """dx-only row-subset backward: bf16 storage = one rounding of the fp32
     result (same dG, same gather order), so it equals the fp32 call cast."""
@@ -845,12 +886,13 @@ def test_rowsub_data_bf16_storage(dtopo, level, cout):
     dvm = ops.vm_empty(bsz, v, 32, dtype=torch.bfloat16, device=DEV)
     ops.spiral_conv_bwd_data_rowsub(dpre, dtopo.enc_flat[level], w, v, elu_y=ops.to_vm(ey16), out=dvm)
     assert ops.is_vm(dvm) and torch.equal(dvm, d16)
-    # and the fp32 dx equals the fused rowsub backward's dx
+    # and the fp32 dx equals the fused rowsub backward's dx (at batch 16 that
+    # one multiplies each list entry into one MFMA accumulator: fp32 rounding)
     x = torch.randn(bsz, v, 32, generator=g).to(DEV)
     dxf = torch.empty_like(d32)
     ops.spiral_conv_bwd_rowsub(x, dtopo.enc_rows[level], dpre, dtopo.enc_flat[level], w, None, None, dxf,
                                elu_y=ey16.float())
-    assert torch.equal(dxf, d32)
+    close(dxf, d32, 1e-5, "fused rowsub dx vs dG + gather")
 
 
 @pytest.mark.parametrize("i,bsz", [(0, 16), (0, 3), (1, 4)])

@@ -249,7 +249,7 @@ def build_cases(names=()):
     ev = E.SDVAEEngine(T, E.ModelSpec(), device="cuda", vertex_major=True)
     v = ev.buffers(16)
     for t in (v.dec_up[3], v.dec_out[3], v.dpre_dec[3], v.dec_up[2], v.dpre_dec[2], v.enc_out[0],
-              v.dpre_enc[0]):
+              v.dpre_enc[0], v.dpre_enc[1]):
         t.copy_(torch.randn(t.shape, device="cuda", generator=g))
     v.dec_out[3].copy_(torch.nn.functional.elu(v.dec_out[3]))
     w3v, b3v = ev._dec_w(3)
@@ -280,6 +280,13 @@ def build_cases(names=()):
                                                        ev._enc_w(1)[1], 1, v.enc_out[1])
     cases["dw_e1_vm"] = lambda: ops.spiral_conv_bwd_weight_x(v.enc_out[0], T.enc_rows[1], v.dpre_enc[1], None, None,
                                                              v.ws_dw[("enc", 1)])
+    we1v = ev._enc_w(1)[0]
+    cases["rowsub_e1_vm"] = lambda: ops.spiral_conv_bwd_rowsub(v.enc_out[0], T.enc_rows[1], v.dpre_enc[1],
+                                                               T.enc_flat[1], we1v, None, None, dx=v.dpre_enc[0],
+                                                               elu_y=v.enc_out[0], workspace=v.ws_dw[("enc", 1)])
+    cases["dgonly_e1_vm"] = lambda: ops.spiral_conv_bwd_data_rowsub(v.dpre_enc[1], T.enc_flat[1], we1v, T.n_verts[1],
+                                                                    elu_y=v.enc_out[0], out=v.dpre_enc[0],
+                                                                    workspace=v.ws)
     cases["spmm_up0_vm"] = lambda: ops.spmm_x(T.up_csr[0], v.dec_out[2], T.n_verts[0], out=v.dec_up[3],
                                               uniform=T.up_uniform[0])
     cases["spmm_up0T_vm"] = lambda: ops.spmm_x(T.upT_csr[0], v.g_dec_up[3], T.n_verts[1], elu_y=v.dec_out[2],

@@ -989,3 +989,26 @@ def test_engine_forward_fused_latent_equals_unfused(dtopo):
         outs.append((b.z.clone(), b.h.clone(), b.out.clone(), b.dlat.clone(), b.terms.clone()))
     for a, c in zip(outs[0], outs[1]):
         assert torch.equal(a, c)
+
+
+def test_trainstep_two_step_graph_matches_eager(dtopo):
+    """TrainStep.run(k) on a captured single-GPU runner replays the two-step
+    graph k // 2 times (+ the one-step graph): the parameters, moments and
+    losses of k eager steps, bit for bit."""
+    from craniofacialsd_vae_amd import step as ST
+    res = []
+    for captured in (False, True):
+        data = E.ResidentData(torch.from_numpy(recipe.normalized_meshes(12)).to(DEV), bs=4,
+                              rows=list(range(12)), shuffle=True)
+        eng = make_engine(dtopo, recipe.golden_weights())
+        ts = ST.TrainStep(eng, data)
+        if captured:
+            ts.capture()  # (runs one real step eagerly first)
+            ts.run(5)
+        else:
+            ts.run(6)
+        torch.cuda.synchronize()
+        P = eng.params
+        res.append([t.clone() for t in (P.data, P.exp_avg, P.exp_avg_sq, eng.loss_acc)])
+    for a, c in zip(*res):
+        assert torch.equal(a, c)

@@ -21,6 +21,10 @@ int launch_fwd(const float* x, const int* idx, const float* w, const float* bias
 // layout) vertex-major (dpvm / dxvm) or batch-major; 32 -> 32/64.
 int launch_dx_flat(const float* dpre, int dpvm, int dxvm, const int* flat, int width, const float* w,
                    const float* elu_y, float* dx, int vsrc, int rows, int batch, int cin, int cout, hipStream_t st);
+// launch_dx_flat with batch-major fp32 dpre and bf16 dx / elu_y (32 -> 32):
+// the bf16 step's E1 data gradient, the fp32 sum rounded once.
+int launch_dx_flat_b16(const float* dpre, const int* flat, int width, const float* w, const bf16_t* elu_y,
+                       bf16_t* dx, int dxvm, int vsrc, int rows, int batch, int cin, int cout, hipStream_t st);
 // The row-subset (Enblock) backward, 32 -> 32, batch-major dpre at the kept rows:
 // launch_dx_flat's data gradient (dx / elu_y vertex-major when dxvm, else
 // batch-major) and the dW slabs described by `d` (its nb is set here;

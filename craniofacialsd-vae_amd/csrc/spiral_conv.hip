@@ -2821,6 +2821,16 @@ extern "C" int cfsd_spiral_conv_bwd_data_rowsub(const float* dpre, const int32_t
   if (dg_el * sizeof(float) >= (size_t)kAbsentRow)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_rowsub: dG exceeds 32-bit buffer offsets");
   hipStream_t st = (hipStream_t)stream;
+  if (batch % 16 == 0 && cout == 32 && (flat_width == 4 || flat_width == 8 || flat_width == 12 || flat_width == 16)) {
+    // 16-mesh batches, 32 -> 32: dx straight from dpre by the flat-list MFMA
+    // kernel (no dG round trip, no gather launch; the bf16 step's E1: dG 11.0
+    // + gather 7.0 us), the fp32 sum rounded once for bf16 storage
+    if (dx_dt == CFSD_DT_BF16)
+      return vm32::launch_dx_flat_b16(dpre, inv_flat, flat_width, w, (const bf16_t*)elu_y, (bf16_t*)dx, dxvm, vsrc,
+                                      rows, batch, cin, cout, st);
+    return vm32::launch_dx_flat(dpre, 0, dxvm, inv_flat, flat_width, w, (const float*)elu_y, (float*)dx, vsrc, rows,
+                                batch, cin, cout, st);
+  }
   const int total = batch * rows;
   DgArgs a{dpre, w, workspace, total, rowsub_groups((total + 15) / 16, kSeq * cin / 16), 0};
   a.nb = (int)(((total + 15) / 16 + 3) / 4) * a.n_groups;

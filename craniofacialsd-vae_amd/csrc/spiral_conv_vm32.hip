@@ -161,10 +161,12 @@ __global__ __launch_bounds__(256, kVm32FwdOcc) void conv_fwd_vm32(const float* _
 // next tile's list is loaded at the start of this one.
 constexpr int kVm32DxPd = 2;  // list entries in flight ahead of the one being multiplied
 constexpr int kVm32DxOcc = 1;
-template <int CIN, int COUT, int FW>
+// TY: storage of dx and elu_y (fp32, or bf16 for the bf16 step's E1: the
+// fp32 sum rounded once)
+template <int CIN, int COUT, int FW, typename TY = float>
 __device__ __forceinline__ void dx_flat_body(const float* __restrict__ dpre, const int4* __restrict__ flat,
-                                             const float* __restrict__ w, const float* __restrict__ elu_y,
-                                             float* __restrict__ dx, int vsrc, int rows, int batch, int dpvm,
+                                             const float* __restrict__ w, const TY* __restrict__ elu_y,
+                                             TY* __restrict__ dx, int vsrc, int rows, int batch, int dpvm,
                                              int dxvm, int vb, int nvb, float* lwt) {
   constexpr int K = kS * CIN, OP = COUT + 8, NT = CIN / 16, OC = COUT / 16, FQ = FW / 4;
   constexpr int RB = COUT * 4;  // dpre row bytes
@@ -244,28 +246,28 @@ __device__ __forceinline__ void dx_flat_body(const float* __restrict__ dpre, con
     for (int t = 0; t < NT; ++t) {
       f32x4 v = acc[t];
       if (elu_y) {
-        const f32x4 ey = ld4(elu_y + row * CIN + 16 * t + 4 * g);
+        const f32x4 ey = ld4f(elu_y + row * CIN + 16 * t + 4 * g);
         v.x *= elu_grad_from_out(ey.x);
         v.y *= elu_grad_from_out(ey.y);
         v.z *= elu_grad_from_out(ey.z);
         v.w *= elu_grad_from_out(ey.w);
       }
-      st4(dx + row * CIN + 16 * t + 4 * g, v);
+      st4f(dx + row * CIN + 16 * t + 4 * g, v);
     }
 #pragma unroll
     for (int e = 0; e < FW; ++e) pe[e] = pn[e];
   }
 }
-template <int CIN, int COUT, int FW>
+template <int CIN, int COUT, int FW, typename TY = float>
 __global__ __launch_bounds__(512, kVm32DxOcc) void conv_dx_flat_vm32(const float* __restrict__ dpre,
                                                          const int4* __restrict__ flat,
                                                          const float* __restrict__ w,
-                                                         const float* __restrict__ elu_y,
-                                                         float* __restrict__ dx, int vsrc, int rows,
+                                                         const TY* __restrict__ elu_y,
+                                                         TY* __restrict__ dx, int vsrc, int rows,
                                                          int batch, int dpvm, int dxvm) {
   extern __shared__ float lwt[];
-  dx_flat_body<CIN, COUT, FW>(dpre, flat, w, elu_y, dx, vsrc, rows, batch, dpvm, dxvm, blockIdx.x, gridDim.x,
-                              lwt);
+  dx_flat_body<CIN, COUT, FW, TY>(dpre, flat, w, elu_y, dx, vsrc, rows, batch, dpvm, dxvm, blockIdx.x, gridDim.x,
+                                  lwt);
 }
 
 // The row-subset Enblock backward with vertex-major x / dx (the fp32 step's
@@ -762,11 +764,11 @@ int launch_fwd(const float* x, const int* idx, const float* w, const float* bias
                              : fwd_pick<64, CFSD_ACT_NONE>(x, idx, w, bias, y, yvm, vsrc, rows, batch, st);
 }
 
-template <int CIN, int COUT, int FW>
-static int dxf_t(const float* dpre, int dpvm, int dxvm, const int* flat, const float* w, const float* elu_y,
-                 float* dx, int vsrc, int rows, int batch, hipStream_t st) {
+template <int CIN, int COUT, int FW, typename TY = float>
+static int dxf_t(const float* dpre, int dpvm, int dxvm, const int* flat, const float* w, const TY* elu_y,
+                 TY* dx, int vsrc, int rows, int batch, hipStream_t st) {
   constexpr size_t lds = (size_t)kS * CIN * (COUT + 8) * sizeof(float);
-  auto kern = conv_dx_flat_vm32<CIN, COUT, FW>;
+  auto kern = conv_dx_flat_vm32<CIN, COUT, FW, TY>;
   const long tiles = (long)vsrc * (batch / 16);
   const unsigned grid = balanced_blocks(tiles, 8, resident(kern, 512, lds));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows,
@@ -802,6 +804,19 @@ int launch_bwd_flat_pair(const float* dpre, const int* flat, int width, const fl
 #undef BP
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub (vertex-major): unsupported channels %d -> %d / width %d",
                    cin, cout, width);
+}
+
+int launch_dx_flat_b16(const float* dpre, const int* flat, int width, const float* w, const bf16_t* elu_y,
+                       bf16_t* dx, int dxvm, int vsrc, int rows, int batch, int cin, int cout, hipStream_t st) {
+  if (!(batch % 16 == 0 && cin == 32 && cout == 32))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat (bf16 dx): batch %% 16 == 0 and 32 -> 32 only");
+  if ((long)batch * rows * cout * 4 >= (long)kAbsent)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat (bf16 dx): dpre exceeds 32-bit buffer offsets");
+  if (width == 4) return dxf_t<32, 32, 4, bf16_t>(dpre, 0, dxvm, flat, w, elu_y, dx, vsrc, rows, batch, st);
+  if (width == 8) return dxf_t<32, 32, 8, bf16_t>(dpre, 0, dxvm, flat, w, elu_y, dx, vsrc, rows, batch, st);
+  if (width == 12) return dxf_t<32, 32, 12, bf16_t>(dpre, 0, dxvm, flat, w, elu_y, dx, vsrc, rows, batch, st);
+  if (width == 16) return dxf_t<32, 32, 16, bf16_t>(dpre, 0, dxvm, flat, w, elu_y, dx, vsrc, rows, batch, st);
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_flat (bf16 dx): width %d", width);
 }
 
 int launch_dx_flat(const float* dpre, int dpvm, int dxvm, const int* flat, int width, const float* w,

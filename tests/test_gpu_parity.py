@@ -870,7 +870,8 @@ def test_rowsub_backward_vertex_major(otopo, dtopo, level, cout, deferred):
 @pytest.mark.parametrize("level,cout", [(1, 32), (2, 32), (3, 64)])
 def test_rowsub_data_bf16_storage(dtopo, level, cout):
     """dx-only row-subset backward: bf16 storage = one rounding of the fp32
-    result (same dG, same gather order), so it equals the fp32 call cast."""
+    result (the same fp32 sums: flat-list MFMA at 32 -> 32, dG + gather at
+    32 -> 64), so it equals the fp32 call cast."""
     bsz = 16
     g = torch.Generator().manual_seed(level + cout)
     v, rows = dtopo.n_verts[level], dtopo.n_verts[level + 1]

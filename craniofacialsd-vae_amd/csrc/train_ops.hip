@@ -381,21 +381,21 @@ __global__ __launch_bounds__(kLatThreads) void latent_fwd_k(const LatentArgs a) 
 // Latent head + decoder Linear (model.py:184-188 then :167-168) in ONE
 // launch: the Linear's input z is made in each workgroup's own LDS, so the
 // kernel boundary between them (and the z round trip through memory) is gone.
-// Workgroup g owns 64 columns of y = z W^T + b: its W slice ([64][k],
+// Workgroup g owns 32 columns of y = z W^T + b: its W slice ([32][k],
 // contiguous) is loaded coalesced into registers before the latent phases
 // and parked in LDS after them (lane stride k floats: k odd or 2 mod 4 keeps
 // the reads conflict-free); thread (column, row pair) then runs the same
 // fmaf chain per output as linear_fwd_nred (bit-identical y), z rows read as
-// wave-uniform LDS broadcasts.  64-column slices: 67 workgroups at n = 4288
+// wave-uniform LDS broadcasts.  32-column slices: 134 workgroups at n = 4288
 // (256-column slices with 8 outputs per thread left the Linear's chain of
 // LDS reads as long as the latent head: 18.6 us vs 6.6 + 9.8 + 7.9 for the
-// separate launches; 64 columns: 11.3-11.7 us at 512 or 1024 threads).
+// separate launches; 64 columns: 10.6-10.9 us, 32: 10.1-10.2, 128: 12.6).
 // Every workgroup holds all of z and the LC distances in LDS and writes the
 // LC gradient elements of its 1/grid slice; workgroup 0 also the KL pieces,
 // z and terms with latent_fwd_k's thread mapping and sum tree (1024
 // threads): z, dlat, terms and y all bit-identical to the two launches.
 constexpr int kLatLinThreads = 1024;
-constexpr int kLatLinCols = 64;
+constexpr int kLatLinCols = 32;
 constexpr int kLatLinRows = kLatLinThreads / kLatLinCols;  // row groups (waves) of 2 rows
 constexpr int kLatLinMaxK = 80;  // latent width (configs: 75, 33)
 constexpr int kLatLinWPer = (kLatLinCols * kLatLinMaxK + kLatLinThreads - 1) / kLatLinThreads;

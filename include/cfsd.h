@@ -369,7 +369,7 @@ int cfsd_latent_fwd(const float* mulv, const float* eps, const int32_t* key, flo
  * y [batch, n] = z w^T + bias, w [n, latent], in ONE launch: z, dlat and y are
  * bit-identical to cfsd_latent_fwd + cfsd_linear_fwd(z, w, bias, y, batch,
  * latent, n), terms[] included.  _supported: latent <= 80 and the LDS of z,
- * the pair distances and a 64-row W slice <= 159 KB. */
+ * the pair distances and a 32-row W slice <= 159 KB. */
 int cfsd_latent_linear_fwd_supported(int batch, int latent, int n);
 int cfsd_latent_linear_fwd(const float* mulv, const float* eps, const int32_t* key, float* z,
                            float* dlat, float* terms, int batch, int latent, int region_size,

@@ -439,8 +439,9 @@ __global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restr
 // per SIMD with every memory latency exposed per tile; here a unit's
 // memory traffic is one flat list, 9 contiguous dout blocks and the 2-KiB x /
 // dx blocks.
+constexpr int kBoWaves = 4;  // waves per workgroup (one workgroup = one dW slab)
 template <typename TX, int FW>
-__global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__ dout,
+__global__ __launch_bounds__(64 * kBoWaves, kBoWaves) void conv_bwd_out_vm(const float* __restrict__ dout,
                                                        const int4* __restrict__ flat,
                                                        const float* __restrict__ w,
                                                        const TX* __restrict__ elu_y,
@@ -452,9 +453,9 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
   constexpr int TS = 17;  // T row stride: conflict-free A reads of the dW step
   constexpr int FQ = FW / 4;
   __shared__ float wl[KP * WS];
-  __shared__ float tl_all[4 * 32 * TS];
+  __shared__ float tl_all[kBoWaves * 32 * TS];
   __shared__ float red[NEL];
-  __shared__ float dbl[4 * 48];
+  __shared__ float dbl[kBoWaves * 48];
   const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
   const int i = lane & 15, g = lane >> 4;
   // W'[k][c] = W[o][s*CIN + c], k = 3s + o; row 27 (padding) zero
@@ -477,10 +478,15 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
 #pragma unroll
     for (int b = 0; b < 2; ++b) dwacc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float dbs = 0.f;
-  // software pipeline over the wave's units: the next unit's flat list and
-  // dout dwords are in flight while this unit runs its MFMAs; x / elu_y are
-  // issued at the top of the unit (independent of the dout chain)
-  const TileSweep sw = xcd_sweep(n_units, 4, wave);
+  // Each unit issues its flat list, dout dwords, x and elu_y at its top and
+  // waits for them: no cross-unit prefetch.  Prefetching the next unit's
+  // list + dout (one or two units ahead, scalar or vector-loaded lists) was
+  // 2-7 us SLOWER (kbench, round 4): four waves per SIMD already keep the
+  // CU's vector-memory pipeline at its limit (TD busy ~60 %, most of it
+  // stalled on the L1; SQ counters) and the prefetch registers cost
+  // occupancy.  A per-slot head-row table that removes the list's slot decode
+  // (~40 % fewer scalar instructions) did not help either (28.1 vs 26.4 us).
+  const TileSweep sw = xcd_sweep(n_units, kBoWaves, wave);
   const int voffl = lane < 48 ? lane * 4 : kAbsent;
   auto load_list = [&](long unit, int (&pe)[FW]) {
     const int u = uni((int)unit) / G16;
@@ -501,12 +507,6 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
       v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                            rs, voff, pe[e] >= 0 ? (pe[e] / kS) * rstride : kAbsent, 0));
   };
-  int pe[FW], pn[FW];
-  float v[FW], vn[FW];
-  if (sw.begin < sw.end) {
-    load_list(sw.begin, pe);
-    load_dout(sw.begin, pe, v);
-  }
   for (long unit = sw.begin; unit < sw.end; unit += sw.step) {
     const int un = uni((int)unit);
     const int u = un / G16, mg = un - u * G16;
@@ -523,8 +523,10 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) ey[ct] = ld4f(elu_y + row * CIN + 16 * ct + 4 * g);
     }
-    const bool more = unit + sw.step < sw.end;  // uniform
-    if (more) load_list(unit + sw.step, pn);
+    int pe[FW];
+    float v[FW];
+    load_list(unit, pe);
+    load_dout(unit, pe, v);
     float t[kS];
 #pragma unroll
     for (int s = 0; s < kS; ++s) t[s] = 0.f;
@@ -549,7 +551,6 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
 #pragma unroll
       for (int s = 0; s < kS; ++s) tl[(CO * s + o3) * TS + m3] = t[s];
     }
-    if (more) load_dout(unit + sw.step, pn, vn);
     wave_sync_lds();
     // dx^T = W'^T . T  (2 column tiles x 7 k-steps)
     f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
@@ -580,17 +581,10 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
         for (int nt = 0; nt < 2; ++nt) dwacc[mt][nt] = mfma16(a, xv[q][nt], dwacc[mt][nt]);
       }
     wave_sync_lds();  // T image free for the next unit
-    if (more) {
-#pragma unroll
-      for (int e = 0; e < FW; ++e) {
-        pe[e] = pn[e];
-        v[e] = vn[e];
-      }
-    }
   }
   // block combine in fixed wave order -> one slab
   if (lane < 48) dbl[wave * 48 + lane] = dbs;
-  for (int wv = 0; wv < 4; ++wv) {
+  for (int wv = 0; wv < kBoWaves; ++wv) {
     if (wave == wv) {
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
@@ -609,12 +603,12 @@ __global__ __launch_bounds__(256) void conv_bwd_out_vm(const float* __restrict__
   }
   if (threadIdx.x < CO) {
     float sdb = 0.f;
-    for (int wv = 0; wv < 4; ++wv)
+    for (int wv = 0; wv < kBoWaves; ++wv)
       for (int m = 0; m < 16; ++m) sdb += dbl[wv * 48 + m * CO + threadIdx.x];
     red[CO * K + threadIdx.x] = sdb;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < NEL; e += 256) ws[(long)blockIdx.x * NEL + e] = red[e];
+  for (int e = threadIdx.x; e < NEL; e += 64 * kBoWaves) ws[(long)blockIdx.x * NEL + e] = red[e];
 }
 
 
@@ -888,7 +882,7 @@ int launch_dw(const float* x, const int* idx, const float* dpre, float* ws, floa
 template <typename TX, int FW>
 static int bwd_out_t(const float* dout, const int* flat, const float* w, const TX* elu_y, const TX* x, TX* dx,
                      float* ws, int n_slabs, int vsrc, int rows, int batch, hipStream_t st) {
-  hipLaunchKernelGGL((conv_bwd_out_vm<TX, FW>), dim3(n_slabs), dim3(256), 0, st, dout, (const int4*)flat, w,
+  hipLaunchKernelGGL((conv_bwd_out_vm<TX, FW>), dim3(n_slabs), dim3(64 * kBoWaves), 0, st, dout, (const int4*)flat, w,
                      elu_y, x, dx, ws, vsrc, rows, batch);
   return launch_status("spiral_conv_bwd_out_vm");
 }

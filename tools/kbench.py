@@ -232,6 +232,12 @@ def build_cases(names=()):
                                                               c.ws_dw[("enc", 1)])
     cases["dw_d2_b16"] = lambda: ops.spiral_conv_bwd_weight_x(c.dec_up[2], T.spiral[1], c.dpre_dec[2], None, None,
                                                               c.ws_dw[("dec", 2)])
+    c.dout.copy_(torch.randn(c.dout.shape, device="cuda", generator=g))
+    wo16 = e16.params.view("de_layers.5.layer.weight")
+    cases["dout_bwd_flat_b16"] = lambda: ops.spiral_conv_bwd_out_flat(c.dec_out[3], T.spiral[0], c.dout,
+                                                                      T.spiral_flat[0], wo16, None, None,
+                                                                      dx=c.dpre_dec[3], elu_y=c.dec_out[3],
+                                                                      workspace=c.ws_dw["out"])
     bm_up, bm_out = c.dec_up[3].contiguous(), c.dec_out[3].contiguous()
     bm_dp, bm_g = c.dpre_dec[3].contiguous(), c.g_dec_up[3].contiguous()
     cases["fwd_d3_b16_bm"] = lambda: ops.spiral_conv_fwd_x(bm_up, T.spiral[0], w3h, w16, b3h, 1, bm_out)

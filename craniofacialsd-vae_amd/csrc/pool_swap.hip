@@ -316,8 +316,13 @@ __global__ __launch_bounds__(256) void spmm_sched_csr_k(const int* __restrict__ 
                                                         TY* __restrict__ y, int m, int n, int c4,
                                                         int groups, int bpg, int per, int xvm,
                                                         int yvm) {
-  const int g = (int)blockIdx.x % groups;
-  const int t = (int)(blockIdx.x / groups) * (int)blockDim.x + (int)threadIdx.x;
+  int blk = (int)blockIdx.x;
+  if (xvm) {  // (groups == 1) XCD-contiguous slot ranges: XCD k (= blockIdx % 8) runs the k-th eighth of the schedule
+    const int nb = (int)gridDim.x, k = blk & 7, j = blk >> 3, q8 = nb >> 3, r8 = nb & 7;
+    blk = k * q8 + (k < r8 ? k : r8) + j;
+  }
+  const int g = blk % groups;
+  const int t = (blk / groups) * (int)blockDim.x + (int)threadIdx.x;
   if (t >= per) return;
   const int rowq = bpg * c4;  // threads per schedule slot
   const int slot = t / rowq, rem = t - slot * rowq;

@@ -191,6 +191,7 @@ class DeviceTopology:
         self.upT_order = []     # row schedule of each up transpose (None: short rows)
         self.up_uniform = []    # entries per row of each up matrix when uniform (else 0)
         self.upT_sched = []     # each up transpose stored in its visiting order (None: short rows)
+        self.upT_nat = []       # the same in natural row order (vertex-major x: XCD-contiguous row ranges)
         self.np_spirals = [np.asarray(s, np.int64) for s in spirals]
         for l in range(self.n_levels):
             sp = np.asarray(spirals[l], np.int64)
@@ -227,6 +228,9 @@ class DeviceTopology:
             self.upT_order.append(_dev(sched, self.device) if sched is not None else None)
             self.upT_sched.append(tuple(_dev(a, self.device) for a in scheduled_csr(*upT, sched))
                                   if sched is not None else None)
+            self.upT_nat.append(tuple(_dev(a, self.device) for a in
+                                      scheduled_csr(*upT, np.arange(len(upT[0]) - 1)))
+                                if sched is not None else None)
         # composite up-sampling rows of every spiral position (the Deblock
         # forward's fused Pool(up) gather, cfsd_spiral_conv_fwd_up): for up
         # matrix ui (level ui+1 -> level ui, uniform 3-entry rows) and spiral

@@ -296,13 +296,7 @@ def build_cases(names=()):
     cases["spmm_up0_vm"] = lambda: ops.spmm_x(T.up_csr[0], v.dec_out[2], T.n_verts[0], out=v.dec_up[3],
                                               uniform=T.up_uniform[0])
     cases["spmm_up0T_vm"] = lambda: ops.spmm_x(T.upT_csr[0], v.g_dec_up[3], T.n_verts[1], elu_y=v.dec_out[2],
-                                               out=v.dpre_dec[2], sched=T.upT_sched[0])
-    if any(n.startswith("spmm_up0T_nat") for n in names):  # the up0 transpose in natural row order
-        up_np = [a.cpu().numpy() for a in T.upT_csr[0]]
-        nat = tuple(t.to("cuda") for t in (torch.from_numpy(np.asarray(a)) for a in
-                                           topology.scheduled_csr(*up_np, np.arange(T.n_verts[1]))))
-        cases["spmm_up0T_nat"] = lambda: ops.spmm_x(T.upT_csr[0], v.g_dec_up[3], T.n_verts[1], elu_y=v.dec_out[2],
-                                                    out=v.dpre_dec[2], sched=nat)
+                                               out=v.dpre_dec[2], sched=T.upT_nat[0])
     if "red_items" in names:  # the step's batched slab reduce, item by item (HIP events)
         cap = []
         orig = ops.dw_reduce_batch

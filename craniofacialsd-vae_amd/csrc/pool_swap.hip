@@ -316,11 +316,10 @@ __global__ __launch_bounds__(256) void spmm_sched_csr_k(const int* __restrict__ 
                                                         TY* __restrict__ y, int m, int n, int c4,
                                                         int groups, int bpg, int per, int xvm,
                                                         int yvm) {
-  int blk = (int)blockIdx.x;
-  if (xvm) {  // (groups == 1) XCD-contiguous slot ranges: XCD k (= blockIdx % 8) runs the k-th eighth of the schedule
-    const int nb = (int)gridDim.x, k = blk & 7, j = blk >> 3, q8 = nb >> 3, r8 = nb & 7;
-    blk = k * q8 + (k < r8 ? k : r8) + j;
-  }
+  // vertex-major x (groups == 1): XCD k runs the k-th eighth of the schedule,
+  // so the rows sharing a source block meet in one L2 (natural row order:
+  // up0T 112.9 -> 64.1 MB of HBM traffic, 21.8 -> 20.0 us)
+  const int blk = xvm ? xcd_block() : (int)blockIdx.x;
   const int g = blk % groups;
   const int t = (blk / groups) * (int)blockDim.x + (int)threadIdx.x;
   if (t >= per) return;

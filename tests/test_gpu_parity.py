@@ -257,6 +257,14 @@ def test_pool_scheduled_transpose(dtopo, bsz, dts):
         b.zero_()
         ops.spmm_x(dtopo.upT_csr[level], x, m, elu_y=ey, out=b, sched=dtopo.upT_sched[level])
         assert torch.equal(a, b), f"level {level} (visiting-order CSR)"
+        # vertex-major source (the engine's levels 0/1): XCD-contiguous row ranges, either order
+        xv, eyv = ops.to_vm(x), ops.to_vm(ey)
+        for sch in (dtopo.upT_sched[level], dtopo.upT_nat[level]):
+            if sch is None:
+                continue
+            c = ops.vm_empty(bsz, m, 32, dtype=dt[dts[1]], device=DEV)
+            ops.spmm_x(dtopo.upT_csr[level], xv, m, elu_y=eyv, out=c, sched=sch)
+            assert torch.equal(a, c), f"level {level} (vertex-major)"
 
 
 @pytest.mark.parametrize("bsz", [16, 3])

@@ -140,6 +140,7 @@ class Runner:
 
     def capture(self):
         self.ts.capture()
+        self.ts.capture_pair()  # the two-step graph the timed run(k) replays, recorded before timing
 
     def step(self):
         self.ts.step()
@@ -255,10 +256,49 @@ def launch_cost(name, a):
     if name == "cfsd_linear_bwd_split":
         m, k, n = a[6:9]
         return 4.0 * m * k * n, f4 * (m * n + 2 * n * k + m * k), FP32_PEAK_TFLOPS
+    if name == "cfsd_spiral_conv_bwd_out_flat":  # xyz output conv: dx (with ELU') + dW in one pass
+        sx = sz(a[1])  # x, elu_y, dx storage
+        B, vs, rows, S, ci, co = a[14:20]
+        dx, elu = a[9] is not None, a[8] is not None
+        fl = 2.0 * B * rows * S * ci * co * (2 if dx else 1)
+        by = (sx * B * vs * ci + 4 * B * rows * co + 4 * co * S * ci + 4 * vs * a[6]
+              + (sx * B * vs * ci * (2 if elu else 1) if dx else 0))
+        return fl, by, FP32_PEAK_TFLOPS
+    if name == "cfsd_spiral_conv_fwd_up":  # Deblock: Pool(up) inside the conv gather
+        B, nc, rows, S, ci, co = a[8:14]
+        up_out = a[7] is not None
+        fl = 2.0 * B * rows * S * ci * co + 2.0 * 3 * B * rows * ci
+        by = (f4 * (B * nc * ci + B * rows * co + co * S * ci + (B * rows * ci if up_out else 0))
+              + 4 * rows * S + 8 * 3 * rows)  # idx + the up matrix (3 entries per row: col + val)
+        return fl, by, FP32_PEAK_TFLOPS
+    if name == "cfsd_spiral_conv_bwd_rowsub_x":  # row-subset dx + dW, x / dx / elu_y in x_dt
+        sx = sz(a[1])
+        B, vs, rows, S, ci, co = a[13:19]
+        elu = a[7] is not None
+        return (4.0 * B * rows * S * ci * co,
+                sx * B * vs * ci * (2 if elu else 1) + sx * B * vs * ci + f4 * (B * rows * co + co * S * ci)
+                + 4 * rows * S + 4 * vs * a[5], FP32_PEAK_TFLOPS)
+    if name == "cfsd_latent_linear_fwd":  # latent head (KL, LC, reparameterisation) + decoder Linear
+        bsz, lat, n = a[6], a[7], a[19]
+        nin = 2 * lat if a[10] else lat
+        return (2.0 * bsz * lat * n + 10.0 * bsz * lat,
+                f4 * (bsz * nin + bsz * lat * 4 + n * lat + n + bsz * n), FP32_PEAK_TFLOPS)
+    if name in ("cfsd_latent_bwd", "cfsd_latent_bwd_parts"):  # latent head backward
+        bsz, lat = (a[6], a[7]) if name == "cfsd_latent_bwd" else (a[7], a[8])
+        return 10.0 * bsz * lat, f4 * bsz * lat * 8, FP32_PEAK_TFLOPS
+    if name == "cfsd_dw_reduce_batch_adam":  # the slab reduction is bookkeeping; Adam's 7 streams are not
+        n = a[7].value if hasattr(a[7], "value") else a[7]
+        return 0.0, 7.0 * f4 * n, None
     if name == "cfsd_adam":
         n = a[5].value if hasattr(a[5], "value") else a[5]
         return 0.0, 7.0 * f4 * n, None
     return 0.0, 0.0, None
+
+
+# Launches that do no work the algorithm requires (priced at zero by
+# launch_cost): step counter / noise / batch pick, loss reduction, the
+# deferred weight-gradient slab reduction, gradient scaling.
+BOOKKEEPING = ("cfsd_step_begin", "cfsd_loss_finalize", "cfsd_dw_reduce_batch", "cfsd_scale")
 
 
 def step_roofline(runner, ms_per_step):
@@ -292,8 +332,10 @@ def step_roofline(runner, ms_per_step):
         "frac_of_step_time": ideal_sum / (ms_per_step * 1e-3),
         "achieved_tflops_step": flop_sum / (ms_per_step * 1e-3) / 1e12,
         "note": "frac = sum over launches of max(flop/peak, bytes/HBM) / measured time; "
-                "bookkeeping launches (latent head, loss finalise, dW slab reduce, step_begin) "
-                "count as time with no required work",
+                "bookkeeping launches (" + ", ".join(BOOKKEEPING) + ") count as time with no required "
+                "work; cfsd_dw_reduce_batch_adam is priced at Adam's 7 x 4 B per parameter only",
+        "unpriced_work_launches": sorted({n for n, _, fl, by, _ in rows if fl == 0 and by == 0
+                                          and n not in BOOKKEEPING}),
         "top_launches": [{"name": n, "us": t * 1e6, "frac": (i / t if t else None)}
                          for n, t, _, _, i in top],
     }

@@ -21,8 +21,9 @@ struct FwdKsArgs {
   const float* bias;    // [COUT] or null
   float* y;             // [batch, rows, COUT] in layout yvm
   float* yup;           // UP: the up-sampled input [batch, rows, CIN] (written), or null
-  const int* up_col;    // UP: 3 columns per fine vertex (uniform-row up matrix), else null
-  const float* up_val;  // UP: 3 values per fine vertex
+  const int* up_col;    // UP (conv_fwd_pt): composite table [rows][9][3], the 3 coarse columns of the
+                        // up-sampled row at spiral position (r, s) (topology.up_comp), else null
+  const float* up_val;  // UP: the matching [rows][9][3] values
   int vsrc, rows, batch, n_coarse;
   long total_rows;      // batch * rows
   int xvm, yvm, elu;

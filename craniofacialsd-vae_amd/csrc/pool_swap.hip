@@ -430,10 +430,10 @@ __global__ __launch_bounds__(256) void spectral_blend_k(const float* __restrict_
 // Dataset normalisation (data_loading.py:259-260, (verts - mean) / std with
 // per-vertex [nv, c] statistics): subtraction then IEEE division, the two
 // roundings of the reference's torch ops, so the result is bit-exact.
-__global__ __launch_bounds__(256) void normalize_k(const float* __restrict__ x,
+__global__ __launch_bounds__(256) void normalize_k(const float* x,  // may alias out (in-place normalisation)
                                                    const float* __restrict__ mean,
                                                    const float* __restrict__ std,
-                                                   float* __restrict__ out, int per_mesh, long total) {
+                                                   float* out, int per_mesh, long total) {
 #pragma clang fp contract(off)
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;

@@ -63,14 +63,15 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_fwd_ks(c
   constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN, SPW = kSeq / NSG;
   constexpr int LDC = COUT + 4;  // partial row stride (kg rows land on distinct banks)
   static_assert(kSeq % NSG == 0, "slot groups");
+  // fused Pool(up) lives in conv_fwd_pt only (its composite [rows][9][3] table)
+  static_assert(!UP, "conv_fwd_ks has no fused up-sampling: use conv_fwd_pt<.., 1>");
   __shared__ f32x4 part4[NSG * RT * 16 * LDC / 4];
   float* part = reinterpret_cast<float*>(part4);
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const long rt0 = (long)xcd_block() * RT;
   const long M = a.total_rows;
-  const int nv_x = UP ? a.n_coarse : a.vsrc;
-  const Lay lx = make_lay(a.xvm, a.batch, nv_x);
+  const Lay lx = make_lay(a.xvm, a.batch, a.vsrc);
   // this lane's row in each tile (x's layout), its mesh / vertex and spiral
   int bq[RT], src[RT][SPW];
 #pragma unroll
@@ -92,51 +93,13 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_fwd_ks(c
 #pragma unroll
       for (int t = 0; t < NCT; ++t) bw[j][c][t] = ld4(wb + (long)t * 16 * K + (g * SPW + j) * CIN + 16 * c);
   f32x4 av[RT][SPW][CH];
-  if constexpr (UP) {
-    int cc[RT][SPW][3];
-    float vv[RT][SPW][3];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+  for (int rt = 0; rt < RT; ++rt) {
+    const float* xb = a.x + (long)bq[rt] * lx.bs * CIN + 4 * kg;
 #pragma unroll
-      for (int j = 0; j < SPW; ++j)
+    for (int j = 0; j < SPW; ++j)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          cc[rt][j][k] = a.up_col[src[rt][j] * 3 + k];
-          vv[rt][j][k] = a.up_val[src[rt][j] * 3 + k];
-        }
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const float* xb = a.x + (long)bq[rt] * lx.bs * CIN + 4 * kg;
-#pragma unroll
-      for (int j = 0; j < SPW; ++j)
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          const f32x4 x0 = ld4(xb + (long)cc[rt][j][0] * lx.vs * CIN + 16 * c);
-          const f32x4 x1 = ld4(xb + (long)cc[rt][j][1] * lx.vs * CIN + 16 * c);
-          const f32x4 x2 = ld4(xb + (long)cc[rt][j][2] * lx.vs * CIN + 16 * c);
-          av[rt][j][c] = up_row4(x0, x1, x2, vv[rt][j][0], vv[rt][j][1], vv[rt][j][2]);
-        }
-    }
-    // slot 0 of spiral row r is r itself: wave 0 holds the tile's up-sampled rows
-    if (g == 0 && a.yup) {
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        const long m = (rt0 + rt) * 16 + r16;
-        if (m < M) {
-#pragma unroll
-          for (int c = 0; c < CH; ++c) st4(a.yup + m * CIN + 16 * c + 4 * kg, av[rt][0][c]);
-        }
-      }
-    }
-  } else {
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const float* xb = a.x + (long)bq[rt] * lx.bs * CIN + 4 * kg;
-#pragma unroll
-      for (int j = 0; j < SPW; ++j)
-#pragma unroll
-        for (int c = 0; c < CH; ++c) av[rt][j][c] = ld4(xb + (long)src[rt][j] * lx.vs * CIN + 16 * c);
-    }
+      for (int c = 0; c < CH; ++c) av[rt][j][c] = ld4(xb + (long)src[rt][j] * lx.vs * CIN + 16 * c);
   }
   f32x4 acc[RT][NCT];
 #pragma unroll

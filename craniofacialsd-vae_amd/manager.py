@@ -93,6 +93,10 @@ class ModelManager:
         self.to_mm_const = configurations["data"].get("to_mm_constant", 1.0)
         self.device = torch.device(device)
         self._swap_features = bool(configurations["data"].get("swap_features", True))
+        if float(configurations["optimization"]["latent_consistency_weight"]) > 0 and not self._swap_features:
+            # model_manager.py:93-94 (assert self._swap_features): the latent
+            # consistency loss is defined on swapped bs x bs groups only
+            raise ValueError("latent_consistency_weight > 0 needs data.swap_features: True")
         self.template = precompute.load_template(configurations["data"]["template_path"])
         self.topology_arrays = load_or_build_topology(configurations, self.template, precomputed_storage_path)
         self.topology = topology.DeviceTopology.from_npz(self.topology_arrays, device=self.device)
@@ -214,6 +218,33 @@ class ModelManager:
             writer.add_scalar(phase + "/" + str(k), losses[k], epoch + 1)
 
     # ------------------------------------------------------------ model access
+    @property
+    def net(self):
+        """The drop-in :class:`model.Model` (``ModelManager._net``,
+        ``model_manager.py:60-67``) over the engine's parameter STORAGE: its
+        ``nn.Parameter``s are views of the flat buffer, so the engine's Adam
+        updates are what it computes with.  Autograd runs through libcfsd
+        (``model.py`` autograd Functions); parameter gradients it produces
+        land in the module's own ``.grad`` tensors, not in the engine's."""
+        if getattr(self, "_net", None) is None:
+            self._net = _engine_model(self.engine, self.topology_arrays, self._model_params, self.device)
+        return self._net
+
+    def forward(self, data):
+        """``ModelManager.forward`` (``model_manager.py:240-241``):
+        ``self._net(data.x)`` in the module's current train / eval mode, with
+        autograd.  ``data``: an object with ``.x`` [B, V, 3] (a ``Data``
+        batch) or the tensor itself."""
+        x = data.x if hasattr(data, "x") else data
+        return self.net(x.to(self.device))
+
+    def generate_for_opt(self, z):
+        """``ModelManager.generate_for_opt`` (``model_manager.py:253-255``):
+        decode in train mode WITH autograd, so a caller can optimise ``z``
+        (the reference's latent fitting).  Returns [N, V, 3]."""
+        self.net.train()
+        return self.net.decode(z.to(self.device))
+
     def encode(self, x):
         """Eval-mode latents of device meshes [N, V, 3] (model_manager.py:243-246)."""
         return self.engine.encode_all(x, batch_size=self.bs * self.bs)
@@ -237,3 +268,32 @@ class ModelManager:
 
     def resume(self, checkpoint_dir):
         return self.engine.resume(checkpoint_dir)
+
+
+def _engine_model(engine, arrays, model_params, device):
+    """A :class:`model.Model` built from the precomputed topology (int64
+    spirals, sparse-COO transforms in file order, as the reference unpickles
+    them) whose parameters are re-bound to views of ``engine.params.data``."""
+    import torch.nn as nn
+
+    from . import model as M
+    n = int(arrays["n_levels"])
+    spirals = [torch.from_numpy(np.asarray(arrays[f"spiral_{l}"], np.int64)).to(device) for l in range(n)]
+
+    def sp(name, l):
+        idx = np.stack([arrays[f"{name}_{l}_row"], arrays[f"{name}_{l}_col"]]).astype(np.int64)
+        return torch.sparse_coo_tensor(torch.from_numpy(idx),
+                                       torch.from_numpy(np.asarray(arrays[f"{name}_{l}_val"], np.float32)),
+                                       tuple(np.asarray(arrays[f"{name}_{l}_shape"]).tolist()))
+
+    S = engine.spec
+    net = M.Model(S.in_ch, S.out_ch, S.latent, spirals, [sp("down", l) for l in range(n)],
+                  [sp("up", l) for l in range(n)], pre_z_sigmoid=bool(model_params.get("pre_z_sigmoid", False)),
+                  is_vae=S.is_vae).to(device)
+    for name, _ in list(net.named_parameters()):
+        *path, leaf = name.split(".")
+        mod = net
+        for p in path:
+            mod = getattr(mod, p)
+        setattr(mod, leaf, nn.Parameter(engine.params.view(name)))  # shares the flat buffer's storage
+    return net

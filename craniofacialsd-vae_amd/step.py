@@ -17,8 +17,8 @@ Step anatomy (every launch on one stream; nothing synchronises with the host):
   reduce.  On one GPU Adam rides in that reduce (``cfsd_dw_reduce_batch_adam``);
 * ``part_c``: (data-parallel only) Adam, after the gradient all-reduce.
 
-One GPU: the three parts are ONE graph (and a second graph holds two whole
-steps, which :meth:`TrainStep.run` replays for consecutive steps).  Data-parallel: three graphs, with
+One GPU: the three parts are ONE graph (and a second graph, recorded on the
+first :meth:`TrainStep.run` of two or more steps, holds two whole steps).  Data-parallel: three graphs, with
 the two RCCL all-reduce buckets issued between the replays -- the decoder /
 bottleneck bucket right after ``part_a`` so it overlaps ``part_b`` (RCCL runs
 on its own stream, ordered after the work already queued), the encoder-conv
@@ -117,20 +117,24 @@ class TrainStep:
             with torch.cuda.graph(g):
                 self.part_a()
                 self.part_b()
-            # two steps in one graph: run(k) replays it k // 2 times, halving
-            # the per-replay launch gap (~8 us between consecutive replays)
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2):
-                for _ in range(2):
-                    self.part_a()
-                    self.part_b()
             self.graphs = [g]
-            self.graph2 = g2
         else:
             self.graphs = [torch.cuda.CUDAGraph() for _ in range(3)]
             for g, fn in zip(self.graphs, (self.part_a, self.part_b, self.part_c)):
                 with torch.cuda.graph(g):
                     fn()
+
+    def capture_pair(self):
+        """Record (once) the single-GPU graph holding two whole steps, which
+        :meth:`run` replays k // 2 times: half the per-replay launch gaps
+        (~8 us between consecutive replays).  Nothing runs while recording."""
+        if self.graph2 is None and self.graphs is not None and self.avg is None:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                for _ in range(2):
+                    self.part_a()
+                    self.part_b()
+            self.graph2 = g2
 
     def step(self):
         if self.graphs is None:
@@ -151,6 +155,8 @@ class TrainStep:
         """``k`` training steps (the same steps as ``k`` calls of :meth:`step`);
         a captured single-GPU runner replays the two-step graph."""
         if self.graphs is not None and self.avg is None:
+            if k >= 2:
+                self.capture_pair()
             for _ in range(k // 2):
                 self.graph2.replay()
             if k % 2:

@@ -58,7 +58,9 @@ def make_workspace(tmp_path_factory, topo_npz, n_meshes=40, swap=True):
     for i in range(n_meshes):
         v = m["verts"][i % 12] + (0 if i < 12 else rs.normal(0, 0.002, m["verts"][0].shape))
         write_obj(d / "meshes" / f"{'nacm'[i % 4]}_{i:03d}.obj", v.astype(np.float32))
-    cfg = dict(CONFIG, data={"template_path": str(d / "template.ply"), "precomputed_path": str(d / "pre"),
+    opt = dict(CONFIG["optimization"], latent_consistency_weight=CONFIG["optimization"]
+               ["latent_consistency_weight"] if swap else 0.0)  # LC needs the swap (model_manager.py:93-94)
+    cfg = dict(CONFIG, optimization=opt, data={"template_path": str(d / "template.ply"), "precomputed_path": str(d / "pre"),
                              "dataset_path": str(d / "meshes"), "normalize_data": True, "to_mm_constant": 89.11,
                              "swap_features": swap, "stratified_split": False})
     with open(d / "config.yaml", "w") as f:
@@ -149,6 +151,54 @@ def test_epoch_without_swap_matches_oracle(tmp_path_factory, topo_npz, otopo):
     assert got_t["latent_consistency"] == 0.0 and got_v["latent_consistency"] == 0.0
     np.testing.assert_allclose([got_t[k] for k in keys], sums / 7, rtol=1e-4, atol=1e-9)
     np.testing.assert_allclose([got_v[k] for k in keys], vs, rtol=1e-4, atol=1e-9)
+
+
+def test_manager_forward_and_generate_for_opt(workspace, otopo):
+    """``ModelManager.forward`` (model_manager.py:240-241: the net on data.x
+    with autograd) and ``generate_for_opt`` (:253-255: decode in train mode
+    with autograd, the reference's latent fitting): the drop-in Model over the
+    engine's parameter storage.  Eval reconstructions equal the goldens the
+    reference's model.py produced; dL/dz of a decode equals the oracle's."""
+    from craniofacialsd_vae_amd import manager as M
+    d, cfg = workspace
+    man = M.ModelManager(cfg, device="cuda", precomputed_storage_path=cfg["data"]["precomputed_path"],
+                         seed=5, use_graph=False)
+    w = recipe.golden_weights()
+    man.engine.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
+    assert list(man.net.state_dict().keys()) == list(w.keys())
+    # parameters are views of the engine's flat buffer (Adam updates are seen)
+    p = man.net.de_layers[0].weight
+    assert p.data_ptr() == man.engine.params.view("de_layers.0.weight").data_ptr()
+    ge = np.load(f"{recipe.HERE}/golden_eval.npz")
+    man.net.eval()
+    with torch.no_grad():
+        out, z, mu, lv = man.forward(torch.from_numpy(recipe.normalized_meshes(8)).cuda())
+    assert np.abs(out.cpu().numpy() - ge["recon"]).sum(-1).max() <= 1e-4
+    assert np.abs(mu.cpu().numpy() - ge["mu"]).max() <= 1e-4
+    g = torch.Generator().manual_seed(5)
+    z0 = torch.randn(16, 75, generator=g)
+    r = torch.randn(16, 17039, 3, generator=g)
+    zd = z0.cuda().requires_grad_(True)
+    out = man.generate_for_opt(zd)
+    assert man.net.training
+    (out * r.cuda()).sum().backward()
+    P = O.make_params(w)
+    zo = z0.clone().requires_grad_(True)
+    oo = O.decode(P, zo, otopo)
+    (oo * r).sum().backward()
+    assert np.abs(out.detach().cpu().numpy() - oo.detach().numpy()).sum(-1).max() <= 1e-4
+    ref = zo.grad.numpy()
+    err = np.abs(zd.grad.cpu().numpy() - ref).max() / (1 + np.abs(ref).max())
+    assert err < 1e-4, err
+
+
+def test_lc_without_swap_is_refused(workspace):
+    """model_manager.py:93-94: latent consistency needs swapped batches."""
+    from craniofacialsd_vae_amd import manager as M
+    d, cfg = workspace
+    bad = dict(cfg, data=dict(cfg["data"], swap_features=False))
+    with pytest.raises(ValueError):
+        M.ModelManager(bad, device="cuda", precomputed_storage_path=cfg["data"]["precomputed_path"])
 
 
 def test_cli_end_to_end_and_resume(workspace, tmp_path):

@@ -9,6 +9,7 @@
 // SwapFeatures (swap_batch_transform.py:13-52): bs base meshes -> bs^2 meshes,
 // out[i*bs + j] = mesh i with the swapped region's feature vertices from j.
 #include "cfsd_common.h"
+#include "side_work.h"
 
 namespace cfsd {
 
@@ -315,11 +316,17 @@ __global__ __launch_bounds__(256) void spmm_sched_csr_k(const int* __restrict__ 
                                                         const TY* __restrict__ elu_y,
                                                         TY* __restrict__ y, int m, int n, int c4,
                                                         int groups, int bpg, int per, int xvm,
-                                                        int yvm) {
+                                                        int yvm, int n_main, const SideJob side) {
+  const int n_side = side_grid(side);
+  if ((int)blockIdx.x < n_side) {  // side work riding in this launch (side_work.h)
+    if ((int)blockIdx.x < side.n_blocks) side_block<4>(side, (int)blockIdx.x);
+    return;
+  }
+  const int bid = (int)blockIdx.x - n_side;
   // vertex-major x (groups == 1): XCD k runs the k-th eighth of the schedule,
   // so the rows sharing a source block meet in one L2 (natural row order:
   // up0T 112.9 -> 64.1 MB of HBM traffic, 21.8 -> 20.0 us)
-  const int blk = xvm ? xcd_block() : (int)blockIdx.x;
+  const int blk = xvm ? xcd_block_of(bid, n_main) : bid;
   const int g = blk % groups;
   const int t = (blk / groups) * (int)blockDim.x + (int)threadIdx.x;
   if (t >= per) return;
@@ -649,6 +656,14 @@ extern "C" int cfsd_spmm_sched_csr(const int32_t* ptr_s, const int32_t* col_s, c
                                    const int32_t* rows_s, const void* x, int x_dt,
                                    const void* elu_y, void* y, int y_dt, int batch, int m, int n,
                                    int c, void* stream) {
+  return cfsd_spmm_sched_csr_side(ptr_s, col_s, val_s, rows_s, x, x_dt, elu_y, y, y_dt, batch, m, n, c, nullptr,
+                                  stream);
+}
+
+extern "C" int cfsd_spmm_sched_csr_side(const int32_t* ptr_s, const int32_t* col_s, const float* val_s,
+                                        const int32_t* rows_s, const void* x, int x_dt, const void* elu_y,
+                                        void* y, int y_dt, int batch, int m, int n, int c,
+                                        const cfsd_side_work* side, void* stream) {
   if (!ptr_s || !col_s || !val_s || !rows_s || !x || !y)
     return set_error(CFSD_EINVAL, "spmm_sched_csr: null pointer");
   if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
@@ -664,11 +679,14 @@ extern "C" int cfsd_spmm_sched_csr(const int32_t* ptr_s, const int32_t* col_s, c
   const int groups = (!xvm && batch % 8 == 0) ? 8 : 1, bpg = batch / groups;
   const int per = bpg * m * (c / 4);
   const unsigned nb = (unsigned)(groups * ((per + 255) / 256));
+  SideJob J;
+  const int rc = make_side_job(side, J);
+  if (rc) return rc;
   const hipStream_t st = (hipStream_t)stream;
-#define SPSC(TX, TY)                                                                             \
-  hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY>), dim3(nb), dim3(256), 0, st, ptr_s, col_s, val_s, \
-                     rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, groups, bpg, per,   \
-                     xvm, yvm)
+#define SPSC(TX, TY)                                                                                        \
+  hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY>), dim3(nb + side_grid(J)), dim3(256), 0, st, ptr_s, col_s, val_s, \
+                     rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, groups, bpg, per, xvm, yvm,  \
+                     (int)nb, J)
   if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPSC(float, float);
   else if (x_dt == CFSD_DT_F32) SPSC(float, bf16_t);
   else if (y_dt == CFSD_DT_F32) SPSC(bf16_t, float);

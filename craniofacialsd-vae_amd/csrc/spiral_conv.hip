@@ -22,6 +22,7 @@
 #include "conv_vm32.h"
 #include "conv_coarse.h"
 #include "conv_lat.h"
+#include "side_work.h"
 
 namespace cfsd {
 
@@ -1027,8 +1028,13 @@ struct DxLatArgs {
   int nb;
 };
 template <int CIN, int COUT, int CTW>
-__global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, const DwLatArgs d) {
-  const int bid = blockIdx.x, both = 2 * min(a.nb, d.nb);
+__global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, const DwLatArgs d, const SideJob side) {
+  const int n_side = side_grid(side);
+  if ((int)blockIdx.x < n_side) {  // side work riding in this launch (side_work.h)
+    if ((int)blockIdx.x < side.n_blocks) side_block<4>(side, (int)blockIdx.x);
+    return;
+  }
+  const int bid = (int)blockIdx.x - n_side, both = 2 * min(a.nb, d.nb);
   bool is_dx;
   int vb;
   if (bid < both) {
@@ -2570,7 +2576,29 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
                                     float* dx, float* dw, float* db, float* workspace,
                                     size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
                                     int cin, int cout, void* stream) {
-  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
+  return cfsd_spiral_conv_bwd_side(x, idx, dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, dw, db, workspace,
+                                   workspace_bytes, batch, vsrc, rows, seq, cin, cout, nullptr, stream);
+}
+
+extern "C" int cfsd_spiral_conv_bwd_side(const float* x, const int32_t* idx, const float* dpre,
+                                         const int32_t* inv_ptr, const int32_t* inv_row,
+                                         const int32_t* inv_head, const float* w, const float* elu_y,
+                                         float* dx, float* dw, float* db, float* workspace,
+                                         size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
+                                         int cin, int cout, const cfsd_side_work* side, void* stream) {
+  SideJob J;
+  int rc = make_side_job(side, J);
+  if (rc) return rc;
+  // hosts that cannot carry it (every shape but the paired lat launch) run
+  // the side work in a launch of its own right after the conv
+  const bool hosted = J.n_blocks > 0 && dx && !bwd_ks_paired(batch, vsrc, rows, cin, cout) &&
+                      bwd_paired(batch, vsrc, rows, cin, cout);
+  if (J.n_blocks > 0 && !hosted) {
+    rc = cfsd_spiral_conv_bwd_side(x, idx, dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, dw, db, workspace,
+                                   workspace_bytes, batch, vsrc, rows, seq, cin, cout, nullptr, stream);
+    return rc ? rc : cfsd_side_work_run(side, stream);
+  }
+  rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
   if (!inv_ptr || !inv_row || !inv_head || !w || !workspace)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd: null inverse table / w / workspace");
@@ -2611,11 +2639,11 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
                 (int)((dw_tasks + 3) / 4), batch, 0, 0};
     const int ctw = dx_lat_ctw(cin, cout, M);
     a.nb = (int)(((M + 15) / 16 * (cin / 16 / ctw) + 3) / 4);
-    const dim3 grid((unsigned)(a.nb + d.nb));
+    const dim3 grid((unsigned)(a.nb + d.nb + side_grid(J)));
     const int n_el = cout * kSeq * cin + cout;
 #define PAIR(CIN_, COUT_, CTW_)                                                                 \
   if (cin == CIN_ && cout == COUT_ && ctw == CTW_) {                                            \
-    hipLaunchKernelGGL((conv_bwd_lat_pair<CIN_, COUT_, CTW_>), grid, dim3(256), 0, st, a, d);    \
+    hipLaunchKernelGGL((conv_bwd_lat_pair<CIN_, COUT_, CTW_>), grid, dim3(256), 0, st, a, d, J); \
     rc = launch_status("spiral_conv_bwd_lat_pair");                                             \
     if (rc || !dw) return rc;                                                                   \
     hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), dim3((unsigned)((n_el + 63) / 64)),        \
@@ -3199,6 +3227,98 @@ extern "C" int cfsd_spiral_conv_bwd_out_flat(const void* x, int x_dt, const int3
   return launch_status("spiral_conv_bwd_out_flat_reduce");
 }
 
+// Slab geometry of one deferred weight-gradient item (kind, slab count,
+// slab length, db partials): what the producing launch chose.
+template <typename Item>
+static int fill_red_item(const cfsd_dw_slabs& q, int i, Item& d) {
+  if (!q.workspace || !q.dw || !q.db) return set_error(CFSD_EINVAL, "dw_reduce_batch: item %d null", i);
+  if (q.batch <= 0 || q.rows <= 0 || q.vsrc <= 0 || q.cin <= 0 || q.cout <= 0)
+    return set_error(CFSD_EINVAL, "dw_reduce_batch: item %d bad sizes", i);
+  d.ws = q.workspace;
+  d.ws_db = nullptr;
+  d.dw = q.dw;
+  d.db = q.db;
+  d.cin = q.cin;
+  d.cout = q.cout;
+  const int K = kSeq * q.cin;
+  if (q.fused == 2 && mfma_shape(q.cin, q.cout)) {  // bf16 MFMA dW: plain slabs
+    d.kind = 1;
+    d.n_slabs = bf::dw_slabs(q.batch, q.rows, q.cin, q.cout);
+    d.n_el = q.cout * K + q.cout;
+  } else if (q.fused && fused_small(q.cin, q.cout)) {
+    d.kind = 1;
+    d.n_slabs = fused_small_gx((long)q.batch * q.vsrc);
+    d.n_el = q.cout * K + q.cout;
+  } else {
+    const DwGeom g = dw_geom(q.batch, q.rows, q.cin, q.cout);
+    if (g.kind == kDwNone) return set_error(CFSD_EINVAL, "dw_reduce_batch: item %d unsupported channels", i);
+    if (g.kind == kDwMfma || g.kind == kDwLat) {
+      const int U = (int)dw_units(q.cin, q.cout);
+      d.kind = 0;
+      const bool vm = q.fused == 3 && dw_vm32_path(1, 1, q.cin, q.cout, q.batch);  // as dw_f32 chose
+      d.n_slabs = g.kind == kDwLat ? g.gx
+                  : vm             ? vm32::dw_slabs(q.batch, q.rows, g.gx)
+                                   : dw_mfma_slabs(q.cin, q.cout, g.gx);
+      d.n_el = U * 1024 + q.cout;
+      d.ws_db = q.workspace + (size_t)g.gx * U * 1024;
+    } else {
+      d.kind = 1;
+      d.n_slabs = g.gx;
+      d.n_el = q.cout * K + q.cout;
+    }
+  }
+  return CFSD_OK;
+}
+
+int cfsd::make_side_job(const cfsd_side_work* w, SideJob& J) {
+  J = SideJob{};
+  if (!w || (w->n_items <= 0 && w->n_ranges <= 0)) return CFSD_OK;
+  if (w->n_items > kSideItems || w->n_ranges > kSideRanges || w->n_items < 0 || w->n_ranges < 0)
+    return set_error(CFSD_EINVAL, "side work: %d items / %d ranges (max %d / %d)", w->n_items, w->n_ranges,
+                     kSideItems, kSideRanges);
+  if ((w->n_items && !w->items) || (w->n_ranges && !w->ranges)) return set_error(CFSD_EINVAL, "side work: null list");
+  if (w->n_ranges && !w->adam) return set_error(CFSD_EINVAL, "side work: ranges need adam = 1");
+  if (w->adam && (!w->param || !w->grad || !w->exp_avg || !w->exp_avg_sq || !w->step))
+    return set_error(CFSD_EINVAL, "side work: adam needs param / grad / exp_avg / exp_avg_sq / step");
+  int blk = 0;
+  J.n_items = w->n_items;
+  for (int i = 0; i < w->n_items; ++i) {
+    const int rc = fill_red_item(w->items[i], i, J.it[i]);
+    if (rc) return rc;
+    if (w->adam && (J.it[i].dw < w->grad || J.it[i].db < w->grad))
+      return set_error(CFSD_EINVAL, "side work: item %d outside the flat gradient", i);
+    J.it[i].blk0 = blk;
+    blk += (J.it[i].n_el + 63) / 64;
+  }
+  J.blk_items = blk;
+  J.n_ranges = w->n_ranges;
+  int rb = 0;
+  for (int r = 0; r < w->n_ranges; ++r) {
+    J.lo[r] = (long)w->ranges[2 * r];
+    J.hi[r] = (long)w->ranges[2 * r + 1];
+    if (J.hi[r] < J.lo[r]) return set_error(CFSD_EINVAL, "side work: range %d inverted", r);
+    J.rblk0[r] = rb;
+    rb += (int)((J.hi[r] - J.lo[r] + kSideRangeBlock - 1) / kSideRangeBlock);
+  }
+  J.rblk0[w->n_ranges] = rb;
+  J.n_blocks = blk + rb;
+  J.adam = w->adam;
+  J.p = w->param;
+  J.g = w->grad;
+  J.m = w->exp_avg;
+  J.v = w->exp_avg_sq;
+  J.shadow = reinterpret_cast<bf16_t*>(w->param_bf16);
+  J.step = w->step;
+  J.lr = w->lr;
+  J.b1 = w->beta1;
+  J.b2 = w->beta2;
+  J.eps = w->eps;
+  J.wd = w->weight_decay;
+  return CFSD_OK;
+}
+
+__global__ __launch_bounds__(256) void side_work_k(const SideJob J) { side_block<4>(J, blockIdx.x); }
+
 static int dw_reduce_batch_launch(const cfsd_dw_slabs* items, int n, const DwAdam* adam, long n_params,
                                   void* stream) {
   if (n <= 0 && !adam) return CFSD_OK;
@@ -3208,45 +3328,9 @@ static int dw_reduce_batch_launch(const cfsd_dw_slabs* items, int n, const DwAda
   B.n = n;
   int blk = 0;
   for (int i = 0; i < n; ++i) {
-    const cfsd_dw_slabs& q = items[i];
-    if (!q.workspace || !q.dw || !q.db) return set_error(CFSD_EINVAL, "dw_reduce_batch: item %d null", i);
-    if (q.batch <= 0 || q.rows <= 0 || q.vsrc <= 0 || q.cin <= 0 || q.cout <= 0)
-      return set_error(CFSD_EINVAL, "dw_reduce_batch: item %d bad sizes", i);
     DwRedItem& d = B.it[i];
-    d.ws = q.workspace;
-    d.ws_db = nullptr;
-    d.dw = q.dw;
-    d.db = q.db;
-    d.cin = q.cin;
-    d.cout = q.cout;
-    const int K = kSeq * q.cin;
-    if (q.fused == 2 && mfma_shape(q.cin, q.cout)) {  // bf16 MFMA dW: plain slabs
-      d.kind = 1;
-      d.n_slabs = bf::dw_slabs(q.batch, q.rows, q.cin, q.cout);
-      d.n_el = q.cout * K + q.cout;
-    } else if (q.fused && fused_small(q.cin, q.cout)) {
-      d.kind = 1;
-      d.n_slabs = fused_small_gx((long)q.batch * q.vsrc);
-      d.n_el = q.cout * K + q.cout;
-    } else {
-      const DwGeom g = dw_geom(q.batch, q.rows, q.cin, q.cout);
-      if (g.kind == kDwNone)
-        return set_error(CFSD_EINVAL, "dw_reduce_batch: item %d unsupported channels", i);
-      if (g.kind == kDwMfma || g.kind == kDwLat) {
-        const int U = (int)dw_units(q.cin, q.cout);
-        d.kind = 0;
-        const bool vm = q.fused == 3 && dw_vm32_path(1, 1, q.cin, q.cout, q.batch);  // as dw_f32 chose
-        d.n_slabs = g.kind == kDwLat ? g.gx
-                    : vm             ? vm32::dw_slabs(q.batch, q.rows, g.gx)
-                                     : dw_mfma_slabs(q.cin, q.cout, g.gx);
-        d.n_el = U * 1024 + q.cout;
-        d.ws_db = q.workspace + (size_t)g.gx * U * 1024;
-      } else {
-        d.kind = 1;
-        d.n_slabs = g.gx;
-        d.n_el = q.cout * K + q.cout;
-      }
-    }
+    const int rc = fill_red_item(items[i], i, d);
+    if (rc) return rc;
     d.blk0 = blk;
     blk += d.kind == 0 ? (d.n_el + 255) / 256 : (d.n_el + 63) / 64;
   }
@@ -3297,6 +3381,14 @@ static int dw_reduce_batch_launch(const cfsd_dw_slabs* items, int n, const DwAda
   if (blk == 0) return CFSD_OK;
   hipLaunchKernelGGL(dw_reduce_batch_k, dim3(blk), dim3(1024), 0, (hipStream_t)stream, B);
   return launch_status("dw_reduce_batch");
+}
+
+extern "C" int cfsd_side_work_run(const cfsd_side_work* side, void* stream) {
+  SideJob J;
+  const int rc = make_side_job(side, J);
+  if (rc || J.n_blocks == 0) return rc;
+  hipLaunchKernelGGL(side_work_k, dim3(J.n_blocks), dim3(256), 0, (hipStream_t)stream, J);
+  return launch_status("side_work");
 }
 
 extern "C" int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* stream) {

@@ -464,6 +464,9 @@ static int launch_shape(const FwdKsArgs& a, hipStream_t st) {
   const long n_rt = (a.total_rows + 15) / 16;
   if (UP || n_rt >= kMaxTilesFew) {  // persistent: 1 (64-channel layers) or 2 workgroups per CU
     const long per_cu = (UP || CIN * COUT >= 64 * 32) ? 1 : 2;
+    // (one workgroup per tile / balanced grids at 2-3 per CU measured slower:
+    // D0 21.5 vs 18.3, D1 20.2 vs 15.9, E1 11.9 vs 11.0 us -- every workgroup
+    // pays the weight-slice prologue, profiles/round5d_kprof_pt_grid.txt)
     const long grid = n_rt < 256 * per_cu ? n_rt : 256 * per_cu;
     hipLaunchKernelGGL((conv_fwd_pt<CIN, COUT, UP>), dim3((unsigned)grid), dim3(576), 0, st, a);
     return launch_status("spiral_conv_fwd_pt");

@@ -10,6 +10,7 @@
 #include <stdio.h>
 
 #include "cfsd_common.h"
+#include "side_work.h"
 
 namespace cfsd {
 
@@ -453,8 +454,14 @@ __global__ __launch_bounds__(256) void latent_bwd_k(const float* __restrict__ mu
                                                     const float* __restrict__ dlat,
                                                     float* __restrict__ dmulv, int B, int L,
                                                     int train, int is_vae, int sigmoid,
-                                                    const float* __restrict__ zval, int n_parts) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+                                                    const float* __restrict__ zval, int n_parts,
+                                                    int n_main, const SideJob side) {
+  const int n_side = side_grid(side);
+  if ((int)blockIdx.x < n_side) {  // side work riding in this launch (side_work.h)
+    if ((int)blockIdx.x < side.n_blocks) side_block<4>(side, (int)blockIdx.x);
+    return;
+  }
+  const int e = ((int)blockIdx.x - n_side) * blockDim.x + threadIdx.x;
   if (e >= B * L) return;
   const int i = e / L, l = e % L;
   float dzd = dz_dec[e];
@@ -944,7 +951,7 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
 
 using namespace cfsd;
 
-extern "C" int cfsd_version(void) { return (4 << 16) | 5; }  // 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
+extern "C" int cfsd_version(void) { return (4 << 16) | 6; }  // 4.6: cfsd_side_work (side work riding in host launches); 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
 extern "C" const char* cfsd_last_error_string(void) { return g_err; }
 
 extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {
@@ -1142,9 +1149,9 @@ extern "C" int cfsd_latent_bwd(const float* mulv, const float* eps, const float*
                                int latent, int train, int is_vae, int sigmoid, void* stream) {
   if (!mulv || !dz_dec || !dlat || !dmulv) return set_error(CFSD_EINVAL, "latent_bwd: null pointer");
   if (is_vae && train && !eps) return set_error(CFSD_EINVAL, "latent_bwd: eps required");
-  const int n = batch * latent;
-  hipLaunchKernelGGL(latent_bwd_k, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, mulv,
-                     eps, dz_dec, dlat, dmulv, batch, latent, train, is_vae, sigmoid, z, 1);
+  const int n = batch * latent, nb = (n + 255) / 256;
+  hipLaunchKernelGGL(latent_bwd_k, dim3(nb), dim3(256), 0, (hipStream_t)stream, mulv, eps, dz_dec, dlat, dmulv,
+                     batch, latent, train, is_vae, sigmoid, z, 1, nb, SideJob{});
   return launch_status("latent_bwd");
 }
 
@@ -1152,12 +1159,22 @@ extern "C" int cfsd_latent_bwd_parts(const float* mulv, const float* eps, const 
                                      const float* dz_parts, int n_parts, const float* dlat,
                                      float* dmulv, int batch, int latent, int train, int is_vae,
                                      int sigmoid, void* stream) {
+  return cfsd_latent_bwd_parts_side(mulv, eps, z, dz_parts, n_parts, dlat, dmulv, batch, latent, train, is_vae,
+                                    sigmoid, nullptr, stream);
+}
+extern "C" int cfsd_latent_bwd_parts_side(const float* mulv, const float* eps, const float* z,
+                                          const float* dz_parts, int n_parts, const float* dlat, float* dmulv,
+                                          int batch, int latent, int train, int is_vae, int sigmoid,
+                                          const cfsd_side_work* side, void* stream) {
   if (!mulv || !dz_parts || !dlat || !dmulv) return set_error(CFSD_EINVAL, "latent_bwd_parts: null pointer");
   if (n_parts <= 0) return set_error(CFSD_EINVAL, "latent_bwd_parts: n_parts %d", n_parts);
   if (is_vae && train && !eps) return set_error(CFSD_EINVAL, "latent_bwd_parts: eps required");
-  const int n = batch * latent;
-  hipLaunchKernelGGL(latent_bwd_k, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, mulv,
-                     eps, dz_parts, dlat, dmulv, batch, latent, train, is_vae, sigmoid, z, n_parts);
+  SideJob J;
+  const int rc = make_side_job(side, J);
+  if (rc) return rc;
+  const int n = batch * latent, nb = (n + 255) / 256;
+  hipLaunchKernelGGL(latent_bwd_k, dim3(nb + side_grid(J)), dim3(256), 0, (hipStream_t)stream, mulv, eps, dz_parts,
+                     dlat, dmulv, batch, latent, train, is_vae, sigmoid, z, n_parts, nb, J);
   return launch_status("latent_bwd_parts");
 }
 

@@ -182,6 +182,11 @@ class SDVAEEngine:
         self.vertex_major = bool(vertex_major)
         self.fuse_up = True  # coarse Deblocks: Pool(up) fused into the conv gather (False: separate SpMM)
         self.fuse_latent = True  # latent head + decoder Linear in one launch (False: two)
+        # the weight-gradient slab reductions + Adam at the end of a single-process
+        # step: "hosts" = those of finished layers ride in later latency-bound
+        # launches (ops.SideWork), the rest in one side-work launch; "final" = all
+        # in one side-work launch; "off" = cfsd_dw_reduce_batch(_adam)
+        self.side_work = "off"
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -520,11 +525,11 @@ class SDVAEEngine:
             ops.spiral_conv_fwd_x(x, idx, w, w16, bias, act, out)
 
     @classmethod
-    def _spmm(cls, csr, x, m, out, elu_y=None, sched=None, uniform=0):
+    def _spmm(cls, csr, x, m, out, elu_y=None, sched=None, uniform=0, side=None):
         if cls._plain(x, out):
-            ops.spmm(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform)
+            ops.spmm(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform, side=side)
         else:
-            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform)
+            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform, side=side)
 
     def _lin_names(self):
         n = self.spec.n
@@ -656,19 +661,44 @@ class SDVAEEngine:
         bottleneck: ~96 % of the parameters), after the encoder-Linear
         backward; then the encoder convs at the end.  ``fuse_adam`` (no hook):
         the Adam step runs in the final weight-gradient reduce launch."""
-        self.backward_head(b, split=bucket_hook is not None)
+        fuse = fuse_adam and bucket_hook is None
+        self.backward_head(b, split=bucket_hook is not None, fuse_adam=fuse)
         if bucket_hook is not None:
             bucket_hook(self.params.grad[self.enc_conv_numel():])
-        self.backward_tail(b, fuse_adam=fuse_adam and bucket_hook is None)
+        self.backward_tail(b, fuse_adam=fuse)
         if bucket_hook is not None:
             bucket_hook(self.params.grad[:self.enc_conv_numel()])
 
-    def backward_head(self, b, split=False):
+    def _grad_range(self, t):
+        """Flat [lo, hi) of a view of the gradient buffer."""
+        lo = (t.data_ptr() - self.params.grad.data_ptr()) // 4
+        return (lo, lo + t.numel())
+
+    def backward_head(self, b, split=False, fuse_adam=False):
         """Losses -> decoder -> latent head -> encoder Linear.  ``split``:
         reduce the decoder conv weight gradients here (their bucket is then
-        final) instead of in backward_tail's single batched reduce."""
+        final) instead of in backward_tail's single batched reduce.
+        ``fuse_adam`` (single process, nothing between gradient and update):
+        with ``side_work`` each finished layer's Adam step rides in a later
+        launch of the backward (``b.adam_done`` lists the flat ranges already
+        updated; backward_tail updates the rest)."""
         T, S, P = self.topo, self.spec, self.params
         n = S.n
+        adam = self.adam_args() if fuse_adam else None
+        b.adam_done = []
+        side_items = []  # deferred slab sets not yet taken by a host launch
+
+        def take_side():
+            """Every deferred slab set so far (their layers' backward is done) as
+            side work of the next host launch, with their Adam step when fused."""
+            if self.side_work != "hosts" or not side_items:
+                return None
+            sw = ops.SideWork(side_items, adam=adam)
+            if adam is not None:
+                for _, dw, db in side_items:
+                    b.adam_done += [self._grad_range(dw), self._grad_range(db)]
+            side_items.clear()
+            return sw
         pending, acc = getattr(b, "pending_finalize", (False, None))
         if pending:
             ops.recon_lap_bwd_finalize(b.out, b.x, b.unit, T.lapT_csr, b.dout, 1.0, self.w_lap,
@@ -686,10 +716,8 @@ class SDVAEEngine:
         # measured slower on MI355X, 16.3k vs 17.5k meshes/s: the persistent
         # level-0 kernels slow ~2x when sharing the chip and every fork/join
         # costs 6-17 us inside the graph -> one stream)
-        deferred = []
-
         def defer(d, name):
-            deferred.append((d, P.gview(name + ".weight"), P.gview(name + ".bias")))
+            side_items.append((d, P.gview(name + ".weight"), P.gview(name + ".bias")))
 
         weight_grad = ops.spiral_conv_bwd_weight
 
@@ -717,8 +745,12 @@ class SDVAEEngine:
                     ops.spiral_conv_bwd_data_x(b.dpre_dec[i], T.spiral_inv[lv], w16, T.n_verts[lv],
                                                out=b.g_dec_up[i])
             elif b.paired[("dec", i)]:  # dx + dW slabs in one launch
+                # the paired launch of a ~1k-vertex layer (latency-bound, lat pair) hosts
+                # the slab reductions (+ Adam) of the layers finished before it
+                host = b.bsz * T.n_verts[lv] >= 8192
                 _, d = ops.spiral_conv_bwd(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_inv[lv],
-                                           w, None, None, dx=b.g_dec_up[i], workspace=b.ws_dw[("dec", i)])
+                                           w, None, None, dx=b.g_dec_up[i], workspace=b.ws_dw[("dec", i)],
+                                           side=take_side() if host else None)
                 defer(d, f"de_layers.{i + 1}.conv.layer")
             else:
                 defer(weight_grad(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
@@ -729,11 +761,15 @@ class SDVAEEngine:
             # k-th eighth of the rows (neighbouring rows share source blocks in its L2):
             # 17-19 vs 21.6 us at level 0; batch-major keeps the longest-rows-first order
             sch = T.upT_nat[ui] if lv in b.xl else T.upT_sched[ui]
+            # the coarse transposes (latency-bound) host the slab reduction (+ Adam)
+            # of every layer finished so far; the level-0/1 ones stream ~40 / 10 MB
+            # and are not hosts
+            sw = take_side() if (sch is not None and lv >= 2) else None
             if i > 0:  # through Pool(up) into the previous Deblock's ELU
                 self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dpre_dec[i - 1],
-                           elu_y=b.dec_out[i - 1], sched=sch)
+                           elu_y=b.dec_out[i - 1], sched=sch, side=sw)
             else:
-                self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh, sched=sch)
+                self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh, sched=sch, side=sw)
         # decoder Linear: dW/db and dz (as 64-row-slice partial products,
         # summed by the latent head's backward) in one launch
         if b.dz_parts is not None:
@@ -745,11 +781,26 @@ class SDVAEEngine:
                            dw=P.gview("de_layers.0.weight"), db=P.gview("de_layers.0.bias"),
                            workspace=b.lin_ws)
             dz = b.dz
-        ops.latent_bwd(b.mulv, b.eps, b.z, dz, b.dlat, b.dmulv, S.latent, True, S.is_vae, S.sigmoid)
+        # the latent head hosts the decoder Linear's Adam step (its gradient is
+        # final and its weight no longer read) and any slab set still pending
+        sw = None
+        if self.side_work == "hosts" and b.dz_parts is not None:
+            rng = []
+            if adam is not None:
+                lo, _ = self._grad_range(P.gview("de_layers.0.weight"))
+                _, hi = self._grad_range(P.gview("de_layers.0.bias"))
+                rng = [(lo, hi)]
+                b.adam_done.append((lo, hi))
+            if side_items:
+                sw = take_side()
+                sw.ranges += rng
+            elif rng:
+                sw = ops.SideWork(ranges=rng, adam=adam)
+        ops.latent_bwd(b.mulv, b.eps, b.z, dz, b.dlat, b.dmulv, S.latent, True, S.is_vae, S.sigmoid, side=sw)
         if split:
-            ops.dw_reduce_batch(deferred)
-            deferred = []
-        b.deferred = deferred
+            ops.dw_reduce_batch(side_items)
+            side_items.clear()
+        b.deferred = list(side_items)
         # stacked encoder Linear; ELU of the last Enblock folded into dx
         W, _ = self._enc_lin()
         gW, gB = self._enc_lin(P.grad)
@@ -852,6 +903,21 @@ class SDVAEEngine:
                                          out=b.g_pooled[prev], workspace=b.ws)
                 ops.spmm(T.downT_csr[prev], b.g_pooled[prev], T.n_verts[prev], elu_y=b.enc_full[prev],
                          out=b.dpre_enc[prev])
+        done = getattr(b, "adam_done", [])
+        if fuse_adam and (done or self.side_work != "off"):
+            # Adam of everything the side work has not updated yet: the
+            # remaining slab sets' layers and the flat ranges between
+            covered = sorted(done + [self._grad_range(t) for _, dw, db in deferred for t in (dw, db)])
+            rest, cur = [], 0
+            for lo, hi in covered:
+                if lo > cur:
+                    rest.append((cur, lo))
+                cur = max(cur, hi)
+            if cur < P.numel:
+                rest.append((cur, P.numel))
+            ops.side_work_run(ops.SideWork(deferred, ranges=rest, adam=self.adam_args()))
+            b.adam_done = []
+            return
         ops.dw_reduce_batch(deferred, adam=self.adam_args() if fuse_adam else None)
 
     def adam_step(self):

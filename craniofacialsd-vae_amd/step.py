@@ -74,7 +74,7 @@ class TrainStep:
                        adam_step=eng.params.step)
         eng.load_batch(b, d)
         eng.forward(b, train=True, acc=self.acc, finalize=False)
-        eng.backward_head(b, split=self.avg is not None)
+        eng.backward_head(b, split=self.avg is not None, fuse_adam=self.avg is None)
 
     def part_b(self):
         self.eng.backward_tail(self.b, fuse_adam=self.avg is None)

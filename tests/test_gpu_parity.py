@@ -333,8 +333,9 @@ def test_swap_bit_exact(otopo, dtopo):
 
 
 # --------------------------------------------------------------- full model
-def make_engine(dtopo, weights, bs=4, precision="fp32"):
-    eng = E.SDVAEEngine(dtopo, E.ModelSpec(), swap_bs=bs, device=DEV, precision=precision)
+def make_engine(dtopo, weights, bs=4, precision="fp32", vertex_major=True):
+    eng = E.SDVAEEngine(dtopo, E.ModelSpec(), swap_bs=bs, device=DEV, precision=precision,
+                        vertex_major=vertex_major)
     eng.load_state_dict({k: torch.from_numpy(v) for k, v in weights.items()})
     return eng
 
@@ -462,22 +463,26 @@ def test_train_step_deterministic(dtopo):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_fused_reduce_adam_matches_separate(dtopo, precision):
-    """cfsd_dw_reduce_batch_adam (train_step_on without a gradient hook) ==
-    cfsd_dw_reduce_batch + cfsd_adam, bit for bit: parameters, gradients,
-    both Adam moments and (bf16) the weight shadow after two steps -- in bf16
-    also the bf16-MFMA weight-gradient items of the fused reduce."""
+@pytest.mark.parametrize("precision,vertex_major", [("fp32", True), ("fp32", False), ("bf16", True)])
+def test_fused_reduce_adam_matches_separate(dtopo, precision, vertex_major):
+    """The single-process step's fused updates == cfsd_dw_reduce_batch +
+    cfsd_adam, bit for bit: parameters, gradients, both Adam moments and
+    (bf16) the weight shadow after two steps.  Fused two ways: the side work
+    (ABI 4.6: slab reductions + Adam of finished layers riding in the
+    up-sampling transposes and the latent backward, the rest in one side-work
+    launch) and, with side_work off, cfsd_dw_reduce_batch_adam; in bf16 also
+    the bf16-MFMA weight-gradient items."""
     w = recipe.golden_weights()
     x = torch.from_numpy(O.swap_features(recipe.normalized_meshes(4), [np.asarray(r) for r in
                                          O.Topology(recipe.load_topology()).region_features], 2)).to(DEV)
     eps = torch.from_numpy(recipe.train_eps(0)).to(DEV)
     outs = []
-    for fused in (True, False):
-        eng = make_engine(dtopo, w, precision=precision)
+    for mode in ("hosts", "final", "off", "separate"):
+        eng = make_engine(dtopo, w, precision=precision, vertex_major=vertex_major)
+        eng.side_work = "off" if mode == "separate" else mode
         for _ in range(2):
             b = eng.set_batch(x, key_index=2, eps=eps)
-            if fused:
+            if mode != "separate":
                 eng.train_step_on(b)
             else:
                 eng.advance_step(b)
@@ -489,8 +494,9 @@ def test_fused_reduce_adam_matches_separate(dtopo, precision):
         bufs = [P.data, P.grad, P.exp_avg, P.exp_avg_sq] + ([P.shadow] if P.shadow is not None else [])
         outs.append([t.cpu().clone() for t in bufs])
     assert len(outs[0]) == (5 if precision == "bf16" else 4)
-    for a, c in zip(*outs):
-        assert torch.equal(a, c)
+    for other in outs[1:]:
+        for a, c in zip(outs[0], other):
+            assert torch.equal(a, c)
 
 
 # --------------------------------------------------------------- dense Linears

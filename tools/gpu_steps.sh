@@ -24,7 +24,7 @@ for s in ${*:-tests bench prof32}; do
       rm -rf $O/prof_$P
       cat $O/timeline_$P.txt ;;
     pmc32)
-      CASES="fwd_d3_vm:conv_fwd_vm32<32, 32, 1, 2, 1>:conv_fwd_d3_vm dxf_d3_vm:conv_dx_flat_vm32<32, 32, 16:conv_dx_d3_vm dw_d3_vm:conv_dw_vm32:conv_dw_d3_vm" OUT=$O/traffic32 TAG=$TAG bash tools/pmc_traffic.sh > /dev/null
+      CASES="fwd_d3_vm:conv_fwd_vm32<32, 32, 1, 2, 1>:conv_fwd_d3_vm dxf_d3_vm:conv_dx_flat_vm32<32, 32, 16, float>:conv_dx_d3_vm dw_d3_vm:conv_dw_vm32:conv_dw_d3_vm" OUT=$O/traffic32 TAG=$TAG bash tools/pmc_traffic.sh > /dev/null
       cat $O/traffic32/*.json ;;
     pmc16)
       CASES="fwd_d3_b16:conv_fwd_vm16<32, 32, 1, unsigned short>:conv_fwd_d3_bf16_vm dxf_d3_b16:conv_dx_flat_vm16<32, 32, unsigned short, 16>:conv_dx_d3_bf16_vm dw_d3_b16:conv_dw_vm16<unsigned short>:conv_dw_d3_bf16_vm" OUT=$O/traffic16 TAG=$TAG bash tools/pmc_traffic.sh > /dev/null
@@ -32,6 +32,20 @@ for s in ${*:-tests bench prof32}; do
     kbench)
       timeout -k 10 300 python tools/kbench.py ${KB_CASES} > $O/kbench.txt 2>&1 || { tail -30 $O/kbench.txt; exit 1; }
       cat $O/kbench.txt ;;
+    kprof)  # kbench cases under a kernel trace: per-kernel device time (KPROF_ENVS: "A=1 B=2;C=3" variants)
+      IFS=';' read -ra VARS <<< "${KPROF_ENVS:-NONE=0}"
+      i=0
+      for v in "${VARS[@]}"; do
+        i=$((i+1))
+        env $v timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kprof$i -o kb -- python3 tools/kbench.py ${KB_CASES} > $O/kprof$i.log 2>&1 || { tail -20 $O/kprof$i.log; exit 1; }
+        echo "-- variant $v" >> $O/kprof.txt
+        python tools/prof_summary.py $(find $O/kprof$i -name '*.db' | head -1) 40 >> $O/kprof.txt
+        rm -rf $O/kprof$i
+      done
+      grep -v "at::native\|rocclr\|distribution_elementwise" $O/kprof.txt ;;
+    sq)
+      KB="${SQ_CASES}" OUT=$O/sq bash tools/pmc_sq.sh > /dev/null
+      cat $O/sq/summary.txt ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -30 $O/smoke.log; exit 1; }
       tail -2 $O/smoke.log ;;

@@ -297,6 +297,46 @@ def build_cases(names=()):
                                               uniform=T.up_uniform[0])
     cases["spmm_up0T_vm"] = lambda: ops.spmm_x(T.upT_csr[0], v.g_dec_up[3], T.n_verts[1], elu_y=v.dec_out[2],
                                                out=v.dpre_dec[2], sched=T.upT_nat[0])
+    # the coarse chain exactly as the fp32 vertex-major step launches it
+    for t in (v.h, v.dec_up[0], v.dec_up[1], v.dpre_dec[0], v.dpre_dec[1], v.g_dec_up[1], v.g_dec_up[0],
+              v.enc_out[1], v.enc_out[2], v.enc_out[3], v.dpre_enc[2], v.dpre_enc[3], v.dh, v.z, v.mulv):
+        t.copy_(torch.randn(t.shape, device="cuda", generator=g))
+    w0v, b0v = ev._dec_w(0)
+    w1v, b1v = ev._dec_w(1)
+    Pv = ev.params
+    cases["fwd_d0_up"] = lambda: ops.spiral_conv_fwd_up(v.h, T.up_comp[3], T.spiral[3], w0v, b0v, 1,
+                                                        out=v.dec_out[0], up_out=v.dec_up[0])
+    cases["fwd_d1_vm"] = lambda: ops.spiral_conv_fwd(v.dec_up[1], T.spiral[2], w1v, b1v, 1, out=v.dec_out[1],
+                                                     workspace=v.ws)
+    cases["pair_d1_vm"] = lambda: ops.spiral_conv_bwd(v.dec_up[1], T.spiral[2], v.dpre_dec[1], T.spiral_inv[2], w1v,
+                                                      None, None, dx=v.g_dec_up[1], workspace=v.ws_dw[("dec", 1)])
+    cases["pair_d0_vm"] = lambda: ops.spiral_conv_bwd(v.dec_up[0], T.spiral[3], v.dpre_dec[0], T.spiral_inv[3], w0v,
+                                                      None, None, dx=v.g_dec_up[0], workspace=v.ws_dw[("dec", 0)])
+    for lv in (2, 3):
+        cases[f"fwd_e{lv}_vm"] = (lambda lv=lv: ops.spiral_conv_fwd(v.enc_out[lv - 1], T.enc_rows[lv], *ev._enc_w(lv), 1,
+                                                                    out=v.enc_out[lv], workspace=v.ws))
+    cases["rowsub_e2_vm"] = lambda: ops.spiral_conv_bwd_rowsub(v.enc_out[1], T.enc_rows[2], v.dpre_enc[2], T.enc_flat[2],
+                                                               ev._enc_w(2)[0], None, None, dx=v.dpre_enc[1],
+                                                               elu_y=v.enc_out[1], workspace=v.ws_dw[("enc", 2)])
+    cases["rowsub_e3_vm"] = lambda: ops.spiral_conv_bwd_rowsub(v.enc_out[2], T.enc_rows[3], v.dpre_enc[3], T.enc_flat[3],
+                                                               ev._enc_w(3)[0], None, None, dx=v.dpre_enc[2],
+                                                               elu_y=v.enc_out[2], workspace=v.ws_dw[("enc", 3)])
+    for lv, (gin, outb, ey) in enumerate([(v.g_dec_up[2], v.dpre_dec[1], v.dec_out[1]),
+                                          (v.g_dec_up[1], v.dpre_dec[0], v.dec_out[0]),
+                                          (v.g_dec_up[0], v.dh, None)], start=1):
+        cases[f"spmm_up{lv}T_vm"] = (lambda lv=lv, gin=gin, outb=outb, ey=ey: ops.spmm_x(
+            T.upT_csr[lv], gin, T.n_verts[lv + 1], elu_y=ey, out=outb,
+            sched=T.upT_nat[lv] if lv == 1 else T.upT_sched[lv]))  # level 1 is vertex-major (engine.backward_head)
+    Wdv, Bdv = Pv.view("de_layers.0.weight"), Pv.view("de_layers.0.bias")
+    W_encv, _ = ev._enc_lin()
+    gW_encv, gB_encv = ev._enc_lin(Pv.grad)
+    flatv = v.enc_out[3].view(16, -1)
+    cases["lin_dec_split"] = lambda: ops.linear_bwd_split(v.z, Wdv, v.dh.view(16, -1), v.dz_parts,
+                                                          Pv.gview("de_layers.0.weight"), Pv.gview("de_layers.0.bias"))
+    cases["latent_bwd"] = lambda: ops.latent_bwd(v.mulv, v.eps, v.z, v.dz_parts, v.dlat, v.dmulv, 75, True, True, False)
+    cases["lin_enc_pair"] = lambda: ops.linear_bwd(flatv, W_encv, v.dmulv, dx=v.dpre_enc[3].view(16, -1),
+                                                   dw=gW_encv.view(W_encv.shape), db=gB_encv, elu_y=flatv)
+    cases["lin_enc_fwd_vm"] = lambda: ops.linear_fwd(flatv, W_encv, ev._enc_lin()[1], out=v.mulv, workspace=v.lin_ws)
     if "red_items" in names:  # the step's batched slab reduce, item by item (HIP events)
         cap = []
         orig = ops.dw_reduce_batch

@@ -237,6 +237,22 @@ inline int resident_blocks_of(K kernel, int block_threads, size_t dyn_lds) {
   return resident_blocks(reinterpret_cast<const void*>(kernel), block_threads, dyn_lds);
 }
 
+// CUs of the current device (cached).
+int device_cus();
+// Integer tuning knob from the environment (read once per name; unset or
+// unparsable: dflt).  Used for same-box A/B sweeps of launch geometry.
+int env_knob(const char* name, int dflt);
+// Persistent grid with the SAME number of workgroups (bpc) on every CU,
+// capped at one workgroup per `per_block` units: a grid that is not a multiple
+// of the CU count leaves some CUs a third more waves than others, and those
+// set the kernel's time.
+inline unsigned cu_blocks(long units, int per_block, int bpc) {
+  long need = (units + per_block - 1) / per_block;
+  if (need < 1) need = 1;
+  const long full = (long)bpc * device_cus();
+  return (unsigned)(need < full ? need : full);
+}
+
 // Balanced persistent grid: `units` work items, `per_block` processed per
 // block-iteration, at most `max_blocks` blocks.
 inline unsigned balanced_blocks(long units, int per_block, long max_blocks) {

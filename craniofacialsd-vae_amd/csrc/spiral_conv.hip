@@ -2530,7 +2530,9 @@ namespace {
 bool fused_small(int cin, int cout) { return cout * kSeq <= 32 && (cin == 32 || cin == 64); }
 int fused_small_gx(long m_src) {  // ~2 32-row tiles per wave
   long gx = ((m_src + 31) / 32 + 7) / 8;
-  return (int)(gx > 1024 ? 1024 : (gx < 1 ? 1 : gx));
+  static const int bpc = env_knob("CFSD_BWDOUT_BPC", 0);  // A/B: workgroups per CU
+  const long cap = bpc > 0 ? (long)bpc * device_cus() : 1024;
+  return (int)(gx > cap ? cap : (gx < 1 ? 1 : gx));
 }
 }  // namespace
 

@@ -562,7 +562,9 @@ static int fwd16_t(const bf16_t* x, const int* idx, const bf16_t* w, const float
   constexpr size_t lds = (size_t)COUT * (kS * CIN + 8) * sizeof(bf16_t);
   auto kern = conv_fwd_vm16<CIN, COUT, ACT, TY>;
   const long tiles = (long)rows * (batch / 16);
-  const unsigned grid = balanced_blocks(tiles, 8, resident(kern, lds));  // >= 2 tiles per wave
+  static const int bpc = env_knob("CFSD_FWD16_BPC", 0);
+  const unsigned grid = bpc > 0 ? cu_blocks(tiles, 4, bpc)
+                                : balanced_blocks(tiles, 8, resident(kern, lds));  // >= 2 tiles per wave
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
   return launch_status("spiral_conv_fwd_vm16");
 }
@@ -635,6 +637,9 @@ int launch_dx_vm16(const void* dpre, int dpre_dt, const int* inv_ptr, const int*
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_data_vm16: unsupported channels %d -> %d", cin, cout);
 }
 
+// bf16 flat-list data gradient: 3 workgroups on every CU (19.6 vs 21.1 us
+// with the balanced-iteration grid, profiles/round5r_kprof_grid_bf16_out.txt)
+constexpr int kVm16DxBpc = 3;
 template <int CIN, int COUT, typename TD, int FW>
 static int dxf16_t(const TD* dpre, const int* flat, const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, int vsrc,
                    int rows, int batch, hipStream_t st) {
@@ -642,7 +647,8 @@ static int dxf16_t(const TD* dpre, const int* flat, const bf16_t* w, const bf16_
   auto kern = conv_dx_flat_vm16<CIN, COUT, TD, FW>;
   const long tiles = (long)vsrc * (batch / 16);
   const int r = resident_blocks_of(kern, 512, lds);
-  const unsigned grid = balanced_blocks(tiles, 8, r > 0 ? r : 1);
+  static const int bpc = env_knob("CFSD_DX16_BPC", kVm16DxBpc);
+  const unsigned grid = bpc > 0 ? cu_blocks(tiles, 8, bpc) : balanced_blocks(tiles, 8, r > 0 ? r : 1);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows,
                      batch);
   return launch_status("spiral_conv_bwd_data_flat");

@@ -624,6 +624,9 @@ __global__ __launch_bounds__(64 * kBoWaves, kBoWaves) void conv_bwd_out_vm(const
 // (slot by slot, 4 channels by fmaf per lane, then the xor tree 4, 2, 1 over
 // the 8 lanes of the row, then the bias), so both layouts give the same bits.
 constexpr int kVmOutU = 1;
+// output-conv forward: 6 workgroups on every CU (17.7 vs 18.9 us with the
+// balanced-iteration grid, profiles/round5r_kprof_grid_bf16_out.txt)
+constexpr int kVmOutFwdBpc = 6;
 template <int CO, int ACT, int U, typename TX>
 __global__ __launch_bounds__(256) void conv_fwd_out_vm(const TX* __restrict__ x, const int* __restrict__ idx,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
@@ -720,13 +723,23 @@ static int resident(Kern k, int threads, size_t lds) {
   return r > 0 ? r : 1;
 }
 
+// Persistent grids of the D3 / D2 forward and data gradient: the same
+// number of workgroups on every CU (cu_blocks) -- the balanced-iteration grid
+// (710 / 533 workgroups for D3 / D2) left some CUs a third more waves.
+// Same-box kbench (profiles/round5q_kprof_grid.txt): forward 4 per CU D3
+// 57.4 vs 60.7 us, D2 19.9 vs 23.5; data gradient 2 per CU D3 54.3-55.3 vs
+// 57.2, D2 20.6-20.8 vs 22.9.  (0 = the balanced-iteration grid.)
+constexpr int kVm32FwdBpc = 4;
+constexpr int kVm32DxBpc = 2;
+
 template <int CIN, int COUT, int ACT, int UPT, int PD>
 static int fwd_t(const float* x, const int* idx, const float* w, const float* bias, float* y, int yvm,
                  int vsrc, int rows, int batch, hipStream_t st) {
   constexpr size_t lds = (size_t)COUT * (kS * CIN + 8) * sizeof(float);
   auto kern = conv_fwd_vm32<CIN, COUT, ACT, UPT, PD>;
   const long tiles = ((long)rows * (batch / 16) + UPT - 1) / UPT;
-  const unsigned grid = balanced_blocks(tiles, 4, resident(kern, 256, lds));
+  static const int bpc = env_knob("CFSD_FWD32_BPC", kVm32FwdBpc);
+  const unsigned grid = bpc > 0 ? cu_blocks(tiles, 4, bpc) : balanced_blocks(tiles, 4, resident(kern, 256, lds));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
   return launch_status("spiral_conv_fwd_vm32");
 }
@@ -764,7 +777,8 @@ static int dxf_t(const float* dpre, int dpvm, int dxvm, const int* flat, const f
   constexpr size_t lds = (size_t)kS * CIN * (COUT + 8) * sizeof(float);
   auto kern = conv_dx_flat_vm32<CIN, COUT, FW, TY>;
   const long tiles = (long)vsrc * (batch / 16);
-  const unsigned grid = balanced_blocks(tiles, 8, resident(kern, 512, lds));
+  static const int bpc = env_knob("CFSD_DX32_BPC", kVm32DxBpc);
+  const unsigned grid = bpc > 0 ? cu_blocks(tiles, 8, bpc) : balanced_blocks(tiles, 8, resident(kern, 512, lds));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows,
                      batch, dpvm, dxvm);
   return launch_status("spiral_conv_bwd_data_flat_vm32");
@@ -836,7 +850,8 @@ static int fwd_out_t(const TX* x, const int* idx, const float* w, const float* b
   constexpr int U = kVmOutU;
   auto kern = conv_fwd_out_vm<CO, ACT, U, TX>;
   const long its = ((long)rows * (batch / 8) + U - 1) / U;
-  const unsigned grid = balanced_blocks(its, 4, resident(kern, 256, 0));
+  static const int bpc = env_knob("CFSD_FWDOUT_BPC", kVmOutFwdBpc);
+  const unsigned grid = bpc > 0 ? cu_blocks(its, 4, bpc) : balanced_blocks(its, 4, resident(kern, 256, 0));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
   return launch_status("spiral_conv_fwd_out_vm");
 }

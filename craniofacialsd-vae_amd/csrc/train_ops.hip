@@ -24,6 +24,27 @@ int set_error(int code, const char* fmt, ...) {
   return code;
 }
 
+int device_cus() {
+  static thread_local int dev_cached = -1, cus_cached = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != dev_cached) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    dev_cached = dev;
+    cus_cached = cus;
+  }
+  return cus_cached;
+}
+
+int env_knob(const char* name, int dflt) {
+  const char* e = getenv(name);
+  if (!e || !*e) return dflt;
+  char* end = nullptr;
+  const long v = strtol(e, &end, 10);
+  return (end && *end == 0) ? (int)v : dflt;
+}
+
 int resident_blocks(const void* kernel, int block_threads, size_t dyn_lds) {
   struct Key {
     const void* k;

@@ -260,6 +260,14 @@ def build_cases(names=()):
     v.dec_out[3].copy_(torch.nn.functional.elu(v.dec_out[3]))
     w3v, b3v = ev._dec_w(3)
     cases["fwd_d3_vm"] = lambda: ops.spiral_conv_fwd_x(v.dec_up[3], T.spiral[0], w3v, None, b3v, 1, v.dec_out[3])
+    # diagnosis of the D3 forward: gathers that hit L1 (self), neighbours in
+    # index order (shift), no ELU epilogue, and twice the meshes (fixed costs)
+    cases["fwd_d3_vm_self"] = lambda: ops.spiral_conv_fwd_x(v.dec_up[3], self_idx, w3v, None, b3v, 1, v.dec_out[3])
+    cases["fwd_d3_vm_shift"] = lambda: ops.spiral_conv_fwd_x(v.dec_up[3], shift_idx, w3v, None, b3v, 1, v.dec_out[3])
+    cases["fwd_d3_vm_noact"] = lambda: ops.spiral_conv_fwd_x(v.dec_up[3], T.spiral[0], w3v, None, b3v, 0, v.dec_out[3])
+    x32 = ops.to_vm(torch.randn(32, T.n_verts[0], 32, device="cuda", generator=g))
+    y32 = ops.vm_empty(32, T.n_verts[0], 32, dtype=torch.float32, device="cuda")
+    cases["fwd_d3_vm_x2"] = lambda: ops.spiral_conv_fwd_x(x32, T.spiral[0], w3v, None, b3v, 1, y32)
     cases["dxf_d3_vm"] = lambda: ops.spiral_conv_bwd_data_flat(v.dpre_dec[3], T.spiral_flat[0], w3v, T.n_verts[0],
                                                                out=v.g_dec_up[3])
     cases["dw_d3_vm"] = lambda: ops.spiral_conv_bwd_weight_x(v.dec_up[3], T.spiral[0], v.dpre_dec[3], None, None,

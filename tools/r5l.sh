@@ -1,0 +1,3 @@
+set -e
+CFSD_VM32_FWD_PIPE=1 TAG=round5l PYTEST_FILES="tests/test_gpu_vm32.py" PYTEST_K="fwd" bash tools/gpu_steps.sh tests
+TAG=round5l KB_CASES="fwd_d3_vm fwd_d2_vm" KPROF_ENVS="CFSD_VM32_FWD_PIPE=0;CFSD_VM32_FWD_PIPE=1;CFSD_VM32_FWD_EXP=6;CFSD_VM32_FWD_PIPE=0;CFSD_VM32_FWD_PIPE=1" bash tools/gpu_steps.sh kprof

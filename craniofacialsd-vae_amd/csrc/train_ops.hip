@@ -863,11 +863,15 @@ __global__ __launch_bounds__(256) void linear_bwd_pair_k(const float* __restrict
 // the last thread.  Same per-element arithmetic as a scalar loop.
 // With `shadow` != NULL the updated parameters are also written as bf16 (the
 // weights the bf16 kernels read: fp32 master + bf16 copy in one pass).
-__global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, const float* __restrict__ g,
+// SCALED (cfsd_adam_scaled, the data-parallel step): the gradient is first
+// multiplied by gscale (1 / world after the all-reduce SUM) and written back,
+// the same fp32 product cfsd_scale forms -- one launch instead of two.
+template <bool SCALED>
+__global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v,
                                               const int* __restrict__ step, long n, float lr,
                                               float b1, float b2, float eps, float wd,
-                                              bf16_t* __restrict__ shadow) {
+                                              bf16_t* __restrict__ shadow, float gscale) {
   const long q = (long)blockIdx.x * blockDim.x + threadIdx.x, n4 = n / 4;
   if (q > n4) return;
   const int t = *step;
@@ -878,7 +882,12 @@ __global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, const float
     const f32x4 pv = ld4(p + 4 * q), mv = ld4(m + 4 * q), vv = ld4(v + 4 * q), gv = ld4(g + 4 * q);
     float pa[4] = {pv.x, pv.y, pv.z, pv.w}, ma[4] = {mv.x, mv.y, mv.z, mv.w};
     float va[4] = {vv.x, vv.y, vv.z, vv.w};
-    const float ga[4] = {gv.x, gv.y, gv.z, gv.w};
+    float ga[4] = {gv.x, gv.y, gv.z, gv.w};
+    if constexpr (SCALED) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ga[j] *= gscale;
+      st4(g + 4 * q, f32x4{ga[0], ga[1], ga[2], ga[3]});
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) adam_elem(pa[j], ga[j], ma[j], va[j], b1, b2, eps, wd, step_size, sqrt_bc2);
     st4(p + 4 * q, f32x4{pa[0], pa[1], pa[2], pa[3]});
@@ -887,7 +896,12 @@ __global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, const float
     st4(v + 4 * q, f32x4{va[0], va[1], va[2], va[3]});
   } else {
     for (long i = 4 * n4; i < n; ++i) {
-      adam_elem(p[i], g[i], m[i], v[i], b1, b2, eps, wd, step_size, sqrt_bc2);
+      float gi = g[i];
+      if constexpr (SCALED) {
+        gi *= gscale;
+        g[i] = gi;
+      }
+      adam_elem(p[i], gi, m[i], v[i], b1, b2, eps, wd, step_size, sqrt_bc2);
       if (shadow) stf(shadow + i, p[i]);
     }
   }
@@ -972,7 +986,7 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
 
 using namespace cfsd;
 
-extern "C" int cfsd_version(void) { return (4 << 16) | 6; }  // 4.6: cfsd_side_work (side work riding in host launches); 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
+extern "C" int cfsd_version(void) { return (4 << 16) | 7; }  // 4.7: cfsd_adam_scaled; 4.6: cfsd_side_work (side work riding in host launches); 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
 extern "C" const char* cfsd_last_error_string(void) { return g_err; }
 
 extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {
@@ -1293,9 +1307,23 @@ extern "C" int cfsd_adam(float* param, const float* grad, float* m, float* v,
   if (n == 0) return CFSD_OK;
   if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v | (uintptr_t)param_bf16 * 2) & 15)
     return set_error(CFSD_EINVAL, "adam: param/grad/m/v must be 16-B aligned");
-  hipLaunchKernelGGL(adam_k, dim3((unsigned)((n / 4 + 1 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     param, grad, m, v, step, (long)n, lr, beta1, beta2, eps, weight_decay, param_bf16);
+  hipLaunchKernelGGL(adam_k<false>, dim3((unsigned)((n / 4 + 1 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     param, const_cast<float*>(grad), m, v, step, (long)n, lr, beta1, beta2, eps, weight_decay,
+                     param_bf16, 1.f);
   return launch_status("adam");
+}
+
+extern "C" int cfsd_adam_scaled(float* param, float* grad, float* m, float* v, const int32_t* step, size_t n,
+                                float grad_scale, float lr, float beta1, float beta2, float eps,
+                                float weight_decay, uint16_t* param_bf16, void* stream) {
+  if (!param || !grad || !m || !v || !step) return set_error(CFSD_EINVAL, "adam_scaled: null pointer");
+  if (n == 0) return CFSD_OK;
+  if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v | (uintptr_t)param_bf16 * 2) & 15)
+    return set_error(CFSD_EINVAL, "adam_scaled: param/grad/m/v must be 16-B aligned");
+  hipLaunchKernelGGL(adam_k<true>, dim3((unsigned)((n / 4 + 1 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     param, grad, m, v, step, (long)n, lr, beta1, beta2, eps, weight_decay, param_bf16,
+                     grad_scale);
+  return launch_status("adam_scaled");
 }
 
 extern "C" int cfsd_step_begin(int32_t* counter, unsigned long long seed, float* eps, int n_eps,

@@ -84,11 +84,13 @@ class GradientAverager:
             self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
                                                async_op=True))
 
-    def finish(self, grad):
+    def finish(self, grad, scale=True):
+        """Join the bucket all-reduces; ``scale=False`` leaves the 1/world
+        factor to the caller (``TrainStep`` folds it into Adam)."""
         works, self._works = self._works, []
         for w in works:
             w.wait()
-        if self.world > 1:
+        if self.world > 1 and scale:
             self.scale(grad, 1.0 / self.world)
         return grad
 

@@ -920,10 +920,16 @@ class SDVAEEngine:
             return
         ops.dw_reduce_batch(deferred, adam=self.adam_args() if fuse_adam else None)
 
-    def adam_step(self):
+    def adam_step(self, grad_scale=None):
+        """Adam over the flat buffers; ``grad_scale`` (data-parallel: 1/world
+        after the all-reduce SUM) scales the gradient in the same launch."""
         P = self.params
-        ops.adam(P.data, P.grad, P.exp_avg, P.exp_avg_sq, P.step, self.lr, beta1=self.betas[0],
-                 beta2=self.betas[1], eps=self.adam_eps, weight_decay=self.weight_decay, shadow=P.shadow)
+        kw = dict(beta1=self.betas[0], beta2=self.betas[1], eps=self.adam_eps, weight_decay=self.weight_decay,
+                  shadow=P.shadow)
+        if grad_scale is None:
+            ops.adam(P.data, P.grad, P.exp_avg, P.exp_avg_sq, P.step, self.lr, **kw)
+        else:
+            ops.adam_scaled(P.data, P.grad, P.exp_avg, P.exp_avg_sq, P.step, grad_scale, self.lr, **kw)
 
     def advance_step(self, b=None):
         """t += 1 on device (the Adam bias-correction step) and, for a VAE

@@ -791,6 +791,22 @@ def adam(param, grad, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_d
          stream_ptr())
 
 
+def adam_scaled(param, grad, m, v, step, grad_scale, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0,
+                shadow=None):
+    """``scale(grad, grad_scale)`` then :func:`adam` in one launch (the
+    data-parallel step's 1/world averaging folded into the update); ``grad``
+    receives the scaled gradient."""
+    n = param.numel()
+    for t, nm in ((param, "param"), (grad, "grad"), (m, "m"), (v, "v")):
+        _need(t, (n,), name=nm)
+    _need(step, (1,), torch.int32, "step")
+    if shadow is not None:
+        _need(shadow, (n,), torch.bfloat16, "shadow")
+    call("cfsd_adam_scaled", ptr(param), ptr(grad), ptr(m), ptr(v), ptr(step), ctypes.c_size_t(n),
+         float(grad_scale), float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), ptr(shadow),
+         stream_ptr())
+
+
 def step_begin(counter, seed, eps=None, key=None, n_regions=0, batch_idx=None, bs=0,
                n_batches=0, perm=None, adam_step=None, n_items=None, shuffle=False):
     """Per-step device bookkeeping (``cfsd_step_begin``): counter, swap key,

@@ -22,7 +22,8 @@ first :meth:`TrainStep.run` of two or more steps, holds two whole steps).  Data-
 the two RCCL all-reduce buckets issued between the replays -- the decoder /
 bottleneck bucket right after ``part_a`` so it overlaps ``part_b`` (RCCL runs
 on its own stream, ordered after the work already queued), the encoder-conv
-bucket after ``part_b`` -- then ``cfsd_scale(1/world)`` and Adam.  The
+bucket after ``part_b`` -- then Adam with the 1/world averaging folded in
+(``cfsd_adam_scaled``).  The
 justification for data parallelism is that every loss term is intra-swap-group
 (``model_manager.py:360-393``): each rank trains its own groups and the only
 exchange is the flat fp32 gradient.
@@ -80,8 +81,8 @@ class TrainStep:
         self.eng.backward_tail(self.b, fuse_adam=self.avg is None)
 
     def part_c(self):
-        if self.avg is not None:
-            self.eng.adam_step()
+        if self.avg is not None:  # the 1/world averaging rides in the Adam launch
+            self.eng.adam_step(grad_scale=1.0 / self.avg.world)
 
     # ------------------------------------------------------------ buckets
     def _bucket_dec(self):
@@ -90,7 +91,7 @@ class TrainStep:
     def _bucket_enc_and_finish(self):
         grad = self.eng.params.grad
         self.avg.bucket_ready(grad[:self._split])
-        self.avg.finish(grad)
+        self.avg.finish(grad, scale=False)
 
     # ------------------------------------------------------------ running
     def eager_step(self):

@@ -457,6 +457,15 @@ int cfsd_adam(float* param, const float* grad, float* m, float* v, const int32_t
               float lr, float beta1, float beta2, float eps, float weight_decay,
               uint16_t* param_bf16, void* stream);
 
+/* cfsd_scale(grad, n, grad_scale) then cfsd_adam in ONE launch (ABI 4.7): the
+ * data-parallel step's 1/world averaging after the gradient all-reduce (SUM)
+ * folded into the update (model_manager.py:316 on the averaged gradient).
+ * `grad` receives the scaled gradient; same values bit for bit as the two
+ * launches. */
+int cfsd_adam_scaled(float* param, float* grad, float* m, float* v, const int32_t* step, size_t n,
+                     float grad_scale, float lr, float beta1, float beta2, float eps,
+                     float weight_decay, uint16_t* param_bf16, void* stream);
+
 /* Per-step device bookkeeping (graph-replayable, no host input):
  * t = ++*counter; key = hash(seed, t) % n_regions (replaces random.choice,
  * swap_batch_transform.py:26); eps[n_eps] ~ N(0,1) (replaces randn_like,

@@ -683,6 +683,29 @@ def test_adam_matches_torch(n, wd):
     close(m, opt.state[ref]["exp_avg"], 1e-6, "adam m")
 
 
+@pytest.mark.parametrize("n,world", [(1081881, 2), (1023, 8), (7, 3)])
+def test_adam_scaled_equals_scale_then_adam(n, world):
+    """cfsd_adam_scaled (the data-parallel step's 1/world averaging folded into
+    Adam) == cfsd_scale then cfsd_adam, bit for bit: parameters, both moments,
+    the bf16 shadow and the scaled gradient left in `grad`."""
+    g = torch.Generator().manual_seed(n + world)
+    p0, gr0 = torch.randn(n, generator=g).to(DEV), torch.randn(n, generator=g).to(DEV)
+    step = torch.full((1,), 3, dtype=torch.int32, device=DEV)
+    outs = []
+    for fused in (False, True):
+        p, gr = p0.clone(), gr0.clone()
+        m, v = torch.full((n,), 0.1, device=DEV), torch.full((n,), 0.2, device=DEV)
+        sh = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        if fused:
+            ops.adam_scaled(p, gr, m, v, step, 1.0 / world, 1e-3, weight_decay=1e-4, shadow=sh)
+        else:
+            ops.scale(gr, 1.0 / world)
+            ops.adam(p, gr, m, v, step, 1e-3, weight_decay=1e-4, shadow=sh)
+        outs.append((p, gr, m, v, sh))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 # --------------------------------------------------------------- evaluation (a17, f4)
 @pytest.mark.parametrize("bsz,nv,normalise", [(1, 67, False), (3, 1065, True), (16, 17039, False)])
 def test_vertex_errors_vs_oracle(bsz, nv, normalise):

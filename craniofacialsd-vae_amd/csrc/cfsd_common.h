@@ -71,10 +71,15 @@ inline int launch_status(const char* what) {
   return CFSD_OK;
 }
 
-__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
-// ELU with the hardware exp (v_exp_f32): exp(x) - 1, the form PyTorch's ELU
-// kernel evaluates; |error| <~ 1e-7 absolute.  Used in MFMA epilogues.
-__device__ __forceinline__ float elu_fast(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
+// ELU (alpha = 1, model.py's F.elu) with the hardware exp (v_exp_f32):
+// x > 0 ? x : exp(x) - 1, branch-free (5 VALU).  |error| vs expm1 < ~1.2e-7
+// absolute (one ulp of 1.0, near x = 0-), i.e. below the fp32 rounding of the
+// conv sums feeding it.  The libm expm1f it replaces is a chain of divergent
+// branches: 6.4 of the D3 forward's 60.5 us (kbench, ELU vs no activation,
+// profiles/round5_d3_forward_diagnosis.txt).  Every fp32 and bf16 kernel uses
+// this one function, so the layouts stay bit-identical to each other.
+__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
+__device__ __forceinline__ float elu_fast(float x) { return elu_f(x); }
 // dELU/dx written from the ELU OUTPUT y (alpha = 1): 1 for y > 0, else y + 1 = exp(x).
 __device__ __forceinline__ float elu_grad_from_out(float y) { return y > 0.f ? 1.f : y + 1.f; }
 

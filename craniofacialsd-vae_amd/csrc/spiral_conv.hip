@@ -2380,7 +2380,8 @@ DwGeom dw_geom(int batch, int rows, int cin, int cout) {
   if ((cin == 32 || cin == 64) && (cout == 32 || cout == 64) && M < kLatDwMax) {
     // few rows: one wave per (dW unit, row chunk); ~2k waves
     const long U = (long)dw_units(cin, cout);
-    long R = (M * U / kDwLatWaves + 15) / 16 * 16;
+    static const int lat_waves = env_knob("CFSD_LATDW_WAVES", kDwLatWaves);  // A/B knob
+    long R = (M * U / lat_waves + 15) / 16 * 16;
     R = R < 32 ? 32 : (R > 512 ? 512 : R);
     g.kind = kDwLat;
     g.rchunk = (int)R;

@@ -319,6 +319,19 @@ def launch_cost(name, a):
     if name == "cfsd_adam":
         n = a[5].value if hasattr(a[5], "value") else a[5]
         return 0.0, 7.0 * f4 * n, None
+    if name == "cfsd_adam_scaled":  # + the scaled gradient written back
+        n = a[5].value if hasattr(a[5], "value") else a[5]
+        return 0.0, 8.0 * f4 * n, None
+    if name == "cfsd_bottleneck_bwd":  # Pool(up)^T + decoder Linear + latent head + encoder Linear
+        n_up, cup, nd = a[4], a[5], a[11]
+        ke, ne, B, lat = a[25], a[26], a[29], a[30]
+        elu = a[21] is not None
+        fl = 4.0 * B * lat * nd + 10.0 * B * lat + 4.0 * B * ke * ne
+        by = (f4 * B * cup * n_up + 12 * nd // cup * 3      # fine gradient + the CSR (dh never stored)
+              + f4 * (2 * nd * lat + B * lat)               # W_d, dW_d, z
+              + f4 * B * lat * 8                            # latent head
+              + f4 * (2 * ne * ke + B * ke * (2 + int(elu)) + B * ne))  # W_e, dW_e, x_e, dx_e (elu_y), dmulv
+        return fl, by, FP32_PEAK_TFLOPS
     return 0.0, 0.0, None
 
 

@@ -857,6 +857,317 @@ __global__ __launch_bounds__(256) void linear_bwd_pair_k(const float* __restrict
   }
 }
 
+// ----------------------------------------------------------- bottleneck backward, one launch
+// The step's bottleneck backward -- Pool(up)^T of the coarsest Deblock
+// (model.py:172-173), the decoder Linear's dW/db/dz (:167-168), the latent
+// head (:184-188) and the stacked encoder Linear's dx/dW/db (:158-160) -- as
+// ONE launch of five workgroup roles instead of four launches (spmm_sched_csr,
+// linear_bwd_split, latent_bwd, linear_bwd_pair):
+//   A  [0, ndx_d)            decoder-Linear dz partials of one 64-row W slice;
+//                             its dy slice (= one coarse vertex of dh) folded
+//                             from the fine gradient on the fly (no dh round trip)
+//   L  next nb_lat           latent head: waits for every A, then dmulv
+//   D  next ndw_d            decoder-Linear dW/db rows (dy folded the same way)
+//   E  next ndx_e + ndw_e    encoder-Linear dx / dW (8 rows per workgroup);
+//                             each loads its W / x operands, then waits for L
+// A waiting workgroup only waits for workgroups of LOWER index, which the
+// dispatcher places first on every XCD, so the lowest unfinished workgroup can
+// always run: no deadlock for any residency.  Writers arrive with an
+// agent-scope release (L2 writeback: the partials / dmulv reach memory);
+// waiters poll relaxed and then read with plain loads (see bn_ld); the last
+// L workgroup raises one flag per E group and the E workgroups count
+// themselves out in two levels, the last one zeroing every counter, so graph
+// replays and eager calls start from zero.  A wait gives up after ~2^20 polls
+// (a broken launch returns garbage instead of hanging the GPU).  Every value
+// is formed by the same per-element operations in the same order as the four
+// launches: bit-identical (GPU-tested).  Per-workgroup timestamps (round 5):
+// A 0-11.7 us, L 12.1-15.9, E 16.3-21.4; the four launches take ~29 us.
+// Measured on the way (each fixed): acquiring polls 173 us, an acq_rel
+// done-count 44 us, one shared done-counter 33 us, uncached exchanged loads
+// ~29 us.
+struct BneckArgs {
+  const int* up_ptr;  // CSR of Pool(up)^T, rows = coarse vertices (plain per-row order)
+  const int* up_col;
+  const float* up_val;
+  const float* g;  // fine-level gradient [m][n_up][cup], batch-major
+  int n_up, cup;
+  const float* z;  // decoder Linear: z [m][kd], W_d [nd][kd] (nd = coarse vertices x cup)
+  const float* wd;
+  float* parts;  // [ndx_d][m][kd]
+  float* dwd;
+  float* dbd;
+  int m, kd, nd, ndx_d, ndw_d;
+  const float* mulv;  // latent head (latent_bwd_k's operands)
+  const float* eps;
+  const float* dlat;
+  float* dmulv;
+  const float* zval;
+  int L, train, is_vae, sigmoid, nb_lat;
+  const float* xe;  // encoder Linear: x_e [m][ke], W_e [ne][ke]
+  const float* we;
+  const float* elu_y;
+  float* dxe;
+  float* dwe;
+  float* dbe;
+  int ke, ne, accumulate, ndx_x, ndx_e, ndw_x, ndw_g;
+  int* sync;  // kBnSyncInts counters, one 128-B line each: A done, L done, E groups done, E done per group
+};
+constexpr int kBnSyncLine = 32;  // ints per 128-B line
+constexpr int kBnGroups = 8;
+constexpr int kBnSyncA = 0, kBnSyncL = kBnSyncLine, kBnSyncTop = 2 * kBnSyncLine, kBnSyncSub = 3 * kBnSyncLine;
+constexpr int kBnSyncFlag = kBnSyncSub + kBnGroups * kBnSyncLine;  // L-done flag per E group
+static_assert(kBnSyncFlag + kBnGroups * kBnSyncLine == 608, "cfsd.h documents 608 sync ints");
+constexpr int kBnDwRows = 4;  // encoder dW rows per E workgroup (x loaded once for all of them)
+constexpr int kBnWPer = kLinSplitN * kLinSplitK / 256;  // W-slice floats per thread of an A workgroup
+constexpr int kBnMaxParts = 80;                          // decoder-Linear partials (nd <= 80 x 64)
+
+__device__ __forceinline__ void bn_arrive(int* ctr) {
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+// relaxed polls (an acquiring poll invalidates the XCD's L2 every time: the
+// waiting workgroups then evict the running ones' operands -- 173 vs ~20 us)
+__device__ __forceinline__ void bn_wait(int* ctr, int target) {
+  if (threadIdx.x == 0) {
+    for (int it = 0; it < (1 << 20); ++it) {
+      if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  __syncthreads();
+}
+// The exchanged values (dz partials, dmulv) are read with plain, L2-cached
+// loads after the counter / flag is seen.  No line of them can be stale in a
+// reader's L2: every dispatch starts with the caches invalidated, nothing
+// reads them in this launch before the writers' release (an L2 writeback),
+// and the writer's own XCD keeps the written (then clean) lines.  Acquiring
+// each wait instead (an L2 invalidate by each of ~600 workgroups) cost ~20
+// us, and agent-scope atomic loads (uncached) of the 9.6-KB dmulv by every E
+// workgroup put ~12k requests on a handful of lines (~15 us).
+__device__ __forceinline__ float bn_ld(const float* p) { return *p; }
+
+// dst[i * ds + c] = dh[i][c0 + c], c < nc (nc <= cup, inside one coarse vertex):
+// the transposed Pool's sequential fold of spmm_fold_prefetch (acc = acc +
+// x * v over the row's entries in order, contraction off)
+__device__ __forceinline__ void bn_fold_dh(const BneckArgs& a, int c0, int nc, float* dst, int ds) {
+#pragma clang fp contract(off)
+  const int v = c0 / a.cup, ch0 = c0 - v * a.cup, q4 = nc / 4;
+  const int beg = a.up_ptr[v], end = a.up_ptr[v + 1];
+  for (int t = threadIdx.x; t < a.m * q4; t += blockDim.x) {
+    const int i = t / q4, q = t - i * q4;
+    const float* xb = a.g + (long)i * a.n_up * a.cup + ch0 + 4 * q;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int e0 = beg; e0 < end; e0 += 8) {
+      f32x4 xv[8];
+      float vv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = min(e0 + j, end - 1);
+        xv[j] = ld4(xb + (long)a.up_col[e] * a.cup);
+        vv[j] = a.up_val[e];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (e0 + j < end) {
+          acc.x = acc.x + xv[j].x * vv[j];
+          acc.y = acc.y + xv[j].y * vv[j];
+          acc.z = acc.z + xv[j].z * vv[j];
+          acc.w = acc.w + xv[j].w * vv[j];
+        }
+      }
+    }
+    st4(dst + i * ds + 4 * q, acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
+  extern __shared__ float bn_lds[];
+  const int bid = blockIdx.x;
+  const int b_lat = a.ndx_d, b_dwd = b_lat + a.nb_lat, b_enc = b_dwd + a.ndw_d;
+  const int n_enc = a.ndx_e + a.ndw_x * a.ndw_g;
+  const int m = a.m;
+  if (bid < b_lat) {  // A: parts[bid][i][kk] = sum_{c in slice} dy[i][c] W_d[c][kk]
+    float* wl = bn_lds;                    // [64][kd]
+    float* dl = bn_lds + kLinSplitN * a.kd;  // [m][64]
+    const int c0 = bid * kLinSplitN, nc = min(kLinSplitN, a.nd - c0);
+    // the W slice's loads go out first and land while the dh fold's own
+    // gathers are in flight (one memory round trip for both, not 3 + 2)
+    const float* ws = a.wd + (long)c0 * a.kd;
+    const int nw = nc * a.kd;
+    float wv[kBnWPer];
+#pragma unroll
+    for (int j = 0; j < kBnWPer; ++j) {
+      const int e = j * 256 + (int)threadIdx.x;
+      wv[j] = e < nw ? ws[e] : 0.f;
+    }
+    bn_fold_dh(a, c0, nc, dl, kLinSplitN);
+#pragma unroll
+    for (int j = 0; j < kBnWPer; ++j) {
+      const int e = j * 256 + (int)threadIdx.x;
+      if (e < nw) wl[e] = wv[j];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < m * a.kd; e += blockDim.x) {
+      const int i = e / a.kd, kk = e % a.kd;
+      float acc = 0.f;
+      for (int c = 0; c < nc; ++c) acc = fmaf(dl[i * kLinSplitN + c], wl[c * a.kd + kk], acc);
+      a.parts[(long)bid * m * a.kd + e] = acc;
+    }
+    bn_arrive(a.sync + kBnSyncA);
+    return;
+  }
+  if (bid < b_dwd) {  // L: latent_bwd_k's element map
+    bn_wait(a.sync + kBnSyncA, a.ndx_d);
+    const int e = (bid - b_lat) * blockDim.x + threadIdx.x;
+    if (e < m * a.L) {
+      const int B = m, L = a.L, i = e / L, l = e % L;
+      // every partial in flight at once (one round trip; 16-load batches were
+      // 5 trips, 4.5 us), then summed in part order as latent_bwd_k
+      float t[kBnMaxParts];
+#pragma unroll
+      for (int j = 0; j < kBnMaxParts; ++j) t[j] = bn_ld(a.parts + (long)min(j, a.ndx_d - 1) * B * L + e);
+      float dzd = t[0];
+#pragma unroll
+      for (int j = 1; j < kBnMaxParts; ++j)
+        if (j < a.ndx_d) dzd += t[j];
+      const float dz = dzd + a.dlat[i * 3 * L + l];
+      if (a.is_vae) {
+        const float lv = a.mulv[i * 2 * L + l];
+        const float dmu = dz + a.dlat[i * 3 * L + L + l];
+        float dlv = a.dlat[i * 3 * L + 2 * L + l];
+        if (a.train) dlv += dz * a.eps[e] * 0.5f * expf(0.5f * lv);
+        a.dmulv[i * 2 * L + l] = dlv;
+        a.dmulv[i * 2 * L + L + l] = dmu;
+      } else {
+        float dmu = dz;
+        if (a.sigmoid) dmu *= a.zval[e] * (1.f - a.zval[e]);
+        a.dmulv[i * L + l] = dmu;
+      }
+    }
+    // the last L workgroup raises one flag per E group (the E workgroups poll
+    // their group's line, not one shared address)
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(a.sync + kBnSyncL, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == a.nb_lat - 1) {
+      for (int g = 0; g < kBnGroups; ++g)
+        __hip_atomic_store(a.sync + kBnSyncFlag + kBnSyncLine * g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  if (bid < b_enc) {  // D: dW_d / db_d rows c0 .. c0 + 15 (linear_bwd_split_k's dW body)
+    float* xl = bn_lds;              // [m][kd]
+    float* dl = bn_lds + m * a.kd;   // [m][16]
+    const int c0 = (bid - b_dwd) * kLinDwRows, nc = min(kLinDwRows, a.nd - c0);
+    stage_lds(a.z, xl, m * a.kd);
+    bn_fold_dh(a, c0, nc, dl, kLinDwRows);
+    __syncthreads();
+    for (int e = threadIdx.x; e < nc * a.kd; e += blockDim.x) {
+      const int c = e / a.kd, kk = e % a.kd;
+      float acc = 0.f;
+      for (int i = 0; i < m; ++i) acc = fmaf(dl[i * kLinDwRows + c], xl[i * a.kd + kk], acc);
+      a.dwd[(long)c0 * a.kd + e] = acc;
+    }
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+      float acc = 0.f;
+      for (int i = 0; i < m; ++i) acc += dl[i * kLinDwRows + c];
+      a.dbd[c0 + c] = acc;
+    }
+    return;
+  }
+  // E: encoder Linear, operands loaded before the wait for dmulv
+  const int ej = bid - b_enc;
+  const int n = a.ne, k = a.ke;
+  if (ej < a.ndx_e) {  // dx: linear_dx_nsmall_body (row quad by, 64 k-columns bx)
+    const int bx = ej % a.ndx_x, by = ej / a.ndx_x;
+    float* ds = bn_lds;                  // [4][n]
+    float* part = bn_lds + 4 * n;        // [4 waves][4 rows][64]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i0 = by * 4, mr = min(4, m - i0);
+    const int kk = bx * 64 + lane;
+    const int kc = kk < k ? kk : k - 1;
+    const int per = (n + 3) / 4, c0 = wave * per, c1 = min(n, c0 + per);
+    // the wave's whole c-range is one kLinDxChunk chunk (n <= 4 x 40, checked
+    // by the host): its W column loads are in flight while this workgroup waits
+    float wv[kLinDxChunk];
+#pragma unroll
+    for (int u = 0; u < kLinDxChunk; ++u) wv[u] = c0 + u < c1 ? a.we[(long)(c0 + u) * k + kc] : 0.f;
+    bn_wait(a.sync + kBnSyncFlag + kBnSyncLine * (ej % kBnGroups), 1);
+    for (int e = threadIdx.x; e < mr * n; e += blockDim.x) ds[e] = bn_ld(a.dmulv + (long)i0 * n + e);
+    __syncthreads();
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < kLinDxChunk; ++u) {
+      const int c = min(c0 + u, n - 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = fmaf(ds[i * n + c], wv[u], acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[(wave * 4 + i) * 64 + lane] = acc[i];
+    __syncthreads();
+    if (wave < mr && kk < k) {
+      const int i = wave;
+      float v = part[(0 * 4 + i) * 64 + lane] + part[(1 * 4 + i) * 64 + lane] + part[(2 * 4 + i) * 64 + lane] +
+                part[(3 * 4 + i) * 64 + lane];
+      const long o = (long)(i0 + i) * k + kk;
+      if (a.elu_y) v *= elu_grad_from_out(a.elu_y[o]);
+      a.dxe[o] = a.accumulate ? a.dxe[o] + v : v;
+    }
+  } else {  // dW rows nn0 .. nn0 + 7 over the 256 k-columns bx (linear_dw_body per row), db by bx == 0
+    const int j = ej - a.ndx_e, bx = j % a.ndw_x, nn0 = (j / a.ndw_x) * kBnDwRows;
+    const int kk = bx * blockDim.x + threadIdx.x;
+    const bool on = kk < k;
+    float xv[kLinSplitM];
+#pragma unroll
+    for (int i = 0; i < kLinSplitM; ++i) xv[i] = (on && i < m) ? a.xe[(long)i * k + kk] : 0.f;
+    bn_wait(a.sync + kBnSyncFlag + kBnSyncLine * (ej % kBnGroups), 1);
+    // the block's dmulv columns [m][8] in ONE round of vector loads (per-row
+    // scalar loads were 8 dependent trips to memory: 40 us for this phase)
+    float* dl = bn_lds;  // [m][kBnDwRows]
+    if ((int)threadIdx.x < m * kBnDwRows) {
+      const int i = threadIdx.x / kBnDwRows, r = threadIdx.x % kBnDwRows;
+      dl[threadIdx.x] = nn0 + r < n ? bn_ld(a.dmulv + (long)i * n + nn0 + r) : 0.f;
+    }
+    __syncthreads();
+    for (int r = 0; r < kBnDwRows; ++r) {
+      const int nn = nn0 + r;
+      if (nn >= n) break;
+      if (on) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < kLinSplitM; ++i)
+          if (i < m) s = fmaf(dl[i * kBnDwRows + r], xv[i], s);
+        a.dwe[(long)nn * k + kk] = s;
+      }
+      if (bx == 0 && threadIdx.x == 0) {
+        float s = 0.f;
+        for (int i = 0; i < m; ++i) s += dl[i * kBnDwRows + r];
+        a.dbe[nn] = s;
+      }
+    }
+  }
+  // the last E workgroup resets the counters for the next launch.  Counted in
+  // two levels (8 group counters on their own cache lines, then one top
+  // counter): 591 RMWs on ONE address serialise at its memory channel (the E
+  // stage cost ~17 us that way).  Relaxed: a counting RMW needs no cache
+  // maintenance (acq_rel is an L2 writeback + invalidate per workgroup).
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int grp = ej % kBnGroups, n_grp = n_enc < kBnGroups ? n_enc : kBnGroups;
+    const int quota = (n_enc - grp + kBnGroups - 1) / kBnGroups;
+    int* sub = a.sync + kBnSyncSub + kBnSyncLine * grp;
+    if (__hip_atomic_fetch_add(sub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == quota - 1) {
+      __hip_atomic_store(sub, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.sync + kBnSyncFlag + kBnSyncLine * grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int* top = a.sync + kBnSyncTop;
+      if (__hip_atomic_fetch_add(top, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_grp - 1) {
+        __hip_atomic_store(a.sync + kBnSyncA, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.sync + kBnSyncL, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(top, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------------- Adam
 // Four elements per thread in 16-B accesses (the four state arrays are
 // streamed once: 7 x 4 B per element of HBM traffic); the n % 4 tail goes to
@@ -986,7 +1297,7 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
 
 using namespace cfsd;
 
-extern "C" int cfsd_version(void) { return (4 << 16) | 7; }  // 4.7: cfsd_adam_scaled; 4.6: cfsd_side_work (side work riding in host launches); 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
+extern "C" int cfsd_version(void) { return (4 << 16) | 8; }  // 4.8: cfsd_bottleneck_bwd; 4.7: cfsd_adam_scaled; 4.6: cfsd_side_work (side work riding in host launches); 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
 extern "C" const char* cfsd_last_error_string(void) { return g_err; }
 
 extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {
@@ -1298,6 +1609,75 @@ extern "C" int cfsd_linear_bwd_split(const float* x, const float* w, const float
   hipLaunchKernelGGL(linear_bwd_split_k, dim3(ndx + ndw), dim3(256), 0, (hipStream_t)stream, x, w, dy,
                      dx_parts, dw, db, m, k, n, ndx);
   return launch_status("linear_bwd_split");
+}
+
+extern "C" int cfsd_bottleneck_bwd(const int32_t* up_ptr, const int32_t* up_col, const float* up_val,
+                                   const float* g, int n_up, int cup, const float* z, const float* wd,
+                                   float* dz_parts, float* dwd, float* dbd, int nd, const float* mulv,
+                                   const float* eps, const float* dlat, float* dmulv, int train, int is_vae,
+                                   int sigmoid, const float* xe, const float* we, const float* elu_y, float* dxe,
+                                   float* dwe, float* dbe, int ke, int ne, int accumulate, int32_t* sync, int batch,
+                                   int latent, void* stream) {
+  if (!up_ptr || !up_col || !up_val || !g || !z || !wd || !dz_parts || !dwd || !dbd || !mulv || !dlat || !dmulv ||
+      !xe || !we || !dxe || !dwe || !dbe || !sync)
+    return set_error(CFSD_EINVAL, "bottleneck_bwd: null pointer");
+  if (is_vae && train && !eps) return set_error(CFSD_EINVAL, "bottleneck_bwd: eps required");
+  const int m = batch, kd = latent;
+  if (m <= 0 || m > kLinSplitM || kd <= 0 || kd > kLinSplitK || cup <= 0 || cup % kLinSplitN || nd <= 0 ||
+      nd % cup || nd > kBnMaxParts * kLinSplitN || n_up <= 0 || ke <= 0 || ne <= 0 || ne > 4 * kLinDxChunk ||
+      ne != (is_vae ? 2 : 1) * latent)
+    return set_error(CFSD_EINVAL,
+                     "bottleneck_bwd: sizes batch=%d latent=%d cup=%d nd=%d ke=%d ne=%d (batch <= %d, latent <= %d, "
+                     "cup a multiple of %d, ne <= %d)",
+                     m, kd, cup, nd, ke, ne, kLinSplitM, kLinSplitK, kLinSplitN, 4 * kLinDxChunk);
+  BneckArgs a{};
+  a.up_ptr = up_ptr;
+  a.up_col = up_col;
+  a.up_val = up_val;
+  a.g = g;
+  a.n_up = n_up;
+  a.cup = cup;
+  a.z = z;
+  a.wd = wd;
+  a.parts = dz_parts;
+  a.dwd = dwd;
+  a.dbd = dbd;
+  a.m = m;
+  a.kd = kd;
+  a.nd = nd;
+  a.ndx_d = cfsd_linear_bwd_split_parts(nd);
+  a.ndw_d = (nd + kLinDwRows - 1) / kLinDwRows;
+  a.mulv = mulv;
+  a.eps = eps;
+  a.dlat = dlat;
+  a.dmulv = dmulv;
+  a.zval = z;
+  a.L = latent;
+  a.train = train;
+  a.is_vae = is_vae;
+  a.sigmoid = sigmoid;
+  a.nb_lat = (m * latent + 255) / 256;
+  a.xe = xe;
+  a.we = we;
+  a.elu_y = elu_y;
+  a.dxe = dxe;
+  a.dwe = dwe;
+  a.dbe = dbe;
+  a.ke = ke;
+  a.ne = ne;
+  a.accumulate = accumulate;
+  a.ndx_x = (ke + 63) / 64;
+  a.ndx_e = a.ndx_x * ((m + 3) / 4);
+  a.ndw_x = (ke + 255) / 256;
+  a.ndw_g = (ne + kBnDwRows - 1) / kBnDwRows;
+  a.sync = sync;
+  const int nb = a.ndx_d + a.nb_lat + a.ndw_d + a.ndx_e + a.ndw_x * a.ndw_g;
+  size_t lds = (size_t)kLinSplitN * kd + (size_t)m * kLinSplitN;
+  lds = std::max(lds, (size_t)m * kd + (size_t)m * kLinDwRows);
+  lds = std::max(lds, (size_t)4 * ne + 16 * 64);
+  lds = std::max(lds, (size_t)m * kBnDwRows);
+  hipLaunchKernelGGL(bottleneck_bwd_k, dim3(nb), dim3(256), lds * sizeof(float), (hipStream_t)stream, a);
+  return launch_status("bottleneck_bwd");
 }
 
 extern "C" int cfsd_adam(float* param, const float* grad, float* m, float* v,

@@ -18,6 +18,7 @@ MI355X design:
   epilogue, deterministic gather-based transposes, no atomics).
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -187,6 +188,9 @@ class SDVAEEngine:
         # launches (ops.SideWork), the rest in one side-work launch; "final" = all
         # in one side-work launch; "off" = cfsd_dw_reduce_batch(_adam)
         self.side_work = "off"
+        # the bottleneck backward (coarsest Pool(up)^T, decoder Linear, latent
+        # head, encoder Linear) as one launch (cfsd_bottleneck_bwd)
+        self.fuse_bottleneck = os.environ.get("CFSD_FUSE_BOTTLENECK", "1") != "0"
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -411,6 +415,7 @@ class SDVAEEngine:
         b.dz_parts = (f(ops.linear_bwd_split_parts(flat_out), bsz, lat)
                       if bsz <= 16 and lat <= 128 else None)
         b.dmulv = torch.empty_like(b.mulv)
+        b.bn_sync = torch.zeros(ops.BN_SYNC_INTS, dtype=torch.int32, device=dev)  # cfsd_bottleneck_bwd's counters
         b.dpre_enc = [f(bsz, nv[lv + 1], cout) if (lv == last_enc or not T.enc_select[lv])
                       else fl(lv + 1, bsz, nv[lv + 1], cout) for (cin, cout, lv) in S.enc_layers()]
         b.g_enc_in = [None] + [f(bsz, nv[lv], cin) if not T.enc_select[lv - 1] else None
@@ -731,6 +736,7 @@ class SDVAEEngine:
                            dx=b.dpre_dec[-1], elu_y=last_in, workspace=b.ws_dw["out"])
         defer(d, f"de_layers.{n + 1}.layer")
         dec = S.dec_layers()
+        fused_bn = self._fused_bottleneck_ok(b)
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]
             w, _ = self._dec_w(i)
@@ -768,8 +774,15 @@ class SDVAEEngine:
             if i > 0:  # through Pool(up) into the previous Deblock's ELU
                 self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dpre_dec[i - 1],
                            elu_y=b.dec_out[i - 1], sched=sch, side=sw)
-            else:
+            elif not fused_bn:
                 self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh, sched=sch, side=sw)
+        if fused_bn:  # Pool(up)^T + decoder Linear + latent head + encoder Linear: one launch
+            self._bottleneck_bwd_fused(b)
+            if split:
+                ops.dw_reduce_batch(side_items)
+                side_items.clear()
+            b.deferred = list(side_items)
+            return
         # decoder Linear: dW/db and dz (as 64-row-slice partial products,
         # summed by the latent head's backward) in one launch
         if b.dz_parts is not None:
@@ -813,6 +826,35 @@ class SDVAEEngine:
         else:
             ops.linear_bwd(flat, W, b.dmulv, dx=b.g_pooled[last].view(b.bsz, -1), dw=gW.view(W.shape),
                            db=gB, workspace=b.lin_ws)
+            ops.spmm(T.downT_csr[last], b.g_pooled[last], T.n_verts[last], elu_y=b.enc_full[last],
+                     out=b.dpre_enc[last])
+
+    def _fused_bottleneck_ok(self, b):
+        """cfsd_bottleneck_bwd applies: partial-products decoder Linear, no
+        side work hosted by the latent head, the coarsest Deblock's gradient
+        batch-major fp32 with 64-multiple channels, batch <= 16, latent <= 128."""
+        S = self.spec
+        g = b.g_dec_up[0]
+        ne = S.latent * (2 if S.is_vae else 1)
+        return (self.fuse_bottleneck and b.dz_parts is not None and self.side_work != "hosts"
+                and g.dtype == torch.float32 and not ops.is_vm(g) and g.is_contiguous()
+                and g.shape[2] % 64 == 0 and b.h.numel() // b.bsz <= 5120 and b.bsz <= 16 and S.latent <= 128
+                and ne <= 160)
+
+    def _bottleneck_bwd_fused(self, b):
+        T, S, P = self.topo, self.spec, self.params
+        ui = S.dec_layers()[0][3]
+        W, _ = self._enc_lin()
+        gW, gB = self._enc_lin(P.grad)
+        last = S.enc_layers()[-1][2]
+        flat = b.enc_out[last].view(b.bsz, -1)
+        select = T.enc_select[last]
+        dxe = b.dpre_enc[last].view(b.bsz, -1) if select else b.g_pooled[last].view(b.bsz, -1)
+        ops.bottleneck_bwd(T.upT_csr[ui], b.g_dec_up[0], b.z, P.view("de_layers.0.weight"), b.dz_parts,
+                           P.gview("de_layers.0.weight"), P.gview("de_layers.0.bias"), b.mulv, b.eps, b.dlat,
+                           b.dmulv, S.is_vae, S.sigmoid, flat, W, dxe, gW.view(W.shape), gB, b.bn_sync,
+                           elu_y=flat if select else None)
+        if not select:
             ops.spmm(T.downT_csr[last], b.g_pooled[last], T.n_verts[last], elu_y=b.enc_full[last],
                      out=b.dpre_enc[last])
 

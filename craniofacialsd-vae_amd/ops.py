@@ -747,6 +747,49 @@ def latent_bwd(mulv, eps, z, dz_dec, dlat, dmulv, latent, train, is_vae, sigmoid
          latent, int(train), int(is_vae), int(sigmoid), stream_ptr())
 
 
+BN_SYNC_INTS = 608  # cfsd_bottleneck_bwd's counters and flags (19 x one 128-B line)
+
+
+def bottleneck_bwd(up_csr, g, z, wd, dz_parts, dwd, dbd, mulv, eps, dlat, dmulv, is_vae, sigmoid, xe, we, dxe,
+                   dwe, dbe, sync, elu_y=None, accumulate=False, train=True):
+    """The bottleneck backward in one launch (``cfsd_bottleneck_bwd``): the
+    coarsest Pool(up) transpose over ``g`` [B, n_up, cup] (``up_csr`` =
+    (row_ptr, col, val), plain per-row order), the decoder Linear backward
+    (``wd`` [nd, latent]; ``dz_parts`` as :func:`linear_bwd_split`), the
+    latent head backward (:func:`latent_bwd`) and the encoder Linear backward
+    (:func:`linear_bwd` with ``xe`` [B, ke], ``we`` [ne, ke], dy = ``dmulv``).
+    ``sync``: BN_SYNC_INTS zeroed device int32, left zeroed."""
+    row_ptr, col, val = up_csr
+    bsz, n_up, cup = g.shape
+    _need(g, None, name="g")
+    if is_vm(g):
+        raise ValueError("g must be batch-major")
+    m, lat = z.shape
+    nd, kd = wd.shape
+    ne, ke = we.shape
+    if kd != lat or m != bsz or nd % cup:
+        raise ValueError(f"bottleneck_bwd: z {tuple(z.shape)}, wd {tuple(wd.shape)}, g {tuple(g.shape)}")
+    _need(row_ptr, (nd // cup + 1,), torch.int32, "up_ptr")
+    _need(col, None, torch.int32, "up_col")
+    _need(val, (col.numel(),), name="up_val")
+    _need(z, (m, lat), name="z")
+    _need(dz_parts, (linear_bwd_split_parts(nd), m, lat), name="dz_parts")
+    _need(dwd, (nd, lat), name="dwd")
+    _need(dbd, (nd,), name="dbd")
+    _need(dmulv, tuple(mulv.shape), name="dmulv")
+    _need(xe, (m, ke), name="xe")
+    _need(dxe, (m, ke), name="dxe")
+    if elu_y is not None:
+        _need(elu_y, (m, ke), name="elu_y")
+    _need(dwe, (ne, ke), name="dwe")
+    _need(dbe, (ne,), name="dbe")
+    _need(sync, (BN_SYNC_INTS,), torch.int32, "sync")
+    call("cfsd_bottleneck_bwd", ptr(row_ptr), ptr(col), ptr(val), ptr(g), n_up, cup, ptr(z), ptr(wd), ptr(dz_parts),
+         ptr(dwd), ptr(dbd), nd, ptr(mulv), ptr(eps), ptr(dlat), ptr(dmulv), int(train), int(is_vae), int(sigmoid),
+         ptr(xe), ptr(we), ptr(elu_y), ptr(dxe), ptr(dwe), ptr(dbe), ke, ne, int(accumulate), ptr(sync), m, lat,
+         stream_ptr())
+
+
 def linear_bwd_split_parts(n):
     return int(_abi.lib().cfsd_linear_bwd_split_parts(n))
 

@@ -499,6 +499,97 @@ def test_fused_reduce_adam_matches_separate(dtopo, precision, vertex_major):
             assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("precision,vertex_major", [("fp32", True), ("fp32", False), ("bf16", True)])
+def test_fused_bottleneck_matches_four_launches(dtopo, precision, vertex_major):
+    """cfsd_bottleneck_bwd (ABI 4.8: coarsest Pool(up)^T + decoder Linear +
+    latent head + encoder Linear in one launch, later workgroups waiting on
+    device counters) == spmm + linear_bwd_split + latent_bwd + linear_bwd,
+    bit for bit over two whole training steps: parameters, gradients, Adam
+    moments, dmulv and the encoder-Linear data gradient; the counters are
+    left zero."""
+    w = recipe.golden_weights()
+    x = torch.from_numpy(O.swap_features(recipe.normalized_meshes(4), [np.asarray(r) for r in
+                                         O.Topology(recipe.load_topology()).region_features], 2)).to(DEV)
+    eps = torch.from_numpy(recipe.train_eps(0)).to(DEV)
+    outs = []
+    for fused in (False, True):
+        eng = make_engine(dtopo, w, precision=precision, vertex_major=vertex_major)
+        eng.fuse_bottleneck = fused
+        for _ in range(2):
+            b = eng.set_batch(x, key_index=2, eps=eps)
+            assert eng._fused_bottleneck_ok(b) == fused
+            eng.train_step_on(b)
+        torch.cuda.synchronize()
+        P = eng.params
+        last = eng.spec.enc_layers()[-1][2]
+        outs.append([t.cpu().clone() for t in (P.data, P.grad, P.exp_avg, P.exp_avg_sq, b.dmulv,
+                                               b.dpre_enc[last])])
+        if fused:
+            assert not b.bn_sync.any()
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("is_vae,select,sigmoid", [(1, True, 0), (0, True, 1), (1, False, 0)])
+def test_bottleneck_bwd_op_vs_separate(is_vae, select, sigmoid):
+    """The op on random operands (batch 16, the craniofacial bottleneck: 267
+    -> 67 coarse vertices x 64 channels, latent 75, encoder flat 4288) ==
+    the four separate launches, bit for bit, three calls in a row (the
+    counters reset themselves); VAE / plain-AE-with-sigmoid latent heads, with
+    and without the encoder-Linear ELU."""
+    g = torch.Generator().manual_seed(7 + is_vae + 2 * select)
+    rnd = lambda *s: torch.randn(*s, generator=g).to(DEV)
+    B, L, cup, n_up, nv, ke = 16, 75, 64, 267, 67, 4288
+    ne = 2 * L if is_vae else L
+    # a Pool(up)^T-shaped CSR: each fine vertex feeds 3 coarse vertices
+    cols = [[] for _ in range(nv)]
+    for f in range(n_up):
+        for k in range(3):
+            cols[(f * 7 + k * 11) % nv].append((f, 0.1 + 0.3 * k))
+    row_ptr = torch.tensor([0] + list(np.cumsum([len(c) for c in cols])), dtype=torch.int32, device=DEV)
+    col = torch.tensor([f for c in cols for f, _ in c], dtype=torch.int32, device=DEV)
+    val = torch.tensor([v for c in cols for _, v in c], dtype=torch.float32, device=DEV)
+    gfine0, z, wd = rnd(B, n_up, cup), rnd(B, L), rnd(nv * cup, L)
+    mulv, epsv, dlat0 = rnd(B, ne), rnd(B, L), rnd(B, 3 * L)
+    zval = torch.sigmoid(z)
+    xe, we = rnd(B, ke), rnd(ne, ke)
+    elu_y = torch.nn.functional.elu(rnd(B, ke)) if select else None
+    parts_n = ops.linear_bwd_split_parts(nv * cup)
+    hist_s, hist_f = [], []
+    res = []
+    for fused in (False, True):
+        gfine, dlat = gfine0.clone(), dlat0.clone()
+        out = dict(parts=torch.zeros(parts_n, B, L, device=DEV), dwd=torch.zeros(nv * cup, L, device=DEV),
+                   dbd=torch.zeros(nv * cup, device=DEV), dmulv=torch.zeros(B, ne, device=DEV),
+                   dxe=torch.zeros(B, ke, device=DEV), dwe=torch.zeros(ne, ke, device=DEV),
+                   dbe=torch.zeros(ne, device=DEV))
+        sync = torch.zeros(ops.BN_SYNC_INTS, dtype=torch.int32, device=DEV)
+        zin = zval if (sigmoid and not is_vae) else z
+        for it in range(3):  # fresh operands per call: a stale cached value from the previous call would show
+            gfine.mul_(0.5 + it)
+            dlat.add_(0.25)
+            if fused:
+                ops.bottleneck_bwd((row_ptr, col, val), gfine, zin, wd, out["parts"], out["dwd"], out["dbd"], mulv,
+                                   epsv, dlat, out["dmulv"], is_vae, sigmoid, xe, we, out["dxe"], out["dwe"],
+                                   out["dbe"], sync, elu_y=elu_y)
+            else:
+                dh = ops.spmm((row_ptr, col, val), gfine, nv)
+                ops.linear_bwd_split(zin, wd, dh.view(B, -1), out["parts"], out["dwd"], out["dbd"])
+                ops.latent_bwd(mulv, epsv, zin, out["parts"], dlat, out["dmulv"], L, True, is_vae, sigmoid)
+                ops.linear_bwd(xe, we, out["dmulv"], dx=out["dxe"], dw=out["dwe"], db=out["dbe"], elu_y=elu_y)
+            res_it = {k: v.cpu().clone() for k, v in out.items()}
+            res.append(res_it) if it == 2 else None
+            (hist_f if fused else hist_s).append(res_it)
+        torch.cuda.synchronize()
+        if fused:
+            assert not sync.any()
+    for a_, c_ in zip(hist_s, hist_f):  # every call, not only the last
+        for k in a_:
+            assert torch.equal(a_[k], c_[k]), k
+    for k in res[0]:
+        assert torch.equal(res[0][k], res[1][k]), k
+
+
 # --------------------------------------------------------------- dense Linears
 # Both bottleneck shapes of the model (encoder [m x 4288] -> 150 stacked
 # mu/logvar, decoder 75 -> 4288) plus ragged m (not a multiple of the 4-row /

@@ -198,6 +198,8 @@ def build_cases(names=()):
         cases[f"dx_e{lv}"] = (lambda lv=lv: ops.spiral_conv_bwd_data(
             b.dpre_enc[lv], T.enc_inv[lv], eng._enc_w(lv)[0], T.n_verts[lv], elu_y=b.enc_out[lv - 1],
             out=b.dpre_enc[lv - 1], workspace=b.ws))
+    # the fused bottleneck backward on the engine's buffers (kprof with CFSD_BN_EXP phases)
+    cases["bneck"] = lambda: eng._bottleneck_bwd_fused(b)
     W_enc, B_enc = eng._enc_lin()
     gW_enc, gB_enc = eng._enc_lin(P.grad)
     flat = b.enc_out[3].view(16, -1)

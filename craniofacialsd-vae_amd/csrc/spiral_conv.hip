@@ -1309,28 +1309,30 @@ __global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
     src = d.ws + f;
     stride = d.n_el;
   }
-  // slabs p = wv, wv + 16, ... summed in that order; 16 loads in flight per
-  // batch (the level-0 items have ~512 slabs: 32 per wave)
+  // slabs p = wv, wv + 16, ... summed in that order; every pass issues its
+  // 16 loads together, the partial last pass too (clamped loads, masked adds:
+  // a per-slab tail loop paid one memory round trip per slab -- up to 14 for
+  // the ~200-slab lat items)
   f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-  int p = wv;
+  const int last = d.n_slabs - 1;
   if (vec) {
-    for (; p + 16 * 15 < d.n_slabs; p += 16 * 16) {
+    for (int p = wv; p < d.n_slabs; p += 16 * 16) {
       f32x4 t[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) t[j] = ld4(src + (long)(p + 16 * j) * stride);
+      for (int j = 0; j < 16; ++j) t[j] = ld4(src + (long)min(p + 16 * j, last) * stride);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) sum += t[j];
+      for (int j = 0; j < 16; ++j)
+        if (p + 16 * j < d.n_slabs) sum += t[j];
     }
-    for (; p < d.n_slabs; p += 16) sum += ld4(src + (long)p * stride);
   } else {
-    for (; p + 16 * 15 < d.n_slabs; p += 16 * 16) {
+    for (int p = wv; p < d.n_slabs; p += 16 * 16) {
       float t[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) t[j] = src[(long)(p + 16 * j) * stride];
+      for (int j = 0; j < 16; ++j) t[j] = src[(long)min(p + 16 * j, last) * stride];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) sum.x += t[j];
+      for (int j = 0; j < 16; ++j)
+        if (p + 16 * j < d.n_slabs) sum.x += t[j];
     }
-    for (; p < d.n_slabs; p += 16) sum.x += src[(long)p * stride];
   }
   part[wv][lane] = sum;
   __syncthreads();

@@ -142,7 +142,7 @@ class Runner:
 
     def capture(self):
         self.ts.capture()
-        self.ts.capture_pair()  # the two-step graph the timed run(k) replays, recorded before timing
+        self.ts.capture_multi()  # the multi-step graph the timed run(k) replays, recorded before timing
 
     def step(self):
         self.ts.step()
@@ -660,7 +660,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    runner.run(args.steps)  # exactly args.steps training steps (two per replay of the 2-step graph)
+    runner.run(args.steps)  # exactly args.steps training steps (steps_per_graph per replay of the multi-step graph)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

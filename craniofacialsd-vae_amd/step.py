@@ -18,7 +18,9 @@ Step anatomy (every launch on one stream; nothing synchronises with the host):
 * ``part_c``: (data-parallel only) Adam, after the gradient all-reduce.
 
 One GPU: the three parts are ONE graph (and a second graph, recorded on the
-first :meth:`TrainStep.run` of two or more steps, holds two whole steps).  Data-parallel: three graphs, with
+first :meth:`TrainStep.run` of ``steps_per_graph`` or more steps, holds that
+many whole steps back to back: the host gap between consecutive replays,
+~8 us, is paid once per replay instead of once per step).  Data-parallel: three graphs, with
 the two RCCL all-reduce buckets issued between the replays -- the decoder /
 bottleneck bucket right after ``part_a`` so it overlaps ``part_b`` (RCCL runs
 on its own stream, ordered after the work already queued), the encoder-conv
@@ -28,6 +30,8 @@ justification for data parallelism is that every loss term is intra-swap-group
 (``model_manager.py:360-393``): each rank trains its own groups and the only
 exchange is the flat fp32 gradient.
 """
+import os
+
 import torch
 
 from . import ops
@@ -55,7 +59,9 @@ class TrainStep:
         self.b = engine.buffers(engine.step_rows)
         self.acc = engine.loss_acc if acc is None else acc
         self.graphs = None
-        self.graph2 = None
+        self.graph_multi = None
+        # steps recorded into the multi-step graph run(k) replays (env: A/B)
+        self.steps_per_graph = max(1, int(os.environ.get("CFSD_STEPS_PER_GRAPH", "16")))
         self._split = engine.enc_conv_numel()
 
     @property
@@ -125,17 +131,20 @@ class TrainStep:
                 with torch.cuda.graph(g):
                     fn()
 
-    def capture_pair(self):
-        """Record (once) the single-GPU graph holding two whole steps, which
-        :meth:`run` replays k // 2 times: half the per-replay launch gaps
-        (~8 us between consecutive replays).  Nothing runs while recording."""
-        if self.graph2 is None and self.graphs is not None and self.avg is None:
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2):
-                for _ in range(2):
+    def capture_multi(self):
+        """Record (once) the single-GPU graph holding ``steps_per_graph``
+        whole steps, which :meth:`run` replays k // steps_per_graph times: the
+        per-replay host gap (~8 us between consecutive replays) is paid once
+        per that many steps.  Nothing runs while recording."""
+        if self.graph_multi is None and self.graphs is not None and self.avg is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(self.steps_per_graph):
                     self.part_a()
                     self.part_b()
-            self.graph2 = g2
+            self.graph_multi = g
+
+    capture_pair = capture_multi  # (round-4 name)
 
     def step(self):
         if self.graphs is None:
@@ -154,13 +163,14 @@ class TrainStep:
 
     def run(self, k):
         """``k`` training steps (the same steps as ``k`` calls of :meth:`step`);
-        a captured single-GPU runner replays the two-step graph."""
+        a captured single-GPU runner replays the multi-step graph."""
         if self.graphs is not None and self.avg is None:
-            if k >= 2:
-                self.capture_pair()
-            for _ in range(k // 2):
-                self.graph2.replay()
-            if k % 2:
+            n = self.steps_per_graph
+            if k >= n:
+                self.capture_multi()
+            for _ in range(k // n):
+                self.graph_multi.replay()
+            for _ in range(k % n):
                 self.graphs[0].replay()
             return
         for _ in range(k):

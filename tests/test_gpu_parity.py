@@ -1120,10 +1120,12 @@ def test_engine_forward_fused_latent_equals_unfused(dtopo):
         assert torch.equal(a, c)
 
 
-def test_trainstep_two_step_graph_matches_eager(dtopo):
-    """TrainStep.run(k) on a captured single-GPU runner replays the two-step
-    graph k // 2 times (+ the one-step graph): the parameters, moments and
-    losses of k eager steps, bit for bit."""
+def test_trainstep_multi_step_graph_matches_eager(dtopo):
+    """TrainStep.run(k) on a captured single-GPU runner replays the
+    steps_per_graph-step graph k // steps_per_graph times (+ the one-step
+    graph): the parameters, moments and losses of k eager steps, bit for bit
+    (epoch boundaries inside the multi-step graph included: 3 batches per
+    epoch)."""
     from craniofacialsd_vae_amd import step as ST
     res = []
     for captured in (False, True):
@@ -1131,11 +1133,12 @@ def test_trainstep_two_step_graph_matches_eager(dtopo):
                               rows=list(range(12)), shuffle=True)
         eng = make_engine(dtopo, recipe.golden_weights())
         ts = ST.TrainStep(eng, data)
+        n = ts.steps_per_graph
         if captured:
             ts.capture()  # (runs one real step eagerly first)
-            ts.run(5)
+            ts.run(2 * n + 3)
         else:
-            ts.run(6)
+            ts.run(2 * n + 4)
         torch.cuda.synchronize()
         P = eng.params
         res.append([t.clone() for t in (P.data, P.exp_avg, P.exp_avg_sq, eng.loss_acc)])

@@ -260,6 +260,12 @@ def launch_cost(name, a):
         B, m, n, c = a[6:10]
         elu = a[4] is not None
         return 0.0, f4 * B * c * (n + m * (2 if elu else 1)), None
+    if name == "cfsd_spiral_conv_fwd_in_swap":  # the swap + the xyz input conv (spiral length 9)
+        bs, vs, rows, ci, co = a[4], a[14], a[15], a[16], a[17]
+        B, S = bs * bs, 9
+        return (2.0 * B * rows * S * ci * co,
+                f4 * (bs * vs * ci + B * vs * ci) + vs + sz(a[13]) * B * rows * co + f4 * co * S * ci + 4 * rows * S,
+                FP32_PEAK_TFLOPS)
     if name in ("cfsd_swap_features", "cfsd_swap_features_x"):
         bs, nv, c = a[5:8] if name == "cfsd_swap_features" else a[6:9]
         return 0.0, f4 * (bs * nv * c + bs * bs * nv * c) + nv, None

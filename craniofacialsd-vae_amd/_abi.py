@@ -77,6 +77,8 @@ SIGNATURES = {
     "cfsd_loss_finalize": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P]),
     "cfsd_adam": (_I, [_P, _P, _P, _P, _P, _Z, _F, _F, _F, _F, _F, _P, _P]),
     "cfsd_adam_scaled": (_I, [_P, _P, _P, _P, _P, _Z, _F, _F, _F, _F, _F, _F, _P, _P]),
+    "cfsd_spiral_conv_fwd_in_swap": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I,
+                                          _I, _P]),
     "cfsd_bottleneck_bwd": (_I, [_P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _I,
                                  _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
     "cfsd_spiral_conv_fwd_x": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

@@ -242,6 +242,27 @@ inline int resident_blocks_of(K kernel, int block_threads, size_t dyn_lds) {
   return resident_blocks(reinterpret_cast<const void*>(kernel), block_threads, dyn_lds);
 }
 
+// The feature swap's source mesh of output mesh ob at vertex v
+// (SwapFeatures, swap_batch_transform.py:13-42): ob = i * bs + j takes mesh
+// batch_idx[j]'s vertex when i != j and v lies in region k's mask, else mesh
+// batch_idx[i]'s.  Range-guarded: a key outside [0, n_regions) swaps nothing,
+// a mesh index outside [0, n_meshes) is clamped (the host validates both).
+struct SwapSrc {
+  const float* data;  // resident set [n_meshes][nv][c], batch-major
+  const int* batch_idx;
+  const unsigned char* mask;  // [n_regions][nv]
+  const int* key;
+  int bs, n_meshes, n_regions;
+};
+__device__ __forceinline__ long swap_src_mesh(const SwapSrc& s, int k, int ob, int v, int nv) {
+  const int i = ob / s.bs, j = ob % s.bs;
+  // both candidates loaded up front: the mask load is the only one the
+  // choice waits on (a gather through the swap is one load deeper, not two)
+  const int bi = s.batch_idx[i], bj = s.batch_idx[j];
+  const bool take = (i != j) && k >= 0 && k < s.n_regions && s.mask[(long)k * nv + v];
+  return min(max(take ? bj : bi, 0), s.n_meshes - 1);
+}
+
 // CUs of the current device (cached).
 int device_cus();
 // Integer tuning knob from the environment (read once per name; unset or

@@ -366,10 +366,8 @@ __global__ __launch_bounds__(256) void swap_k(const float* __restrict__ x,
   if (t >= total) return;
   int ob, v;  // thread t = row t of the output storage (vertex-major: the bs^2 meshes of a vertex adjacent)
   split_row(t, yvm, bs * bs, nv, ob, v);
-  const int i = ob / bs, j = ob % bs;
-  const int k = *key;
-  const bool take = (i != j) && k >= 0 && k < n_regions && mask[(long)k * nv + v];
-  const long src_mesh = min(max(batch_idx[take ? j : i], 0), n_meshes - 1);
+  const SwapSrc sw{x, batch_idx, mask, key, bs, n_meshes, n_regions};
+  const long src_mesh = swap_src_mesh(sw, *key, ob, v, nv);
   const float* src = x + (src_mesh * nv + v) * c;
   float* dst = out + t * c;
   if (c == 3) {  // xyz: one dwordx3 load and store

@@ -306,14 +306,16 @@ __global__ __launch_bounds__(256, CIN == 32 ? 8 : 4) void conv_fwd_out_small(con
 // and keeps the half it feeds to v_mfma_f32_32x32x2_f32 (k-permuted: half h
 // owns k in [h*KH, h*KH + KH)); W^T lives in registers.  Output rows are
 // stored as 128-B coalesced segments.
-template <int CS, int COUT, int ACT, typename TY = float>
-__global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict__ x,
-                                                        const int* __restrict__ idx,
-                                                        const float* __restrict__ w,
-                                                        const float* __restrict__ bias,
-                                                        TY* __restrict__ y, int vsrc, int rows,
-                                                        long total_rows, int batch, int xvm,
-                                                        int yvm) {
+// SWAP: the input is NOT read from x but gathered straight from the
+// resident set through the feature swap (SwapSrc: each neighbour row's
+// source mesh), so the swap and this conv need no order between them
+// (conv_fwd_in_swap runs both as two roles of one launch).
+template <int CS, int COUT, int ACT, typename TY, bool SWAP>
+__device__ __forceinline__ void conv_fwd_in_body(int vb, int nvb, const float* __restrict__ x,
+                                                 const SwapSrc& sw, const int* __restrict__ idx,
+                                                 const float* __restrict__ w, const float* __restrict__ bias,
+                                                 TY* __restrict__ y, int vsrc, int rows, long total_rows,
+                                                 int batch, int xvm, int yvm) {
   constexpr int K = kSeq * CS, KH = (K + 1) / 2, NCT = COUT / 32;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
@@ -329,7 +331,8 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
     }
   }
   const long n_tiles = (total_rows + 31) / 32;
-  for (long tile = (long)blockIdx.x * 4 + wave; tile < n_tiles; tile += (long)gridDim.x * 4) {
+  const int key = SWAP ? *sw.key : 0;
+  for (long tile = (long)vb * 4 + wave; tile < n_tiles; tile += (long)nvb * 4) {
     long m = tile * 32 + i;
     if (m >= total_rows) m = total_rows - 1;
     int b, r;
@@ -340,9 +343,17 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
     const float* xb = x + (long)b * lx.bs * CS;
     const int* ir = idx + (long)r * kSeq;
     float g[2 * KH];
+    if constexpr (SWAP) {
+      long src[kSeq];
 #pragma unroll
-    for (int s = 0; s < kSeq; ++s) {
-      ld_row<CS>(xb + (long)ir[s] * lx.vs * CS, &g[s * CS]);
+      for (int s = 0; s < kSeq; ++s) src[s] = swap_src_mesh(sw, key, b, ir[s], vsrc);
+#pragma unroll
+      for (int s = 0; s < kSeq; ++s) ld_row<CS>(sw.data + (src[s] * vsrc + ir[s]) * CS, &g[s * CS]);
+    } else {
+#pragma unroll
+      for (int s = 0; s < kSeq; ++s) {
+        ld_row<CS>(xb + (long)ir[s] * lx.vs * CS, &g[s * CS]);
+      }
     }
 #pragma unroll
     for (int k = K; k < 2 * KH; ++k) g[k] = 0.f;
@@ -372,6 +383,44 @@ __global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict_
         }
       }
   }
+}
+template <int CS, int COUT, int ACT, typename TY = float>
+__global__ __launch_bounds__(256) void conv_fwd_in_mfma(const float* __restrict__ x,
+                                                        const int* __restrict__ idx,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bias,
+                                                        TY* __restrict__ y, int vsrc, int rows,
+                                                        long total_rows, int batch, int xvm,
+                                                        int yvm) {
+  conv_fwd_in_body<CS, COUT, ACT, TY, false>(blockIdx.x, gridDim.x, x, SwapSrc{}, idx, w, bias, y, vsrc, rows,
+                                             total_rows, batch, xvm, yvm);
+}
+
+// The feature swap (swap_k: x = the swapped batch, every vertex) and the
+// first Enblock's conv (gathering through the swap from the resident set)
+// as two independent roles of ONE launch: workgroups [0, n_conv) the conv,
+// the rest one swap row per thread.  Same values as swap_features + the
+// conv launch (the conv's inputs are the same copies).
+template <int CS, int COUT, int ACT, typename TY>
+__global__ __launch_bounds__(256) void conv_fwd_in_swap(const SwapSrc sw, float* __restrict__ x, int n_conv,
+                                                        long swap_total, const int* __restrict__ idx,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bias, TY* __restrict__ y,
+                                                        int vsrc, int rows, long total_rows, int batch,
+                                                        int xvm, int yvm) {
+  if ((int)blockIdx.x < n_conv) {
+    conv_fwd_in_body<CS, COUT, ACT, TY, true>(blockIdx.x, n_conv, x, sw, idx, w, bias, y, vsrc, rows, total_rows,
+                                              batch, xvm, yvm);
+    return;
+  }
+  const long t = (long)((int)blockIdx.x - n_conv) * blockDim.x + threadIdx.x;
+  if (t >= swap_total) return;
+  int ob, v;  // row t of x's storage
+  split_row(t, xvm, batch, vsrc, ob, v);
+  const long src_mesh = swap_src_mesh(sw, *sw.key, ob, v, vsrc);
+  float r3[CS];
+  ld_row<CS>(sw.data + (src_mesh * vsrc + v) * CS, r3);
+  st_row<CS>(x + t * CS, r3);
 }
 
 // ==========================================================================
@@ -2928,6 +2977,50 @@ static bool dt_ok(int dt) {
   return (dt & ~(CFSD_VM | 0xf)) == 0 && (CFSD_DT_TYPE(dt) == CFSD_DT_F32 || CFSD_DT_TYPE(dt) == CFSD_DT_BF16);
 }
 static int vm_of(int dt) { return (dt & CFSD_VM) != 0; }
+
+extern "C" int cfsd_spiral_conv_fwd_in_swap(const float* data, const int32_t* batch_idx,
+                                            const uint8_t* region_mask, const int32_t* key, int bs, int n_meshes,
+                                            int n_regions, float* x, int x_dt, const int32_t* idx, const float* w,
+                                            const float* bias, void* y, int y_dt, int vsrc, int rows, int cin,
+                                            int cout, int act, void* stream) {
+  if (!data || !batch_idx || !region_mask || !key || !x || !idx || !w || !y)
+    return set_error(CFSD_EINVAL, "spiral_conv_fwd_in_swap: null pointer");
+  if (bs <= 0 || n_meshes <= 0 || n_regions <= 0 || vsrc <= 0 || rows <= 0)
+    return set_error(CFSD_EINVAL, "spiral_conv_fwd_in_swap: bad sizes");
+  if (cin != 3 || (cout != 32 && cout != 64))
+    return set_error(CFSD_EINVAL, "spiral_conv_fwd_in_swap: the xyz input conv (3 -> 32/64) only");
+  if (act != CFSD_ACT_NONE && act != CFSD_ACT_ELU) return set_error(CFSD_EINVAL, "bad act %d", act);
+  if (!dt_ok(x_dt) || !dt_ok(y_dt) || CFSD_DT_TYPE(x_dt) != CFSD_DT_F32)
+    return set_error(CFSD_EINVAL, "spiral_conv_fwd_in_swap: fp32 x, fp32 or bf16 y");
+  const int batch = bs * bs;
+  const long M = (long)batch * rows, swap_total = (long)batch * vsrc;
+  if (swap_total >= (1L << 31)) return set_error(CFSD_EINVAL, "spiral_conv_fwd_in_swap: bs^2 x nv >= 2^31");
+  const int xvm = vm_of(x_dt), yvm = vm_of(y_dt);
+  const SwapSrc sw{data, batch_idx, region_mask, key, bs, n_meshes, n_regions};
+  const long tiles = (M + 31) / 32;
+  const int n_conv = (int)((tiles + 3) / 4 < 2048 ? (tiles + 3) / 4 : 2048);
+  const dim3 grid((unsigned)(n_conv + (swap_total + 255) / 256));
+  const hipStream_t st = (hipStream_t)stream;
+  const bool ybf = CFSD_DT_TYPE(y_dt) == CFSD_DT_BF16;
+#define FSW(CO_, ACT_, TY_)                                                                                 \
+  hipLaunchKernelGGL((conv_fwd_in_swap<3, CO_, ACT_, TY_>), grid, dim3(256), 0, st, sw, x, n_conv, swap_total, \
+                     idx, w, bias, (TY_*)y, vsrc, rows, M, batch, xvm, yvm)
+  if (cout == 32) {
+    if (act == CFSD_ACT_ELU) {
+      if (ybf) FSW(32, CFSD_ACT_ELU, bf16_t); else FSW(32, CFSD_ACT_ELU, float);
+    } else {
+      if (ybf) FSW(32, CFSD_ACT_NONE, bf16_t); else FSW(32, CFSD_ACT_NONE, float);
+    }
+  } else {
+    if (act == CFSD_ACT_ELU) {
+      if (ybf) FSW(64, CFSD_ACT_ELU, bf16_t); else FSW(64, CFSD_ACT_ELU, float);
+    } else {
+      if (ybf) FSW(64, CFSD_ACT_NONE, bf16_t); else FSW(64, CFSD_ACT_NONE, float);
+    }
+  }
+#undef FSW
+  return launch_status("spiral_conv_fwd_in_swap");
+}
 
 extern "C" int cfsd_spiral_conv_fwd_x(const void* x, int x_dt, const int32_t* idx, const float* w,
                                       const uint16_t* w_bf16, const float* bias, void* y, int y_dt,

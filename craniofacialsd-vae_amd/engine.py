@@ -191,6 +191,8 @@ class SDVAEEngine:
         # the bottleneck backward (coarsest Pool(up)^T, decoder Linear, latent
         # head, encoder Linear) as one launch (cfsd_bottleneck_bwd)
         self.fuse_bottleneck = os.environ.get("CFSD_FUSE_BOTTLENECK", "1") != "0"
+        # the feature swap and the first Enblock's conv as one launch (cfsd_spiral_conv_fwd_in_swap)
+        self.fuse_swap = os.environ.get("CFSD_FUSE_SWAP", "1") != "0"
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -558,9 +560,13 @@ class SDVAEEngine:
         """Enblocks + stacked mu/logvar Linear (model.py:146-160)."""
         T, S = self.topo, self.spec
         h = b.x
+        swap_from, b.swap_from = getattr(b, "swap_from", None), None
         for (cin, cout, lv) in S.enc_layers():
             w, bias = self._enc_w(lv)
-            if T.enc_select[lv]:
+            if lv == 0 and swap_from is not None:  # feature swap + this conv in one launch
+                ops.spiral_conv_fwd_in_swap(swap_from, b.batch_idx, T.region_mask, b.key, self.swap_bs, b.x,
+                                            T.enc_rows[0], w, bias, ACT_ELU, b.enc_out[0])
+            elif T.enc_select[lv]:
                 self._conv_fwd(b, h, T.enc_rows[lv], f"en_layers.{lv}.conv.layer", ACT_ELU, b.enc_out[lv])
             else:
                 ops.spiral_conv_fwd(h, T.spiral[lv], w, bias, ACT_ELU, out=b.enc_full[lv],
@@ -1035,10 +1041,22 @@ class SDVAEEngine:
     def load_batch(self, b, data):
         """The step's input from the picked base meshes: the on-device feature
         swap (bs -> bs^2) or, with ``swap_features`` False, the bs meshes."""
-        if self.swap:
+        b.swap_from = None
+        if self.swap and self._swap_in_conv_ok(b, data):
+            b.swap_from = data.meshes  # the swap rides in the first Enblock's conv launch (encode)
+        elif self.swap:
             ops.swap_features(data.meshes, b.batch_idx, self.topo.region_mask, b.key, self.swap_bs, out=b.x)
         else:
             ops.gather_meshes(data.meshes, b.batch_idx, self.swap_bs, out=b.x)
+
+    def _swap_in_conv_ok(self, b, data):
+        """cfsd_spiral_conv_fwd_in_swap applies: the first Enblock is the xyz
+        conv evaluated at its kept rows (3 -> 32/64), fp32 input meshes."""
+        S, T = self.spec, self.topo
+        cin, cout, lv = S.enc_layers()[0]
+        return (self.fuse_swap and lv == 0 and cin == 3 and cout in (32, 64) and T.enc_select[0]
+                and data.meshes.dtype == torch.float32 and data.meshes.shape[2] == 3
+                and b.x.dtype == torch.float32 and b.bsz == self.swap_bs ** 2)
 
 
 class ResidentData:

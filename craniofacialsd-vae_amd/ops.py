@@ -500,6 +500,31 @@ def swap_features(x_all, batch_idx, region_mask, key, bs, out=None):
     return y
 
 
+def spiral_conv_fwd_in_swap(x_all, batch_idx, region_mask, key, bs, x_out, idx, w, bias, act, out):
+    """:func:`swap_features` into ``x_out`` and the xyz input conv of the first
+    Enblock (``out`` = act(conv(x_out)) at the rows of ``idx``) in one launch
+    (``cfsd_spiral_conv_fwd_in_swap``): the conv gathers through the swap
+    straight from ``x_all``.  ``x_out`` fp32, either layout; ``out`` fp32 or
+    bf16, either layout."""
+    n_meshes, nv, c = x_all.shape
+    rows, seq = idx.shape
+    cout = w.shape[0]
+    _need(x_all, None, name="x_all")
+    _need(batch_idx, (bs,), torch.int32, "batch_idx")
+    if region_mask is None or region_mask.dim() != 2:
+        raise ValueError("region_mask [n_regions, nv] is required")
+    _need(region_mask, (region_mask.shape[0], nv), torch.uint8, "region_mask")
+    _need(key, (1,), torch.int32, "key")
+    _needl(x_out, (bs * bs, nv, c), "x_out", torch.float32)
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(w, (cout, seq * c), name="w")
+    _needl(out, (bs * bs, rows, cout), "out", out.dtype)
+    call("cfsd_spiral_conv_fwd_in_swap", ptr(x_all), ptr(batch_idx), ptr(region_mask), ptr(key), bs, n_meshes,
+         int(region_mask.shape[0]), ptr(x_out), _st(x_out), ptr(idx), ptr(w), ptr(bias), ptr(out), _st(out), nv, rows,
+         c, cout, int(act), stream_ptr())
+    return out
+
+
 def spiral_conv_fwd_up_supported(bsz, rows, seq, cin, cout):
     return bool(_abi.lib().cfsd_spiral_conv_fwd_up_supported(bsz, rows, seq, cin, cout))
 

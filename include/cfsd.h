@@ -209,6 +209,18 @@ int cfsd_spiral_conv_bwd_rowsub(const float* x, const int32_t* idx, const float*
                                 const float* elu_y, float* dx, float* dw, float* db,
                                 float* workspace, size_t workspace_bytes, int batch, int vsrc,
                                 int rows, int seq, int cin, int cout, void* stream);
+/* The feature swap (cfsd_swap_features_x: x = the swapped batch of bs^2
+ * meshes from the resident set `data` [n_meshes][vsrc][3], in x_dt's layout)
+ * and the first Enblock's xyz conv (cfsd_spiral_conv_fwd_x with cin = 3:
+ * y = act(conv(x)) at the `rows` rows of idx) in ONE launch (ABI 4.9): the
+ * conv gathers its inputs through the swap straight from `data`, so the two
+ * are independent roles of the launch.  Same values as the two launches.
+ * x fp32; y fp32 or bf16; cout 32 or 64. */
+int cfsd_spiral_conv_fwd_in_swap(const float* data, const int32_t* batch_idx, const uint8_t* region_mask,
+                                 const int32_t* key, int bs, int n_meshes, int n_regions, float* x, int x_dt,
+                                 const int32_t* idx, const float* w, const float* bias, void* y, int y_dt,
+                                 int vsrc, int rows, int cin, int cout, int act, void* stream);
+
 /* The same with the source level's layout (ABI 4.4): x_dt = CFSD_DT_F32
  * [| CFSD_VM] describes x, dx and elu_y (the fp32 step's E1 reads and writes
  * the vertex-major level-1 tensors); dpre stays batch-major fp32.  Few-row

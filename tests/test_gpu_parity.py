@@ -530,6 +530,33 @@ def test_fused_bottleneck_matches_four_launches(dtopo, precision, vertex_major):
         assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("precision,vertex_major", [("fp32", True), ("fp32", False), ("bf16", True)])
+def test_swap_in_first_conv_matches_two_launches(dtopo, precision, vertex_major):
+    """cfsd_spiral_conv_fwd_in_swap (ABI 4.9: the feature swap and the first
+    Enblock's xyz conv as two roles of one launch, the conv gathering through
+    the swap from the resident set) == swap_features + the conv launch, bit
+    for bit over two resident-data training steps: the swapped batch, the
+    first Enblock's output, parameters and gradients."""
+    from craniofacialsd_vae_amd.step import TrainStep
+    data_meshes = torch.from_numpy(recipe.normalized_meshes(12)).to(DEV)
+    outs = []
+    for fused in (False, True):
+        eng = make_engine(dtopo, recipe.golden_weights(), precision=precision, vertex_major=vertex_major)
+        eng.fuse_swap = fused
+        data = E.ResidentData(data_meshes.clone(), bs=4, shuffle=True)
+        ts = TrainStep(eng, data)
+        assert eng._swap_in_conv_ok(ts.b, data) == fused
+        for _ in range(2):
+            ts.step()
+        torch.cuda.synchronize()
+        grads = eng.grads()
+        outs.append([ts.b.x.cpu().clone(), ts.b.enc_out[0].float().cpu()]
+                    + [v.cpu().clone() for v in eng.state_dict().values()] + [grads[k].cpu().clone() for k in grads])
+    assert len(outs[0]) == len(outs[1])
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+
+
 @pytest.mark.parametrize("is_vae,select,sigmoid", [(1, True, 0), (0, True, 1), (1, False, 0)])
 def test_bottleneck_bwd_op_vs_separate(is_vae, select, sigmoid):
     """The op on random operands (batch 16, the craniofacial bottleneck: 267

@@ -6,7 +6,7 @@ import sys
 c = sqlite3.connect(sys.argv[1])
 back = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 rows = c.execute("select name, start, end from kernels order by start").fetchall()
-idx = [i for i, r in enumerate(rows) if "swap_k" in r[0]]
+idx = [i for i, r in enumerate(rows) if "swap_k" in r[0] or "conv_fwd_in_swap" in r[0]]  # the step's first kernel
 i0, i1 = idx[-back], idx[-back + 1]
 t0 = rows[i0][1]
 busy = 0

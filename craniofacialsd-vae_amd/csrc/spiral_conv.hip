@@ -1054,8 +1054,9 @@ __global__ __launch_bounds__(256) void conv_dw_lat(const float* __restrict__ x,
                                                    float* __restrict__ ws_db, int vsrc, int rows,
                                                    int total_rows, int rchunk, int n_chunks, int batch,
                                                    int xvm, int dpvm) {
+  __shared__ float red[lat_red_floats(4)];
   conv_dw_lat_body<CIN, COUT>(blockIdx.x, gridDim.x, x, idx, dpre, ws, ws_db, vsrc, rows,
-                              total_rows, rchunk, n_chunks, batch, xvm, dpvm);
+                              total_rows, rchunk, n_chunks, batch, xvm, dpvm, red);
 }
 
 // Both gradients of one coarse-level conv in ONE launch (horizontal fusion):
@@ -1093,12 +1094,13 @@ __global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, cons
     is_dx = a.nb > d.nb;
     vb = bid - both + both / 2;
   }
+  __shared__ float red[lat_red_floats(4)];
   if (is_dx)
     conv_dx_lat_body<CIN, COUT, CTW>(vb, a.nb, a.dpre, a.inv_ptr, a.inv_row, a.inv_head, a.w,
                                      a.elu_y, a.dx, a.vsrc, a.rows, a.total_rows);
   else
     conv_dw_lat_body<CIN, COUT>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows,
-                                d.total_rows, d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm);
+                                d.total_rows, d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm, red);
 }
 
 // ==========================================================================
@@ -1198,6 +1200,7 @@ __device__ __forceinline__ void conv_dg_body(int vb, int vnb, const DgArgs& g, f
 template <int CIN, int COUT>
 __global__ __launch_bounds__(256) void conv_bwd_rowsub_pair(const DgArgs a, const DwLatArgs d) {
   extern __shared__ float wl[];
+  __shared__ float red[lat_red_floats(4)];
   const int bid = blockIdx.x, both = 2 * min(a.nb, d.nb);
   bool is_dg;
   int vb;
@@ -1212,7 +1215,7 @@ __global__ __launch_bounds__(256) void conv_bwd_rowsub_pair(const DgArgs a, cons
     conv_dg_body<CIN, COUT>(vb, a.nb, a, wl);
   else
     conv_dw_lat_body<CIN, COUT>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows,
-                                d.total_rows, d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm);
+                                d.total_rows, d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm, red);
 }
 
 // (2): a thread per (source row, 16-B channel chunk); the row's flat list
@@ -2505,7 +2508,7 @@ static int dw_f32(const float* x, int xvm, const int32_t* idx, const float* dpre
   const dim3 rg((unsigned)((n_el + 63) / 64));
   if (g.kind == kDwLat) {
     float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
-    const long tasks = (long)g.gx * (long)dw_units(cin, cout);
+    const long tasks = lat_tasks(g.gx, dw_units(cin, cout));
 #define DWL(CIN_, COUT_)                                                                        \
   if (cin == CIN_ && cout == COUT_) {                                                           \
     hipLaunchKernelGGL((conv_dw_lat<CIN_, COUT_>), dim3((unsigned)((tasks + 3) / 4)), dim3(256), \
@@ -2514,7 +2517,7 @@ static int dw_f32(const float* x, int xvm, const int32_t* idx, const float* dpre
     rc = launch_status("spiral_conv_bwd_weight_lat");                                           \
     if (rc || deferred) return rc;                                                              \
     hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), rg, dim3(1024), 0, st, workspace, ws_db,  \
-                       dw, db, g.gx);                                                           \
+                       dw, db, lat_slabs(g.gx));                                                \
     return launch_status("spiral_conv_bwd_weight_reduce");                                      \
   }
     DWL(32, 32) DWL(32, 64) DWL(64, 32) DWL(64, 64)
@@ -2671,13 +2674,13 @@ extern "C" int cfsd_spiral_conv_bwd_side(const float* x, const int32_t* idx, con
     const coarse::DxKsArgs a{dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, batch,
                              (long)batch * vsrc};
     const DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, batch * rows, g.rchunk, g.gx, 0, batch, 0, 0};
-    rc = coarse::launch_bwd_ks_pair(a, d, (long)g.gx * dw_units(cin, cout), cin, cout, st);
+    rc = coarse::launch_bwd_ks_pair(a, d, lat_tasks(g.gx, dw_units(cin, cout)), cin, cout, st);
     if (rc || !dw) return rc;
     const int n_el = cout * kSeq * cin + cout;
 #define KSR(CIN_, COUT_)                                                                             \
   if (cin == CIN_ && cout == COUT_) {                                                                \
     hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), dim3((unsigned)((n_el + 63) / 64)), dim3(1024), 0, st, \
-                       workspace, ws_db, dw, db, g.gx);                                              \
+                       workspace, ws_db, dw, db, lat_slabs(g.gx));                                   \
     return launch_status("spiral_conv_bwd_weight_reduce");                                           \
   }
     KSR(32, 32) KSR(32, 64) KSR(64, 32) KSR(64, 64)
@@ -2686,7 +2689,7 @@ extern "C" int cfsd_spiral_conv_bwd_side(const float* x, const int32_t* idx, con
   if (dx && bwd_paired(batch, vsrc, rows, cin, cout)) {
     const DwGeom g = dw_geom(batch, rows, cin, cout);
     const long M = (long)batch * vsrc;
-    const long dw_tasks = (long)g.gx * dw_units(cin, cout);
+    const long dw_tasks = lat_tasks(g.gx, dw_units(cin, cout));
     float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
     DxLatArgs a{dpre, inv_ptr, inv_row, (const int4*)inv_head, w, elu_y, dx, vsrc, rows, M, 0};
     DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, batch * rows, g.rchunk, g.gx,
@@ -2701,7 +2704,7 @@ extern "C" int cfsd_spiral_conv_bwd_side(const float* x, const int32_t* idx, con
     rc = launch_status("spiral_conv_bwd_lat_pair");                                             \
     if (rc || !dw) return rc;                                                                   \
     hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), dim3((unsigned)((n_el + 63) / 64)),        \
-                       dim3(1024), 0, st, workspace, ws_db, dw, db, g.gx);                      \
+                       dim3(1024), 0, st, workspace, ws_db, dw, db, lat_slabs(g.gx));           \
     return launch_status("spiral_conv_bwd_weight_reduce");                                      \
   }
     PAIR(32, 32, 1) PAIR(32, 32, 2) PAIR(64, 32, 1) PAIR(64, 32, 2)
@@ -2821,7 +2824,7 @@ static int bwd_rowsub(const float* x, int xvm, const int32_t* idx, const float* 
   const bool lat = g.kind == kDwLat;
   float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
   DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, total, g.rchunk, g.gx, 0, batch, xvm, 0};
-  if (lat) d.nb = (int)(((long)g.gx * (long)dw_units(cin, cout) + 3) / 4);
+  if (lat) d.nb = (int)((lat_tasks(g.gx, dw_units(cin, cout)) + 3) / 4);
   if (xvm && !lat) return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_x: vertex-major x needs a few-row layer");
   const int n_el = cout * kSeq * cin + cout;
   if (lat && batch % 16 == 0 && cin == 32 && cout == 32 && (flat_width == 8 || flat_width == 12 || flat_width == 16)) {
@@ -2833,12 +2836,12 @@ static int bwd_rowsub(const float* x, int xvm, const int32_t* idx, const float* 
     // dx sums each entry's MFMA products into one accumulator (the dG path
     // rounds every dG element first): equal to fp32 rounding, not bit for bit.
     rc = vm32::launch_bwd_flat_pair(dpre, inv_flat, flat_width, w, elu_y, dx, xvm, vsrc, rows, batch, cin, cout,
-                                    d, (long)g.gx * (long)dw_units(cin, cout), st);
+                                    d, lat_tasks(g.gx, dw_units(cin, cout)), st);
     if (rc || !dw) return rc;
 #define RSR(CIN_, COUT_)                                                                          \
     if (cin == CIN_ && cout == COUT_)                                                             \
       hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), dim3((unsigned)((n_el + 63) / 64)),       \
-                         dim3(1024), 0, st, workspace, ws_db, dw, db, g.gx);
+                         dim3(1024), 0, st, workspace, ws_db, dw, db, lat_slabs(g.gx));
     RSR(32, 32) RSR(32, 64)
 #undef RSR
     return launch_status("spiral_conv_bwd_rowsub_reduce");
@@ -2851,7 +2854,7 @@ static int bwd_rowsub(const float* x, int xvm, const int32_t* idx, const float* 
     rc = launch_status("spiral_conv_bwd_rowsub_pair");                                           \
     if (!rc && lat && dw)                                                                         \
       hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), dim3((unsigned)((n_el + 63) / 64)),       \
-                         dim3(1024), 0, st, workspace, ws_db, dw, db, g.gx);                      \
+                         dim3(1024), 0, st, workspace, ws_db, dw, db, lat_slabs(g.gx));           \
   }
   RSP(32, 32) RSP(32, 64)
 #undef RSP
@@ -3354,7 +3357,7 @@ static int fill_red_item(const cfsd_dw_slabs& q, int i, Item& d) {
       const int U = (int)dw_units(q.cin, q.cout);
       d.kind = 0;
       const bool vm = q.fused == 3 && dw_vm32_path(1, 1, q.cin, q.cout, q.batch);  // as dw_f32 chose
-      d.n_slabs = g.kind == kDwLat ? g.gx
+      d.n_slabs = g.kind == kDwLat ? lat_slabs(g.gx)
                   : vm             ? vm32::dw_slabs(q.batch, q.rows, g.gx)
                                    : dw_mfma_slabs(q.cin, q.cout, g.gx);
       d.n_el = U * 1024 + q.cout;

@@ -295,12 +295,13 @@ __device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
+template <int CIN, int NSG, int RT>
+__host__ __device__ constexpr int dx_ks_lds_f4() { return NSG * RT * 16 * (CIN + 4) / 4; }
 template <int CIN, int COUT, int NSG, int RT>
-__device__ __forceinline__ void conv_dx_ks_body(int vb, int vnb, const DxKsArgs& a) {
+__device__ __forceinline__ void conv_dx_ks_body(int vb, int vnb, const DxKsArgs& a, f32x4* part4) {
   constexpr int CHO = COUT / 16, NCT = CIN / 16, K = kSeq * CIN, SPW = kSeq / NSG;
   constexpr int LDC = CIN + 4, RB = COUT * (int)sizeof(float);
   static_assert(kSeq % NSG == 0, "slot groups");
-  __shared__ f32x4 part4[NSG * RT * 16 * LDC / 4];
   float* part = reinterpret_cast<float*>(part4);
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -404,7 +405,8 @@ __device__ __forceinline__ void conv_dx_ks_body(int vb, int vnb, const DxKsArgs&
 }
 template <int CIN, int COUT, int NSG, int RT>
 __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_dx_ks(const DxKsArgs a) {
-  conv_dx_ks_body<CIN, COUT, NSG, RT>(blockIdx.x, gridDim.x, a);
+  __shared__ f32x4 part4[dx_ks_lds_f4<CIN, NSG, RT>()];
+  conv_dx_ks_body<CIN, COUT, NSG, RT>(blockIdx.x, gridDim.x, a, part4);
 }
 
 // The data gradient and the weight-gradient slabs of one coarse conv in ONE
@@ -424,11 +426,14 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_bwd_ks_p
     is_dx = nb_dx > d.nb;
     vb = bid - both + both / 2;
   }
+  // one LDS array for both roles (the dW role's chunk-group sums alias the dx partials)
+  __shared__ f32x4 part4[dx_ks_lds_f4<CIN, NSG, RT>()];
+  static_assert(dx_ks_lds_f4<CIN, NSG, RT>() * 4 >= lat_red_floats(NSG), "dW chunk-group LDS");
   if (is_dx)
-    conv_dx_ks_body<CIN, COUT, NSG, RT>(vb, nb_dx, a);
+    conv_dx_ks_body<CIN, COUT, NSG, RT>(vb, nb_dx, a, part4);
   else
     conv_dw_lat_body<CIN, COUT, NSG>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows, d.total_rows,
-                                     d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm);
+                                     d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm, reinterpret_cast<float*>(part4));
 }
 
 // ------------------------------------------------------------------ host side
@@ -495,7 +500,7 @@ int launch_bwd_ks_pair(const DxKsArgs& a, const DwLatArgs& d0, long dw_tasks, in
   const long n_rt = (a.total_rows + 15) / 16;
   const int nb_dx = (int)((n_rt + 1) / 2);
   DwLatArgs d = d0;
-  d.nb = (int)((dw_tasks + 8) / 9);
+  d.nb = (int)((dw_tasks + 7) / 8);  // waves 0-7 of each 9-wave workgroup (whole chunk groups)
 #define SHAPE(CI_, CO_)                                                                                   \
   if (cin == CI_ && cout == CO_) {                                                                        \
     hipLaunchKernelGGL((conv_bwd_ks_pair<CI_, CO_, 9, 2>), dim3((unsigned)(nb_dx + d.nb)), dim3(576), 0, st, a, \

@@ -301,7 +301,7 @@ __global__ __launch_bounds__(512) void conv_bwd_flat_pair(const DxFlatArgs a, co
                                 a.nb, lwt);
   else
     conv_dw_lat_body<CIN, COUT, 8>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows, d.total_rows,
-                                   d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm);
+                                   d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm, lwt);  // lwt >= lat_red_floats(8)
 }
 
 

@@ -785,15 +785,15 @@ static int dxf_t(const float* dpre, int dpvm, int dxvm, const int* flat, const f
 }
 
 template <int CIN, int COUT, int FW>
-static int pair_t(const float* dpre, const int* flat, const float* w, const float* elu_y, float* dx, int dxvm,
-                  int vsrc, int rows, int batch, DwLatArgs d, long dw_tasks, hipStream_t st) {
+static int pair_t(const float* dpre, int dpvm, const int* flat, const float* w, const float* elu_y, float* dx,
+                  int dxvm, int vsrc, int rows, int batch, DwLatArgs d, long dw_tasks, hipStream_t st) {
   constexpr size_t lds = (size_t)kS * CIN * (COUT + 8) * sizeof(float);
   auto kern = conv_bwd_flat_pair<CIN, COUT, FW>;
   const long tiles = (long)vsrc * (batch / 16);
   d.nb = (int)((dw_tasks + 7) / 8);
   const int res = resident(kern, 512, lds);
-  const DxFlatArgs a{dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows, batch, 0, dxvm,
-                     (int)balanced_blocks(tiles, 8, res > d.nb ? res - d.nb : 8)};
+  const DxFlatArgs a{dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows, batch, dpvm, dxvm,
+                     (int)balanced_blocks(tiles, 8, res - d.nb > res / 2 ? res - d.nb : res / 2)};
   hipLaunchKernelGGL(kern, dim3((unsigned)(a.nb + d.nb)), dim3(512), lds, st, a, d);
   return launch_status("spiral_conv_bwd_flat_pair");
 }
@@ -807,11 +807,22 @@ int launch_bwd_flat_pair(const float* dpre, const int* flat, int width, const fl
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub (vertex-major): dpre exceeds 32-bit buffer offsets");
 #define BP(CO, FW_)                                                                                         \
   if (cout == CO && width == FW_)                                                                           \
-    return pair_t<32, CO, FW_>(dpre, flat, w, elu_y, dx, dxvm, vsrc, rows, batch, d, dw_tasks, st);
+    return pair_t<32, CO, FW_>(dpre, 0, flat, w, elu_y, dx, dxvm, vsrc, rows, batch, d, dw_tasks, st);
   BP(32, 8) BP(32, 12) BP(32, 16)
 #undef BP
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub (vertex-major): unsupported channels %d -> %d / width %d",
                    cin, cout, width);
+}
+
+int launch_bwd_flat_pair_vm(const float* dpre, const int* flat, int width, const float* w, const float* elu_y,
+                            float* dx, int vsrc, int rows, int batch, const DwLatArgs& d, long dw_tasks,
+                            hipStream_t st) {
+  if (batch % 16) return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair: batch %% 16 != 0");
+#define BV(FW_) \
+  if (width == FW_) return pair_t<32, 32, FW_>(dpre, 1, flat, w, elu_y, dx, 1, vsrc, rows, batch, d, dw_tasks, st);
+  BV(8) BV(12) BV(16) BV(20)
+#undef BV
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair: flat width %d", width);
 }
 
 int launch_dx_flat_b16(const float* dpre, const int* flat, int width, const float* w, const bf16_t* elu_y,

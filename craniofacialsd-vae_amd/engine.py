@@ -193,6 +193,10 @@ class SDVAEEngine:
         self.fuse_bottleneck = os.environ.get("CFSD_FUSE_BOTTLENECK", "1") != "0"
         # the feature swap and the first Enblock's conv as one launch (cfsd_spiral_conv_fwd_in_swap)
         self.fuse_swap = os.environ.get("CFSD_FUSE_SWAP", "1") != "0"
+        # vertex-major levels whose fp32 Deblock backward runs as one dx + dW launch
+        # (cfsd_spiral_conv_bwd_flat_pair); none by default: D2 59.6 vs 20.8 + 19.9 us,
+        # the coarse-geometry dW is one latency chain per 300-row chunk at 68k rows
+        self.vm_pair_levels = {int(c) for c in os.environ.get("CFSD_VM_PAIR_LEVELS", "") if c.isdigit()}
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -471,11 +475,20 @@ class SDVAEEngine:
                 return
             if low:
                 nb = ops.spiral_conv_bwd_weight_x_workspace(bsz, rows, seq, cin, cout, ldt if cin > 3 else torch.float32)
+                if b.vm_pair.get(key):
+                    nb = max(nb, ops.spiral_conv_bwd_flat_pair_workspace(bsz, rows, seq, cin, cout))
             else:
                 nb = (ops.spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout) if b.paired[key]
                       else ops.spiral_conv_bwd_weight_workspace(bsz, rows, seq, cin, cout))
             regions.append((key, nb))
 
+        # fp32 vertex-major Deblocks (levels in vm_pair_levels): dx + dW slabs in one launch
+        b.vm_pair = {}
+        for i, (cin, cout, lv, _) in enumerate(S.dec_layers()):
+            b.vm_pair[("dec", i)] = (lv in lp and lv in self.vm_pair_levels and ldt == torch.float32
+                                     and cin == 32 and cout == 32 and self._flat_dx(b, lv, cin, cout)
+                                     and ops.spiral_conv_bwd_flat_pair_workspace(bsz, nv[lv], T.seq[lv], cin,
+                                                                                 cout) > 0)
         for i, (cin, cout, lv, _) in enumerate(S.dec_layers()):
             dw_region(("dec", i), nv[lv], nv[lv], T.seq[lv], cin, cout, True, lv in lp)
         for (cin, cout, lv) in S.enc_layers():
@@ -746,7 +759,11 @@ class SDVAEEngine:
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]
             w, _ = self._dec_w(i)
-            if lv in b.xl:  # vertex-major (bf16 or fp32) operands: dW slabs + dx
+            if b.vm_pair.get(("dec", i)):  # fp32 vertex-major: flat dx + dW slabs in one launch
+                defer(ops.spiral_conv_bwd_flat_pair(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_flat[lv],
+                                                    w, None, None, b.g_dec_up[i],
+                                                    workspace=b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
+            elif lv in b.xl:  # vertex-major (bf16 or fp32) operands: dW slabs + dx
                 defer(ops.spiral_conv_bwd_weight_x(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
                                                    b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
                 w16 = self._wx(f"de_layers.{i + 1}.conv.layer.weight")

@@ -1060,6 +1060,44 @@ def spiral_conv_bwd_weight_x(x, idx, dpre, dw, db, workspace):
     return None
 
 
+def spiral_conv_bwd_flat_pair_workspace(bsz, rows, seq, cin, cout):
+    return int(_abi.lib().cfsd_spiral_conv_bwd_flat_pair_workspace(bsz, rows, seq, cin, cout))
+
+
+def spiral_conv_bwd_flat_pair(x, idx, dpre, flat, w, dw, db, dx, elu_y=None, workspace=None):
+    """Both gradients of a full 32 -> 32 conv whose x, dpre, dx (and elu_y)
+    are all vertex-major fp32 (the fp32 step's level-0/1 Deblocks) in ONE
+    launch (``cfsd_spiral_conv_bwd_flat_pair``, ABI 4.10): the flat-list dx
+    of :func:`spiral_conv_bwd_data_flat` and coarse-geometry dW slabs.
+    ``dw is db is None`` defers the reduction (returns a DeferredDw)."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = dpre.shape[2]
+    table, width = flat
+    for t, nm, shp in ((x, "x", (bsz, vsrc, cin)), (dpre, "dpre", (bsz, rows, cout)), (dx, "dx", (bsz, vsrc, cin))):
+        _needl(t, shp, nm, torch.float32)
+        if not is_vm(t):
+            raise ValueError(f"spiral_conv_bwd_flat_pair: {nm} must be vertex-major")
+    if elu_y is not None:
+        _needl(elu_y, (bsz, vsrc, cin), "elu_y", torch.float32)
+        _same_layout(dx, elu_y, "dx and elu_y")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(table, (vsrc, width), torch.int32, "inv_flat")
+    _need(w, (cout, seq * cin), torch.float32, "w")
+    if dw is not None or db is not None:
+        _need(dw, (cout, seq * cin), name="dw")
+        _need(db, (cout,), name="db")
+    need = spiral_conv_bwd_flat_pair_workspace(bsz, rows, seq, cin, cout)
+    if need == 0:
+        raise ValueError(f"no vertex-major pair for {cin} -> {cout} channels")
+    ws, nb = _conv_ws(workspace, x.device, need)
+    call("cfsd_spiral_conv_bwd_flat_pair", ptr(x), ptr(idx), ptr(dpre), ptr(table), width, ptr(w), ptr(elu_y),
+         ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    if dw is None:
+        return DeferredDw(ws, bsz, vsrc, rows, cin, cout, 4)
+    return None
+
+
 def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None):
     """Fused dx + dW of the xyz output conv with bf16 (or fp32) x / elu_y /
     dx in either layout."""

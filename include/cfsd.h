@@ -110,7 +110,8 @@ size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int seq, int c
  * came from cfsd_spiral_conv_bwd(_x) on a small-output layer (cout*seq <= 32);
  * 2: from cfsd_spiral_conv_bwd_weight_x on a 32/64-channel layer (bf16); 3: from
  * cfsd_spiral_conv_bwd_weight_x on a 32 -> 32 fp32 layer with vertex-major x
- * and dpre, batch % 16 == 0 (ABI 4.3). */
+ * and dpre, batch % 16 == 0 (ABI 4.3); 4: from cfsd_spiral_conv_bwd_flat_pair
+ * (ABI 4.10). */
 typedef struct {
   const float* workspace;
   float* dw;
@@ -220,6 +221,21 @@ int cfsd_spiral_conv_fwd_in_swap(const float* data, const int32_t* batch_idx, co
                                  const int32_t* key, int bs, int n_meshes, int n_regions, float* x, int x_dt,
                                  const int32_t* idx, const float* w, const float* bias, void* y, int y_dt,
                                  int vsrc, int rows, int cin, int cout, int act, void* stream);
+/* Both gradients of a full 32 -> 32 SpiralConv (a Deblock conv, model.py:27-41
+ * autograd) with EVERY operand vertex-major fp32 (x, dpre, dx, elu_y:
+ * [vertex][batch][32]), batch % 16 == 0, in ONE launch (ABI 4.10): the
+ * flat-list data gradient of cfsd_spiral_conv_bwd_data_flat (dx = elu'(elu_y)
+ * times the sum over u's flat inverse list, elu_y may be NULL) and the
+ * weight-gradient slabs of the coarse-geometry dW body (one wave per 32x32
+ * unit and row chunk, four chunks summed per slab) as interleaved workgroups.
+ * dw == db == NULL defers (cfsd_dw_reduce_batch item with fused = 4).
+ * inv_flat as cfsd_spiral_conv_bwd_data_flat (flat_width in {8, 12, 16, 20}).
+ * workspace: cfsd_spiral_conv_bwd_flat_pair_workspace() bytes (0 = unsupported). */
+size_t cfsd_spiral_conv_bwd_flat_pair_workspace(int batch, int rows, int seq, int cin, int cout);
+int cfsd_spiral_conv_bwd_flat_pair(const float* x, const int32_t* idx, const float* dpre, const int32_t* inv_flat,
+                                   int flat_width, const float* w, const float* elu_y, float* dx, float* dw,
+                                   float* db, float* workspace, size_t workspace_bytes, int batch, int vsrc,
+                                   int rows, int seq, int cin, int cout, void* stream);
 
 /* The same with the source level's layout (ABI 4.4): x_dt = CFSD_DT_F32
  * [| CFSD_VM] describes x, dx and elu_y (the fp32 step's E1 reads and writes

@@ -162,6 +162,51 @@ def test_dw_vm32(mods, otopo, dtopo, table, level, bsz, cout, dpvm):
     assert torch.equal(dw2, dw) and torch.equal(db2, db)
 
 
+@pytest.mark.parametrize("level,bsz", [(0, 16), (1, 16), (1, 32), (2, 16), (3, 48)])
+@pytest.mark.parametrize("with_elu", [False, True])
+def test_bwd_flat_pair_vm32(mods, otopo, dtopo, level, bsz, with_elu):
+    """cfsd_spiral_conv_bwd_flat_pair (ABI 4.10: flat-list dx + coarse-geometry
+    dW slabs in one launch, every operand vertex-major fp32): dx bit-identical
+    to cfsd_spiral_conv_bwd_data_flat (same body); dW / db vs float64 and vs
+    the vm32 weight-gradient kernel (another summation order) rel 1e-5; the
+    deferred slabs through the batched reduce == the direct reduce; two
+    calls bit-identical (deterministic)."""
+    _, ops, _ = mods
+    g = torch.Generator().manual_seed(level * 5 + bsz + with_elu)
+    idx = dtopo.spiral[level]
+    sp = idx.cpu().numpy()
+    v = dtopo.n_verts[level]
+    x = torch.nn.functional.elu(torch.randn(bsz, v, 32, generator=g))
+    w = torch.randn(32, 288, generator=g) * 0.1
+    dpre = torch.randn(bsz, v, 32, generator=g)
+    gx = gather(x.double(), sp).reshape(bsz * v, -1)
+    dref = dpre.double().reshape(bsz * v, 32)
+    dw_ref, db_ref = dref.T @ gx, dref.sum(0)
+    xv, dpv = ops.to_vm(x.to(DEV)), ops.to_vm(dpre.to(DEV))
+    ey = xv if with_elu else None
+    flat = dtopo.spiral_flat[level]
+    nb = ops.spiral_conv_bwd_flat_pair_workspace(bsz, v, 9, 32, 32)
+    assert nb > 0
+    ws = torch.zeros(nb // 4 + 64, device=DEV)
+    dw, db = torch.empty(32, 288, device=DEV), torch.empty(32, device=DEV)
+    dx = ops.vm_empty(bsz, v, 32, device=DEV)
+    ops.spiral_conv_bwd_flat_pair(xv, idx, dpv, flat, w.to(DEV), dw, db, dx, elu_y=ey, workspace=ws)
+    dx_ref = ops.spiral_conv_bwd_data_flat(dpv, flat, w.to(DEV), v, elu_y=ey)
+    assert torch.equal(dx, dx_ref)
+    assert err_rel_max(dw, dw_ref) <= 1e-5 and err_rel_max(db, db_ref) <= 1e-5
+    nbx = ops.spiral_conv_bwd_weight_x_workspace(bsz, v, 9, 32, 32, torch.float32)
+    wsx = torch.zeros(nbx // 4 + 64, device=DEV)
+    dw_x, db_x = torch.empty_like(dw), torch.empty_like(db)
+    ops.spiral_conv_bwd_weight_x(xv, idx, dpv, dw_x, db_x, wsx)
+    assert err_rel_max(dw, dw_x) <= 1e-5 and err_rel_max(db, db_x) <= 1e-5
+    ws.zero_()
+    dx2 = ops.vm_empty(bsz, v, 32, device=DEV)
+    d = ops.spiral_conv_bwd_flat_pair(xv, idx, dpv, flat, w.to(DEV), None, None, dx2, elu_y=ey, workspace=ws)
+    dw2, db2 = torch.empty_like(dw), torch.empty_like(db)
+    ops.dw_reduce_batch([(d, dw2, db2)])
+    assert torch.equal(dx2, dx) and torch.equal(dw2, dw) and torch.equal(db2, db)
+
+
 def test_xyz_layers_vm32(mods, otopo, dtopo):
     """The xyz input / output layers with fp32 vertex-major 32-channel
     operands: forwards bit-exact to batch-major; the fused output backward's

@@ -32,11 +32,13 @@ int launch_dx_flat_b16(const float* dpre, const int* flat, int width, const floa
 int launch_bwd_flat_pair(const float* dpre, const int* flat, int width, const float* w, const float* elu_y,
                          float* dx, int dxvm, int vsrc, int rows, int batch, int cin, int cout, const DwLatArgs& d,
                          long dw_tasks, hipStream_t st);
-// The same pair for a full (not row-subset) conv with dpre, x, dx and elu_y
-// all vertex-major (fp32 D2 / D3): flat-list dx + lat dW slabs, 32 -> 32.
-int launch_bwd_flat_pair_vm(const float* dpre, const int* flat, int width, const float* w, const float* elu_y,
-                            float* dx, int vsrc, int rows, int batch, const DwLatArgs& d, long dw_tasks,
-                            hipStream_t st);
+// Both gradients of a full (not row-subset) 32 -> 32 conv with dpre, x, dx
+// and elu_y all vertex-major fp32 (the fp32 D2 / D3) in ONE launch: the
+// flat-list dx and the launch_dw slabs (n_slabs = dw_slabs(), same layout and
+// values as launch_dw up to summation order within a slab: bit-identical).
+int launch_bwd_vm_pair(const float* dpre, const int* flat, int width, const float* w, const float* elu_y, float* dx,
+                       const float* x, const int* idx, float* ws, float* ws_db, int n_slabs, int vsrc, int rows,
+                       int batch, hipStream_t st);
 // dW/db slabs (conv_dw_mfma layout: [n_slabs][9][32][32], db [n_slabs][32] at
 // ws_db) of a 32 -> 32 conv, x and dpre vertex-major, batch % 16 == 0.
 // Workgroups (= slabs) launch_dw uses; max_slabs = the workspace's slab capacity.

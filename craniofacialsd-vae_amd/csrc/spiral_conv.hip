@@ -2428,8 +2428,7 @@ int dw_mfma_slabs(int cin, int cout, int gx) {
 }
 
 constexpr int kDwLatWaves = 2048;
-// one wave per (dW unit, row chunk), ~2k waves; no cap on the rows (the
-// vertex-major pair, cfsd_spiral_conv_bwd_flat_pair, uses it on 68k-272k rows)
+// one wave per (dW unit, row chunk), ~2k waves (the few-row layers)
 DwGeom lat_geom(int batch, int rows, int cin, int cout) {
   DwGeom g{kDwLat, 0, 0, 0};
   const long M = (long)batch * rows;
@@ -3189,10 +3188,13 @@ extern "C" int cfsd_spiral_conv_bwd_data_flat(const void* dpre, int dpre_dt, con
                                  (hipStream_t)stream);
 }
 
-// ---- vertex-major pair (ABI 4.10): flat-list dx + coarse-geometry dW slabs in one launch
+// ---- vertex-major pair (ABI 4.10): flat-list dx + vm32 dW slabs in one launch
+static bool vm_pair_shape(int batch, int rows, int cin, int cout) {
+  return cin == 32 && cout == 32 && batch % 16 == 0 && dw_geom(batch, rows, cin, cout).kind == kDwMfma;
+}
 extern "C" size_t cfsd_spiral_conv_bwd_flat_pair_workspace(int batch, int rows, int seq, int cin, int cout) {
-  if (batch <= 0 || rows <= 0 || seq != kSeq || cin != 32 || cout != 32) return 0;
-  return lat_geom(batch, rows, cin, cout).ws_floats * sizeof(float);
+  if (batch <= 0 || rows <= 0 || seq != kSeq || !vm_pair_shape(batch, rows, cin, cout)) return 0;
+  return dw_geom(batch, rows, cin, cout).ws_floats * sizeof(float);
 }
 
 extern "C" int cfsd_spiral_conv_bwd_flat_pair(const float* x, const int32_t* idx, const float* dpre,
@@ -3204,8 +3206,9 @@ extern "C" int cfsd_spiral_conv_bwd_flat_pair(const float* x, const int32_t* idx
   if (rc) return rc;
   if (!inv_flat || !w || !dx || !workspace)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair: null inv_flat / w / dx / workspace");
-  if (cin != 32 || cout != 32 || batch % 16)
-    return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair: 32 -> 32 channels, batch %% 16 == 0 only");
+  if (!vm_pair_shape(batch, rows, cin, cout))
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair: 32 -> 32, batch %% 16 == 0, batch x rows >= %d only",
+                     kLatDwMax);
   if (flat_width <= 0 || flat_width > 20 || flat_width % 4)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair: flat_width %d not in {4, ..., 20}", flat_width);
   if ((uintptr_t)inv_flat & 15) return set_error(CFSD_EINVAL, "inv_flat must be 16-B aligned");
@@ -3216,16 +3219,15 @@ extern "C" int cfsd_spiral_conv_bwd_flat_pair(const float* x, const int32_t* idx
   const size_t need = cfsd_spiral_conv_bwd_flat_pair_workspace(batch, rows, seq, cin, cout);
   if (workspace_bytes < need) return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
   hipStream_t st = (hipStream_t)stream;
-  const DwGeom g = lat_geom(batch, rows, cin, cout);
-  const int U = (int)dw_units(cin, cout);
-  float* ws_db = workspace + (size_t)g.gx * U * 1024;
-  const DwLatArgs d{x, idx, dpre, workspace, ws_db, vsrc, rows, batch * rows, g.rchunk, g.gx, 0, batch, 1, 1};
-  rc = vm32::launch_bwd_flat_pair_vm(dpre, inv_flat, flat_width, w, elu_y, dx, vsrc, rows, batch, d,
-                                     lat_tasks(g.gx, U), st);
+  const DwGeom g = dw_geom(batch, rows, cin, cout);
+  float* ws_db = workspace + (size_t)g.gx * dw_units(cin, cout) * 1024;
+  const int nslab = vm32::dw_slabs(batch, rows, g.gx);  // as cfsd_dw_reduce_batch's fused = 3 items
+  rc = vm32::launch_bwd_vm_pair(dpre, inv_flat, flat_width, w, elu_y, dx, x, idx, workspace, ws_db, nslab, vsrc,
+                                rows, batch, st);
   if (rc || !dw) return rc;
   const int n_el = cout * kSeq * cin + cout;
   hipLaunchKernelGGL((conv_dw_reduce<32, 32>), dim3((unsigned)((n_el + 63) / 64)), dim3(1024), 0, st, workspace,
-                     ws_db, dw, db, lat_slabs(g.gx));
+                     ws_db, dw, db, nslab);
   return launch_status("spiral_conv_bwd_flat_pair_reduce");
 }
 
@@ -3388,17 +3390,6 @@ static int fill_red_item(const cfsd_dw_slabs& q, int i, Item& d) {
   d.cin = q.cin;
   d.cout = q.cout;
   const int K = kSeq * q.cin;
-  if (q.fused == 4) {  // lat slabs of the vertex-major pair (any row count)
-    if (!((q.cin == 32 || q.cin == 64) && (q.cout == 32 || q.cout == 64)))
-      return set_error(CFSD_EINVAL, "dw_reduce_batch: item %d fused 4 needs 32/64 channels", i);
-    const DwGeom g = lat_geom(q.batch, q.rows, q.cin, q.cout);
-    const int U = (int)dw_units(q.cin, q.cout);
-    d.kind = 0;
-    d.n_slabs = lat_slabs(g.gx);
-    d.n_el = U * 1024 + q.cout;
-    d.ws_db = q.workspace + (size_t)g.gx * U * 1024;
-    return CFSD_OK;
-  }
   if (q.fused == 2 && mfma_shape(q.cin, q.cout)) {  // bf16 MFMA dW: plain slabs
     d.kind = 1;
     d.n_slabs = bf::dw_slabs(q.batch, q.rows, q.cin, q.cout);

@@ -163,7 +163,7 @@ constexpr int kVm32DxPd = 2;  // list entries in flight ahead of the one being m
 constexpr int kVm32DxOcc = 1;
 // TY: storage of dx and elu_y (fp32, or bf16 for the bf16 step's E1: the
 // fp32 sum rounded once)
-template <int CIN, int COUT, int FW, typename TY = float>
+template <int CIN, int COUT, int FW, typename TY = float, int WPB = 8>
 __device__ __forceinline__ void dx_flat_body(const float* __restrict__ dpre, const int4* __restrict__ flat,
                                              const float* __restrict__ w, const TY* __restrict__ elu_y,
                                              TY* __restrict__ dx, int vsrc, int rows, int batch, int dpvm,
@@ -185,7 +185,7 @@ __device__ __forceinline__ void dx_flat_body(const float* __restrict__ dpre, con
   // mesh part per lane, row part as the entry's SGPR offset either way
   const int rstride = dpvm ? batch * RB : RB;  // bytes between two rows of one mesh
   const int mstride = dpvm ? RB : rows * RB;   // bytes between two meshes of one row
-  const TileSweep sw = xcd_sweep_v(n_tiles, 8, wave, true, vb, nvb);
+  const TileSweep sw = xcd_sweep_v(n_tiles, WPB, wave, true, vb, nvb);
 
   auto load_list = [&](long tile, int (&pe)[FW]) {
     const int u = uni((int)tile) / G16;
@@ -324,21 +324,26 @@ constexpr int kDwvNs = 3;  // slots per wave (3: a slot group of three, 9: all n
 constexpr int kDwvNr = 4;  // unit ranges per workgroup (waves = NR * 9 / NS)
 constexpr int DWV_NS = kDwvNs, DWV_NR = kDwvNr, DWV_WAVES = DWV_NR * (kS / DWV_NS);
 constexpr int DWV_THREADS = DWV_WAVES * 64;
-__global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restrict__ x,
-                                                            const int* __restrict__ idx,
-                                                            const float* __restrict__ dpre,
-                                                            float* __restrict__ ws, float* __restrict__ ws_db,
-                                                            int vsrc, int rows, int batch) {
+constexpr int DWV_LDS = kS * 1024 + DWV_NR * 64;  // floats: the block's slab image + db partials
+// PF: the next unit's operands loaded during this unit's MFMAs (the dW-only
+// kernel, 125 VGPRs); PF = 0 keeps the body under 80 VGPRs so that two
+// 12-wave workgroups share a CU (conv_bwd_vm_pair).  bid / nb: this
+// workgroup's slab and the slab count; lds: DWV_LDS floats.
+template <int PF>
+__device__ __forceinline__ void dw_vm32_body(const float* __restrict__ x, const int* __restrict__ idx,
+                                             const float* __restrict__ dpre, float* __restrict__ ws,
+                                             float* __restrict__ ws_db, int vsrc, int rows, int batch, int bid,
+                                             int nb, float* __restrict__ lds) {
   constexpr int C = 32, NEL = kS * 1024, NS = DWV_NS, NG = kS / NS;
-  __shared__ float red[NEL];
-  __shared__ float dbl[DWV_NR * 64];
+  float* red = lds;
+  float* dbl = lds + NEL;
   const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
   const int sg = wave % NG, vg = wave / NG;  // slot group, unit range
   const int G16 = batch >> 4;
   const long n_units = (long)rows * G16;
   // XCD-contiguous unit ranges: blocks b, b + 8, ... (one XCD) split one 1/8
-  const int nb = gridDim.x, G = nb < 8 ? nb : 8;
-  const int grp = blockIdx.x % G, lb = blockIdx.x / G, nb_g = (nb - grp + G - 1) / G;
+  const int G = nb < 8 ? nb : 8;
+  const int grp = bid % G, lb = bid / G, nb_g = (nb - grp + G - 1) / G;
   const long per = (n_units + G - 1) / G;
   const long g0 = grp * per, g1 = min(n_units, g0 + per);
   const int nr = nb_g * DWV_NR, ri = lb * DWV_NR + vg;
@@ -372,9 +377,10 @@ __global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restr
         db[k][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff + 256 * j, sx, 0));
     }
   };
-  if (u0 < u1) load_unit(u0, a, b);
+  if (PF && u0 < u1) load_unit(u0, a, b);
   for (long un = u0; un < u1; un += ustep) {
-    const bool more = un + ustep < u1;  // uniform
+    const bool more = PF && un + ustep < u1;  // uniform
+    if (!PF) load_unit(un, a, b);
     if (more) load_unit(un + ustep, an, bn);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
@@ -407,13 +413,54 @@ __global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restr
     }
     __syncthreads();
   }
-  float* slab = ws + (long)blockIdx.x * NEL;
+  float* slab = ws + (long)bid * NEL;
   for (int e = threadIdx.x; e < NEL / 4; e += DWV_THREADS) st4(slab + 4 * e, ld4(red + 4 * e));
   if (threadIdx.x < C) {  // lanes o and o + 32 of each range hold meshes 2j and 2j + 1
     float t = 0.f;
     for (int g = 0; g < DWV_NR; ++g) t += dbl[g * 64 + threadIdx.x] + dbl[g * 64 + 32 + threadIdx.x];
-    ws_db[(long)blockIdx.x * C + threadIdx.x] = t;
+    ws_db[(long)bid * C + threadIdx.x] = t;
   }
+}
+__global__ __launch_bounds__(DWV_THREADS) void conv_dw_vm32(const float* __restrict__ x,
+                                                            const int* __restrict__ idx,
+                                                            const float* __restrict__ dpre,
+                                                            float* __restrict__ ws, float* __restrict__ ws_db,
+                                                            int vsrc, int rows, int batch) {
+  __shared__ float lds[DWV_LDS];
+  dw_vm32_body<1>(x, idx, dpre, ws, ws_db, vsrc, rows, batch, blockIdx.x, gridDim.x, lds);
+}
+
+// Both gradients of a vertex-major 32 -> 32 conv in ONE launch: data-gradient
+// workgroups (dx_flat_body, 12 waves) and weight-gradient workgroups
+// (dw_vm32_body without prefetch, one slab each), interleaved.  Both bodies
+// fit 80 VGPRs, so a CU holds one workgroup of each (6 waves per SIMD) and the
+// two latency-bound MFMA streams hide each other's memory waits.
+struct DwVmArgs {
+  const float* x;
+  const int* idx;
+  float* ws;
+  float* ws_db;
+  int nb;
+};
+template <int FW>
+__global__ __launch_bounds__(DWV_THREADS, 2 * DWV_WAVES / 4) void conv_bwd_vm_pair(const DxFlatArgs a,
+                                                                                const DwVmArgs d) {
+  extern __shared__ float lds[];
+  const int bid = blockIdx.x, both = 2 * min(a.nb, d.nb);
+  bool is_dx;
+  int vb;
+  if (bid < both) {
+    is_dx = (bid & 1) == 0;
+    vb = bid >> 1;
+  } else {
+    is_dx = a.nb > d.nb;
+    vb = bid - both + both / 2;
+  }
+  if (is_dx)
+    dx_flat_body<32, 32, FW, float, DWV_WAVES>(a.dpre, a.flat, a.w, a.elu_y, a.dx, a.vsrc, a.rows, a.batch, 1, 1,
+                                               vb, a.nb, lds);
+  else
+    dw_vm32_body<0>(d.x, d.idx, a.dpre, d.ws, d.ws_db, a.vsrc, a.rows, a.batch, vb, d.nb, lds);
 }
 
 
@@ -814,12 +861,22 @@ int launch_bwd_flat_pair(const float* dpre, const int* flat, int width, const fl
                    cin, cout, width);
 }
 
-int launch_bwd_flat_pair_vm(const float* dpre, const int* flat, int width, const float* w, const float* elu_y,
-                            float* dx, int vsrc, int rows, int batch, const DwLatArgs& d, long dw_tasks,
-                            hipStream_t st) {
+int launch_bwd_vm_pair(const float* dpre, const int* flat, int width, const float* w, const float* elu_y, float* dx,
+                       const float* x, const int* idx, float* ws, float* ws_db, int n_slabs, int vsrc, int rows,
+                       int batch, hipStream_t st) {
   if (batch % 16) return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair: batch %% 16 != 0");
-#define BV(FW_) \
-  if (width == FW_) return pair_t<32, 32, FW_>(dpre, 1, flat, w, elu_y, dx, 1, vsrc, rows, batch, d, dw_tasks, st);
+  if ((long)vsrc * batch * 128 >= (long)kAbsent || (long)rows * batch * 128 >= (long)kAbsent)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair: operands exceed 32-bit offsets");
+  constexpr size_t lds_dx = (size_t)kS * 32 * (32 + 8) * sizeof(float);
+  constexpr size_t lds = lds_dx > DWV_LDS * sizeof(float) ? lds_dx : DWV_LDS * sizeof(float);
+  static const int dxb = env_knob("CFSD_VMPAIR_DXB", 0);  // dx workgroups (0: one per CU)
+  DxFlatArgs a{dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows, batch, 1, 1, dxb > 0 ? dxb : device_cus()};
+  const DwVmArgs d{x, idx, ws, ws_db, n_slabs};
+#define BV(FW_)                                                                                              \
+  if (width == FW_) {                                                                                        \
+    hipLaunchKernelGGL((conv_bwd_vm_pair<FW_>), dim3((unsigned)(a.nb + d.nb)), dim3(DWV_THREADS), lds, st, a, d); \
+    return launch_status("spiral_conv_bwd_vm_pair");                                                         \
+  }
   BV(8) BV(12) BV(16) BV(20)
 #undef BV
   return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair: flat width %d", width);

@@ -194,9 +194,10 @@ class SDVAEEngine:
         # the feature swap and the first Enblock's conv as one launch (cfsd_spiral_conv_fwd_in_swap)
         self.fuse_swap = os.environ.get("CFSD_FUSE_SWAP", "1") != "0"
         # vertex-major levels whose fp32 Deblock backward runs as one dx + dW launch
-        # (cfsd_spiral_conv_bwd_flat_pair); none by default: D2 59.6 vs 20.8 + 19.9 us,
-        # the coarse-geometry dW is one latency chain per 300-row chunk at 68k rows
-        self.vm_pair_levels = {int(c) for c in os.environ.get("CFSD_VM_PAIR_LEVELS", "") if c.isdigit()}
+        # (cfsd_spiral_conv_bwd_flat_pair): level 1 (D2: 37.8 vs 20.8 + 19.9 us,
+        # step 0.563 vs 0.568 ms same-box); at level 0 the pair is slower (117.5 vs
+        # 51.4 + 52.0 us: the dx role's 12-wave workgroups lose to its 2-per-CU kernel)
+        self.vm_pair_levels = {int(c) for c in os.environ.get("CFSD_VM_PAIR_LEVELS", "1") if c.isdigit()}
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:

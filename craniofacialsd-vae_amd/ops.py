@@ -1094,7 +1094,7 @@ def spiral_conv_bwd_flat_pair(x, idx, dpre, flat, w, dw, db, dx, elu_y=None, wor
     call("cfsd_spiral_conv_bwd_flat_pair", ptr(x), ptr(idx), ptr(dpre), ptr(table), width, ptr(w), ptr(elu_y),
          ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb), bsz, vsrc, rows, seq, cin, cout, stream_ptr())
     if dw is None:
-        return DeferredDw(ws, bsz, vsrc, rows, cin, cout, 4)
+        return DeferredDw(ws, bsz, vsrc, rows, cin, cout, 3)
     return None
 
 

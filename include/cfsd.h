@@ -110,7 +110,7 @@ size_t cfsd_spiral_conv_bwd_weight_workspace(int batch, int rows, int seq, int c
  * came from cfsd_spiral_conv_bwd(_x) on a small-output layer (cout*seq <= 32);
  * 2: from cfsd_spiral_conv_bwd_weight_x on a 32/64-channel layer (bf16); 3: from
  * cfsd_spiral_conv_bwd_weight_x on a 32 -> 32 fp32 layer with vertex-major x
- * and dpre, batch % 16 == 0 (ABI 4.3); 4: from cfsd_spiral_conv_bwd_flat_pair
+ * and dpre, batch % 16 == 0 (ABI 4.3), or from cfsd_spiral_conv_bwd_flat_pair
  * (ABI 4.10). */
 typedef struct {
   const float* workspace;
@@ -223,13 +223,14 @@ int cfsd_spiral_conv_fwd_in_swap(const float* data, const int32_t* batch_idx, co
                                  int vsrc, int rows, int cin, int cout, int act, void* stream);
 /* Both gradients of a full 32 -> 32 SpiralConv (a Deblock conv, model.py:27-41
  * autograd) with EVERY operand vertex-major fp32 (x, dpre, dx, elu_y:
- * [vertex][batch][32]), batch % 16 == 0, in ONE launch (ABI 4.10): the
- * flat-list data gradient of cfsd_spiral_conv_bwd_data_flat (dx = elu'(elu_y)
- * times the sum over u's flat inverse list, elu_y may be NULL) and the
- * weight-gradient slabs of the coarse-geometry dW body (one wave per 32x32
- * unit and row chunk, four chunks summed per slab) as interleaved workgroups.
- * dw == db == NULL defers (cfsd_dw_reduce_batch item with fused = 4).
- * inv_flat as cfsd_spiral_conv_bwd_data_flat (flat_width in {8, 12, 16, 20}).
+ * [vertex][batch][32]), batch % 16 == 0, batch x rows >= 65536, in ONE
+ * launch (ABI 4.10): the flat-list data gradient of
+ * cfsd_spiral_conv_bwd_data_flat (dx = elu'(elu_y) times the sum over u's
+ * flat inverse list, elu_y may be NULL) and the weight-gradient slabs of
+ * cfsd_spiral_conv_bwd_weight_x as interleaved workgroups, two per CU.
+ * Bit-identical to those two calls.  dw == db == NULL defers
+ * (cfsd_dw_reduce_batch item with fused = 3).  inv_flat as
+ * cfsd_spiral_conv_bwd_data_flat (flat_width in {8, 12, 16, 20}).
  * workspace: cfsd_spiral_conv_bwd_flat_pair_workspace() bytes (0 = unsupported). */
 size_t cfsd_spiral_conv_bwd_flat_pair_workspace(int batch, int rows, int seq, int cin, int cout);
 int cfsd_spiral_conv_bwd_flat_pair(const float* x, const int32_t* idx, const float* dpre, const int32_t* inv_flat,

@@ -162,15 +162,15 @@ def test_dw_vm32(mods, otopo, dtopo, table, level, bsz, cout, dpvm):
     assert torch.equal(dw2, dw) and torch.equal(db2, db)
 
 
-@pytest.mark.parametrize("level,bsz", [(0, 16), (1, 16), (1, 32), (2, 16), (3, 48)])
+@pytest.mark.parametrize("level,bsz", [(0, 16), (1, 16), (1, 32)])
 @pytest.mark.parametrize("with_elu", [False, True])
 def test_bwd_flat_pair_vm32(mods, otopo, dtopo, level, bsz, with_elu):
-    """cfsd_spiral_conv_bwd_flat_pair (ABI 4.10: flat-list dx + coarse-geometry
-    dW slabs in one launch, every operand vertex-major fp32): dx bit-identical
-    to cfsd_spiral_conv_bwd_data_flat (same body); dW / db vs float64 and vs
-    the vm32 weight-gradient kernel (another summation order) rel 1e-5; the
-    deferred slabs through the batched reduce == the direct reduce; two
-    calls bit-identical (deterministic)."""
+    """cfsd_spiral_conv_bwd_flat_pair (ABI 4.10: the flat-list dx and the
+    vm32 dW slabs as interleaved workgroups of one launch, every operand
+    vertex-major fp32): dx and dW / db bit-identical to
+    cfsd_spiral_conv_bwd_data_flat + cfsd_spiral_conv_bwd_weight_x (same
+    bodies, same slab split); dW vs float64 rel 1e-5; the deferred slabs
+    through the batched reduce == the direct reduce."""
     _, ops, _ = mods
     g = torch.Generator().manual_seed(level * 5 + bsz + with_elu)
     idx = dtopo.spiral[level]
@@ -198,7 +198,7 @@ def test_bwd_flat_pair_vm32(mods, otopo, dtopo, level, bsz, with_elu):
     wsx = torch.zeros(nbx // 4 + 64, device=DEV)
     dw_x, db_x = torch.empty_like(dw), torch.empty_like(db)
     ops.spiral_conv_bwd_weight_x(xv, idx, dpv, dw_x, db_x, wsx)
-    assert err_rel_max(dw, dw_x) <= 1e-5 and err_rel_max(db, db_x) <= 1e-5
+    assert torch.equal(dw, dw_x) and torch.equal(db, db_x)
     ws.zero_()
     dx2 = ops.vm_empty(bsz, v, 32, device=DEV)
     d = ops.spiral_conv_bwd_flat_pair(xv, idx, dpv, flat, w.to(DEV), None, None, dx2, elu_y=ey, workspace=ws)

@@ -260,6 +260,12 @@ def launch_cost(name, a):
         B, m, n, c = a[6:10]
         elu = a[4] is not None
         return 0.0, f4 * B * c * (n + m * (2 if elu else 1)), None
+    if name == "cfsd_spiral_conv_bwd_flat_pair":  # flat-list dx + vm32 dW of one vertex-major conv
+        B, vs, rows, S, ci, co = a[12:18]
+        elu = a[6] is not None
+        return (4.0 * B * rows * S * ci * co,
+                f4 * (B * rows * co + B * vs * ci * (2 + int(elu)) + 2 * co * S * ci) + 4 * rows * S
+                + 4 * vs * a[4], FP32_PEAK_TFLOPS)
     if name == "cfsd_spiral_conv_fwd_in_swap":  # the swap + the xyz input conv (spiral length 9)
         bs, vs, rows, ci, co = a[4], a[14], a[15], a[16], a[17]
         B, S = bs * bs, 9

@@ -39,6 +39,12 @@ constexpr int kDwVm16F32dp = 1;
 bool dw_vm16_ok(int batch, int cin, int cout, int xvm, int dpvm, int dpre_bf16);
 int launch_dw_vm16(const bf16_t* x, const int* idx, const void* dpre, int dpre_bf16, float* ws, int n_slabs, int vsrc,
                    int rows, int batch, hipStream_t st);
+// The bf16 vertex-major Deblock backward (32 -> 32, dpre / x / dx / elu_y bf16
+// vertex-major) in ONE launch: launch_dx_flat_vm16's dx and launch_dw_vm16's
+// n_slabs slabs (same values) as interleaved workgroup roles.
+int launch_bwd_vm16_pair(const bf16_t* x, const int* idx, const bf16_t* dpre, const int* flat, int width,
+                         const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, float* ws, int n_slabs, int vsrc, int rows,
+                         int batch, hipStream_t st);
 int launch_fwd_vm16(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, void* y, int y_dt,
                     int vsrc, int rows, int batch, int cin, int cout, int act, hipStream_t st);
 int launch_dx_vm16(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_row, const int* inv_head,

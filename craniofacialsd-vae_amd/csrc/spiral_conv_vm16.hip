@@ -303,18 +303,17 @@ __global__ __launch_bounds__(256) void conv_dx_vm16(const TD* __restrict__ dpre,
 // entry (9 per vertex on average, FW padded with out-of-range loads) instead
 // of 3 head rows per slot, and the products are exact bf16 x bf16 in fp32
 // (no bf16 rounding of row sums).  One MFMA per entry and 16-column tile.
-template <int CIN, int COUT, typename TD, int FW>
-__global__ __launch_bounds__(512) void conv_dx_flat_vm16(const TD* __restrict__ dpre,
-                                                         const int4* __restrict__ flat,
-                                                         const bf16_t* __restrict__ w,
-                                                         const bf16_t* __restrict__ elu_y,
-                                                         bf16_t* __restrict__ dx, int vsrc, int rows,
-                                                         int batch) {
+// (vb, nvb: the workgroup's index and count among the WPB-wave workgroups
+// running this body; lwt: the W^T image, as conv_dx_vm16)
+template <int CIN, int COUT, typename TD, int FW, int WPB = 8>
+__device__ __forceinline__ void dx_flat_vm16_body(const TD* __restrict__ dpre, const int4* __restrict__ flat,
+                                                  const bf16_t* __restrict__ w, const bf16_t* __restrict__ elu_y,
+                                                  bf16_t* __restrict__ dx, int vsrc, int rows, int batch, int vb,
+                                                  int nvb, bf16_t* lwt) {
   constexpr int K = kS * CIN, OP = COUT + 8, OC = COUT / 32, NT = CIN / 16, CPL = 4 * NT;
   constexpr int RB = COUT * (int)sizeof(TD);
   constexpr int NL = sizeof(TD) == 2 ? 1 : 2;
   constexpr int FQ = FW / 4, PD = 2, NB = PD + 1;
-  extern __shared__ bf16_t lwt[];  // as conv_dx_vm16
   coop_copy<12, bf16_t>(
       COUT * K, [&](int e) { return w[e]; },
       [&](int e, bf16_t v) {
@@ -330,7 +329,7 @@ __global__ __launch_bounds__(512) void conv_dx_flat_vm16(const TD* __restrict__ 
   const int nbytes = (int)((long)batch * rows * RB);
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<TD*>(dpre), 0, nbytes, 0x00020000);
   const int rstride = batch * RB;
-  const TileSweep sw = xcd_sweep(n_tiles, 8, wave, true);
+  const TileSweep sw = xcd_sweep_v(n_tiles, WPB, wave, true, vb, nvb);
   // the walk stops at the list's first -1 (uniform branch), entries e + 1,
   // e + 2 in flight while e runs its MFMAs, the next tile's list loaded at
   // the start of this one (as the fp32 conv_dx_flat_vm32)
@@ -416,6 +415,17 @@ __global__ __launch_bounds__(512) void conv_dx_flat_vm16(const TD* __restrict__ 
   }
 }
 
+template <int CIN, int COUT, typename TD, int FW>
+__global__ __launch_bounds__(512) void conv_dx_flat_vm16(const TD* __restrict__ dpre,
+                                                         const int4* __restrict__ flat,
+                                                         const bf16_t* __restrict__ w,
+                                                         const bf16_t* __restrict__ elu_y,
+                                                         bf16_t* __restrict__ dx, int vsrc, int rows,
+                                                         int batch) {
+  extern __shared__ bf16_t lwt[];
+  dx_flat_vm16_body<CIN, COUT, TD, FW>(dpre, flat, w, elu_y, dx, vsrc, rows, batch, blockIdx.x, gridDim.x, lwt);
+}
+
 // ------------------------------------------------------------------ weight gradient (32 -> 32)
 // dW_s[o][c] = sum over (vertex v, mesh m) of dpre[v][m][o] x[idx[v][s]][m][c]
 // (model.py:34, 40) for vertex-major bf16 x and dpre, batch % 16 == 0.  A unit
@@ -449,21 +459,24 @@ __device__ __forceinline__ bf16x8 tr_frag32(const bf16_t* blk, int lane) {
 
 // TD = float: an Enblock's dpre, fp32 batch-major at the kept rows (rounded to
 // bf16 when staged, as conv_dw_b16 rounds it).
-template <typename TD>
-__global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __restrict__ x,
-                                                             const int* __restrict__ idx,
-                                                             const TD* __restrict__ dpre,
-                                                             float* __restrict__ ws, int vsrc, int rows, int batch) {
+constexpr int DW16_LDS_BYTES = DW16_WAVES * 4 * 16 * 32 * 2 + DW16_NR * 64 * 4;  // block slots (red) + db partials
+// PD: units in flight (2: the dW-only kernel; 1: the pair, under 80 VGPRs);
+// bid / nb: this workgroup's slab and the slab count; lds: DW16_LDS_BYTES.
+template <typename TD, int PD>
+__device__ __forceinline__ void dw_vm16_body(const bf16_t* __restrict__ x, const int* __restrict__ idx,
+                                             const TD* __restrict__ dpre, float* __restrict__ ws, int vsrc, int rows,
+                                             int batch, int bid, int nb, char* lds_raw) {
   constexpr int C = 32, K = kS * C, NEL = C * K + C, NS = 3;
   constexpr int SLOT = 16 * C;  // bf16 elements of one 1-KiB block
-  __shared__ __attribute__((aligned(16))) bf16_t lds[DW16_WAVES * (1 + NS) * SLOT];  // 48 KiB, reused by red
+  bf16_t* lds = reinterpret_cast<bf16_t*>(lds_raw);  // 48 KiB, reused by red
+  float* dbl = reinterpret_cast<float*>(lds_raw + DW16_WAVES * (1 + NS) * SLOT * 2);
   const int lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
   const int sg = wave % 3, vg = wave / 3;
   bf16_t* my = lds + wave * (1 + NS) * SLOT;  // [dpre][x_0][x_1][x_2]
   const int G16 = batch >> 4;
   const long n_units = (long)rows * G16;
-  const int nb = gridDim.x, G = nb < 8 ? nb : 8;
-  const int grp = blockIdx.x % G, lb = blockIdx.x / G, nb_g = (nb - grp + G - 1) / G;
+  const int G = nb < 8 ? nb : 8;
+  const int grp = bid % G, lb = bid / G, nb_g = (nb - grp + G - 1) / G;
   const long per = (n_units + G - 1) / G;
   const long g0 = grp * per, g1 = min(n_units, g0 + per);
   const int nr = nb_g * DW16_NR;
@@ -477,9 +490,8 @@ __global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __res
 #pragma unroll
   for (int k = 0; k < NS; ++k) acc[k] = (f32x16){0.f};
   float dbs = 0.f;
-  // DW16_PD units' blocks in flight (a unit is only 3 MFMAs: one unit ahead
+  // PD units' blocks in flight (a unit is only 3 MFMAs: one unit ahead
   // left every unit waiting out a memory latency)
-  constexpr int PD = kDw16Pd;
   u32x4 ring[PD][1 + NS];
   auto load_unit = [&](long un, u32x4 (&b)[1 + NS]) {
     const int uu = uni((int)un);
@@ -525,7 +537,6 @@ __global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __res
   // ranges summed in fixed order in LDS (reused) -> one plain slab per workgroup
   __syncthreads();
   float* red = reinterpret_cast<float*>(lds);
-  __shared__ float dbl[DW16_NR * 64];
   for (int g = 0; g < DW16_NR; ++g) {
     if (vg == g) {
 #pragma unroll
@@ -545,8 +556,43 @@ __global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __res
     red[C * K + threadIdx.x] = t;
   }
   __syncthreads();
-  float* slab = ws + (long)blockIdx.x * NEL;
+  float* slab = ws + (long)bid * NEL;
   for (int e = threadIdx.x; e < NEL; e += DW16_THREADS) slab[e] = red[e];
+}
+template <typename TD>
+__global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __restrict__ x,
+                                                             const int* __restrict__ idx,
+                                                             const TD* __restrict__ dpre,
+                                                             float* __restrict__ ws, int vsrc, int rows, int batch) {
+  __shared__ __attribute__((aligned(16))) char lds[DW16_LDS_BYTES];
+  dw_vm16_body<TD, kDw16Pd>(x, idx, dpre, ws, vsrc, rows, batch, blockIdx.x, gridDim.x, lds);
+}
+
+// The bf16 step's vertex-major Deblock backward in ONE launch: flat-list dx
+// workgroups (12 waves) and weight-gradient workgroups (one unit in flight,
+// one slab each) interleaved; both fit 80 VGPRs, so a CU holds one of each
+// (as vm32::conv_bwd_vm_pair for fp32).  Same values as the two kernels.
+template <int FW>
+__global__ __launch_bounds__(DW16_THREADS, 2 * DW16_WAVES / 4) void conv_bwd_vm16_pair(
+    const bf16_t* __restrict__ x, const int* __restrict__ idx, const bf16_t* __restrict__ dpre,
+    const int4* __restrict__ flat, const bf16_t* __restrict__ w, const bf16_t* __restrict__ elu_y,
+    bf16_t* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, int batch, int nb_dx, int nb_dw) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  const int bid = blockIdx.x, both = 2 * min(nb_dx, nb_dw);
+  bool is_dx;
+  int vb;
+  if (bid < both) {
+    is_dx = (bid & 1) == 0;
+    vb = bid >> 1;
+  } else {
+    is_dx = nb_dx > nb_dw;
+    vb = bid - both + both / 2;
+  }
+  if (is_dx)
+    dx_flat_vm16_body<32, 32, bf16_t, FW, DW16_WAVES>(dpre, flat, w, elu_y, dx, vsrc, rows, batch, vb, nb_dx,
+                                                      reinterpret_cast<bf16_t*>(lds_raw));
+  else
+    dw_vm16_body<bf16_t, 1>(x, idx, dpre, ws, vsrc, rows, batch, vb, nb_dw, lds_raw);
 }
 
 // ------------------------------------------------------------------ launchers
@@ -585,6 +631,27 @@ int launch_dw_vm16(const bf16_t* x, const int* idx, const void* dpre, int dpre_b
     hipLaunchKernelGGL(conv_dw_vm16<float>, dim3(n_slabs), dim3(DW16_THREADS), 0, st, x, idx, (const float*)dpre, ws,
                        vsrc, rows, batch);
   return launch_status("spiral_conv_bwd_weight_vm16");
+}
+
+int launch_bwd_vm16_pair(const bf16_t* x, const int* idx, const bf16_t* dpre, const int* flat, int width,
+                         const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, float* ws, int n_slabs, int vsrc, int rows,
+                         int batch, hipStream_t st) {
+  if (batch % 16) return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair (bf16): batch %% 16 != 0");
+  if ((long)vsrc * batch * 64 >= (long)kAbsent || (long)rows * batch * 64 >= (long)kAbsent)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair (bf16): operands exceed 32-bit offsets");
+  constexpr size_t lds_dx = (size_t)kS * 32 * (32 + 8) * sizeof(bf16_t);
+  constexpr size_t lds = lds_dx > (size_t)DW16_LDS_BYTES ? lds_dx : (size_t)DW16_LDS_BYTES;
+  static const int dxb = env_knob("CFSD_VM16PAIR_DXB", 0);  // dx workgroups (0: one per CU)
+  const int nb_dx = dxb > 0 ? dxb : device_cus();
+#define BV(FW_)                                                                                             \
+  if (width == FW_) {                                                                                       \
+    hipLaunchKernelGGL((conv_bwd_vm16_pair<FW_>), dim3((unsigned)(nb_dx + n_slabs)), dim3(DW16_THREADS), lds, st, \
+                       x, idx, dpre, (const int4*)flat, w, elu_y, dx, ws, vsrc, rows, batch, nb_dx, n_slabs);   \
+    return launch_status("spiral_conv_bwd_vm16_pair");                                                      \
+  }
+  BV(8) BV(12) BV(16) BV(20)
+#undef BV
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair (bf16): flat width %d", width);
 }
 
 bool vm16_ok(int batch, int cin, int cout) {

@@ -198,6 +198,9 @@ class SDVAEEngine:
         # step 0.563 vs 0.568 ms same-box); at level 0 the pair is slower (117.5 vs
         # 51.4 + 52.0 us: the dx role's 12-wave workgroups lose to its 2-per-CU kernel)
         self.vm_pair_levels = {int(c) for c in os.environ.get("CFSD_VM_PAIR_LEVELS", "1") if c.isdigit()}
+        # the bf16 step's pair (cfsd_spiral_conv_bwd_flat_pair_bf16) at both vertex-major
+        # levels: D3 29.0 vs 20.0 + 19.0 us, D2 14.7 vs 10.4 + 11.6 us, step 0.427 -> 0.409 ms
+        self.vm_pair_levels16 = {int(c) for c in os.environ.get("CFSD_VM16_PAIR_LEVELS", "01") if c.isdigit()}
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -486,10 +489,13 @@ class SDVAEEngine:
         # fp32 vertex-major Deblocks (levels in vm_pair_levels): dx + dW slabs in one launch
         b.vm_pair = {}
         for i, (cin, cout, lv, _) in enumerate(S.dec_layers()):
-            b.vm_pair[("dec", i)] = (lv in lp and lv in self.vm_pair_levels and ldt == torch.float32
-                                     and cin == 32 and cout == 32 and self._flat_dx(b, lv, cin, cout)
-                                     and ops.spiral_conv_bwd_flat_pair_workspace(bsz, nv[lv], T.seq[lv], cin,
-                                                                                 cout) > 0)
+            flat_ok = lv in lp and cin == 32 and cout == 32 and self._flat_dx(b, lv, cin, cout)
+            if ldt == torch.float32:
+                b.vm_pair[("dec", i)] = (flat_ok and lv in self.vm_pair_levels
+                                         and ops.spiral_conv_bwd_flat_pair_workspace(bsz, nv[lv], T.seq[lv], cin,
+                                                                                     cout) > 0)
+            else:
+                b.vm_pair[("dec", i)] = flat_ok and lv in self.vm_pair_levels16
         for i, (cin, cout, lv, _) in enumerate(S.dec_layers()):
             dw_region(("dec", i), nv[lv], nv[lv], T.seq[lv], cin, cout, True, lv in lp)
         for (cin, cout, lv) in S.enc_layers():
@@ -760,7 +766,12 @@ class SDVAEEngine:
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]
             w, _ = self._dec_w(i)
-            if b.vm_pair.get(("dec", i)):  # fp32 vertex-major: flat dx + dW slabs in one launch
+            if b.vm_pair.get(("dec", i)) and b.dec_up[i].dtype == torch.bfloat16:  # bf16: the same pair
+                defer(ops.spiral_conv_bwd_flat_pair_bf16(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_flat[lv],
+                                                         self._wx(f"de_layers.{i + 1}.conv.layer.weight"),
+                                                         b.g_dec_up[i], workspace=b.ws_dw[("dec", i)]),
+                      f"de_layers.{i + 1}.conv.layer")
+            elif b.vm_pair.get(("dec", i)):  # fp32 vertex-major: flat dx + dW slabs in one launch
                 defer(ops.spiral_conv_bwd_flat_pair(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_flat[lv],
                                                     w, None, None, b.g_dec_up[i],
                                                     workspace=b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")

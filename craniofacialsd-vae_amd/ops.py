@@ -1098,6 +1098,34 @@ def spiral_conv_bwd_flat_pair(x, idx, dpre, flat, w, dw, db, dx, elu_y=None, wor
     return None
 
 
+def spiral_conv_bwd_flat_pair_bf16(x, idx, dpre, flat, w16, dx, elu_y=None, workspace=None):
+    """:func:`spiral_conv_bwd_flat_pair` on the bf16 step's tensors (x, dpre,
+    dx, elu_y bf16 vertex-major; ``w16`` the bf16 weight shadow), always
+    deferred (``cfsd_spiral_conv_bwd_flat_pair_bf16``, ABI 4.11): the dx of
+    :func:`spiral_conv_bwd_data_flat` and the slabs of
+    :func:`spiral_conv_bwd_weight_x` in one launch; returns the DeferredDw."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = dpre.shape[2]
+    table, width = flat
+    for t, nm, shp in ((x, "x", (bsz, vsrc, cin)), (dpre, "dpre", (bsz, rows, cout)), (dx, "dx", (bsz, vsrc, cin))):
+        _needl(t, shp, nm, torch.bfloat16)
+        if not is_vm(t):
+            raise ValueError(f"spiral_conv_bwd_flat_pair_bf16: {nm} must be vertex-major")
+    if elu_y is not None:
+        _needl(elu_y, (bsz, vsrc, cin), "elu_y", torch.bfloat16)
+        _same_layout(dx, elu_y, "dx and elu_y")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(table, (vsrc, width), torch.int32, "inv_flat")
+    _need(w16, (cout, seq * cin), torch.bfloat16, "w16")
+    _need(workspace, None, name="workspace")
+    nbytes = workspace.numel() * workspace.element_size()
+    call("cfsd_spiral_conv_bwd_flat_pair_bf16", ptr(x), ptr(idx), ptr(dpre), ptr(table), width, ptr(w16),
+         ptr(elu_y), ptr(dx), ptr(workspace), ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout,
+         stream_ptr())
+    return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2)
+
+
 def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None):
     """Fused dx + dW of the xyz output conv with bf16 (or fp32) x / elu_y /
     dx in either layout."""

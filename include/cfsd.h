@@ -237,6 +237,15 @@ int cfsd_spiral_conv_bwd_flat_pair(const float* x, const int32_t* idx, const flo
                                    int flat_width, const float* w, const float* elu_y, float* dx, float* dw,
                                    float* db, float* workspace, size_t workspace_bytes, int batch, int vsrc,
                                    int rows, int seq, int cin, int cout, void* stream);
+/* The same pair on the bf16 step's tensors (ABI 4.11): x, dpre, dx, elu_y
+ * bf16 vertex-major, w the bf16 weight shadow; always deferred
+ * (cfsd_dw_reduce_batch item with fused = 2; workspace as
+ * cfsd_spiral_conv_bwd_weight_x_workspace).  Same values as
+ * cfsd_spiral_conv_bwd_data_flat + cfsd_spiral_conv_bwd_weight_x. */
+int cfsd_spiral_conv_bwd_flat_pair_bf16(const void* x, const int32_t* idx, const void* dpre, const int32_t* inv_flat,
+                                        int flat_width, const void* w, const void* elu_y, void* dx, float* workspace,
+                                        size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
+                                        int cout, void* stream);
 
 /* The same with the source level's layout (ABI 4.4): x_dt = CFSD_DT_F32
  * [| CFSD_VM] describes x, dx and elu_y (the fp32 step's E1 reads and writes

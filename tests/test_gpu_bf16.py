@@ -420,3 +420,34 @@ def test_bf16_graph_step_runs(mods, dtopo):
         assert torch.isfinite(res[-1][1]).all()
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     assert torch.equal(res[0][2], res[1][2])
+
+
+@pytest.mark.parametrize("level", [0, 1])
+@pytest.mark.parametrize("with_elu", [False, True])
+def test_bwd_flat_pair_bf16(mods, dtopo, level, with_elu):
+    """cfsd_spiral_conv_bwd_flat_pair_bf16 (ABI 4.11: the bf16 flat-list dx
+    and the conv_dw_vm16 slabs as two workgroup roles of one launch) == the
+    deferred cfsd_spiral_conv_bwd_weight_x + cfsd_spiral_conv_bwd_data_flat
+    on the same bf16 operands, bit for bit (dx, and dW / db through the
+    batched reduce)."""
+    _, ops, _ = mods
+    g = torch.Generator().manual_seed(31 + level + with_elu)
+    bsz, v = 16, dtopo.n_verts[level]
+    idx = dtopo.spiral[level]
+    x = ops.to_vm(torch.randn(bsz, v, 32, generator=g).to(DEV).bfloat16())
+    dpre = ops.to_vm(torch.randn(bsz, v, 32, generator=g).to(DEV).bfloat16())
+    ey = ops.to_vm(torch.nn.functional.elu(torch.randn(bsz, v, 32, generator=g)).to(DEV).bfloat16()) if with_elu else None
+    w16 = (torch.randn(32, 288, generator=g) * 0.1).to(DEV).bfloat16()
+    flat = dtopo.spiral_flat[level]
+    nb = ops.spiral_conv_bwd_weight_x_workspace(bsz, v, 9, 32, 32)
+    ws_a = torch.zeros(nb // 4 + 64, device=DEV)
+    ws_b = torch.zeros_like(ws_a)
+    dx_a = ops.vm_empty(bsz, v, 32, dtype=torch.bfloat16, device=DEV)
+    d_a = ops.spiral_conv_bwd_flat_pair_bf16(x, idx, dpre, flat, w16, dx_a, elu_y=ey, workspace=ws_a)
+    dx_b = ops.spiral_conv_bwd_data_flat(dpre, flat, w16, v, elu_y=ey)
+    d_b = ops.spiral_conv_bwd_weight_x(x, idx, dpre, None, None, ws_b)
+    dw_a, db_a = torch.empty(32, 288, device=DEV), torch.empty(32, device=DEV)
+    dw_b, db_b = torch.empty_like(dw_a), torch.empty_like(db_a)
+    ops.dw_reduce_batch([(d_a, dw_a, db_a), (d_b, dw_b, db_b)])
+    assert torch.equal(dx_a, dx_b)
+    assert torch.equal(dw_a, dw_b) and torch.equal(db_a, db_b)

@@ -266,6 +266,12 @@ def launch_cost(name, a):
         return (4.0 * B * rows * S * ci * co,
                 f4 * (B * rows * co + B * vs * ci * (2 + int(elu)) + 2 * co * S * ci) + 4 * rows * S
                 + 4 * vs * a[4], FP32_PEAK_TFLOPS)
+    if name == "cfsd_spiral_conv_bwd_flat_pair_bf16":  # the same pair on bf16 operands
+        B, vs, rows, S, ci, co = a[10:16]
+        elu = a[6] is not None
+        return (4.0 * B * rows * S * ci * co,
+                2.0 * (B * rows * co + B * vs * ci * (2 + int(elu)) + co * S * ci) + 4 * rows * S + 4 * vs * a[4],
+                BF16_PEAK_TFLOPS)
     if name == "cfsd_spiral_conv_fwd_in_swap":  # the swap + the xyz input conv (spiral length 9)
         bs, vs, rows, ci, co = a[4], a[14], a[15], a[16], a[17]
         B, S = bs * bs, 9
@@ -437,6 +443,10 @@ def kernel_probe(runner, n_iter=20):
                                                                    T.n_verts[0], out=b.g_dec_up[i3]))
         timed("conv_dw_D3", lambda: ops.spiral_conv_bwd_weight_x(b.dec_up[i3], T.spiral[0], b.dpre_dec[i3],
                                                                  None, None, b.ws_dw[("dec", i3)]))
+        if b.vm_pair.get(("dec", i3)) and runner.precision == "bf16":  # the step runs dx + dW as one launch
+            timed("conv_pair_D3", lambda: ops.spiral_conv_bwd_flat_pair_bf16(
+                b.dec_up[i3], T.spiral[0], b.dpre_dec[i3], T.spiral_flat[0], wx, b.g_dec_up[i3],
+                workspace=b.ws_dw[("dec", i3)]))
     else:
         timed("conv_fwd_D3", lambda: ops.spiral_conv_fwd(b.dec_up[i3], T.spiral[0], w3, bias3, 1,
                                                           out=b.dec_out[i3]))
@@ -726,12 +736,23 @@ def main():
                             "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                             "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS, "algorithmic_flop": flops,
                             "traffic": traffic, "traffic_source": traffic_src}
-        dom = max(d3, key=lambda k: d3[k]["us_per_launch"])
+        if "conv_pair_D3" in probe:  # bf16: the step runs D3's dx + dW as one launch (ABI 4.11)
+            t = probe["conv_pair_D3"]
+            pb = 3 * s_act * 16 * nv * 32 + 2 * 32 * 288 + nv * 9 * 4 + nv * 20 * 4
+            d3["conv_pair_D3"] = {"us_per_launch": t * 1e6, "bound": "hbm", "achieved": pb / t / 1e9,
+                                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": pb / t / 1e9 / HBM_PEAK_GBS,
+                                  "tflops": 2 * flops / t / 1e12, "algorithmic_bytes": pb, "traffic": None,
+                                  "traffic_source": None}
+            for k in ("conv_dx_D3", "conv_dw_D3"):
+                d3[k]["in_step"] = False  # measured standalone; the step runs the pair
+        dom = max((k for k in d3 if d3[k].get("in_step", True)), key=lambda k: d3[k]["us_per_launch"])
         if bf:
             kern_names = {"conv_fwd_D3": "conv_fwd_vm16<32,32> (decoder level 0 forward, bf16, vertex-major)",
                           "conv_dx_D3": "conv_dx_flat_vm16<32,32> (decoder level 0 data gradient, bf16, "
                                         "vertex-major flat list)",
-                          "conv_dw_D3": "conv_dw_vm16 (decoder level 0 weight gradient, bf16, vertex-major)"}
+                          "conv_dw_D3": "conv_dw_vm16 (decoder level 0 weight gradient, bf16, vertex-major)",
+                          "conv_pair_D3": "conv_bwd_vm16_pair (decoder level 0 dx + dW slabs, bf16, vertex-major, "
+                                          "one launch)"}
         elif vm0:
             kern_names = {"conv_fwd_D3": "conv_fwd_vm32<32,32> (decoder level 0 forward, vertex-major)",
                           "conv_dx_D3": "conv_dx_flat_vm32<32,32> (decoder level 0 data gradient, vertex-major "

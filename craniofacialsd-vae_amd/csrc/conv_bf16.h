@@ -45,6 +45,12 @@ int launch_dw_vm16(const bf16_t* x, const int* idx, const void* dpre, int dpre_b
 int launch_bwd_vm16_pair(const bf16_t* x, const int* idx, const bf16_t* dpre, const int* flat, int width,
                          const bf16_t* w, const bf16_t* elu_y, bf16_t* dx, float* ws, int n_slabs, int vsrc, int rows,
                          int batch, hipStream_t st);
+// The bf16 step's Enblock E1 backward (fp32 batch-major dpre at the kept rows,
+// bf16 vertex-major x / dx / elu_y, fp32 w) in ONE launch: the fp32-product
+// flat dx and the conv_dw_vm16<float> slabs (same values as the two launches).
+int launch_bwd_rowsub16_pair(const bf16_t* x, const int* idx, const float* dpre, const int* flat, int width,
+                             const float* w, const bf16_t* elu_y, bf16_t* dx, float* ws, int n_slabs, int vsrc,
+                             int rows, int batch, hipStream_t st);
 int launch_fwd_vm16(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, void* y, int y_dt,
                     int vsrc, int rows, int batch, int cin, int cout, int act, hipStream_t st);
 int launch_dx_vm16(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_row, const int* inv_head,

@@ -3231,6 +3231,31 @@ extern "C" int cfsd_spiral_conv_bwd_flat_pair(const float* x, const int32_t* idx
   return launch_status("spiral_conv_bwd_flat_pair_reduce");
 }
 
+// ---- the bf16 step's Enblock pair (ABI 4.11): row-subset flat dx + vm16 dW slabs
+extern "C" int cfsd_spiral_conv_bwd_rowsub_pair_bf16(const void* x, const int32_t* idx, const float* dpre,
+                                                     const int32_t* inv_flat, int flat_width, const float* w,
+                                                     const void* elu_y, void* dx, float* workspace,
+                                                     size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
+                                                     int cin, int cout, void* stream) {
+  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!inv_flat || !w || !dx || !workspace)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_pair_bf16: null inv_flat / w / dx / workspace");
+  if (cin != 32 || cout != 32 || batch % 16)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_pair_bf16: 32 -> 32, batch %% 16 == 0 only");
+  if (flat_width <= 0 || flat_width > 16 || flat_width % 4)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_pair_bf16: flat_width %d not in {4, 8, 12, 16}",
+                     flat_width);
+  if ((uintptr_t)inv_flat & 15) return set_error(CFSD_EINVAL, "inv_flat must be 16-B aligned");
+  if ((long)batch * rows * cout * 4 >= (long)kAbsentRow)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_pair_bf16: dpre exceeds 32-bit buffer offsets");
+  const int nslab = bf::dw_slabs(batch, rows, cin, cout);  // as cfsd_dw_reduce_batch's fused = 2 items
+  const size_t need = (size_t)nslab * ((size_t)cout * kSeq * cin + cout) * sizeof(float);
+  if (workspace_bytes < need) return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
+  return bf::launch_bwd_rowsub16_pair((const bf16_t*)x, idx, dpre, inv_flat, flat_width, w, (const bf16_t*)elu_y,
+                                      (bf16_t*)dx, workspace, nslab, vsrc, rows, batch, (hipStream_t)stream);
+}
+
 // ---- the same pair on the bf16 step's tensors (ABI 4.11)
 extern "C" int cfsd_spiral_conv_bwd_flat_pair_bf16(const void* x, const int32_t* idx, const void* dpre,
                                                    const int32_t* inv_flat, int flat_width, const void* w,

@@ -26,6 +26,7 @@
 // ELU uses the hardware exp (elu_fast), so results agree with those kernels to
 // fp32 rounding, not bit for bit.
 #include "conv_bf16.h"
+#include "dx_flat_vm32.h"
 
 namespace cfsd {
 namespace bf {
@@ -631,6 +632,54 @@ int launch_dw_vm16(const bf16_t* x, const int* idx, const void* dpre, int dpre_b
     hipLaunchKernelGGL(conv_dw_vm16<float>, dim3(n_slabs), dim3(DW16_THREADS), 0, st, x, idx, (const float*)dpre, ws,
                        vsrc, rows, batch);
   return launch_status("spiral_conv_bwd_weight_vm16");
+}
+
+// The bf16 step's Enblock E1 backward in ONE launch: the fp32-product flat
+// dx of vm32::launch_dx_flat_b16 (fp32 batch-major dpre at the kept rows, bf16
+// vertex-major dx / elu_y) and the conv_dw_vm16<float> slabs, interleaved
+// workgroup roles, two per CU.  Same values as the two launches.
+template <int FW>
+__global__ __launch_bounds__(DW16_THREADS, 2 * DW16_WAVES / 4) void conv_bwd_rowsub16_pair(
+    const bf16_t* __restrict__ x, const int* __restrict__ idx, const float* __restrict__ dpre,
+    const int4* __restrict__ flat, const float* __restrict__ w, const bf16_t* __restrict__ elu_y,
+    bf16_t* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, int batch, int nb_dx, int nb_dw) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  const int bid = blockIdx.x, both = 2 * min(nb_dx, nb_dw);
+  bool is_dx;
+  int vb;
+  if (bid < both) {
+    is_dx = (bid & 1) == 0;
+    vb = bid >> 1;
+  } else {
+    is_dx = nb_dx > nb_dw;
+    vb = bid - both + both / 2;
+  }
+  if (is_dx)
+    vm32::dx_flat_body<32, 32, FW, bf16_t, DW16_WAVES>(dpre, flat, w, elu_y, dx, vsrc, rows, batch, 0, 1, vb, nb_dx,
+                                                       reinterpret_cast<float*>(lds_raw));
+  else
+    dw_vm16_body<float, 1>(x, idx, dpre, ws, vsrc, rows, batch, vb, nb_dw, lds_raw);
+}
+
+int launch_bwd_rowsub16_pair(const bf16_t* x, const int* idx, const float* dpre, const int* flat, int width,
+                             const float* w, const bf16_t* elu_y, bf16_t* dx, float* ws, int n_slabs, int vsrc,
+                             int rows, int batch, hipStream_t st) {
+  if (batch % 16) return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_pair_bf16: batch %% 16 != 0");
+  if ((long)vsrc * batch * 64 >= (long)kAbsent || (long)rows * batch * 128 >= (long)kAbsent)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_pair_bf16: operands exceed 32-bit offsets");
+  constexpr size_t lds_dx = (size_t)kS * 32 * (32 + 8) * sizeof(float);
+  constexpr size_t lds = lds_dx > (size_t)DW16_LDS_BYTES ? lds_dx : (size_t)DW16_LDS_BYTES;
+  static const int dxb = env_knob("CFSD_RS16PAIR_DXB", 0);  // dx workgroups (0: one per CU)
+  const int nb_dx = dxb > 0 ? dxb : device_cus();
+#define BV(FW_)                                                                                               \
+  if (width == FW_) {                                                                                         \
+    hipLaunchKernelGGL((conv_bwd_rowsub16_pair<FW_>), dim3((unsigned)(nb_dx + n_slabs)), dim3(DW16_THREADS), lds, \
+                       st, x, idx, dpre, (const int4*)flat, w, elu_y, dx, ws, vsrc, rows, batch, nb_dx, n_slabs);  \
+    return launch_status("spiral_conv_bwd_rowsub16_pair");                                                    \
+  }
+  BV(4) BV(8) BV(12) BV(16)
+#undef BV
+  return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_pair_bf16: flat width %d", width);
 }
 
 int launch_bwd_vm16_pair(const bf16_t* x, const int* idx, const bf16_t* dpre, const int* flat, int width,

@@ -1297,7 +1297,7 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
 
 using namespace cfsd;
 
-extern "C" int cfsd_version(void) { return (4 << 16) | 11; }  // 4.11: cfsd_spiral_conv_bwd_flat_pair_bf16; 4.10: cfsd_spiral_conv_bwd_flat_pair; 4.9: cfsd_spiral_conv_fwd_in_swap; 4.8: cfsd_bottleneck_bwd; 4.7: cfsd_adam_scaled; 4.6: cfsd_side_work (side work riding in host launches); 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
+extern "C" int cfsd_version(void) { return (4 << 16) | 11; }  // 4.11: cfsd_spiral_conv_bwd_flat_pair_bf16, cfsd_spiral_conv_bwd_rowsub_pair_bf16; 4.10: cfsd_spiral_conv_bwd_flat_pair; 4.9: cfsd_spiral_conv_fwd_in_swap; 4.8: cfsd_bottleneck_bwd; 4.7: cfsd_adam_scaled; 4.6: cfsd_side_work (side work riding in host launches); 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
 extern "C" const char* cfsd_last_error_string(void) { return g_err; }
 
 extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {

@@ -200,6 +200,7 @@ class SDVAEEngine:
         self.vm_pair_levels = {int(c) for c in os.environ.get("CFSD_VM_PAIR_LEVELS", "1") if c.isdigit()}
         # the bf16 step's pair (cfsd_spiral_conv_bwd_flat_pair_bf16) at both vertex-major
         # levels: D3 29.0 vs 20.0 + 19.0 us, D2 14.7 vs 10.4 + 11.6 us, step 0.427 -> 0.409 ms
+        self.rowsub_pair16 = os.environ.get("CFSD_RS16_PAIR", "1") != "0"
         self.vm_pair_levels16 = {int(c) for c in os.environ.get("CFSD_VM16_PAIR_LEVELS", "01") if c.isdigit()}
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
@@ -931,6 +932,15 @@ class SDVAEEngine:
             prev = lv - 1
             if lv in b.xl and b.rowsub_vm.get(("enc", lv)) and T.enc_select[prev]:
                 pass  # fp32 vertex-major x / dx: the paired row-subset launch below
+            elif (lv in b.xl and self.rowsub_pair16 and lv > 0 and b.rowsub_x.get(lv) and T.enc_select[prev]
+                  and x_in.dtype == torch.bfloat16 and b.dpre_enc[lv].dtype == torch.float32 and cin == 32
+                  and cout == 32 and b.bsz % 16 == 0 and T.enc_flat[lv][1] <= 16):
+                # bf16 Enblock: its flat dx and dW slabs in one launch
+                defer(ops.spiral_conv_bwd_rowsub_pair_bf16(x_in, rows_tab, b.dpre_enc[lv], T.enc_flat[lv], w,
+                                                           b.dpre_enc[prev], elu_y=b.enc_out[prev],
+                                                           workspace=b.ws_dw[("enc", lv)]),
+                      f"en_layers.{lv}.conv.layer")
+                continue
             elif lv in b.xl:  # vertex-major (bf16 or fp32) operands (selection down-sampling)
                 defer(ops.spiral_conv_bwd_weight_x(x_in, rows_tab, b.dpre_enc[lv], None, None,
                                                    b.ws_dw[("enc", lv)]), f"en_layers.{lv}.conv.layer")

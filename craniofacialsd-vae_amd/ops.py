@@ -1126,6 +1126,36 @@ def spiral_conv_bwd_flat_pair_bf16(x, idx, dpre, flat, w16, dx, elu_y=None, work
     return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2)
 
 
+def spiral_conv_bwd_rowsub_pair_bf16(x, idx, dpre, flat, w, dx, elu_y=None, workspace=None):
+    """The bf16 step's Enblock backward in ONE launch
+    (``cfsd_spiral_conv_bwd_rowsub_pair_bf16``, ABI 4.11): the dx of
+    :func:`spiral_conv_bwd_data_rowsub` (fp32 batch-major ``dpre`` at the kept
+    rows, fp32 ``w``; bf16 vertex-major ``dx`` / ``elu_y``) and the deferred
+    slabs of :func:`spiral_conv_bwd_weight_x` (bf16 vertex-major ``x``);
+    returns the DeferredDw."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = dpre.shape[2]
+    table, width = flat
+    for t, nm in ((x, "x"), (dx, "dx")):
+        _needl(t, (bsz, vsrc, cin), nm, torch.bfloat16)
+        if not is_vm(t):
+            raise ValueError(f"spiral_conv_bwd_rowsub_pair_bf16: {nm} must be vertex-major")
+    if elu_y is not None:
+        _needl(elu_y, (bsz, vsrc, cin), "elu_y", torch.bfloat16)
+        _same_layout(dx, elu_y, "dx and elu_y")
+    _need(dpre, (bsz, rows, cout), torch.float32, "dpre")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    _need(table, (vsrc, width), torch.int32, "inv_flat")
+    _need(w, (cout, seq * cin), torch.float32, "w")
+    _need(workspace, None, name="workspace")
+    nbytes = workspace.numel() * workspace.element_size()
+    call("cfsd_spiral_conv_bwd_rowsub_pair_bf16", ptr(x), ptr(idx), ptr(dpre), ptr(table), width, ptr(w),
+         ptr(elu_y), ptr(dx), ptr(workspace), ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout,
+         stream_ptr())
+    return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2)
+
+
 def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None):
     """Fused dx + dW of the xyz output conv with bf16 (or fp32) x / elu_y /
     dx in either layout."""

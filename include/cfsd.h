@@ -237,6 +237,17 @@ int cfsd_spiral_conv_bwd_flat_pair(const float* x, const int32_t* idx, const flo
                                    int flat_width, const float* w, const float* elu_y, float* dx, float* dw,
                                    float* db, float* workspace, size_t workspace_bytes, int batch, int vsrc,
                                    int rows, int seq, int cin, int cout, void* stream);
+/* The bf16 step's Enblock backward (ABI 4.11): the flat-list dx of
+ * cfsd_spiral_conv_bwd_data_rowsub (fp32 batch-major dpre at the kept rows,
+ * fp32 w, fp32 products; dx / elu_y bf16 vertex-major, rounded once) and the
+ * weight-gradient slabs of cfsd_spiral_conv_bwd_weight_x (x bf16
+ * vertex-major) as two workgroup roles of ONE launch; always deferred
+ * (cfsd_dw_reduce_batch item with fused = 2).  32 -> 32, batch % 16 == 0,
+ * flat_width in {4, 8, 12, 16}.  Same values as the two calls. */
+int cfsd_spiral_conv_bwd_rowsub_pair_bf16(const void* x, const int32_t* idx, const float* dpre,
+                                          const int32_t* inv_flat, int flat_width, const float* w, const void* elu_y,
+                                          void* dx, float* workspace, size_t workspace_bytes, int batch, int vsrc,
+                                          int rows, int seq, int cin, int cout, void* stream);
 /* The same pair on the bf16 step's tensors (ABI 4.11): x, dpre, dx, elu_y
  * bf16 vertex-major, w the bf16 weight shadow; always deferred
  * (cfsd_dw_reduce_batch item with fused = 2; workspace as

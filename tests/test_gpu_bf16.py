@@ -451,3 +451,35 @@ def test_bwd_flat_pair_bf16(mods, dtopo, level, with_elu):
     ops.dw_reduce_batch([(d_a, dw_a, db_a), (d_b, dw_b, db_b)])
     assert torch.equal(dx_a, dx_b)
     assert torch.equal(dw_a, dw_b) and torch.equal(db_a, db_b)
+
+
+@pytest.mark.parametrize("with_elu", [False, True])
+def test_bwd_rowsub_pair_bf16(mods, dtopo, with_elu):
+    """cfsd_spiral_conv_bwd_rowsub_pair_bf16 (ABI 4.11: the bf16 step's E1
+    backward -- fp32-product flat dx from fp32 batch-major dpre at the kept
+    rows, and the conv_dw_vm16<float> slabs -- in one launch) == the deferred
+    cfsd_spiral_conv_bwd_weight_x + cfsd_spiral_conv_bwd_data_rowsub, bit for
+    bit (dx, and dW / db through the batched reduce)."""
+    _, ops, _ = mods
+    g = torch.Generator().manual_seed(41 + with_elu)
+    bsz, lv = 16, 1
+    v, rows_tab, flat = dtopo.n_verts[lv], dtopo.enc_rows[lv], dtopo.enc_flat[lv]
+    rows = rows_tab.shape[0]
+    x = ops.to_vm(torch.randn(bsz, v, 32, generator=g).to(DEV).bfloat16())
+    dpre = torch.randn(bsz, rows, 32, generator=g).to(DEV)
+    ey = ops.to_vm(torch.nn.functional.elu(torch.randn(bsz, v, 32, generator=g)).to(DEV).bfloat16()) if with_elu else None
+    w = (torch.randn(32, 288, generator=g) * 0.1).to(DEV)
+    nb = ops.spiral_conv_bwd_weight_x_workspace(bsz, rows, 9, 32, 32)
+    ws_a = torch.zeros(nb // 4 + 64, device=DEV)
+    ws_b = torch.zeros_like(ws_a)
+    dx_a = ops.vm_empty(bsz, v, 32, dtype=torch.bfloat16, device=DEV)
+    dx_b = ops.vm_empty(bsz, v, 32, dtype=torch.bfloat16, device=DEV)
+    d_a = ops.spiral_conv_bwd_rowsub_pair_bf16(x, rows_tab, dpre, flat, w, dx_a, elu_y=ey, workspace=ws_a)
+    d_b = ops.spiral_conv_bwd_weight_x(x, rows_tab, dpre, None, None, ws_b)
+    wsg = torch.empty(ops.spiral_conv_bwd_data_rowsub_workspace(bsz, rows, 9, 32) // 4 + 64, device=DEV)
+    ops.spiral_conv_bwd_data_rowsub(dpre, flat, w, v, elu_y=ey, out=dx_b, workspace=wsg)
+    dw_a, db_a = torch.empty(32, 288, device=DEV), torch.empty(32, device=DEV)
+    dw_b, db_b = torch.empty_like(dw_a), torch.empty_like(db_a)
+    ops.dw_reduce_batch([(d_a, dw_a, db_a), (d_b, dw_b, db_b)])
+    assert torch.equal(dx_a, dx_b)
+    assert torch.equal(dw_a, dw_b) and torch.equal(db_a, db_b)

@@ -272,6 +272,12 @@ def launch_cost(name, a):
         return (4.0 * B * rows * S * ci * co,
                 2.0 * (B * rows * co + B * vs * ci * (2 + int(elu)) + co * S * ci) + 4 * rows * S + 4 * vs * a[4],
                 BF16_PEAK_TFLOPS)
+    if name == "cfsd_spiral_conv_bwd_rowsub_pair_bf16":  # bf16 Enblock: fp32-product dx + bf16 dW
+        B, vs, rows, S, ci, co = a[10:16]
+        elu = a[6] is not None
+        return (4.0 * B * rows * S * ci * co,
+                f4 * (B * rows * co + co * S * ci) + 2.0 * B * vs * ci * (2 + int(elu)) + 4 * rows * S
+                + 4 * vs * a[4], FP32_PEAK_TFLOPS)
     if name == "cfsd_spiral_conv_fwd_in_swap":  # the swap + the xyz input conv (spiral length 9)
         bs, vs, rows, ci, co = a[4], a[14], a[15], a[16], a[17]
         B, S = bs * bs, 9

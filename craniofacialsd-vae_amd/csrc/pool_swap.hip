@@ -268,6 +268,55 @@ __device__ __forceinline__ void spmm_fold_prefetch(int beg, int end, const int* 
   }
 }
 
+// The same fold over 8 consecutive bf16 channels per thread (one 16-B load
+// per entry instead of two 8-B ones; per element the same operations in the
+// same order as two 4-wide threads: bit-identical)
+template <int CK>
+__device__ __forceinline__ void spmm_fold_prefetch8(int beg, int end, const int* __restrict__ col,
+                                                    const float* __restrict__ val,
+                                                    const bf16_t* __restrict__ xb, long rs, f32x4& acc0,
+                                                    f32x4& acc1) {
+#pragma clang fp contract(off)
+  int cc[CK];
+  float vv[CK];
+#pragma unroll
+  for (int j = 0; j < CK; ++j) {
+    const int e = min(beg + j, end - 1);
+    cc[j] = col[e];
+    vv[j] = val[e];
+  }
+  for (int e0 = beg; e0 < end; e0 += CK) {
+    u32x4 xv[CK];
+#pragma unroll
+    for (int j = 0; j < CK; ++j) xv[j] = *reinterpret_cast<const u32x4*>(xb + (long)cc[j] * rs);
+    float vc[CK];
+#pragma unroll
+    for (int j = 0; j < CK; ++j) vc[j] = vv[j];
+    if (e0 + CK < end) {  // next chunk's list while the x rows are in flight
+#pragma unroll
+      for (int j = 0; j < CK; ++j) {
+        const int e = min(e0 + CK + j, end - 1);
+        cc[j] = col[e];
+        vv[j] = val[e];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CK; ++j) {
+      if (e0 + j < end) {
+        const u32x4 q = xv[j];
+        acc0.x = acc0.x + __uint_as_float(q.x << 16) * vc[j];
+        acc0.y = acc0.y + __uint_as_float(q.x & 0xffff0000u) * vc[j];
+        acc0.z = acc0.z + __uint_as_float(q.y << 16) * vc[j];
+        acc0.w = acc0.w + __uint_as_float(q.y & 0xffff0000u) * vc[j];
+        acc1.x = acc1.x + __uint_as_float(q.z << 16) * vc[j];
+        acc1.y = acc1.y + __uint_as_float(q.z & 0xffff0000u) * vc[j];
+        acc1.z = acc1.z + __uint_as_float(q.w << 16) * vc[j];
+        acc1.w = acc1.w + __uint_as_float(q.w & 0xffff0000u) * vc[j];
+      }
+    }
+  }
+}
+
 template <typename TX, typename TY>
 __global__ __launch_bounds__(256) void spmm_sched_k(const int* __restrict__ row_ptr,
                                                     const int* __restrict__ col,
@@ -307,7 +356,7 @@ __global__ __launch_bounds__(256) void spmm_sched_k(const int* __restrict__ row_
 // and extent are independent loads, so the chain is extent -> list -> x rows
 // (spmm_sched_k: order -> row_ptr -> list -> x rows), and a wave's entry
 // lists are contiguous.
-template <typename TX, typename TY>
+template <typename TX, typename TY, int V = 4>
 __global__ __launch_bounds__(256) void spmm_sched_csr_k(const int* __restrict__ ptr_s,
                                                         const int* __restrict__ col_s,
                                                         const float* __restrict__ val_s,
@@ -336,18 +385,37 @@ __global__ __launch_bounds__(256) void spmm_sched_csr_k(const int* __restrict__ 
   const int b = g * bpg + bl, batch = groups * bpg;
   const Lay lx = make_lay(xvm, batch, n), ly = make_lay(yvm, batch, m);
   const int r = rows_s[slot], beg = ptr_s[slot], end = ptr_s[slot + 1];
-  const TX* xb = x + (long)b * lx.bs * c4 * 4 + 4 * q;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  spmm_fold_prefetch<8>(beg, end, col_s, val_s, xb, (long)lx.vs * c4 * 4, acc);
-  const long o = (long)row_of(ly, b, r) * c4 + q;
-  if (elu_y) {
-    f32x4 gy = ld4f(elu_y + o * 4);
-    acc.x *= elu_grad_from_out(gy.x);
-    acc.y *= elu_grad_from_out(gy.y);
-    acc.z *= elu_grad_from_out(gy.z);
-    acc.w *= elu_grad_from_out(gy.w);
+  // (c4: V-channel groups per row; V = 8 for bf16 x, 4 otherwise)
+  const TX* xb = x + (long)b * lx.bs * c4 * V + V * q;
+  if constexpr (V == 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    spmm_fold_prefetch<8>(beg, end, col_s, val_s, xb, (long)lx.vs * c4 * 4, acc);
+    const long o = (long)row_of(ly, b, r) * c4 + q;
+    if (elu_y) {
+      f32x4 gy = ld4f(elu_y + o * 4);
+      acc.x *= elu_grad_from_out(gy.x);
+      acc.y *= elu_grad_from_out(gy.y);
+      acc.z *= elu_grad_from_out(gy.z);
+      acc.w *= elu_grad_from_out(gy.w);
+    }
+    st4f(y + o * 4, acc);
+  } else {
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    spmm_fold_prefetch8<8>(beg, end, col_s, val_s, xb, (long)lx.vs * c4 * 8, acc[0], acc[1]);
+    const long o = ((long)row_of(ly, b, r) * c4 + q) * 8;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x4 v = acc[h];
+      if (elu_y) {
+        const f32x4 gy = ld4f(elu_y + o + 4 * h);
+        v.x *= elu_grad_from_out(gy.x);
+        v.y *= elu_grad_from_out(gy.y);
+        v.z *= elu_grad_from_out(gy.z);
+        v.w *= elu_grad_from_out(gy.w);
+      }
+      st4f(y + o + 4 * h, v);
+    }
   }
-  st4f(y + o * 4, acc);
 }
 
 // out[(i*bs + j), v, :] = x[mesh(i or j), v, :]; one thread per (out mesh,
@@ -675,20 +743,26 @@ extern "C" int cfsd_spmm_sched_csr_side(const int32_t* ptr_s, const int32_t* col
   // vertex-major x: one group, a slot's threads cover every mesh, so each
   // gathered vertex block is one contiguous load
   const int groups = (!xvm && batch % 8 == 0) ? 8 : 1, bpg = batch / groups;
-  const int per = bpg * m * (c / 4);
+  // bf16 x: 8 channels per thread (one 16-B load per entry; bf16 up0T 21.3 ->
+  // see DESIGN) -- the same per-element folds
+  static const int v8 = env_knob("CFSD_SPMM_BF16_V8", 1);
+  const int V = (v8 && x_dt == CFSD_DT_BF16 && c % 8 == 0) ? 8 : 4;
+  const int per = bpg * m * (c / V);
   const unsigned nb = (unsigned)(groups * ((per + 255) / 256));
   SideJob J;
   const int rc = make_side_job(side, J);
   if (rc) return rc;
   const hipStream_t st = (hipStream_t)stream;
-#define SPSC(TX, TY)                                                                                        \
-  hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY>), dim3(nb + side_grid(J)), dim3(256), 0, st, ptr_s, col_s, val_s, \
-                     rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / 4, groups, bpg, per, xvm, yvm,  \
-                     (int)nb, J)
-  if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPSC(float, float);
-  else if (x_dt == CFSD_DT_F32) SPSC(float, bf16_t);
-  else if (y_dt == CFSD_DT_F32) SPSC(bf16_t, float);
-  else SPSC(bf16_t, bf16_t);
+#define SPSC(TX, TY, V_)                                                                                    \
+  hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY, V_>), dim3(nb + side_grid(J)), dim3(256), 0, st, ptr_s, col_s,   \
+                     val_s, rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / V_, groups, bpg, per, xvm, \
+                     yvm, (int)nb, J)
+  if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPSC(float, float, 4);
+  else if (x_dt == CFSD_DT_F32) SPSC(float, bf16_t, 4);
+  else if (V == 8 && y_dt == CFSD_DT_F32) SPSC(bf16_t, float, 8);
+  else if (V == 8) SPSC(bf16_t, bf16_t, 8);
+  else if (y_dt == CFSD_DT_F32) SPSC(bf16_t, float, 4);
+  else SPSC(bf16_t, bf16_t, 4);
 #undef SPSC
   return launch_status("spmm_sched_csr");
 }

@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256) void spmm_sched_k(const int* __restrict__ row_
 // and extent are independent loads, so the chain is extent -> list -> x rows
 // (spmm_sched_k: order -> row_ptr -> list -> x rows), and a wave's entry
 // lists are contiguous.
-template <typename TX, typename TY, int V = 4>
+template <typename TX, typename TY, int V = 4, bool UNI = false>
 __global__ __launch_bounds__(256) void spmm_sched_csr_k(const int* __restrict__ ptr_s,
                                                         const int* __restrict__ col_s,
                                                         const float* __restrict__ val_s,
@@ -380,7 +380,9 @@ __global__ __launch_bounds__(256) void spmm_sched_csr_k(const int* __restrict__ 
   const int t = (blk / groups) * (int)blockDim.x + (int)threadIdx.x;
   if (t >= per) return;
   const int rowq = bpg * c4;  // threads per schedule slot
-  const int slot = t / rowq, rem = t - slot * rowq;
+  // UNI (rowq % 64 == 0: a wave lies inside one slot): the slot, its extent
+  // and entry list are wave-uniform -> scalar loads
+  const int slot = UNI ? __builtin_amdgcn_readfirstlane(t / rowq) : t / rowq, rem = t - slot * rowq;
   const int bl = rem / c4, q = rem - bl * c4;
   const int b = g * bpg + bl, batch = groups * bpg;
   const Lay lx = make_lay(xvm, batch, n), ly = make_lay(yvm, batch, m);
@@ -753,16 +755,30 @@ extern "C" int cfsd_spmm_sched_csr_side(const int32_t* ptr_s, const int32_t* col
   const int rc = make_side_job(side, J);
   if (rc) return rc;
   const hipStream_t st = (hipStream_t)stream;
-#define SPSC(TX, TY, V_)                                                                                    \
-  hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY, V_>), dim3(nb + side_grid(J)), dim3(256), 0, st, ptr_s, col_s,   \
-                     val_s, rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / V_, groups, bpg, per, xvm, \
-                     yvm, (int)nb, J)
-  if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) SPSC(float, float, 4);
-  else if (x_dt == CFSD_DT_F32) SPSC(float, bf16_t, 4);
-  else if (V == 8 && y_dt == CFSD_DT_F32) SPSC(bf16_t, float, 8);
-  else if (V == 8) SPSC(bf16_t, bf16_t, 8);
-  else if (y_dt == CFSD_DT_F32) SPSC(bf16_t, float, 4);
-  else SPSC(bf16_t, bf16_t, 4);
+  static const int uni_k = env_knob("CFSD_SPMM_UNI", 1);
+  const bool uni = uni_k && (bpg * (c / V)) % 64 == 0;
+#define SPSC(TX, TY, V_)                                                                                       \
+  if (uni)                                                                                                     \
+    hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY, V_, true>), dim3(nb + side_grid(J)), dim3(256), 0, st, ptr_s,   \
+                       col_s, val_s, rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / V_, groups, bpg, per, \
+                       xvm, yvm, (int)nb, J);                                                                  \
+  else                                                                                                         \
+    hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY, V_, false>), dim3(nb + side_grid(J)), dim3(256), 0, st, ptr_s,  \
+                       col_s, val_s, rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / V_, groups, bpg, per, \
+                       xvm, yvm, (int)nb, J)
+  if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) {
+    SPSC(float, float, 4);
+  } else if (x_dt == CFSD_DT_F32) {
+    SPSC(float, bf16_t, 4);
+  } else if (V == 8 && y_dt == CFSD_DT_F32) {
+    SPSC(bf16_t, float, 8);
+  } else if (V == 8) {
+    SPSC(bf16_t, bf16_t, 8);
+  } else if (y_dt == CFSD_DT_F32) {
+    SPSC(bf16_t, float, 4);
+  } else {
+    SPSC(bf16_t, bf16_t, 4);
+  }
 #undef SPSC
   return launch_status("spmm_sched_csr");
 }

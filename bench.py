@@ -278,6 +278,13 @@ def launch_cost(name, a):
         return (4.0 * B * rows * S * ci * co,
                 f4 * (B * rows * co + co * S * ci) + 2.0 * B * vs * ci * (2 + int(elu)) + 4 * rows * S
                 + 4 * vs * a[4], FP32_PEAK_TFLOPS)
+    if name == "cfsd_spiral_conv_bwd_weight_spmm_bf16":  # bf16 level-0 dW slabs + Pool(up)^T SpMM
+        B, vs, rows, S, ci, co = a[5:11]
+        m, n, c = a[18:21]
+        elu = a[16] is not None
+        return (2.0 * B * rows * S * ci * co,
+                2.0 * (B * vs * ci + B * rows * co + B * c * (n + m * (2 if elu else 1))) + 4 * co * S * ci
+                + 4 * rows * S, BF16_PEAK_TFLOPS)
     if name == "cfsd_spiral_conv_fwd_in_swap":  # the swap + the xyz input conv (spiral length 9)
         bs, vs, rows, ci, co = a[4], a[14], a[15], a[16], a[17]
         B, S = bs * bs, 9

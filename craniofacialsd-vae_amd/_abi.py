@@ -48,6 +48,8 @@ SIGNATURES = {
                                                  _P]),
     "cfsd_spiral_conv_bwd_rowsub_pair_bf16": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I,
                                                    _I, _P]),
+    "cfsd_spiral_conv_bwd_weight_spmm_bf16": (_I, [_P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P,
+                                                   _P, _P, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_data_rowsub": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _Z, _I, _I, _I, _I, _I, _I,
                                               _P]),
     "cfsd_spiral_conv_bwd_data_rowsub_workspace": (_Z, [_I, _I, _I, _I]),

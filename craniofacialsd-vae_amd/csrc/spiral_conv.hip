@@ -3256,6 +3256,27 @@ extern "C" int cfsd_spiral_conv_bwd_rowsub_pair_bf16(const void* x, const int32_
                                       (bf16_t*)dx, workspace, nslab, vsrc, rows, batch, (hipStream_t)stream);
 }
 
+// ---- bf16 D3 dW slabs + the level-0 -> 1 Pool(up)^T in one launch (ABI 4.11)
+extern "C" int cfsd_spiral_conv_bwd_weight_spmm_bf16(const void* x, const int32_t* idx, const void* dpre,
+                                                     float* workspace, size_t workspace_bytes, int batch, int vsrc,
+                                                     int rows, int seq, int cin, int cout, const int32_t* ptr_s,
+                                                     const int32_t* col_s, const float* val_s,
+                                                     const int32_t* rows_s, const void* sx, const void* elu_y,
+                                                     void* y, int m, int n, int c, void* stream) {
+  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
+  if (rc) return rc;
+  if (!workspace || !ptr_s || !col_s || !val_s || !rows_s || !sx || !y)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_spmm_bf16: null pointer");
+  if (cin != 32 || cout != 32 || batch % 16 || m <= 0 || n <= 0 || c <= 0 || c % 8)
+    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_spmm_bf16: 32 -> 32, batch %% 16, c %% 8 only");
+  const int nslab = bf::dw_slabs(batch, rows, cin, cout);  // as cfsd_dw_reduce_batch's fused = 2 items
+  const size_t need = (size_t)nslab * ((size_t)cout * kSeq * cin + cout) * sizeof(float);
+  if (workspace_bytes < need) return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
+  return bf::launch_dw_spmm16((const bf16_t*)x, idx, (const bf16_t*)dpre, workspace, nslab, vsrc, rows, batch, ptr_s,
+                              col_s, val_s, rows_s, (const bf16_t*)sx, (const bf16_t*)elu_y, (bf16_t*)y, m, n, c,
+                              (hipStream_t)stream);
+}
+
 // ---- the same pair on the bf16 step's tensors (ABI 4.11)
 extern "C" int cfsd_spiral_conv_bwd_flat_pair_bf16(const void* x, const int32_t* idx, const void* dpre,
                                                    const int32_t* inv_flat, int flat_width, const void* w,

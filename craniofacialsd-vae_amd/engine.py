@@ -201,6 +201,7 @@ class SDVAEEngine:
         # the bf16 step's pair (cfsd_spiral_conv_bwd_flat_pair_bf16) at both vertex-major
         # levels: D3 29.0 vs 20.0 + 19.0 us, D2 14.7 vs 10.4 + 11.6 us, step 0.427 -> 0.409 ms
         self.rowsub_pair16 = os.environ.get("CFSD_RS16_PAIR", "1") != "0"
+        self.dw_spmm16 = os.environ.get("CFSD_DW_SPMM16", "0") != "0"
         self.vm_pair_levels16 = {int(c) for c in os.environ.get("CFSD_VM16_PAIR_LEVELS", "01") if c.isdigit()}
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
@@ -496,7 +497,8 @@ class SDVAEEngine:
                                          and ops.spiral_conv_bwd_flat_pair_workspace(bsz, nv[lv], T.seq[lv], cin,
                                                                                      cout) > 0)
             else:
-                b.vm_pair[("dec", i)] = flat_ok and lv in self.vm_pair_levels16
+                b.vm_pair[("dec", i)] = (flat_ok and lv in self.vm_pair_levels16
+                                         and not (lv == 0 and self.dw_spmm16 and i > 0))
         for i, (cin, cout, lv, _) in enumerate(S.dec_layers()):
             dw_region(("dec", i), nv[lv], nv[lv], T.seq[lv], cin, cout, True, lv in lp)
         for (cin, cout, lv) in S.enc_layers():
@@ -767,6 +769,11 @@ class SDVAEEngine:
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]
             w, _ = self._dec_w(i)
+            # bf16: level-0 dW slabs + this level's Pool(up)^T in one launch (after the dx)
+            fuse_up = (self.dw_spmm16 and lv == 0 and i > 0 and lv in b.xl and lv + 1 in b.xl
+                       and b.dec_up[i].dtype == torch.bfloat16 and b.dpre_dec[i - 1].dtype == torch.bfloat16
+                       and not b.vm_pair.get(("dec", i)) and cin == 32 and cout == 32
+                       and T.upT_nat[ui] is not None and self._flat_dx(b, lv, cin, cout))
             if b.vm_pair.get(("dec", i)) and b.dec_up[i].dtype == torch.bfloat16:  # bf16: the same pair
                 defer(ops.spiral_conv_bwd_flat_pair_bf16(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_flat[lv],
                                                          self._wx(f"de_layers.{i + 1}.conv.layer.weight"),
@@ -777,8 +784,9 @@ class SDVAEEngine:
                                                     w, None, None, b.g_dec_up[i],
                                                     workspace=b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
             elif lv in b.xl:  # vertex-major (bf16 or fp32) operands: dW slabs + dx
-                defer(ops.spiral_conv_bwd_weight_x(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
-                                                   b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
+                if not fuse_up:
+                    defer(ops.spiral_conv_bwd_weight_x(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
+                                                       b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
                 w16 = self._wx(f"de_layers.{i + 1}.conv.layer.weight")
                 if self._flat_dx(b, lv, cin, cout):  # vertex-major, batch % 16: one MFMA per list entry
                     ops.spiral_conv_bwd_data_flat(b.dpre_dec[i], T.spiral_flat[lv], w16, T.n_verts[lv],
@@ -807,7 +815,12 @@ class SDVAEEngine:
             # of every layer finished so far; the level-0/1 ones stream ~40 / 10 MB
             # and are not hosts
             sw = take_side() if (sch is not None and lv >= 2) else None
-            if i > 0:  # through Pool(up) into the previous Deblock's ELU
+            if fuse_up:
+                defer(ops.spiral_conv_bwd_weight_spmm_bf16(b.dec_up[i], T.spiral[lv], b.dpre_dec[i],
+                                                           b.ws_dw[("dec", i)], sch, b.g_dec_up[i],
+                                                           T.n_verts[lv + 1], b.dpre_dec[i - 1],
+                                                           elu_y=b.dec_out[i - 1]), f"de_layers.{i + 1}.conv.layer")
+            elif i > 0:  # through Pool(up) into the previous Deblock's ELU
                 self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dpre_dec[i - 1],
                            elu_y=b.dec_out[i - 1], sched=sch, side=sw)
             elif not fused_bn:

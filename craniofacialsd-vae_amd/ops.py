@@ -1156,6 +1156,38 @@ def spiral_conv_bwd_rowsub_pair_bf16(x, idx, dpre, flat, w, dx, elu_y=None, work
     return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2)
 
 
+def spiral_conv_bwd_weight_spmm_bf16(x, idx, dpre, workspace, sched, sx, m, out, elu_y=None):
+    """The bf16 step's D3 weight-gradient slabs (:func:`spiral_conv_bwd_weight_x`
+    deferred) and the visiting-order SpMM ``out = elu'(elu_y) * (P^T sx)``
+    (:func:`spmm_x` with ``sched``) as two roles of ONE launch
+    (``cfsd_spiral_conv_bwd_weight_spmm_bf16``, ABI 4.11); returns the
+    DeferredDw.  Every tensor bf16 vertex-major."""
+    bsz, vsrc, cin = x.shape
+    rows, seq = idx.shape
+    cout = dpre.shape[2]
+    _, n, c = sx.shape
+    for t, nm in ((x, "x"), (dpre, "dpre"), (sx, "sx"), (out, "out")):
+        _needl(t, None, nm, torch.bfloat16)
+        if not is_vm(t):
+            raise ValueError(f"spiral_conv_bwd_weight_spmm_bf16: {nm} must be vertex-major")
+    _needl(out, (bsz, m, c), "out", torch.bfloat16)
+    if elu_y is not None:
+        _needl(elu_y, (bsz, m, c), "elu_y", torch.bfloat16)
+        _same_layout(out, elu_y, "out and elu_y")
+    _need(idx, (rows, seq), torch.int32, "idx")
+    ptr_s, col_s, val_s, rows_s = sched
+    _need(ptr_s, (m + 1,), torch.int32, "ptr_s")
+    _need(rows_s, (m,), torch.int32, "rows_s")
+    _need(col_s, None, torch.int32, "col_s")
+    _need(val_s, (col_s.numel(),), name="val_s")
+    _need(workspace, None, name="workspace")
+    nbytes = workspace.numel() * workspace.element_size()
+    call("cfsd_spiral_conv_bwd_weight_spmm_bf16", ptr(x), ptr(idx), ptr(dpre), ptr(workspace),
+         ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout, ptr(ptr_s), ptr(col_s), ptr(val_s), ptr(rows_s),
+         ptr(sx), ptr(elu_y), ptr(out), m, n, c, stream_ptr())
+    return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2)
+
+
 def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None):
     """Fused dx + dW of the xyz output conv with bf16 (or fp32) x / elu_y /
     dx in either layout."""

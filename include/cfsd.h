@@ -248,6 +248,17 @@ int cfsd_spiral_conv_bwd_rowsub_pair_bf16(const void* x, const int32_t* idx, con
                                           const int32_t* inv_flat, int flat_width, const float* w, const void* elu_y,
                                           void* dx, float* workspace, size_t workspace_bytes, int batch, int vsrc,
                                           int rows, int seq, int cin, int cout, void* stream);
+/* The bf16 step's level-0 Deblock weight-gradient slabs (as
+ * cfsd_spiral_conv_bwd_weight_x deferred, fused = 2: x / dpre bf16
+ * vertex-major, 32 -> 32, batch % 16 == 0) and the visiting-order Pool(up)^T
+ * SpMM of cfsd_spmm_sched_csr (sx, y, elu_y bf16 vertex-major [*][batch][c],
+ * c % 8 == 0) as two workgroup roles of ONE launch (ABI 4.11).  Same values
+ * as the two calls. */
+int cfsd_spiral_conv_bwd_weight_spmm_bf16(const void* x, const int32_t* idx, const void* dpre, float* workspace,
+                                          size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
+                                          int cout, const int32_t* ptr_s, const int32_t* col_s, const float* val_s,
+                                          const int32_t* rows_s, const void* sx, const void* elu_y, void* y, int m,
+                                          int n, int c, void* stream);
 /* The same pair on the bf16 step's tensors (ABI 4.11): x, dpre, dx, elu_y
  * bf16 vertex-major, w the bf16 weight shadow; always deferred
  * (cfsd_dw_reduce_batch item with fused = 2; workspace as

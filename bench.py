@@ -752,10 +752,11 @@ def main():
         if "conv_pair_D3" in probe:  # bf16: the step runs D3's dx + dW as one launch (ABI 4.11)
             t = probe["conv_pair_D3"]
             pb = 3 * s_act * 16 * nv * 32 + 2 * 32 * 288 + nv * 9 * 4 + nv * 20 * 4
+            ptr_, psrc = pmc_traffic("conv_pair_d3_bf16_vm") if args.topology == "craniofacial" else (None, None)
             d3["conv_pair_D3"] = {"us_per_launch": t * 1e6, "bound": "hbm", "achieved": pb / t / 1e9,
                                   "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": pb / t / 1e9 / HBM_PEAK_GBS,
-                                  "tflops": 2 * flops / t / 1e12, "algorithmic_bytes": pb, "traffic": None,
-                                  "traffic_source": None}
+                                  "tflops": 2 * flops / t / 1e12, "algorithmic_bytes": pb, "traffic": ptr_,
+                                  "traffic_source": psrc}
             for k in ("conv_dx_D3", "conv_dw_D3"):
                 d3[k]["in_step"] = False  # measured standalone; the step runs the pair
         dom = max((k for k in d3 if d3[k].get("in_step", True)), key=lambda k: d3[k]["us_per_launch"])

@@ -27,7 +27,7 @@ for s in ${*:-tests bench prof32}; do
       CASES="fwd_d3_vm:conv_fwd_vm32<32, 32, 1, 2, 1>:conv_fwd_d3_vm dxf_d3_vm:conv_dx_flat_vm32<32, 32, 16, float>:conv_dx_d3_vm dw_d3_vm:conv_dw_vm32:conv_dw_d3_vm" OUT=$O/traffic32 TAG=$TAG bash tools/pmc_traffic.sh > /dev/null
       cat $O/traffic32/*.json ;;
     pmc16)
-      CASES="fwd_d3_b16:conv_fwd_vm16<32, 32, 1, unsigned short>:conv_fwd_d3_bf16_vm dxf_d3_b16:conv_dx_flat_vm16<32, 32, unsigned short, 16>:conv_dx_d3_bf16_vm dw_d3_b16:conv_dw_vm16<unsigned short>:conv_dw_d3_bf16_vm" OUT=$O/traffic16 TAG=$TAG bash tools/pmc_traffic.sh > /dev/null
+      CASES="fwd_d3_b16:conv_fwd_vm16<32, 32, 1, unsigned short>:conv_fwd_d3_bf16_vm dxf_d3_b16:conv_dx_flat_vm16<32, 32, unsigned short, 16>:conv_dx_d3_bf16_vm dw_d3_b16:conv_dw_vm16<unsigned short>:conv_dw_d3_bf16_vm pair_d3_b16:conv_bwd_vm16_pair<16>:conv_pair_d3_bf16_vm" OUT=$O/traffic16 TAG=$TAG bash tools/pmc_traffic.sh > /dev/null
       cat $O/traffic16/*.json ;;
     pmc0)  # the level-0 bandwidth kernels: up0 transpose, output-conv forward / backward
       CASES="spmm_up0T_vm:spmm_sched_csr_k:spmm_up0T_vm dout_fwd_vm:conv_fwd_out_vm:conv_out_fwd_vm dout_bwd_flat:conv_bwd_out_vm:conv_out_bwd_vm" OUT=$O/traffic0 TAG=$TAG bash tools/pmc_traffic.sh > /dev/null

@@ -30,7 +30,7 @@ for s in ${*:-tests bench prof32}; do
       CASES="fwd_d3_b16:conv_fwd_vm16<32, 32, 1, unsigned short>:conv_fwd_d3_bf16_vm dxf_d3_b16:conv_dx_flat_vm16<32, 32, unsigned short, 16>:conv_dx_d3_bf16_vm dw_d3_b16:conv_dw_vm16<unsigned short>:conv_dw_d3_bf16_vm pair_d3_b16:conv_bwd_vm16_pair<16>:conv_pair_d3_bf16_vm" OUT=$O/traffic16 TAG=$TAG bash tools/pmc_traffic.sh > /dev/null
       cat $O/traffic16/*.json ;;
     pmc0)  # the level-0 bandwidth kernels: up0 transpose, output-conv forward / backward
-      CASES="spmm_up0T_vm:spmm_sched_csr_k:spmm_up0T_vm dout_fwd_vm:conv_fwd_out_vm:conv_out_fwd_vm dout_bwd_flat:conv_bwd_out_vm:conv_out_bwd_vm" OUT=$O/traffic0 TAG=$TAG bash tools/pmc_traffic.sh > /dev/null
+      CASES="spmm_up0T_vm:spmm_sched_csr_k:spmm_up0T_vm dout_fwd_vm:conv_fwd_out_vm:conv_out_fwd_vm dout_bwd_flat:conv_bwd_out_vm:conv_out_bwd_vm spmm_up0T_b16:spmm_sched_csr_k<unsigned short, unsigned short, 8, true>:spmm_up0T_bf16_vm" OUT=$O/traffic0 TAG=$TAG bash tools/pmc_traffic.sh > /dev/null
       cat $O/traffic0/*.json ;;
     kbench)
       timeout -k 10 300 python tools/kbench.py ${KB_CASES} > $O/kbench.txt 2>&1 || { tail -30 $O/kbench.txt; exit 1; }

@@ -229,6 +229,8 @@ def build_cases(names=()):
     cases["pair_d3_b16"] = lambda: ops.spiral_conv_bwd_flat_pair_bf16(c.dec_up[3], T.spiral[0], c.dpre_dec[3],
                                                                       T.spiral_flat[0], w16, c.g_dec_up[3],
                                                                       workspace=c.ws_dw[("dec", 3)])
+    cases["spmm_up0T_b16"] = lambda: ops.spmm_x(T.upT_csr[0], c.g_dec_up[3], T.n_verts[1], elu_y=c.dec_out[2],
+                                                out=c.dpre_dec[2], sched=T.upT_nat[0])
     cases["spmm_up0_b16"] = lambda: ops.spmm_x(T.up_csr[0], c.dec_out[2], T.n_verts[0], out=c.dec_up[3],
                                                uniform=T.up_uniform[0])
     cases["spmm_up1_b16"] = lambda: ops.spmm_x(T.up_csr[1], c.dec_out[1], T.n_verts[1], out=c.dec_up[2],

@@ -12,7 +12,7 @@ export KB_ITERS=${KB_ITERS:-10}
 CASES=${CASES:-"fwd_d3:conv_fwd_mfma<32, 32, 1, 9>:conv_fwd_d3 dx_d3:conv_dx_mfma<32, 32, 9>:conv_dx_d3 dw_d3:conv_dw_mfma<32, 32>:conv_dw_d3"}
 # bf16: CASES="fwd_d3_b16:conv_fwd_b16<32, 32, 1, unsigned short>:conv_fwd_d3_bf16 ..."
 IFS=$'\n'
-for case in $(echo "$CASES" | sed 's/ \([a-z0-9_]*:\)/\n\1/g'); do
+for case in $(echo "$CASES" | sed 's/ \([A-Za-z0-9_]*:\)/\n\1/g'); do
   kb=${case%%:*}; rest=${case#*:}; pat=${rest%%:*}; name=${rest#*:}
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$kb/pmc_fetch -o run -- python3 tools/kbench.py $kb > $OUT/$kb.fetch.log 2>&1
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$kb/pmc_write -o run -- python3 tools/kbench.py $kb > $OUT/$kb.write.log 2>&1

@@ -1323,7 +1323,11 @@ __device__ __forceinline__ void adam_at(const DwAdam& a, const float* gp, float 
 // item: U*1024 + cout) are reduced four consecutive elements per lane with
 // 16-B loads (256 elements per workgroup); the others (small-channel slabs)
 // one element per lane.  Same per-element summation order either way.
-__global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
+#ifndef CFSD_RED_LOADS
+#define CFSD_RED_LOADS 8
+#endif
+constexpr int kRedLoads = CFSD_RED_LOADS;
+__global__ __launch_bounds__(1024, kRedLoads <= 8 ? 8 : 4) void dw_reduce_batch_k(const DwRedBatch B) {
   const bool fuse = B.adam.p != nullptr;
   if (fuse && (int)blockIdx.x >= B.blk_end) {  // Adam on the elements no item covers
     const DwAdam& a = B.adam;
@@ -1365,24 +1369,27 @@ __global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
   // 16 loads together, the partial last pass too (clamped loads, masked adds:
   // a per-slab tail loop paid one memory round trip per slab -- up to 14 for
   // the ~200-slab lat items)
+  // (kRedLoads slabs per batch: 8 keeps the kernel at <= 64 VGPRs, two
+  // workgroups per CU, so one workgroup's combine / Adam tail overlaps the
+  // other's loads; the per-element order is unchanged)
   f32x4 sum = {0.f, 0.f, 0.f, 0.f};
   const int last = d.n_slabs - 1;
   if (vec) {
-    for (int p = wv; p < d.n_slabs; p += 16 * 16) {
-      f32x4 t[16];
+    for (int p = wv; p < d.n_slabs; p += 16 * kRedLoads) {
+      f32x4 t[kRedLoads];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) t[j] = ld4(src + (long)min(p + 16 * j, last) * stride);
+      for (int j = 0; j < kRedLoads; ++j) t[j] = ld4(src + (long)min(p + 16 * j, last) * stride);
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
+      for (int j = 0; j < kRedLoads; ++j)
         if (p + 16 * j < d.n_slabs) sum += t[j];
     }
   } else {
-    for (int p = wv; p < d.n_slabs; p += 16 * 16) {
-      float t[16];
+    for (int p = wv; p < d.n_slabs; p += 16 * kRedLoads) {
+      float t[kRedLoads];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) t[j] = src[(long)min(p + 16 * j, last) * stride];
+      for (int j = 0; j < kRedLoads; ++j) t[j] = src[(long)min(p + 16 * j, last) * stride];
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
+      for (int j = 0; j < kRedLoads; ++j)
         if (p + 16 * j < d.n_slabs) sum.x += t[j];
     }
   }
@@ -1390,7 +1397,7 @@ __global__ __launch_bounds__(1024) void dw_reduce_batch_k(const DwRedBatch B) {
   __syncthreads();
   if (wv == 0 && valid) {
     f32x4 t = part[0][lane];
-#pragma unroll
+#pragma unroll 3
     for (int q = 1; q < 16; ++q) t += part[q][lane];
     float step_size = 0.f, sqrt_bc2 = 1.f;
     if (fuse) adam_consts(B.adam, step_size, sqrt_bc2);

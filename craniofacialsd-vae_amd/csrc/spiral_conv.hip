@@ -1319,6 +1319,29 @@ __device__ __forceinline__ void adam_at(const DwAdam& a, const float* gp, float 
   if (a.shadow) stf(a.shadow + o, pv);
 }
 
+// Adam on 4 consecutive elements (gradients g) starting at gp: every load
+// issued before the first update (the per-element helper's store-to-load
+// order serialised four memory round trips); same arithmetic per element.
+__device__ __forceinline__ void adam_at4(const DwAdam& a, const float* gp, const f32x4 g, float step_size,
+                                         float sqrt_bc2) {
+  const long o = gp - a.g;
+  float pv[4], mv[4], vv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    pv[e] = a.p[o + e];
+    mv[e] = a.m[o + e];
+    vv[e] = a.v[o + e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    adam_elem(pv[e], g[e], mv[e], vv[e], a.b1, a.b2, a.eps, a.wd, step_size, sqrt_bc2);
+    a.p[o + e] = pv[e];
+    a.m[o + e] = mv[e];
+    a.v[o + e] = vv[e];
+    if (a.shadow) stf(a.shadow + o + e, pv[e]);
+  }
+}
+
 // Items whose slab length is a multiple of 4 (every conv_dw_mfma / lat
 // item: U*1024 + cout) are reduced four consecutive elements per lane with
 // 16-B loads (256 elements per workgroup); the others (small-channel slabs)
@@ -1337,10 +1360,26 @@ __global__ __launch_bounds__(1024, kRedLoads <= 8 ? 8 : 4) void dw_reduce_batch_
     int ri = 0;
     while (ri + 1 < a.n_rest && rb >= a.rest_blk0[ri + 1]) ++ri;
     const long base = a.rest_lo[ri] + (long)(rb - a.rest_blk0[ri]) * 4096;
+    const long hi = a.rest_hi[ri];
+    float gv[4], pv[4], mv[4], vv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // all loads first (clamped), then the updates
+      const long o = min(base + k * 1024 + threadIdx.x, hi - 1);
+      gv[k] = a.g[o];
+      pv[k] = a.p[o];
+      mv[k] = a.m[o];
+      vv[k] = a.v[o];
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const long o = base + k * 1024 + threadIdx.x;
-      if (o < a.rest_hi[ri]) adam_at(a, a.g + o, a.g[o], step_size, sqrt_bc2);
+      if (o < hi) {
+        adam_elem(pv[k], gv[k], mv[k], vv[k], a.b1, a.b2, a.eps, a.wd, step_size, sqrt_bc2);
+        a.p[o] = pv[k];
+        a.m[o] = mv[k];
+        a.v[o] = vv[k];
+        if (a.shadow) stf(a.shadow + o, pv[k]);
+      }
     }
     return;
   }
@@ -1407,10 +1446,8 @@ __global__ __launch_bounds__(1024, kRedLoads <= 8 ? 8 : 4) void dw_reduce_batch_
       if (fuse) adam_at(B.adam, dst, t.x, step_size, sqrt_bc2);
     } else if (f >= nw) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        d.db[f - nw + e] = t[e];
-        if (fuse) adam_at(B.adam, d.db + f - nw + e, t[e], step_size, sqrt_bc2);
-      }
+      for (int e = 0; e < 4; ++e) d.db[f - nw + e] = t[e];
+      if (fuse) adam_at4(B.adam, d.db + f - nw, t, step_size, sqrt_bc2);
     } else {
       // 4 consecutive elements of one 32-wide unit row: 4 consecutive c
       const int CT = d.cin / 32, OT = d.cout / 32;
@@ -1420,10 +1457,8 @@ __global__ __launch_bounds__(1024, kRedLoads <= 8 ? 8 : 4) void dw_reduce_batch_
       const int sl = un / (CT * OT);
       float* dst = d.dw + (long)o * K + sl * d.cin + cc;  // 8-B aligned in the flat buffer
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        dst[e] = t[e];
-        if (fuse) adam_at(B.adam, dst + e, t[e], step_size, sqrt_bc2);
-      }
+      for (int e = 0; e < 4; ++e) dst[e] = t[e];
+      if (fuse) adam_at4(B.adam, dst, t, step_size, sqrt_bc2);
     }
   }
 }

@@ -61,26 +61,42 @@ class GradientAverager:
       has finalised it (RCCL runs on its own stream, ordered after the work
       already queued), ``finish(grad)`` joins them and scales.
     ``scale`` is the in-place scaling routine: libcfsd's ``cfsd_scale`` for
-    device buffers (default), or any callable ``(tensor, alpha)``."""
+    device buffers (default), or any callable ``(tensor, alpha)``.
+    ``always``: issue the collectives even at world 1 (a one-rank RCCL group
+    runs the data-parallel step structure on one GPU: the test that RCCL
+    loads, runs and captures into the step graph, bit-equal to the
+    single-process step)."""
 
-    def __init__(self, world=None, scale=None, group=None):
+    def __init__(self, world=None, scale=None, group=None, always=False):
         self.world = world if world is not None else (dist.get_world_size() if dist.is_initialized() else 1)
         self.group = group
+        self.always = bool(always)
         if scale is None:
             from . import ops
             scale = ops.scale
         self.scale = scale
         self._works = []
 
+    @property
+    def active(self):
+        """True when the step must exchange gradients (world > 1, or forced)."""
+        return self.world > 1 or self.always
+
+    @property
+    def capturable(self):
+        """The collectives can be recorded into a hipGraph: RCCL supports
+        stream capture (gloo runs on the host and cannot be captured)."""
+        return dist.is_initialized() and dist.get_backend(self.group) == "nccl"
+
     def __call__(self, grad):
-        if self.world <= 1:
+        if not self.active:
             return grad
         dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=self.group)
         self.scale(grad, 1.0 / self.world)
         return grad
 
     def bucket_ready(self, view):
-        if self.world > 1:
+        if self.active:
             self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
                                                async_op=True))
 
@@ -90,7 +106,7 @@ class GradientAverager:
         works, self._works = self._works, []
         for w in works:
             w.wait()
-        if self.world > 1 and scale:
+        if self.active and scale and self.world > 1:
             self.scale(grad, 1.0 / self.world)
         return grad
 

@@ -17,15 +17,19 @@ Step anatomy (every launch on one stream; nothing synchronises with the host):
   reduce.  On one GPU Adam rides in that reduce (``cfsd_dw_reduce_batch_adam``);
 * ``part_c``: (data-parallel only) Adam, after the gradient all-reduce.
 
-One GPU: the three parts are ONE graph (and a second graph, recorded on the
-first :meth:`TrainStep.run` of ``steps_per_graph`` or more steps, holds that
-many whole steps back to back: the host gap between consecutive replays,
-~8 us, is paid once per replay instead of once per step).  Data-parallel: three graphs, with
-the two RCCL all-reduce buckets issued between the replays -- the decoder /
-bottleneck bucket right after ``part_a`` so it overlaps ``part_b`` (RCCL runs
-on its own stream, ordered after the work already queued), the encoder-conv
-bucket after ``part_b`` -- then Adam with the 1/world averaging folded in
-(``cfsd_adam_scaled``).  The
+One graph per step whenever the collectives can be captured: on one GPU the
+three parts are ONE graph; data-parallel over RCCL the two bucket all-reduces
+are recorded INTO that graph (RCCL supports stream capture: the decoder /
+bottleneck bucket forks onto RCCL's stream right after ``part_a`` and overlaps
+``part_b``, the encoder-conv bucket follows ``part_b``, both join before
+Adam, which folds in the 1/world averaging -- ``cfsd_adam_scaled``).  A
+second graph, recorded on the first :meth:`TrainStep.run` of
+``steps_per_graph`` or more steps, holds that many whole steps back to back:
+the host gap between consecutive replays (~8 us) is paid once per replay
+instead of once per step.  A backend that cannot be captured (gloo: the
+one-GPU rehearsals and CPU tests) keeps three graphs with the all-reduces
+issued by the host between their replays (``CFSD_DP_GRAPH=three`` forces that
+structure over RCCL for A/B).  The
 justification for data parallelism is that every loss term is intra-swap-group
 (``model_manager.py:360-393``): each rank trains its own groups and the only
 exchange is the flat fp32 gradient.
@@ -42,7 +46,7 @@ class TrainStep:
 
     ``engine``: :class:`engine.SDVAEEngine`; ``data``: :class:`engine.
     ResidentData` (this rank's shard); ``averager``: a
-    :class:`dist.GradientAverager` (``None`` or world 1: single GPU);
+    :class:`dist.GradientAverager` (``None``, or world 1 without ``always``: single GPU);
     ``acc``: the device loss accumulator (default ``engine.loss_acc``).
 
     ``step()`` runs one training step -- eagerly until :meth:`capture` was
@@ -55,7 +59,7 @@ class TrainStep:
     def __init__(self, engine, data, averager=None, acc=None):
         self.eng = engine
         self.data = data
-        self.avg = averager if (averager is not None and averager.world > 1) else None
+        self.avg = averager if (averager is not None and averager.active) else None
         self.b = engine.buffers(engine.step_rows)
         self.acc = engine.loss_acc if acc is None else acc
         self.graphs = None
@@ -63,6 +67,10 @@ class TrainStep:
         # steps recorded into the multi-step graph run(k) replays (env: A/B)
         self.steps_per_graph = max(1, int(os.environ.get("CFSD_STEPS_PER_GRAPH", "16")))
         self._split = engine.enc_conv_numel()
+        # the whole step (collectives included) as one graph, unless the
+        # backend cannot be captured or the three-graph structure is forced
+        self.one_graph = self.avg is None or (os.environ.get("CFSD_DP_GRAPH", "one") != "three"
+                                              and self.avg.capturable)
 
     @property
     def world(self):
@@ -101,6 +109,7 @@ class TrainStep:
 
     # ------------------------------------------------------------ running
     def eager_step(self):
+        """One whole step in stream order (also what a one-graph capture records)."""
         self.part_a()
         if self.avg is not None:
             self._bucket_dec()
@@ -111,7 +120,8 @@ class TrainStep:
 
     def capture(self):
         """One real eager step on a side stream (lazy initialisation of
-        everything the launches touch), then record the graph(s)."""
+        everything the launches touch, RCCL's communicator included), then
+        record the graph(s)."""
         dev = self.eng.device
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -119,11 +129,10 @@ class TrainStep:
             self.eager_step()
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
-        if self.avg is None:
+        if self.one_graph:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.part_a()
-                self.part_b()
+                self.eager_step()
             self.graphs = [g]
         else:
             self.graphs = [torch.cuda.CUDAGraph() for _ in range(3)]
@@ -132,16 +141,15 @@ class TrainStep:
                     fn()
 
     def capture_multi(self):
-        """Record (once) the single-GPU graph holding ``steps_per_graph``
-        whole steps, which :meth:`run` replays k // steps_per_graph times: the
-        per-replay host gap (~8 us between consecutive replays) is paid once
-        per that many steps.  Nothing runs while recording."""
-        if self.graph_multi is None and self.graphs is not None and self.avg is None:
+        """Record (once) the graph holding ``steps_per_graph`` whole steps,
+        which :meth:`run` replays k // steps_per_graph times: the per-replay
+        host gap (~8 us between consecutive replays) is paid once per that
+        many steps.  Nothing runs while recording."""
+        if self.graph_multi is None and self.graphs is not None and self.one_graph:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 for _ in range(self.steps_per_graph):
-                    self.part_a()
-                    self.part_b()
+                    self.eager_step()
             self.graph_multi = g
 
     capture_pair = capture_multi  # (round-4 name)
@@ -149,7 +157,7 @@ class TrainStep:
     def step(self):
         if self.graphs is None:
             return self.eager_step()
-        if self.avg is None:
+        if self.one_graph:
             self.graphs[0].replay()
             return
         ga, gb, gc = self.graphs
@@ -163,8 +171,8 @@ class TrainStep:
 
     def run(self, k):
         """``k`` training steps (the same steps as ``k`` calls of :meth:`step`);
-        a captured single-GPU runner replays the multi-step graph."""
-        if self.graphs is not None and self.avg is None:
+        a one-graph runner replays the multi-step graph."""
+        if self.graphs is not None and self.one_graph:
             n = self.steps_per_graph
             if k >= n:
                 self.capture_multi()

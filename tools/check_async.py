@@ -3,7 +3,15 @@ VGPR still being written by an outstanding global load (i.e. before the
 s_waitcnt vmcnt that retires it), following the layout order of each kernel
 (branches are not followed; loop back-edges are ignored).
 
-usage: python tools/check_async.py file.s kernel_substring [...]"""
+The hazard: ``gload*_async`` (cfsd_common.h) issues a global load in inline
+asm, hidden from hipcc's waitcnt bookkeeping, and ``vm_wait*`` retires it by
+count; if hipcc schedules a read of the destination (or a copy of it) before
+that wait, the kernel silently uses stale data.  ``build()`` runs this over
+every kernel of every source (``make -C craniofacialsd-vae_amd/csrc check``),
+so a compiler update that reintroduces the hazard fails the build.
+
+usage: python tools/check_async.py file.s kernel_substring [...]
+       python tools/check_async.py --all file.s [...]   (every kernel)"""
 import re
 import sys
 
@@ -16,7 +24,7 @@ def regs(tok):
     return {int(m.group(1))} if m else set()
 
 
-def scan(lines, name):
+def scan(lines, name, log=print):
     out = []  # outstanding VMEM ops: (dest regs, line)
     issues = 0
     for ln in lines:
@@ -43,7 +51,7 @@ def scan(lines, name):
             for d, l0 in out:
                 if d & srcs:
                     issues += 1
-                    print(f"  [{name}] address reads in-flight reg: {t}   (load: {l0})")
+                    log(f"  [{name}] address reads in-flight reg: {t}   (load: {l0})")
             out.append((regs(ops[0]), t))
             continue
         if op.startswith(("global_store", "buffer_store", "scratch_store")):
@@ -51,7 +59,7 @@ def scan(lines, name):
             for d, l0 in out:
                 if d & srcs:
                     issues += 1
-                    print(f"  [{name}] store reads in-flight reg: {t}   (load: {l0})")
+                    log(f"  [{name}] store reads in-flight reg: {t}   (load: {l0})")
             out.append((set(), t))
             continue
         # generic instruction: operands after the first are sources (first is dst),
@@ -63,23 +71,47 @@ def scan(lines, name):
         for d, l0 in out:
             if d & srcs:
                 issues += 1
-                print(f"  [{name}] reads in-flight reg: {t}   (load: {l0})")
+                log(f"  [{name}] reads in-flight reg: {t}   (load: {l0})")
         # a write to an in-flight destination is also a hazard (WAW)
         for d, l0 in out:
             if d & dst and not op.startswith("s_"):
                 issues += 1
-                print(f"  [{name}] overwrites in-flight reg: {t}   (load: {l0})")
+                log(f"  [{name}] overwrites in-flight reg: {t}   (load: {l0})")
     return issues
 
 
-src = open(sys.argv[1]).read().splitlines()
-total = 0
-for pat in sys.argv[2:]:
-    starts = [i for i, l in enumerate(src) if pat in l and l.split(";")[0].rstrip().endswith(":") and not l.startswith("\t")]
-    for st in starts:
-        en = next(i for i in range(st, len(src)) if "s_endpgm" in src[i])
-        name = src[st].split(":")[0][:60]
-        n = scan(src[st:en], name)
-        print(f"{name}: {n} potential hazards")
-        total += n
-sys.exit(1 if total else 0)
+def kernels(src, pats=None):
+    """(name, first line, end line) of every kernel body in a -S dump whose
+    label contains one of ``pats`` (all kernels when ``pats`` is None)."""
+    for i, l in enumerate(src):
+        if l.startswith("\t") or not l.split(";")[0].rstrip().endswith(":"):
+            continue
+        if pats is None and not l.startswith("_Z"):
+            continue
+        if pats is not None and not any(p in l for p in pats):
+            continue
+        en = next((j for j in range(i, len(src)) if "s_endpgm" in src[j]), None)
+        if en is not None:
+            yield src[i].split(":")[0], i, en
+
+
+def main(argv, log=print):
+    if argv and argv[0] == "--all":
+        files, pats = argv[1:], None
+    else:
+        files, pats = argv[:1], argv[1:]
+    total, n_k = 0, 0
+    for fn in files:
+        src = open(fn).read().splitlines()
+        for name, st, en in kernels(src, pats):
+            n = scan(src[st:en], name[:60], log)
+            n_k += 1
+            if n or pats is not None:
+                log(f"{name[:60]}: {n} potential hazards")
+            total += n
+    log(f"check_async: {n_k} kernels in {len(files)} file(s), {total} potential hazards")
+    return 1 if total else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))

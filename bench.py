@@ -65,7 +65,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU-baseline sample budget")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-extras", action="store_true",
-                   help="skip the secondary measurements (synthetic ~5k line, kernel trace)")
+                   help="skip the secondary measurements (synthetic ~5k line, kernel trace, bf16 block)")
+    p.add_argument("--no-bf16", action="store_true",
+                   help="skip the bf16 block (configs C3/C5's precision, timed in the same run)")
     return p.parse_args()
 
 
@@ -375,10 +377,11 @@ BOOKKEEPING = ("cfsd_step_begin", "cfsd_loss_finalize", "cfsd_dw_reduce_batch", 
 def step_roofline(runner, ms_per_step):
     """Time-weighted roofline of one training step: every launch of an eager
     step is timed with a HIP event pair on its stream (queued behind a sleep
-    kernel so the device runs them back-to-back, as in the graph), priced at
-    its roofline time max(flop/peak, bytes/8 TB/s) from the work the algorithm
-    requires (Enblock row subset applied), and the sum of those ideal times
-    is divided by the measured time."""
+    kernel so the device runs them back-to-back, as in the graph) and scaled
+    to the graph step (the pairs' own overhead makes the eager sum exceed it),
+    priced at its roofline time max(flop/peak, bytes/8 TB/s) from the work the
+    algorithm requires (Enblock row subset applied), and the sum of those
+    ideal times is divided by the measured time."""
     torch.cuda.synchronize()
     torch.cuda._sleep(50_000_000)
     with _abi.trace_launches() as rec:
@@ -394,15 +397,25 @@ def step_roofline(runner, ms_per_step):
         ideal_sum += ideal
         flop_sum += fl
         byte_sum += by
+    # The eager event pairs add per-launch overhead the graph replay does not
+    # pay (their sum exceeds the graph step): every launch time is scaled by
+    # one factor so that they sum to at most the measured (graph) step.
+    raw_sum = t_sum
+    scale = min(1.0, (ms_per_step * 1e-3) / t_sum) if t_sum else 1.0
+    rows = [(n, t * scale, fl, by, i) for n, t, fl, by, i in rows]
+    t_sum *= scale
     top = sorted(rows, key=lambda r: -r[1])[:8]
     return {
         "launches": len(rows), "kernel_time_us": t_sum * 1e6,
+        "eager_kernel_time_us": raw_sum * 1e6, "eager_to_graph_scale": scale,
         "required_gflop_per_step": flop_sum / 1e9, "algorithmic_mb_per_step": byte_sum / 1e6,
         "ideal_time_us": ideal_sum * 1e6,
         "frac_of_kernel_time": ideal_sum / t_sum if t_sum else None,
         "frac_of_step_time": ideal_sum / (ms_per_step * 1e-3),
         "achieved_tflops_step": flop_sum / (ms_per_step * 1e-3) / 1e12,
-        "note": "frac = sum over launches of max(flop/peak, bytes/HBM) / measured time; "
+        "note": "per-launch times: eager HIP event pairs, scaled by eager_to_graph_scale so that they sum to "
+                "at most the graph-replayed step; "
+                "frac = sum over launches of max(flop/peak, bytes/HBM) / measured time; "
                 "bookkeeping launches (" + ", ".join(BOOKKEEPING) + ") count as time with no required "
                 "work; cfsd_dw_reduce_batch_adam is priced at Adam's 7 x 4 B per parameter only",
         "unpriced_work_launches": sorted({n for n, _, fl, by, _ in rows if fl == 0 and by == 0
@@ -662,6 +675,105 @@ def synth5k_line(device, steps=500, warmup=20):
             "ms_per_step": el / steps * 1e3, "steps": steps}
 
 
+def d3_roofline(runner, probe, topo_name):
+    """Per-launch roofline of the three D3 (decoder level 0, 32 -> 32) conv
+    kernels, 5.02 GFLOP each, from their live HIP-event times (``probe``);
+    returns (kernels, dominant key, kernel names).  fp32: MFMA bound (AI 72
+    flop/B > ridge 19.7); bf16: HBM bound (AI ~140 flop/B < ridge 312),
+    priced on algorithmic bytes (input + output once + indices)."""
+    nv = runner.topo.n_verts[0]
+    flops = 2.0 * 16 * nv * 9 * 32 * 32
+    bf = runner.precision == "bf16"
+    s_act = 2 if bf else 4
+    d3_bytes = {"conv_fwd_D3": s_act * 16 * nv * 64 + nv * 36,
+                "conv_dx_D3": s_act * 16 * nv * 64 + nv * 9 * 16,
+                "conv_dw_D3": s_act * 16 * nv * 64 + nv * 36}
+    d3 = {}
+    vm0 = 0 in runner.b.xl  # level-0 tensors vertex-major (the kernels below)
+    for name, key in (("conv_fwd_D3", "conv_fwd_d3"), ("conv_dx_D3", "conv_dx_d3"), ("conv_dw_D3", "conv_dw_d3")):
+        t = probe[name]
+        key = key + ("_bf16" if bf else "") + ("_vm" if vm0 else "")
+        traffic, traffic_src = pmc_traffic(key) if topo_name == "craniofacial" else (None, None)
+        if bf:
+            d3[name] = {"us_per_launch": t * 1e6, "bound": "hbm", "achieved": d3_bytes[name] / t / 1e9,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": d3_bytes[name] / t / 1e9 / HBM_PEAK_GBS, "tflops": flops / t / 1e12,
+                        "algorithmic_bytes": d3_bytes[name], "traffic": traffic, "traffic_source": traffic_src}
+        else:
+            d3[name] = {"us_per_launch": t * 1e6, "bound": "mfma", "achieved": flops / t / 1e12,
+                        "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS, "algorithmic_flop": flops,
+                        "traffic": traffic, "traffic_source": traffic_src}
+    if "conv_pair_D3" in probe:  # bf16: the step runs D3's dx + dW as one launch (ABI 4.11)
+        t = probe["conv_pair_D3"]
+        pb = 3 * s_act * 16 * nv * 32 + 2 * 32 * 288 + nv * 9 * 4 + nv * 20 * 4
+        ptr_, psrc = pmc_traffic("conv_pair_d3_bf16_vm") if topo_name == "craniofacial" else (None, None)
+        d3["conv_pair_D3"] = {"us_per_launch": t * 1e6, "bound": "hbm", "achieved": pb / t / 1e9,
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": pb / t / 1e9 / HBM_PEAK_GBS,
+                              "tflops": 2 * flops / t / 1e12, "algorithmic_bytes": pb, "traffic": ptr_,
+                              "traffic_source": psrc}
+        for k in ("conv_dx_D3", "conv_dw_D3"):
+            d3[k]["in_step"] = False  # measured standalone; the step runs the pair
+    dom = max((k for k in d3 if d3[k].get("in_step", True)), key=lambda k: d3[k]["us_per_launch"])
+    if bf:
+        kern_names = {"conv_fwd_D3": "conv_fwd_vm16<32,32> (decoder level 0 forward, bf16, vertex-major)",
+                      "conv_dx_D3": "conv_dx_flat_vm16<32,32> (decoder level 0 data gradient, bf16, "
+                                    "vertex-major flat list)",
+                      "conv_dw_D3": "conv_dw_vm16 (decoder level 0 weight gradient, bf16, vertex-major)",
+                      "conv_pair_D3": "conv_bwd_vm16_pair (decoder level 0 dx + dW slabs, bf16, vertex-major, "
+                                      "one launch)"}
+    elif vm0:
+        kern_names = {"conv_fwd_D3": "conv_fwd_vm32<32,32> (decoder level 0 forward, vertex-major)",
+                      "conv_dx_D3": "conv_dx_flat_vm32<32,32> (decoder level 0 data gradient, vertex-major "
+                                    "flat list)",
+                      "conv_dw_D3": "conv_dw_vm32 (decoder level 0 weight gradient, vertex-major)"}
+    else:
+        kern_names = {"conv_fwd_D3": "conv_fwd_mfma<32,32> (decoder level 0 forward)",
+                      "conv_dx_D3": "conv_dx_mfma<32,32> (decoder level 0 data gradient)",
+                      "conv_dw_D3": "conv_dw_mfma<32,32> (decoder level 0 weight gradient)"}
+    return d3, dom, dict({"kernel": "cfsd " + kern_names[dom]}, **d3[dom])
+
+
+def timed(runner, steps, warmup, world, device):
+    """Capture, W untimed warm-up steps, then EXACTLY K steps between a
+    barrier + synchronize on both sides; returns (this rank's seconds, the
+    max over ranks)."""
+    if runner.use_graph:
+        runner.capture()
+    runner.run(warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    runner.run(steps)  # exactly `steps` training steps (steps_per_graph per replay of the multi-step graph)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el_rank = time.perf_counter() - t0
+    return el_rank, cdist.max_over_ranks(el_rank, device)
+
+
+def bf16_block(args, world, rank, device):
+    """Configs C3 / C5's precision in the same run: the same step (same
+    workload, per-GPU batch and parallelism) with bf16 level-0/1 tensors on
+    bf16 MFMA, its own timed region, its own D3 roofline (against HBM)."""
+    runner = Runner(world, rank, device, args.dataset, not args.no_graph, args.topology, "bf16")
+    el_rank, el = timed(runner, args.steps, args.warmup, world, device)
+    losses = runner.eng.loss_acc.cpu().numpy()
+    runner.eng.check_health()
+    probe = kernel_probe(runner)
+    d3, _, roof = d3_roofline(runner, probe, args.topology)
+    out = {"metric": METRIC, "value": 16 * world * args.steps / el, "unit": "meshes/s",
+           "ms_per_step": el / args.steps * 1e3, "steps": args.steps, "warmup": args.warmup, "dtype": "bf16",
+           "config": "the main line's workload and parallelism; levels 0-1 bf16 vertex-major, coarse levels, "
+                     "losses, gradients, Adam and master weights fp32",
+           "roofline": roof, "d3_kernels": d3, "losses_finite": bool(np.isfinite(losses).all())}
+    del runner
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -687,36 +799,25 @@ def main():
     runner = Runner(world, rank, device, args.dataset, not args.no_graph, args.topology, args.precision,
                     meshes=meshes, norm=norm, vertex_major=not args.batch_major)
     del meshes
-    if runner.use_graph:
-        runner.capture()
-    runner.run(args.warmup)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    runner.run(args.steps)  # exactly args.steps training steps (steps_per_graph per replay of the multi-step graph)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el_rank = time.perf_counter() - t0
-    el = cdist.max_over_ranks(el_rank, device)
+    el_rank, el = timed(runner, args.steps, args.warmup, world, device)
     dcheck = dist_check(runner, el_rank, args.steps, backend, os.environ.get("CFSD_SHARE_DEVICE")) \
         if world > 1 else None
     meshes = 16 * world * args.steps
     ms_per_step = el / args.steps * 1e3
     losses = runner.eng.loss_acc.cpu().numpy()
     finite = bool(np.isfinite(losses).all())
+    runner.eng.check_health()  # the one-launch bottleneck backward never gave up waiting
     probe = kernel_probe(runner)
     steprf = None if args.no_extras else step_roofline(runner, ms_per_step)
+    bf = runner.precision == "bf16"
+    bfb = None
+    if not (bf or args.no_extras or args.no_bf16 or args.augmented or args.batch_major):
+        bfb = bf16_block(args, world, rank, device)
     if rank == 0:
         nv = runner.topo.n_verts[0]
-        # dominant kernel: fused gather+contraction of D3 (32 -> 32, nv rows x 16)
-        flops = 2.0 * 16 * nv * 9 * 32 * 32
         gather_bytes = 16 * nv * (32 + 9 * 32) * 4 + nv * 9 * 4
         t_g = probe["spiral_gather_L0"]
         parity = c1_parity(device)
-        bf = runner.precision == "bf16"
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args.cpu_seconds)  # N=1 only
         s5k = None
         if not (args.no_extras or world > 1 or args.topology != "craniofacial" or bf):
@@ -724,58 +825,7 @@ def main():
                 s5k = synth5k_line(device)
             except (ImportError, AttributeError) as e:  # precompute not available
                 s5k = {"error": str(e)}
-        # the three D3 (decoder level 0, 32 -> 32) conv kernels, 5.02 GFLOP
-        # each; `roofline` is the dominant one (longest launch).  fp32: MFMA
-        # bound (AI 72 flop/B > ridge 19.7); bf16: HBM bound (AI ~140 flop/B
-        # < ridge 312), priced on algorithmic bytes (input + output once).
-        s_act = 2 if bf else 4
-        d3_bytes = {"conv_fwd_D3": s_act * 16 * nv * 64 + nv * 36,
-                    "conv_dx_D3": s_act * 16 * nv * 64 + nv * 9 * 16,
-                    "conv_dw_D3": s_act * 16 * nv * 64 + nv * 36}
-        d3 = {}
-        vm0 = 0 in runner.b.xl  # level-0 tensors vertex-major (the kernels below)
-        for name, key in (("conv_fwd_D3", "conv_fwd_d3"), ("conv_dx_D3", "conv_dx_d3"),
-                          ("conv_dw_D3", "conv_dw_d3")):
-            t = probe[name]
-            key = key + ("_bf16" if bf else "") + ("_vm" if vm0 else "")
-            traffic, traffic_src = pmc_traffic(key) if args.topology == "craniofacial" else (None, None)
-            if bf:
-                d3[name] = {"us_per_launch": t * 1e6, "bound": "hbm", "achieved": d3_bytes[name] / t / 1e9,
-                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": d3_bytes[name] / t / 1e9 / HBM_PEAK_GBS, "tflops": flops / t / 1e12,
-                            "algorithmic_bytes": d3_bytes[name], "traffic": traffic, "traffic_source": traffic_src}
-            else:
-                d3[name] = {"us_per_launch": t * 1e6, "bound": "mfma", "achieved": flops / t / 1e12,
-                            "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                            "frac": flops / t / 1e12 / FP32_PEAK_TFLOPS, "algorithmic_flop": flops,
-                            "traffic": traffic, "traffic_source": traffic_src}
-        if "conv_pair_D3" in probe:  # bf16: the step runs D3's dx + dW as one launch (ABI 4.11)
-            t = probe["conv_pair_D3"]
-            pb = 3 * s_act * 16 * nv * 32 + 2 * 32 * 288 + nv * 9 * 4 + nv * 20 * 4
-            ptr_, psrc = pmc_traffic("conv_pair_d3_bf16_vm") if args.topology == "craniofacial" else (None, None)
-            d3["conv_pair_D3"] = {"us_per_launch": t * 1e6, "bound": "hbm", "achieved": pb / t / 1e9,
-                                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": pb / t / 1e9 / HBM_PEAK_GBS,
-                                  "tflops": 2 * flops / t / 1e12, "algorithmic_bytes": pb, "traffic": ptr_,
-                                  "traffic_source": psrc}
-            for k in ("conv_dx_D3", "conv_dw_D3"):
-                d3[k]["in_step"] = False  # measured standalone; the step runs the pair
-        dom = max((k for k in d3 if d3[k].get("in_step", True)), key=lambda k: d3[k]["us_per_launch"])
-        if bf:
-            kern_names = {"conv_fwd_D3": "conv_fwd_vm16<32,32> (decoder level 0 forward, bf16, vertex-major)",
-                          "conv_dx_D3": "conv_dx_flat_vm16<32,32> (decoder level 0 data gradient, bf16, "
-                                        "vertex-major flat list)",
-                          "conv_dw_D3": "conv_dw_vm16 (decoder level 0 weight gradient, bf16, vertex-major)",
-                          "conv_pair_D3": "conv_bwd_vm16_pair (decoder level 0 dx + dW slabs, bf16, vertex-major, "
-                                          "one launch)"}
-        elif vm0:
-            kern_names = {"conv_fwd_D3": "conv_fwd_vm32<32,32> (decoder level 0 forward, vertex-major)",
-                          "conv_dx_D3": "conv_dx_flat_vm32<32,32> (decoder level 0 data gradient, vertex-major "
-                                        "flat list)",
-                          "conv_dw_D3": "conv_dw_vm32 (decoder level 0 weight gradient, vertex-major)"}
-        else:
-            kern_names = {"conv_fwd_D3": "conv_fwd_mfma<32,32> (decoder level 0 forward)",
-                          "conv_dx_D3": "conv_dx_mfma<32,32> (decoder level 0 data gradient)",
-                          "conv_dw_D3": "conv_dw_mfma<32,32> (decoder level 0 weight gradient)"}
+        d3, _, roof = d3_roofline(runner, probe, args.topology)
         out = {
             "metric": METRIC, "value": meshes / el, "unit": "meshes/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
@@ -793,10 +843,13 @@ def main():
                        "global_batch": 16 * world, "per_gpu_batch": 16,
                        "resident_meshes_per_gpu": runner.data.n_items,
                        "parallelism": f"dp{world}", "graph": runner.use_graph,
+                       "step_graph": ("one graph per step" if runner.ts.one_graph else "three graphs") +
+                                     (", collectives captured" if (world > 1 and runner.ts.one_graph) else ""),
                        "collective": None if world == 1 else
                        (("rccl" if backend == "nccl" else backend) + " all_reduce, 2 buckets overlapped")},
-            "roofline": dict({"kernel": "cfsd " + kern_names[dom]}, **d3[dom]),
+            "roofline": roof,
             "d3_kernels": d3,
+            "bf16": bfb,
             "step_roofline": steprf,
             "gather_roofline": {"kernel": "cfsd spiral_gather_k (level 0, 32 ch, 16 meshes)",
                                 "bound": "hbm", "achieved": gather_bytes / t_g / 1e9,

@@ -54,6 +54,7 @@ SIGNATURES = {
                                               _P]),
     "cfsd_spiral_conv_bwd_data_rowsub_workspace": (_Z, [_I, _I, _I, _I]),
     "cfsd_linear_bwd_split_parts": (_I, [_I]),
+    "cfsd_bottleneck_bwd_exchange_floats": (_Z, [_I, _I, _I, _I]),
     "cfsd_linear_bwd_split": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "cfsd_latent_bwd_parts": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spiral_gather": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),

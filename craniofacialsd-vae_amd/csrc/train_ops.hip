@@ -878,13 +878,19 @@ __global__ __launch_bounds__(256) void linear_bwd_pair_k(const float* __restrict
 // L workgroup raises one flag per E group and the E workgroups count
 // themselves out in two levels, the last one zeroing every counter, so graph
 // replays and eager calls start from zero.  A wait gives up after ~2^20 polls
-// (a broken launch returns garbage instead of hanging the GPU).  Every value
+// and raises a sticky bit in sync[kBnSyncErr] (the host checks it: a broken
+// launch fails loudly instead of training on garbage, and never hangs the GPU).
+// Exchanged values travel through `exchange` in LINE-EXCLUSIVE layout: every
+// 128-B line of it is written by exactly one workgroup (A: its partials at a
+// 32-float-aligned stride; L: whole dmulv rows at a 32-float-aligned stride),
+// so no L2 ever holds a partial copy of a line another XCD writes, and a
+// reader's L2 can only hold a line its own XCD wrote completely.  Every value
 // is formed by the same per-element operations in the same order as the four
 // launches: bit-identical (GPU-tested).  Per-workgroup timestamps (round 5):
 // A 0-11.7 us, L 12.1-15.9, E 16.3-21.4; the four launches take ~29 us.
 // Measured on the way (each fixed): acquiring polls 173 us, an acq_rel
 // done-count 44 us, one shared done-counter 33 us, uncached exchanged loads
-// ~29 us.
+// ~29 us, one acquire per waiting workgroup ~20 us.
 struct BneckArgs {
   const int* up_ptr;  // CSR of Pool(up)^T, rows = coarse vertices (plain per-row order)
   const int* up_col;
@@ -893,7 +899,7 @@ struct BneckArgs {
   int n_up, cup;
   const float* z;  // decoder Linear: z [m][kd], W_d [nd][kd] (nd = coarse vertices x cup)
   const float* wd;
-  float* parts;  // [ndx_d][m][kd]
+  float* parts;  // exchange: [ndx_d][pstride], pstride = m x kd rounded up to 32 floats
   float* dwd;
   float* dbd;
   int m, kd, nd, ndx_d, ndw_d;
@@ -902,7 +908,9 @@ struct BneckArgs {
   const float* dlat;
   float* dmulv;
   const float* zval;
-  int L, train, is_vae, sigmoid, nb_lat;
+  int L, train, is_vae, sigmoid, nb_lat, lat_rows;  // L workgroup = lat_rows whole rows of dmulv
+  float* xdmulv;  // exchange: [m][dstride], dstride = ne rounded up to 32 floats
+  int pstride, dstride;
   const float* xe;  // encoder Linear: x_e [m][ke], W_e [ne][ke]
   const float* we;
   const float* elu_y;
@@ -916,7 +924,9 @@ constexpr int kBnSyncLine = 32;  // ints per 128-B line
 constexpr int kBnGroups = 8;
 constexpr int kBnSyncA = 0, kBnSyncL = kBnSyncLine, kBnSyncTop = 2 * kBnSyncLine, kBnSyncSub = 3 * kBnSyncLine;
 constexpr int kBnSyncFlag = kBnSyncSub + kBnGroups * kBnSyncLine;  // L-done flag per E group
+constexpr int kBnSyncErr = kBnSyncTop + 1;  // sticky: bit r set when a role-r wait timed out (host-checked)
 static_assert(kBnSyncFlag + kBnGroups * kBnSyncLine == 608, "cfsd.h documents 608 sync ints");
+static_assert(kBnSyncErr == CFSD_BN_SYNC_ERR, "cfsd.h documents the error word");
 constexpr int kBnDwRows = 4;  // encoder dW rows per E workgroup (x loaded once for all of them)
 constexpr int kBnWPer = kLinSplitN * kLinSplitK / 256;  // W-slice floats per thread of an A workgroup
 constexpr int kBnMaxParts = 80;                          // decoder-Linear partials (nd <= 80 x 64)
@@ -927,12 +937,16 @@ __device__ __forceinline__ void bn_arrive(int* ctr) {
 }
 // relaxed polls (an acquiring poll invalidates the XCD's L2 every time: the
 // waiting workgroups then evict the running ones' operands -- 173 vs ~20 us)
-__device__ __forceinline__ void bn_wait(int* ctr, int target) {
+// A wait that gives up sets `code` in the sticky error word (never cleared by
+// the kernel): the launch then returns wrong values, which the host refuses.
+__device__ __forceinline__ void bn_wait(int* ctr, int target, int* err, int code) {
   if (threadIdx.x == 0) {
-    for (int it = 0; it < (1 << 20); ++it) {
-      if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-      __builtin_amdgcn_s_sleep(8);
+    bool seen = false;
+    for (int it = 0; it < (1 << 20) && !seen; ++it) {
+      seen = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+      if (!seen) __builtin_amdgcn_s_sleep(8);
     }
+    if (!seen) __hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
 }
@@ -940,7 +954,9 @@ __device__ __forceinline__ void bn_wait(int* ctr, int target) {
 // loads after the counter / flag is seen.  No line of them can be stale in a
 // reader's L2: every dispatch starts with the caches invalidated, nothing
 // reads them in this launch before the writers' release (an L2 writeback),
-// and the writer's own XCD keeps the written (then clean) lines.  Acquiring
+// each exchange line has ONE writer workgroup (no XCD holds a partial copy
+// of a line another XCD writes), and the writer's own XCD keeps its written
+// (then clean) lines.  Acquiring
 // each wait instead (an L2 invalidate by each of ~600 workgroups) cost ~20
 // us, and agent-scope atomic loads (uncached) of the 9.6-KB dmulv by every E
 // workgroup put ~12k requests on a handful of lines (~15 us).
@@ -1011,36 +1027,41 @@ __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
       const int i = e / a.kd, kk = e % a.kd;
       float acc = 0.f;
       for (int c = 0; c < nc; ++c) acc = fmaf(dl[i * kLinSplitN + c], wl[c * a.kd + kk], acc);
-      a.parts[(long)bid * m * a.kd + e] = acc;
+      a.parts[(long)bid * a.pstride + e] = acc;
     }
     bn_arrive(a.sync + kBnSyncA);
     return;
   }
-  if (bid < b_dwd) {  // L: latent_bwd_k's element map
-    bn_wait(a.sync + kBnSyncA, a.ndx_d);
-    const int e = (bid - b_lat) * blockDim.x + threadIdx.x;
-    if (e < m * a.L) {
-      const int B = m, L = a.L, i = e / L, l = e % L;
+  if (bid < b_dwd) {  // L: latent_bwd_k's per-element arithmetic, lat_rows whole dmulv rows per workgroup
+    bn_wait(a.sync + kBnSyncA, a.ndx_d, a.sync + kBnSyncErr, 1);
+    const int B = m, L = a.L;
+    const int i = (bid - b_lat) * a.lat_rows + (int)threadIdx.x / L, l = (int)threadIdx.x % L;
+    if ((int)threadIdx.x < a.lat_rows * L && i < B) {
+      const int e = i * L + l;
       // every partial in flight at once (one round trip; 16-load batches were
       // 5 trips, 4.5 us), then summed in part order as latent_bwd_k
       float t[kBnMaxParts];
 #pragma unroll
-      for (int j = 0; j < kBnMaxParts; ++j) t[j] = bn_ld(a.parts + (long)min(j, a.ndx_d - 1) * B * L + e);
+      for (int j = 0; j < kBnMaxParts; ++j) t[j] = bn_ld(a.parts + (long)min(j, a.ndx_d - 1) * a.pstride + e);
       float dzd = t[0];
 #pragma unroll
       for (int j = 1; j < kBnMaxParts; ++j)
         if (j < a.ndx_d) dzd += t[j];
       const float dz = dzd + a.dlat[i * 3 * L + l];
+      float* xr = a.xdmulv + (long)i * a.dstride;  // this workgroup's own lines
       if (a.is_vae) {
         const float lv = a.mulv[i * 2 * L + l];
         const float dmu = dz + a.dlat[i * 3 * L + L + l];
         float dlv = a.dlat[i * 3 * L + 2 * L + l];
         if (a.train) dlv += dz * a.eps[e] * 0.5f * expf(0.5f * lv);
-        a.dmulv[i * 2 * L + l] = dlv;
+        xr[l] = dlv;
+        xr[L + l] = dmu;
+        a.dmulv[i * 2 * L + l] = dlv;  // the caller's copy (not read in this launch)
         a.dmulv[i * 2 * L + L + l] = dmu;
       } else {
         float dmu = dz;
         if (a.sigmoid) dmu *= a.zval[e] * (1.f - a.zval[e]);
+        xr[l] = dmu;
         a.dmulv[i * L + l] = dmu;
       }
     }
@@ -1049,7 +1070,8 @@ __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
     __syncthreads();
     if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(a.sync + kBnSyncL, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == a.nb_lat - 1) {
-      for (int g = 0; g < kBnGroups; ++g)
+      // only groups with members: an empty group's flag would never be reset
+      for (int g = 0; g < kBnGroups && g < n_enc; ++g)
         __hip_atomic_store(a.sync + kBnSyncFlag + kBnSyncLine * g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
@@ -1091,8 +1113,9 @@ __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
     float wv[kLinDxChunk];
 #pragma unroll
     for (int u = 0; u < kLinDxChunk; ++u) wv[u] = c0 + u < c1 ? a.we[(long)(c0 + u) * k + kc] : 0.f;
-    bn_wait(a.sync + kBnSyncFlag + kBnSyncLine * (ej % kBnGroups), 1);
-    for (int e = threadIdx.x; e < mr * n; e += blockDim.x) ds[e] = bn_ld(a.dmulv + (long)i0 * n + e);
+    bn_wait(a.sync + kBnSyncFlag + kBnSyncLine * (ej % kBnGroups), 1, a.sync + kBnSyncErr, 2);
+    for (int e = threadIdx.x; e < mr * n; e += blockDim.x)
+      ds[e] = bn_ld(a.xdmulv + (long)(i0 + e / n) * a.dstride + e % n);
     __syncthreads();
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1119,13 +1142,13 @@ __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
     float xv[kLinSplitM];
 #pragma unroll
     for (int i = 0; i < kLinSplitM; ++i) xv[i] = (on && i < m) ? a.xe[(long)i * k + kk] : 0.f;
-    bn_wait(a.sync + kBnSyncFlag + kBnSyncLine * (ej % kBnGroups), 1);
+    bn_wait(a.sync + kBnSyncFlag + kBnSyncLine * (ej % kBnGroups), 1, a.sync + kBnSyncErr, 4);
     // the block's dmulv columns [m][8] in ONE round of vector loads (per-row
     // scalar loads were 8 dependent trips to memory: 40 us for this phase)
     float* dl = bn_lds;  // [m][kBnDwRows]
     if ((int)threadIdx.x < m * kBnDwRows) {
       const int i = threadIdx.x / kBnDwRows, r = threadIdx.x % kBnDwRows;
-      dl[threadIdx.x] = nn0 + r < n ? bn_ld(a.dmulv + (long)i * n + nn0 + r) : 0.f;
+      dl[threadIdx.x] = nn0 + r < n ? bn_ld(a.xdmulv + (long)i * a.dstride + nn0 + r) : 0.f;
     }
     __syncthreads();
     for (int r = 0; r < kBnDwRows; ++r) {
@@ -1297,7 +1320,7 @@ __global__ void step_begin_k(int* __restrict__ counter, unsigned long long seed,
 
 using namespace cfsd;
 
-extern "C" int cfsd_version(void) { return (4 << 16) | 11; }  // 4.11: cfsd_spiral_conv_bwd_flat_pair_bf16, cfsd_spiral_conv_bwd_rowsub_pair_bf16; 4.10: cfsd_spiral_conv_bwd_flat_pair; 4.9: cfsd_spiral_conv_fwd_in_swap; 4.8: cfsd_bottleneck_bwd; 4.7: cfsd_adam_scaled; 4.6: cfsd_side_work (side work riding in host launches); 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
+extern "C" int cfsd_version(void) { return (4 << 16) | 12; }  // 4.12: cfsd_bottleneck_bwd exchange workspace + sticky error word; 4.11: cfsd_spiral_conv_bwd_flat_pair_bf16, cfsd_spiral_conv_bwd_rowsub_pair_bf16; 4.10: cfsd_spiral_conv_bwd_flat_pair; 4.9: cfsd_spiral_conv_fwd_in_swap; 4.8: cfsd_bottleneck_bwd; 4.7: cfsd_adam_scaled; 4.6: cfsd_side_work (side work riding in host launches); 3.0: per-epoch shuffle, bf16 path; 3.1: row-subset backward; 3.2: uniform / visiting-order SpMM; 3.3: reduce + Adam; 4.0: CFSD_VM vertex-major operands (dx_dt / dpre_dt arguments); 4.1: fp32 vertex-major operands; 4.2: vertex-major swap / loss passes (_x); 4.3: cfsd_dw_slabs.fused == 3 (vertex-major fp32 dW slabs); 4.4: cfsd_gather_meshes
 extern "C" const char* cfsd_last_error_string(void) { return g_err; }
 
 extern "C" int cfsd_recon_lap_blocks(int batch, int nv) {
@@ -1611,14 +1634,22 @@ extern "C" int cfsd_linear_bwd_split(const float* x, const float* w, const float
   return launch_status("linear_bwd_split");
 }
 
+static inline int bn_round32(long n) { return (int)((n + 31) / 32 * 32); }
+
+extern "C" size_t cfsd_bottleneck_bwd_exchange_floats(int batch, int latent, int nd, int ne) {
+  if (batch <= 0 || latent <= 0 || nd <= 0 || ne <= 0) return 0;
+  return (size_t)cfsd_linear_bwd_split_parts(nd) * bn_round32((long)batch * latent) +
+         (size_t)batch * bn_round32(ne);
+}
+
 extern "C" int cfsd_bottleneck_bwd(const int32_t* up_ptr, const int32_t* up_col, const float* up_val,
                                    const float* g, int n_up, int cup, const float* z, const float* wd,
-                                   float* dz_parts, float* dwd, float* dbd, int nd, const float* mulv,
+                                   float* exchange, float* dwd, float* dbd, int nd, const float* mulv,
                                    const float* eps, const float* dlat, float* dmulv, int train, int is_vae,
                                    int sigmoid, const float* xe, const float* we, const float* elu_y, float* dxe,
                                    float* dwe, float* dbe, int ke, int ne, int accumulate, int32_t* sync, int batch,
                                    int latent, void* stream) {
-  if (!up_ptr || !up_col || !up_val || !g || !z || !wd || !dz_parts || !dwd || !dbd || !mulv || !dlat || !dmulv ||
+  if (!up_ptr || !up_col || !up_val || !g || !z || !wd || !exchange || !dwd || !dbd || !mulv || !dlat || !dmulv ||
       !xe || !we || !dxe || !dwe || !dbe || !sync)
     return set_error(CFSD_EINVAL, "bottleneck_bwd: null pointer");
   if (is_vae && train && !eps) return set_error(CFSD_EINVAL, "bottleneck_bwd: eps required");
@@ -1639,7 +1670,9 @@ extern "C" int cfsd_bottleneck_bwd(const int32_t* up_ptr, const int32_t* up_col,
   a.cup = cup;
   a.z = z;
   a.wd = wd;
-  a.parts = dz_parts;
+  a.pstride = bn_round32((long)m * kd);
+  a.dstride = bn_round32(ne);
+  a.parts = exchange;
   a.dwd = dwd;
   a.dbd = dbd;
   a.m = m;
@@ -1656,7 +1689,9 @@ extern "C" int cfsd_bottleneck_bwd(const int32_t* up_ptr, const int32_t* up_col,
   a.train = train;
   a.is_vae = is_vae;
   a.sigmoid = sigmoid;
-  a.nb_lat = (m * latent + 255) / 256;
+  a.lat_rows = 256 / latent;  // >= 2 (latent <= 128)
+  a.nb_lat = (m + a.lat_rows - 1) / a.lat_rows;
+  a.xdmulv = exchange + (size_t)a.ndx_d * a.pstride;
   a.xe = xe;
   a.we = we;
   a.elu_y = elu_y;

@@ -428,6 +428,8 @@ class SDVAEEngine:
                       if bsz <= 16 and lat <= 128 else None)
         b.dmulv = torch.empty_like(b.mulv)
         b.bn_sync = torch.zeros(ops.BN_SYNC_INTS, dtype=torch.int32, device=dev)  # cfsd_bottleneck_bwd's counters
+        b.bn_xchg = (f(ops.bottleneck_exchange_floats(bsz, lat, flat_out, nmulv)) if b.dz_parts is not None
+                     else None)  # cfsd_bottleneck_bwd's line-exclusive hand-off area
         b.dpre_enc = [f(bsz, nv[lv + 1], cout) if (lv == last_enc or not T.enc_select[lv])
                       else fl(lv + 1, bsz, nv[lv + 1], cout) for (cin, cout, lv) in S.enc_layers()]
         b.g_enc_in = [None] + [f(bsz, nv[lv], cin) if not T.enc_select[lv - 1] else None
@@ -899,13 +901,22 @@ class SDVAEEngine:
         flat = b.enc_out[last].view(b.bsz, -1)
         select = T.enc_select[last]
         dxe = b.dpre_enc[last].view(b.bsz, -1) if select else b.g_pooled[last].view(b.bsz, -1)
-        ops.bottleneck_bwd(T.upT_csr[ui], b.g_dec_up[0], b.z, P.view("de_layers.0.weight"), b.dz_parts,
+        ops.bottleneck_bwd(T.upT_csr[ui], b.g_dec_up[0], b.z, P.view("de_layers.0.weight"), b.bn_xchg,
                            P.gview("de_layers.0.weight"), P.gview("de_layers.0.bias"), b.mulv, b.eps, b.dlat,
                            b.dmulv, S.is_vae, S.sigmoid, flat, W, dxe, gW.view(W.shape), gB, b.bn_sync,
                            elu_y=flat if select else None)
         if not select:
             ops.spmm(T.downT_csr[last], b.g_pooled[last], T.n_verts[last], elu_y=b.enc_full[last],
                      out=b.dpre_enc[last])
+
+    def check_health(self):
+        """Raise CfsdError if a device-side wait of any batch's one-launch
+        bottleneck backward timed out (the sticky word of cfsd_bottleneck_bwd:
+        those steps' gradients are invalid).  One device read per batch size:
+        ModelManager.run_epoch calls it once per epoch, bench.py after the
+        timed steps."""
+        for b in self._bufs.values():
+            ops.bottleneck_check(b.bn_sync)
 
     def _flat_out(self, b):
         """The flat-list output-conv backward applies (vertex-major level 0,

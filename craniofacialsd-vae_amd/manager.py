@@ -204,6 +204,8 @@ class ModelManager:
             import torch.distributed as dist
             dist.all_reduce(acc)  # every rank's batches: sums and the batch count
         a = acc.cpu().numpy().astype(np.float64)
+        if train:
+            self.engine.check_health()  # a timed-out device wait invalidates the epoch: fail loudly
         n = max(a[5], 1.0)
         self._losses = {"reconstruction": a[0] / n, "kl": a[1] / n, "latent_consistency": a[2] / n,
                         "laplacian": a[3] / n, "classification": 0.0, "classification_acc": 0.0,

@@ -773,17 +773,35 @@ def latent_bwd(mulv, eps, z, dz_dec, dlat, dmulv, latent, train, is_vae, sigmoid
 
 
 BN_SYNC_INTS = 608  # cfsd_bottleneck_bwd's counters and flags (19 x one 128-B line)
+BN_SYNC_ERR = 65    # CFSD_BN_SYNC_ERR: the sticky timed-out-wait word inside them
 
 
-def bottleneck_bwd(up_csr, g, z, wd, dz_parts, dwd, dbd, mulv, eps, dlat, dmulv, is_vae, sigmoid, xe, we, dxe,
+def bottleneck_exchange_floats(batch, latent, nd, ne):
+    """Size of cfsd_bottleneck_bwd's exchange workspace (device floats)."""
+    return int(_abi.lib().cfsd_bottleneck_bwd_exchange_floats(batch, latent, nd, ne))
+
+
+def bottleneck_check(sync):
+    """Raise CfsdError if any cfsd_bottleneck_bwd launch that used ``sync``
+    gave up waiting (its values are then wrong).  Reads one device int (a
+    host sync): call it at a cadence, e.g. once per epoch, not per step."""
+    err = int(sync[BN_SYNC_ERR].item())
+    if err:
+        raise _abi.CfsdError(f"cfsd_bottleneck_bwd: a wait timed out (roles {err:#x}); the step's "
+                             f"bottleneck gradients are invalid")
+
+
+def bottleneck_bwd(up_csr, g, z, wd, exchange, dwd, dbd, mulv, eps, dlat, dmulv, is_vae, sigmoid, xe, we, dxe,
                    dwe, dbe, sync, elu_y=None, accumulate=False, train=True):
     """The bottleneck backward in one launch (``cfsd_bottleneck_bwd``): the
     coarsest Pool(up) transpose over ``g`` [B, n_up, cup] (``up_csr`` =
     (row_ptr, col, val), plain per-row order), the decoder Linear backward
-    (``wd`` [nd, latent]; ``dz_parts`` as :func:`linear_bwd_split`), the
-    latent head backward (:func:`latent_bwd`) and the encoder Linear backward
-    (:func:`linear_bwd` with ``xe`` [B, ke], ``we`` [ne, ke], dy = ``dmulv``).
-    ``sync``: BN_SYNC_INTS zeroed device int32, left zeroed."""
+    (``wd`` [nd, latent]), the latent head backward (:func:`latent_bwd`) and
+    the encoder Linear backward (:func:`linear_bwd` with ``xe`` [B, ke],
+    ``we`` [ne, ke], dy = ``dmulv``).  ``exchange``: a device float buffer of
+    :func:`bottleneck_exchange_floats` (the launch's line-exclusive hand-off
+    area); ``sync``: BN_SYNC_INTS zeroed device int32, left zeroed (a timed-out
+    wait sets ``sync[BN_SYNC_ERR]``: :func:`bottleneck_check`)."""
     row_ptr, col, val = up_csr
     bsz, n_up, cup = g.shape
     _need(g, None, name="g")
@@ -798,7 +816,7 @@ def bottleneck_bwd(up_csr, g, z, wd, dz_parts, dwd, dbd, mulv, eps, dlat, dmulv,
     _need(col, None, torch.int32, "up_col")
     _need(val, (col.numel(),), name="up_val")
     _need(z, (m, lat), name="z")
-    _need(dz_parts, (linear_bwd_split_parts(nd), m, lat), name="dz_parts")
+    _need(exchange, (bottleneck_exchange_floats(m, lat, nd, ne),), name="exchange")
     _need(dwd, (nd, lat), name="dwd")
     _need(dbd, (nd,), name="dbd")
     _need(dmulv, tuple(mulv.shape), name="dmulv")
@@ -809,7 +827,7 @@ def bottleneck_bwd(up_csr, g, z, wd, dz_parts, dwd, dbd, mulv, eps, dlat, dmulv,
     _need(dwe, (ne, ke), name="dwe")
     _need(dbe, (ne,), name="dbe")
     _need(sync, (BN_SYNC_INTS,), torch.int32, "sync")
-    call("cfsd_bottleneck_bwd", ptr(row_ptr), ptr(col), ptr(val), ptr(g), n_up, cup, ptr(z), ptr(wd), ptr(dz_parts),
+    call("cfsd_bottleneck_bwd", ptr(row_ptr), ptr(col), ptr(val), ptr(g), n_up, cup, ptr(z), ptr(wd), ptr(exchange),
          ptr(dwd), ptr(dbd), nd, ptr(mulv), ptr(eps), ptr(dlat), ptr(dmulv), int(train), int(is_vae), int(sigmoid),
          ptr(xe), ptr(we), ptr(elu_y), ptr(dxe), ptr(dwe), ptr(dbe), ke, ne, int(accumulate), ptr(sync), m, lat,
          stream_ptr())

@@ -415,24 +415,32 @@ int cfsd_linear_bwd_split_parts(int n);
 int cfsd_linear_bwd_split(const float* x, const float* w, const float* dy, float* dx_parts,
                           float* dw, float* db, int m, int k, int n, void* stream);
 
-/* The step's whole bottleneck backward in ONE launch (ABI 4.8): the Pool(up)
+/* The step's whole bottleneck backward in ONE launch (ABI 4.8; 4.12: the
+ * exchange workspace, the sticky error word): the Pool(up)
  * transpose of the coarsest Deblock (model.py:172-173; CSR up_ptr/up_col/
  * up_val in plain per-row order over the fine-level gradient g [batch][n_up]
  * [cup], batch-major), the decoder Linear backward (dh.W with W = wd
- * [nd][latent], nd = coarse vertices x cup; dwd / dbd; dz as dz_parts
- * [cfsd_linear_bwd_split_parts(nd)][batch][latent]), the latent head backward
- * (cfsd_latent_bwd_parts: mulv, eps, dlat -> dmulv) and the encoder Linear
- * backward (cfsd_linear_bwd with x = xe [batch][ke], w = we [ne][ke], dy =
- * dmulv; dxe (x elu'(elu_y) when elu_y != NULL), dwe, dbe).  Workgroups of the
- * later stages wait on device counters for the earlier ones (only ever on
- * workgroups of lower index); `sync` is 608 device int32 (19 counters and flags, one
- * 128-B line each) that must be zero before the first call and are left zero
- * by every call.  Same values bit for
- * bit as spmm + linear_bwd_split + latent_bwd_parts + linear_bwd, except that
- * dh itself is never stored.  batch <= 16, latent <= 128, cup a multiple of
- * 64, nd <= 5120, ne = (is_vae ? 2 : 1) x latent <= 160. */
+ * [nd][latent], nd = coarse vertices x cup; dwd / dbd; dz as the partial
+ * products of cfsd_linear_bwd_split, kept in `exchange`), the latent head
+ * backward (cfsd_latent_bwd_parts: mulv, eps, dlat -> dmulv) and the encoder
+ * Linear backward (cfsd_linear_bwd with x = xe [batch][ke], w = we [ne][ke],
+ * dy = dmulv; dxe (x elu'(elu_y) when elu_y != NULL), dwe, dbe).  Workgroups
+ * of the later stages wait on device counters for the earlier ones (only ever
+ * on workgroups of lower index) and read the values they wait for from
+ * `exchange` (cfsd_bottleneck_bwd_exchange_floats(batch, latent, nd, ne)
+ * device floats, contents unspecified: each 128-B line is written by ONE
+ * workgroup); `sync` is 608 device int32 (19 counters and flags, one 128-B
+ * line each) that must be zero before the first call and are left zero by
+ * every call -- except sync[CFSD_BN_SYNC_ERR], a sticky word a wait that
+ * timed out sets (the values are then wrong: the caller must check it and
+ * refuse the step).  Same values bit for bit as spmm + linear_bwd_split +
+ * latent_bwd_parts + linear_bwd, except that dh itself is never stored.
+ * batch <= 16, latent <= 128, cup a multiple of 64, nd <= 5120, ne =
+ * (is_vae ? 2 : 1) x latent <= 160. */
+#define CFSD_BN_SYNC_ERR 65
+size_t cfsd_bottleneck_bwd_exchange_floats(int batch, int latent, int nd, int ne);
 int cfsd_bottleneck_bwd(const int32_t* up_ptr, const int32_t* up_col, const float* up_val, const float* g,
-                        int n_up, int cup, const float* z, const float* wd, float* dz_parts, float* dwd,
+                        int n_up, int cup, const float* z, const float* wd, float* exchange, float* dwd,
                         float* dbd, int nd, const float* mulv, const float* eps, const float* dlat,
                         float* dmulv, int train, int is_vae, int sigmoid, const float* xe, const float* we,
                         const float* elu_y, float* dxe, float* dwe, float* dbe, int ke, int ne, int accumulate,

@@ -586,23 +586,25 @@ def test_bottleneck_bwd_op_vs_separate(is_vae, select, sigmoid):
     res = []
     for fused in (False, True):
         gfine, dlat = gfine0.clone(), dlat0.clone()
-        out = dict(parts=torch.zeros(parts_n, B, L, device=DEV), dwd=torch.zeros(nv * cup, L, device=DEV),
+        out = dict(dwd=torch.zeros(nv * cup, L, device=DEV),
                    dbd=torch.zeros(nv * cup, device=DEV), dmulv=torch.zeros(B, ne, device=DEV),
                    dxe=torch.zeros(B, ke, device=DEV), dwe=torch.zeros(ne, ke, device=DEV),
                    dbe=torch.zeros(ne, device=DEV))
         sync = torch.zeros(ops.BN_SYNC_INTS, dtype=torch.int32, device=DEV)
+        parts = torch.zeros(parts_n, B, L, device=DEV)
+        xchg = torch.full((ops.bottleneck_exchange_floats(B, L, nv * cup, ne),), float("nan"), device=DEV)
         zin = zval if (sigmoid and not is_vae) else z
         for it in range(3):  # fresh operands per call: a stale cached value from the previous call would show
             gfine.mul_(0.5 + it)
             dlat.add_(0.25)
             if fused:
-                ops.bottleneck_bwd((row_ptr, col, val), gfine, zin, wd, out["parts"], out["dwd"], out["dbd"], mulv,
+                ops.bottleneck_bwd((row_ptr, col, val), gfine, zin, wd, xchg, out["dwd"], out["dbd"], mulv,
                                    epsv, dlat, out["dmulv"], is_vae, sigmoid, xe, we, out["dxe"], out["dwe"],
                                    out["dbe"], sync, elu_y=elu_y)
             else:
                 dh = ops.spmm((row_ptr, col, val), gfine, nv)
-                ops.linear_bwd_split(zin, wd, dh.view(B, -1), out["parts"], out["dwd"], out["dbd"])
-                ops.latent_bwd(mulv, epsv, zin, out["parts"], dlat, out["dmulv"], L, True, is_vae, sigmoid)
+                ops.linear_bwd_split(zin, wd, dh.view(B, -1), parts, out["dwd"], out["dbd"])
+                ops.latent_bwd(mulv, epsv, zin, parts, dlat, out["dmulv"], L, True, is_vae, sigmoid)
                 ops.linear_bwd(xe, we, out["dmulv"], dx=out["dxe"], dw=out["dwe"], db=out["dbe"], elu_y=elu_y)
             res_it = {k: v.cpu().clone() for k, v in out.items()}
             res.append(res_it) if it == 2 else None
@@ -615,6 +617,60 @@ def test_bottleneck_bwd_op_vs_separate(is_vae, select, sigmoid):
             assert torch.equal(a_[k], c_[k]), k
     for k in res[0]:
         assert torch.equal(res[0][k], res[1][k]), k
+
+
+# (batch, latent, is_vae, sigmoid, coarse vertices, cup, fine vertices, encoder width, ELU)
+BN_STRESS = [(16, 75, 1, 0, 67, 64, 267, 4288, True), (1, 75, 1, 0, 67, 64, 267, 4288, False),
+             (3, 33, 0, 1, 27, 64, 108, 1728, True), (7, 80, 1, 0, 20, 128, 80, 2560, True),
+             (16, 128, 0, 0, 80, 64, 320, 5120, True), (5, 16, 1, 0, 80, 64, 320, 1000, False),
+             (16, 2, 0, 1, 1, 64, 4, 64, True), (9, 75, 1, 0, 67, 64, 267, 4288, True)]
+
+
+def test_bottleneck_bwd_stress_varied_shapes():
+    """the one-launch bottleneck backward's counter hand-offs,
+    run many times in ONE process over varied batch / latent / grid sizes
+    (so its workgroups land on different XCDs and CUs from case to case)
+    against the four separate launches -- bit for bit on every call, the
+    counters left zero and the sticky timed-out-wait word never set."""
+    for case_i, (B, L, is_vae, sigmoid, nv, cup, n_up, ke, select) in enumerate(BN_STRESS):
+        g = torch.Generator().manual_seed(100 + case_i)
+        rnd = lambda *s: torch.randn(*s, generator=g).to(DEV)  # noqa: E731
+        ne = 2 * L if is_vae else L
+        cols = [[] for _ in range(nv)]
+        for f in range(n_up):
+            for k in range(3):
+                cols[(f * 7 + k * 11) % nv].append((f, 0.1 + 0.3 * k))
+        row_ptr = torch.tensor([0] + list(np.cumsum([len(c) for c in cols])), dtype=torch.int32, device=DEV)
+        col = torch.tensor([f for c in cols for f, _ in c], dtype=torch.int32, device=DEV)
+        val = torch.tensor([v for c in cols for _, v in c], dtype=torch.float32, device=DEV)
+        z, wd, mulv, epsv = rnd(B, L), rnd(nv * cup, L), rnd(B, ne), rnd(B, L)
+        zin = torch.sigmoid(z) if (sigmoid and not is_vae) else z
+        xe, we = rnd(B, ke), rnd(ne, ke)
+        elu_y = torch.nn.functional.elu(rnd(B, ke)) if select else None
+        parts = torch.zeros(ops.linear_bwd_split_parts(nv * cup), B, L, device=DEV)
+        xchg = torch.zeros(ops.bottleneck_exchange_floats(B, L, nv * cup, ne), device=DEV)
+        sync = torch.zeros(ops.BN_SYNC_INTS, dtype=torch.int32, device=DEV)
+        outs = [{k: torch.zeros(*s, device=DEV) for k, s in
+                 (("dwd", (nv * cup, L)), ("dbd", (nv * cup,)), ("dmulv", (B, ne)), ("dxe", (B, ke)),
+                  ("dwe", (ne, ke)), ("dbe", (ne,)))} for _ in range(2)]
+        for it in range(12):
+            gfine, dlat = rnd(B, n_up, cup), rnd(B, 3 * L)
+            s_, f_ = outs
+            dh = ops.spmm((row_ptr, col, val), gfine, nv)
+            ops.linear_bwd_split(zin, wd, dh.view(B, -1), parts, s_["dwd"], s_["dbd"])
+            ops.latent_bwd(mulv, epsv, zin, parts, dlat, s_["dmulv"], L, True, is_vae, sigmoid)
+            ops.linear_bwd(xe, we, s_["dmulv"], dx=s_["dxe"], dw=s_["dwe"], db=s_["dbe"], elu_y=elu_y)
+            ops.bottleneck_bwd((row_ptr, col, val), gfine, zin, wd, xchg, f_["dwd"], f_["dbd"], mulv, epsv, dlat,
+                               f_["dmulv"], is_vae, sigmoid, xe, we, f_["dxe"], f_["dwe"], f_["dbe"], sync,
+                               elu_y=elu_y)
+            for k in s_:
+                assert torch.equal(s_[k], f_[k]), (case_i, it, k)
+        assert not sync.any(), case_i
+        ops.bottleneck_check(sync)
+    # the sticky word is what the host refuses
+    sync[ops.BN_SYNC_ERR] = 2
+    with pytest.raises(RuntimeError, match="timed out"):
+        ops.bottleneck_check(sync)
 
 
 # --------------------------------------------------------------- dense Linears

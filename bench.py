@@ -122,8 +122,6 @@ class Runner:
                                  seed=1234 + rank, device=device, precision=precision,
                                  vertex_major=vertex_major)
         self.eng.reset_parameters()  # same init on every rank (broadcast below)
-        if os.environ.get("CFSD_SIDE_MODE"):  # A/B of the step's reduce + Adam tail (engine.side_work)
-            self.eng.side_work = os.environ["CFSD_SIDE_MODE"]
         self.world, self.rank = world, rank
         nv = self.topo.n_verts[0]
         if meshes is None:
@@ -154,25 +152,6 @@ class Runner:
 
 
 # ------------------------------------------------------------------ roofline
-def side_adam_bytes(arg):
-    """Required bytes of a cfsd_side_work riding in a launch: Adam's 7 x 4 B
-    per updated element (its slab reductions are bookkeeping, like the
-    deferred reduce launch they replace)."""
-    import ctypes
-    c = getattr(arg, "_obj", None)
-    if c is None or not c.adam:
-        return 0.0
-    n = 0
-    items = ctypes.cast(c.items, ctypes.POINTER(_abi.DwSlabs))
-    for i in range(c.n_items):
-        it = items[i]
-        n += it.cout * 9 * it.cin + it.cout
-    rng = ctypes.cast(c.ranges, ctypes.POINTER(ctypes.c_size_t))
-    for r in range(c.n_ranges):
-        n += rng[2 * r + 1] - rng[2 * r]
-    return 7.0 * 4 * n
-
-
 def launch_cost(name, a):
     """(flop, algorithmic HBM bytes, peak TFLOP/s) of one libcfsd launch from
     its ABI arguments (include/cfsd.h); (0, 0, None) for bookkeeping launches
@@ -194,15 +173,13 @@ def launch_cost(name, a):
     if name == "cfsd_spiral_conv_bwd_weight":
         B, vs, rows, S, ci, co = a[7:13]
         return 2.0 * B * rows * S * ci * co, f4 * (B * vs * ci + B * rows * co + co * S * ci) + 4 * rows * S, FP32_PEAK_TFLOPS
-    if name in ("cfsd_spiral_conv_bwd", "cfsd_spiral_conv_bwd_side"):
+    if name == "cfsd_spiral_conv_bwd":
         B, vs, rows, S, ci, co = a[13:19]
         dx, elu = a[8] is not None, a[7] is not None
         fl = 2.0 * B * rows * S * ci * co * (2 if dx else 1)
         by = f4 * (B * vs * ci + B * rows * co + co * S * ci) + 4 * rows * S
         if dx:
             by += f4 * B * vs * ci * (2 if elu else 1) + 16 * vs * S
-        if name.endswith("_side"):
-            by += side_adam_bytes(a[19])
         return fl, by, FP32_PEAK_TFLOPS
     if name == "cfsd_spiral_conv_bwd_rowsub":  # dx (dG + gather) and dW of a row-subset conv
         B, vs, rows, S, ci, co = a[12:18]
@@ -216,14 +193,11 @@ def launch_cost(name, a):
         elu = a[4] is not None
         return (2.0 * B * rows * S * ci * co, f4 * (B * rows * co + co * S * ci) + sd * B * vs * ci * (2 if elu else 1)
                 + 4 * vs * a[2], FP32_PEAK_TFLOPS)
-    if name in ("cfsd_spmm_csr_sched", "cfsd_spmm_sched_csr", "cfsd_spmm_sched_csr_side"):
+    if name in ("cfsd_spmm_csr_sched", "cfsd_spmm_sched_csr"):
         sx, sy = sz(a[5]), sz(a[8])
         B, m, n, c = a[9:13]
         elu = a[6] is not None
-        side = side_adam_bytes(a[13]) if name.endswith("_side") else 0.0
-        return 0.0, B * c * (sx * n + sy * m * (2 if elu else 1)) + side, None
-    if name == "cfsd_side_work_run":  # slab reduction (bookkeeping) + Adam (7 x 4 B per element)
-        return 0.0, side_adam_bytes(a[0]), None
+        return 0.0, B * c * (sx * n + sy * m * (2 if elu else 1)), None
     if name == "cfsd_spiral_conv_fwd_x":
         sx, sy = sz(a[1]), sz(a[7])
         B, vs, rows, S, ci, co = a[8:14]
@@ -280,13 +254,6 @@ def launch_cost(name, a):
         return (4.0 * B * rows * S * ci * co,
                 f4 * (B * rows * co + co * S * ci) + 2.0 * B * vs * ci * (2 + int(elu)) + 4 * rows * S
                 + 4 * vs * a[4], FP32_PEAK_TFLOPS)
-    if name == "cfsd_spiral_conv_bwd_weight_spmm_bf16":  # bf16 level-0 dW slabs + Pool(up)^T SpMM
-        B, vs, rows, S, ci, co = a[5:11]
-        m, n, c = a[18:21]
-        elu = a[16] is not None
-        return (2.0 * B * rows * S * ci * co,
-                2.0 * (B * vs * ci + B * rows * co + B * c * (n + m * (2 if elu else 1))) + 4 * co * S * ci
-                + 4 * rows * S, BF16_PEAK_TFLOPS)
     if name == "cfsd_spiral_conv_fwd_in_swap":  # the swap + the xyz input conv (spiral length 9)
         bs, vs, rows, ci, co = a[4], a[14], a[15], a[16], a[17]
         B, S = bs * bs, 9
@@ -342,10 +309,9 @@ def launch_cost(name, a):
         nin = 2 * lat if a[10] else lat
         return (2.0 * bsz * lat * n + 10.0 * bsz * lat,
                 f4 * (bsz * nin + bsz * lat * 4 + n * lat + n + bsz * n), FP32_PEAK_TFLOPS)
-    if name in ("cfsd_latent_bwd", "cfsd_latent_bwd_parts", "cfsd_latent_bwd_parts_side"):  # latent head backward
+    if name in ("cfsd_latent_bwd", "cfsd_latent_bwd_parts"):  # latent head backward
         bsz, lat = (a[6], a[7]) if name == "cfsd_latent_bwd" else (a[7], a[8])
-        side = side_adam_bytes(a[12]) if name.endswith("_side") else 0.0
-        return 10.0 * bsz * lat, f4 * bsz * lat * 8 + side, FP32_PEAK_TFLOPS
+        return 10.0 * bsz * lat, f4 * bsz * lat * 8, FP32_PEAK_TFLOPS
     if name == "cfsd_dw_reduce_batch_adam":  # the slab reduction is bookkeeping; Adam's 7 streams are not
         n = a[7].value if hasattr(a[7], "value") else a[7]
         return 0.0, 7.0 * f4 * n, None
@@ -371,7 +337,7 @@ def launch_cost(name, a):
 # Launches that do no work the algorithm requires (priced at zero by
 # launch_cost): step counter / noise / batch pick, loss reduction, the
 # deferred weight-gradient slab reduction, gradient scaling.
-BOOKKEEPING = ("cfsd_step_begin", "cfsd_loss_finalize", "cfsd_dw_reduce_batch", "cfsd_scale", "cfsd_side_work_run")
+BOOKKEEPING = ("cfsd_step_begin", "cfsd_loss_finalize", "cfsd_dw_reduce_batch", "cfsd_scale")
 
 
 def step_roofline(runner, ms_per_step):

@@ -33,8 +33,6 @@ SIGNATURES = {
     "cfsd_spiral_conv_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I,
                                   _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_workspace": (_Z, [_I, _I, _I, _I, _I, _I]),
-    "cfsd_spiral_conv_bwd_side": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I,
-                                       _I, _I, _I, _P, _P]),
     "cfsd_spiral_conv_bwd_paired": (_I, [_I, _I, _I, _I, _I, _I]),
     "cfsd_spiral_conv_bwd_rowsub": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _Z, _I, _I, _I,
                                          _I, _I, _I, _P]),
@@ -48,8 +46,6 @@ SIGNATURES = {
                                                  _P]),
     "cfsd_spiral_conv_bwd_rowsub_pair_bf16": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, _P, _Z, _I, _I, _I, _I, _I,
                                                    _I, _P]),
-    "cfsd_spiral_conv_bwd_weight_spmm_bf16": (_I, [_P, _P, _P, _P, _Z, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P,
-                                                   _P, _P, _I, _I, _I, _P]),
     "cfsd_spiral_conv_bwd_data_rowsub": (_I, [_P, _P, _I, _P, _P, _P, _I, _P, _Z, _I, _I, _I, _I, _I, _I,
                                               _P]),
     "cfsd_spiral_conv_bwd_data_rowsub_workspace": (_Z, [_I, _I, _I, _I]),
@@ -103,9 +99,6 @@ SIGNATURES = {
     "cfsd_spmm_csr_x": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spmm_uniform": (_I, [_I, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
     "cfsd_spmm_sched_csr": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P]),
-    "cfsd_spmm_sched_csr_side": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
-    "cfsd_latent_bwd_parts_side": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
-    "cfsd_side_work_run": (_I, [_P, _P]),
     "cfsd_cast": (_I, [_P, _I, _P, _I, _Z, _P]),
     "cfsd_step_begin": (_I, [_P, _U64, _P, _I, _P, _I, _P, _I, _I, _P, _I, _I, _P, _P]),
     "cfsd_dw_reduce_batch": (_I, [_P, _I, _P]),
@@ -120,14 +113,6 @@ class DwSlabs(ctypes.Structure):
     """``cfsd_dw_slabs`` (include/cfsd.h): one deferred weight-gradient slab set."""
     _fields_ = [("workspace", _P), ("dw", _P), ("db", _P), ("batch", _I), ("vsrc", _I),
                 ("rows", _I), ("cin", _I), ("cout", _I), ("fused", _I)]
-
-
-class SideWorkC(ctypes.Structure):
-    """``cfsd_side_work`` (include/cfsd.h, ABI 4.6)."""
-    _fields_ = [("items", _P), ("n_items", _I), ("ranges", _P), ("n_ranges", _I), ("adam", _I),
-                ("param", _P), ("grad", _P), ("exp_avg", _P), ("exp_avg_sq", _P), ("step", _P),
-                ("lr", _F), ("beta1", _F), ("beta2", _F), ("eps", _F), ("weight_decay", _F),
-                ("param_bf16", _P)]
 
 
 class CfsdError(RuntimeError):

@@ -265,9 +265,6 @@ __device__ __forceinline__ long swap_src_mesh(const SwapSrc& s, int k, int ob, i
 
 // CUs of the current device (cached).
 int device_cus();
-// Integer tuning knob from the environment (read once per name; unset or
-// unparsable: dflt).  Used for same-box A/B sweeps of launch geometry.
-int env_knob(const char* name, int dflt);
 // Persistent grid with the SAME number of workgroups (bpc) on every CU,
 // capped at one workgroup per `per_block` units: a grid that is not a multiple
 // of the CU count leaves some CUs a third more waves than others, and those
@@ -306,6 +303,11 @@ __device__ __forceinline__ void gload1_async(int& d, const int* p) {
 }
 __device__ __forceinline__ void gload1f_async(float& d, const float* p) {
   asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+// The same from a wave-uniform base (SGPR pair) + a 32-bit per-lane byte
+// offset: no 64-bit address arithmetic per load.
+__device__ __forceinline__ void gload1f_async_s(float& d, const float* base, int off) {
+  asm volatile("global_load_dword %0, %1, %2" : "=v"(d) : "v"(off), "s"(base) : "memory");
 }
 // Retire counted loads and hand their 8 destinations back to the compiler.
 template <int N, typename T>

@@ -51,12 +51,6 @@ int launch_bwd_vm16_pair(const bf16_t* x, const int* idx, const bf16_t* dpre, co
 int launch_bwd_rowsub16_pair(const bf16_t* x, const int* idx, const float* dpre, const int* flat, int width,
                              const float* w, const bf16_t* elu_y, bf16_t* dx, float* ws, int n_slabs, int vsrc,
                              int rows, int batch, hipStream_t st);
-// The bf16 D3 weight-gradient slabs (launch_dw_vm16's, one unit in flight)
-// and the visiting-order SpMM sy = elu'(ey) (P^T sx) (bf16 vertex-major sx /
-// sy / ey, c % 8 == 0) as two workgroup roles of ONE launch.
-int launch_dw_spmm16(const bf16_t* x, const int* idx, const bf16_t* dpre, float* ws, int n_slabs, int vsrc, int rows,
-                     int batch, const int* ptr_s, const int* col_s, const float* val_s, const int* rows_s,
-                     const bf16_t* sx, const bf16_t* ey, bf16_t* sy, int m, int n, int c, hipStream_t st);
 int launch_fwd_vm16(const bf16_t* x, const int* idx, const bf16_t* w, const float* bias, void* y, int y_dt,
                     int vsrc, int rows, int batch, int cin, int cout, int act, hipStream_t st);
 int launch_dx_vm16(const void* dpre, int dpre_dt, const int* inv_ptr, const int* inv_row, const int* inv_head,

@@ -36,11 +36,21 @@ __host__ __device__ constexpr int lat_red_floats(int wpb) { return (wpb / kLatGr
 // v_mfma_f32_32x32x2_f32 straight from memory, no LDS: step j covers rows
 // (2j, 2j+1) of the chunk; A[o][k] = dpre[row_k][ot*32 + o] (a 128-B
 // coalesced dpre segment per half-wave), B[k][c] = x[b, idx[r_k][s],
-// ct*32 + c] (a 128-B gathered row segment).  8 steps per batch with all
-// loads issued first, two accumulators.  Output: slab[chunk group][U][32][32]
-// + db[chunk group][COUT] (units with s == 0 && ct == 0 also sum dpre) -- the
-// conv_dw_mfma slab layout, lat_slabs(n_chunks) slabs, reduced by
-// conv_dw_reduce / dw_reduce_batch.  `red`: lat_red_floats(WPB) floats of LDS.
+// ct*32 + c] (a 128-B gathered row segment).  8 steps per batch of 16 rows
+// with all loads issued first, two accumulators.  Output: slab[chunk group]
+// [U][32][32] + db[chunk group][COUT] (units with s == 0 && ct == 0 also sum
+// dpre) -- the conv_dw_mfma slab layout, lat_slabs(n_chunks) slabs, reduced
+// by conv_dw_reduce / dw_reduce_batch.  `red`: lat_red_floats(WPB) floats of
+// LDS.
+//
+// Address work per MFMA (round 6: the SQ counters put these roles at ~15
+// VALU instructions per MFMA, the rows' index arithmetic serialised per lane):
+// a batch's 16 row offsets are computed ONCE, lane-parallel (lane t holds row
+// m0 + t), and handed to the half-wave that needs them with ds_bpermute; the
+// dpre rows are buffer loads at a wave-uniform row offset (SGPR) plus a
+// per-lane constant, and rows past the tensor (the last chunk's tail: chunks
+// are whole 16-row batches) read 0 from the buffer's range check, so no row
+// is masked.  Same products in the same order as before: bit-identical.
 template <int CIN, int COUT, int WPB = 4>
 __device__ __forceinline__ void conv_dw_lat_body(int vb, int vnb, const float* __restrict__ x,
                                                  const int* __restrict__ idx,
@@ -52,7 +62,7 @@ __device__ __forceinline__ void conv_dw_lat_body(int vb, int vnb, const float* _
   constexpr int OT = COUT / 32, CT = CIN / 32, U = kSeq * OT * CT, NB = 8;
   constexpr int GC = kLatGroup, NGB = WPB / GC;  // chunk groups per workgroup
   static_assert(NGB >= 1, "at least kLatGroup waves per workgroup");
-  const int lane = threadIdx.x & 63, li = lane & 31, h = lane >> 5;
+  const int lane = threadIdx.x & 63, li = lane & 31, h = lane >> 5, t16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), sub = wave % GC;
   const long grp = (long)xcd_block_of(vb, vnb) * NGB + wave / GC;  // (chunk group, unit)
   const bool in_grp = wave < NGB * GC && grp < (long)lat_slabs(n_chunks) * U;
@@ -74,75 +84,96 @@ __device__ __forceinline__ void conv_dw_lat_body(int vb, int vnb, const float* _
   {
     const int r0 = chunk * rchunk, r1 = min(total_rows, r0 + rchunk);
     const int rend = act ? r1 : r0;  // an inactive wave skips the loop
-    // (b, r) of this lane's first row (flat dpre row m in dpre's layout:
-    // minor index mi of extent E, major ma), advanced incrementally by 2 per
-    // step; x rows are addressed in x's layout
+    // lane t16's row m of the next batch to describe, (ma, mi) its split in
+    // dpre's layout (minor index mi of extent E); rows past the tensor take
+    // the last row's x (their dpre reads 0)
     const Lay lx = make_lay(xvm, batch, vsrc);
     const int E = dpvm ? batch : rows;
-    int m = r0 + h;
-    int ma = m / E, mi = m - ma * E;
-    const float* dp = dpre + ot * 32 + li;
-    const float* xs = x + ct * 32 + li;
+    int m = r0 + t16, ma, mi;
+    divmod32(m, E, ma, mi);
     int b_last, r_last;
-    split_row(r1 - 1, dpvm, batch, rows, b_last, r_last);
+    split_row(total_rows - 1, dpvm, batch, rows, b_last, r_last);
+    // one batch = 2 NB rows: (ma, mi) advance by (q16, e16) plus a carry
+    const int q16 = (2 * NB) / E, e16 = (2 * NB) % E;
+    const int* idx_s = idx + sl;
+    // (plain value arithmetic, no lambda captures by reference: a select of
+    // captured references compiled to a select of stack addresses -> scratch)
+#define CFSD_LAT_META(BROW, IV)                                                 \
+  {                                                                             \
+    const bool ok_ = m < total_rows;                                            \
+    const int bsel_ = dpvm ? mi : ma, rsel_ = dpvm ? ma : mi;                   \
+    const int b_ = ok_ ? bsel_ : b_last, r_ = ok_ ? rsel_ : r_last;             \
+    BROW = b_ * lx.bs;                                                          \
+    IV = idx_s[r_ * kSeq];                                                      \
+    m += 2 * NB;                                                                \
+    mi += e16;                                                                  \
+    ma += q16;                                                                  \
+    const bool w_ = mi >= E;                                                    \
+    mi = w_ ? mi - E : mi;                                                      \
+    ma += w_ ? 1 : 0;                                                           \
+  }
+    // dpre: rows past the tensor are out of the buffer's range (read as 0);
+    // a batch past the chunk (the second half of a pair, below) gets an
+    // out-of-range row offset, so it reads 0 too
+    const auto drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dpre + ot * 32), 0,
+                                                       (int)(((long)total_rows * COUT - ot * 32) * 4), 0x00020000);
+    const int dvo = (h * COUT + li) * 4;
+    constexpr int kOutOfRange = 0x7ffff000;
+#define CFSD_LAT_LOAD_A(M0, A)                                                                      \
+  {                                                                                                 \
+    const int so_ = (M0) < r1 ? (M0) * COUT * 4 : kOutOfRange;                                     \
+    _Pragma("unroll") for (int j = 0; j < NB; ++j) A[j] = __builtin_bit_cast(                      \
+        float, __builtin_amdgcn_raw_buffer_load_b32(drs, dvo + j * 2 * COUT * 4, so_, 0));          \
+  }
+    // a batch's 16 row offsets (bytes into x, lane t16 = row m0 + t16), handed
+    // to the half-wave that gathers them: lane (li, h) takes row 2j + h
+    const float* xs = x + ct * 32;  // wave-uniform base
+    const int lo4 = li * 4;
+#define CFSD_LAT_PREP(OFF, BROW, IV)                                                                \
+  {                                                                                                 \
+    const int go_ = ((BROW) + (IV) * lx.vs) * (CIN * 4);                                            \
+    _Pragma("unroll") for (int j = 0; j < NB; ++j) OFF[j] =                                         \
+        __builtin_amdgcn_ds_bpermute((2 * j + h) * 4, go_) + lo4;                                   \
+  }
+#define CFSD_LAT_HALF(OFF, A, A_NEXT, M_NEXT, BROW_N, IV_N)                                         \
+  {                                                                                                 \
+    float bv[NB];                                                                                   \
+    _Pragma("unroll") for (int j = 0; j < NB; ++j) gload1f_async_s(bv[j], xs, OFF[j]);              \
+    CFSD_LAT_META(BROW_N, IV_N)                                                                     \
+    CFSD_LAT_LOAD_A(M_NEXT, A_NEXT)                                                                 \
+    vm_wait_arr8<NB + 1>(bv); /* x gathers retired, the next batch's idx + dpre in flight */        \
+    _Pragma("unroll") for (int j = 0; j < NB; ++j) {                                                \
+      acc[j & 1] = mfma32(A[j], bv[j], acc[j & 1]);                                                 \
+      dbs += A[j];                                                                                  \
+    }                                                                                               \
+    CFSD_LAT_PREP(OFF, BROW_N, IV_N)                                                                \
+    /* keep the halves apart: hipcc otherwise hoists the next half's db adds */                   \
+    /* (and their vmcnt waits on its dpre loads) into this one */                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                              \
+  }
     static_assert(NB == 8, "vm_wait_arr8");
-    // Rows past the chunk are clamped to its last row (loads stay in bounds,
-    // no branches) and weighted 0.  Pipelined one batch ahead: while batch i's
-    // 8 dependent x gathers are in flight, batch i+1's 8 idx and 8 dpre loads
-    // are issued, so a batch costs ~one memory latency instead of two.  The x
-    // gathers are counted asm loads retired by an explicit vmcnt in the same
-    // iteration (hipcc's own placement serialised them); the idx / dpre loads
-    // are ordinary loads that hipcc waits for itself -- they cross the loop
-    // back-edge, where an asm-hidden load could be copied before it landed.
-    int srcrow[NB], bvs[NB];
-    float okf[NB], av[NB];
-    auto fetch = [&](int m0_, int (&sr)[NB], int (&bs)[NB], float (&ok_)[NB], float (&a_)[NB]) {
-  #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const bool ok = m < r1;
-        const int b = dpvm ? mi : ma, r = dpvm ? ma : mi;
-        ok_[j] = ok ? 1.f : 0.f;
-        bs[j] = (ok ? b : b_last) * lx.bs;
-        sr[j] = idx[(ok ? r : r_last) * kSeq + sl] * lx.vs;
-        m += 2;
-        mi += 2;
-        bool wrap = mi >= E;
-        mi = wrap ? mi - E : mi;
-        ma = wrap ? ma + 1 : ma;
-        wrap = mi >= E;  // extent 1
-        mi = wrap ? mi - E : mi;
-        ma = wrap ? ma + 1 : ma;
-      }
-  #pragma unroll
-      for (int j = 0; j < NB; ++j) a_[j] = dp[(long)min(m0_ + h + 2 * j, r1 - 1) * COUT];
-    };
-    fetch(r0, srcrow, bvs, okf, av);
-    for (int m0 = r0; m0 < rend; m0 += 2 * NB) {
-      float bv[NB];
-  #pragma unroll
-      for (int j = 0; j < NB; ++j) gload1f_async(bv[j], xs + (long)(bvs[j] + srcrow[j]) * CIN);
-      // the next batch's 16 idx / dpre loads are issued unconditionally (past
-      // the chunk they are clamped in-bounds rows, weighted 0), so the gathers'
-      // outputs flow straight into ONE counted wait: a branch here let hipcc
-      // copy the gather registers ahead of the wait on one path (stale values)
-      int srcrow_n[NB], bvs_n[NB];
-      float okf_n[NB], av_n[NB];
-      fetch(m0 + 2 * NB, srcrow_n, bvs_n, okf_n, av_n);
-      vm_wait_arr8<2 * NB>(bv);  // x gathers retired, the next batch in flight
-  #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const float aj = av[j] * okf[j];
-        acc[j & 1] = mfma32(aj, bv[j], acc[j & 1]);
-        dbs += aj;
-      }
-  #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        srcrow[j] = srcrow_n[j];
-        bvs[j] = bvs_n[j];
-        okf[j] = okf_n[j];
-        av[j] = av_n[j];
-      }
+    // Software pipeline, two batches per trip with alternating register sets
+    // (no copies across the back-edge): while batch i's 8 dependent x gathers
+    // are in flight, batch i+1's idx load and 8 dpre loads are issued, and
+    // batch i+1's gather offsets are formed right after batch i's MFMAs, so
+    // the next gathers issue at once.  The x gathers are counted asm loads
+    // retired by an explicit vmcnt in the same half (hipcc's own placement
+    // serialised them); the idx / dpre loads are ordinary loads that hipcc
+    // waits for itself -- they cross the back-edge, where an asm-hidden load
+    // could be copied before it landed.
+    int brow, iv, off[NB];
+    float aA[NB], aB[NB];
+    CFSD_LAT_META(brow, iv)
+    CFSD_LAT_LOAD_A(r0, aA)
+    CFSD_LAT_PREP(off, brow, iv)
+    for (int m0 = r0; m0 < rend; m0 += 4 * NB) {
+      CFSD_LAT_HALF(off, aA, aB, m0 + 2 * NB, brow, iv)
+      CFSD_LAT_HALF(off, aB, aA, m0 + 4 * NB, brow, iv)
     }
+#undef CFSD_LAT_HALF
+#undef CFSD_LAT_PREP
+#undef CFSD_LAT_LOAD_A
+#undef CFSD_LAT_META
   }
   // every wave parks its partial in its own LDS slot; after one barrier the
   // group's first wave sums the kLatGroup chunks in chunk order and stores

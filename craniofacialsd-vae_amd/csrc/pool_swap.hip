@@ -9,7 +9,6 @@
 // SwapFeatures (swap_batch_transform.py:13-52): bs base meshes -> bs^2 meshes,
 // out[i*bs + j] = mesh i with the swapped region's feature vertices from j.
 #include "cfsd_common.h"
-#include "side_work.h"
 #include "spmm_sched.h"
 
 namespace cfsd {
@@ -264,14 +263,9 @@ __global__ __launch_bounds__(256) void spmm_sched_csr_k(const int* __restrict__ 
                                                         const TY* __restrict__ elu_y,
                                                         TY* __restrict__ y, int m, int n, int c4,
                                                         int groups, int bpg, int per, int xvm,
-                                                        int yvm, int n_main, const SideJob side) {
-  const int n_side = side_grid(side);
-  if ((int)blockIdx.x < n_side) {  // side work riding in this launch (side_work.h)
-    if ((int)blockIdx.x < side.n_blocks) side_block<4>(side, (int)blockIdx.x);
-    return;
-  }
+                                                        int yvm, int n_main) {
   spmm_sched_csr_body<TX, TY, V, UNI>(ptr_s, col_s, val_s, rows_s, x, elu_y, y, m, n, c4, groups, bpg, per, xvm, yvm,
-                                      n_main, (int)blockIdx.x - n_side);
+                                      n_main, (int)blockIdx.x);
 }
 
 // out[(i*bs + j), v, :] = x[mesh(i or j), v, :]; one thread per (out mesh,
@@ -578,14 +572,6 @@ extern "C" int cfsd_spmm_sched_csr(const int32_t* ptr_s, const int32_t* col_s, c
                                    const int32_t* rows_s, const void* x, int x_dt,
                                    const void* elu_y, void* y, int y_dt, int batch, int m, int n,
                                    int c, void* stream) {
-  return cfsd_spmm_sched_csr_side(ptr_s, col_s, val_s, rows_s, x, x_dt, elu_y, y, y_dt, batch, m, n, c, nullptr,
-                                  stream);
-}
-
-extern "C" int cfsd_spmm_sched_csr_side(const int32_t* ptr_s, const int32_t* col_s, const float* val_s,
-                                        const int32_t* rows_s, const void* x, int x_dt, const void* elu_y,
-                                        void* y, int y_dt, int batch, int m, int n, int c,
-                                        const cfsd_side_work* side, void* stream) {
   if (!ptr_s || !col_s || !val_s || !rows_s || !x || !y)
     return set_error(CFSD_EINVAL, "spmm_sched_csr: null pointer");
   if (batch <= 0 || m <= 0 || n <= 0 || c <= 0 || (c % 4))
@@ -601,25 +587,20 @@ extern "C" int cfsd_spmm_sched_csr_side(const int32_t* ptr_s, const int32_t* col
   const int groups = (!xvm && batch % 8 == 0) ? 8 : 1, bpg = batch / groups;
   // bf16 x: 8 channels per thread (one 16-B load per entry; bf16 up0T 21.3 ->
   // see DESIGN) -- the same per-element folds
-  static const int v8 = env_knob("CFSD_SPMM_BF16_V8", 1);
-  const int V = (v8 && x_dt == CFSD_DT_BF16 && c % 8 == 0) ? 8 : 4;
+  const int V = (x_dt == CFSD_DT_BF16 && c % 8 == 0) ? 8 : 4;
   const int per = bpg * m * (c / V);
   const unsigned nb = (unsigned)(groups * ((per + 255) / 256));
-  SideJob J;
-  const int rc = make_side_job(side, J);
-  if (rc) return rc;
   const hipStream_t st = (hipStream_t)stream;
-  static const int uni_k = env_knob("CFSD_SPMM_UNI", 1);
-  const bool uni = uni_k && (bpg * (c / V)) % 64 == 0;
+  const bool uni = (bpg * (c / V)) % 64 == 0;
 #define SPSC(TX, TY, V_)                                                                                       \
   if (uni)                                                                                                     \
-    hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY, V_, true>), dim3(nb + side_grid(J)), dim3(256), 0, st, ptr_s,   \
+    hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY, V_, true>), dim3(nb), dim3(256), 0, st, ptr_s,                 \
                        col_s, val_s, rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / V_, groups, bpg, per, \
-                       xvm, yvm, (int)nb, J);                                                                  \
+                       xvm, yvm, (int)nb);                                                                     \
   else                                                                                                         \
-    hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY, V_, false>), dim3(nb + side_grid(J)), dim3(256), 0, st, ptr_s,  \
+    hipLaunchKernelGGL((spmm_sched_csr_k<TX, TY, V_, false>), dim3(nb), dim3(256), 0, st, ptr_s,                \
                        col_s, val_s, rows_s, (const TX*)x, (const TY*)elu_y, (TY*)y, m, n, c / V_, groups, bpg, per, \
-                       xvm, yvm, (int)nb, J)
+                       xvm, yvm, (int)nb)
   if (x_dt == CFSD_DT_F32 && y_dt == CFSD_DT_F32) {
     SPSC(float, float, 4);
   } else if (x_dt == CFSD_DT_F32) {

@@ -22,7 +22,6 @@
 #include "conv_vm32.h"
 #include "conv_coarse.h"
 #include "conv_lat.h"
-#include "side_work.h"
 
 namespace cfsd {
 
@@ -1078,13 +1077,8 @@ struct DxLatArgs {
   int nb;
 };
 template <int CIN, int COUT, int CTW>
-__global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, const DwLatArgs d, const SideJob side) {
-  const int n_side = side_grid(side);
-  if ((int)blockIdx.x < n_side) {  // side work riding in this launch (side_work.h)
-    if ((int)blockIdx.x < side.n_blocks) side_block<4>(side, (int)blockIdx.x);
-    return;
-  }
-  const int bid = (int)blockIdx.x - n_side, both = 2 * min(a.nb, d.nb);
+__global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, const DwLatArgs d) {
+  const int bid = (int)blockIdx.x, both = 2 * min(a.nb, d.nb);
   bool is_dx;
   int vb;
   if (bid < both) {
@@ -2475,7 +2469,7 @@ DwGeom lat_geom(int batch, int rows, int cin, int cout) {
   DwGeom g{kDwLat, 0, 0, 0};
   const long M = (long)batch * rows;
   const long U = (long)dw_units(cin, cout);
-  static const int lat_waves = env_knob("CFSD_LATDW_WAVES", kDwLatWaves);  // A/B knob
+  constexpr int lat_waves = kDwLatWaves;
   long R = (M * U / lat_waves + 15) / 16 * 16;
   R = R < 32 ? 32 : (R > 512 ? 512 : R);
   g.rchunk = (int)R;
@@ -2632,7 +2626,7 @@ namespace {
 bool fused_small(int cin, int cout) { return cout * kSeq <= 32 && (cin == 32 || cin == 64); }
 int fused_small_gx(long m_src) {  // ~2 32-row tiles per wave
   long gx = ((m_src + 31) / 32 + 7) / 8;
-  static const int bpc = env_knob("CFSD_BWDOUT_BPC", 0);  // A/B: workgroups per CU
+  constexpr int bpc = 0;  // workgroups per CU (0: the occupancy bound)
   const long cap = bpc > 0 ? (long)bpc * device_cus() : 1024;
   return (int)(gx > cap ? cap : (gx < 1 ? 1 : gx));
 }
@@ -2680,29 +2674,7 @@ extern "C" int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const fl
                                     float* dx, float* dw, float* db, float* workspace,
                                     size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
                                     int cin, int cout, void* stream) {
-  return cfsd_spiral_conv_bwd_side(x, idx, dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, dw, db, workspace,
-                                   workspace_bytes, batch, vsrc, rows, seq, cin, cout, nullptr, stream);
-}
-
-extern "C" int cfsd_spiral_conv_bwd_side(const float* x, const int32_t* idx, const float* dpre,
-                                         const int32_t* inv_ptr, const int32_t* inv_row,
-                                         const int32_t* inv_head, const float* w, const float* elu_y,
-                                         float* dx, float* dw, float* db, float* workspace,
-                                         size_t workspace_bytes, int batch, int vsrc, int rows, int seq,
-                                         int cin, int cout, const cfsd_side_work* side, void* stream) {
-  SideJob J;
-  int rc = make_side_job(side, J);
-  if (rc) return rc;
-  // hosts that cannot carry it (every shape but the paired lat launch) run
-  // the side work in a launch of its own right after the conv
-  const bool hosted = J.n_blocks > 0 && dx && !bwd_ks_paired(batch, vsrc, rows, cin, cout) &&
-                      bwd_paired(batch, vsrc, rows, cin, cout);
-  if (J.n_blocks > 0 && !hosted) {
-    rc = cfsd_spiral_conv_bwd_side(x, idx, dpre, inv_ptr, inv_row, inv_head, w, elu_y, dx, dw, db, workspace,
-                                   workspace_bytes, batch, vsrc, rows, seq, cin, cout, nullptr, stream);
-    return rc ? rc : cfsd_side_work_run(side, stream);
-  }
-  rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
+  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
   if (rc) return rc;
   if (!inv_ptr || !inv_row || !inv_head || !w || !workspace)
     return set_error(CFSD_EINVAL, "spiral_conv_bwd: null inverse table / w / workspace");
@@ -2743,11 +2715,11 @@ extern "C" int cfsd_spiral_conv_bwd_side(const float* x, const int32_t* idx, con
                 (int)((dw_tasks + 3) / 4), batch, 0, 0};
     const int ctw = dx_lat_ctw(cin, cout, M);
     a.nb = (int)(((M + 15) / 16 * (cin / 16 / ctw) + 3) / 4);
-    const dim3 grid((unsigned)(a.nb + d.nb + side_grid(J)));
+    const dim3 grid((unsigned)(a.nb + d.nb));
     const int n_el = cout * kSeq * cin + cout;
 #define PAIR(CIN_, COUT_, CTW_)                                                                 \
   if (cin == CIN_ && cout == COUT_ && ctw == CTW_) {                                            \
-    hipLaunchKernelGGL((conv_bwd_lat_pair<CIN_, COUT_, CTW_>), grid, dim3(256), 0, st, a, d, J); \
+    hipLaunchKernelGGL((conv_bwd_lat_pair<CIN_, COUT_, CTW_>), grid, dim3(256), 0, st, a, d);    \
     rc = launch_status("spiral_conv_bwd_lat_pair");                                             \
     if (rc || !dw) return rc;                                                                   \
     hipLaunchKernelGGL((conv_dw_reduce<CIN_, COUT_>), dim3((unsigned)((n_el + 63) / 64)),        \
@@ -3298,27 +3270,6 @@ extern "C" int cfsd_spiral_conv_bwd_rowsub_pair_bf16(const void* x, const int32_
                                       (bf16_t*)dx, workspace, nslab, vsrc, rows, batch, (hipStream_t)stream);
 }
 
-// ---- bf16 D3 dW slabs + the level-0 -> 1 Pool(up)^T in one launch (ABI 4.11)
-extern "C" int cfsd_spiral_conv_bwd_weight_spmm_bf16(const void* x, const int32_t* idx, const void* dpre,
-                                                     float* workspace, size_t workspace_bytes, int batch, int vsrc,
-                                                     int rows, int seq, int cin, int cout, const int32_t* ptr_s,
-                                                     const int32_t* col_s, const float* val_s,
-                                                     const int32_t* rows_s, const void* sx, const void* elu_y,
-                                                     void* y, int m, int n, int c, void* stream) {
-  int rc = check_conv_args(x, idx, dpre, batch, vsrc, rows, seq, cin, cout);
-  if (rc) return rc;
-  if (!workspace || !ptr_s || !col_s || !val_s || !rows_s || !sx || !y)
-    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_spmm_bf16: null pointer");
-  if (cin != 32 || cout != 32 || batch % 16 || m <= 0 || n <= 0 || c <= 0 || c % 8)
-    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_spmm_bf16: 32 -> 32, batch %% 16, c %% 8 only");
-  const int nslab = bf::dw_slabs(batch, rows, cin, cout);  // as cfsd_dw_reduce_batch's fused = 2 items
-  const size_t need = (size_t)nslab * ((size_t)cout * kSeq * cin + cout) * sizeof(float);
-  if (workspace_bytes < need) return set_error(CFSD_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
-  return bf::launch_dw_spmm16((const bf16_t*)x, idx, (const bf16_t*)dpre, workspace, nslab, vsrc, rows, batch, ptr_s,
-                              col_s, val_s, rows_s, (const bf16_t*)sx, (const bf16_t*)elu_y, (bf16_t*)y, m, n, c,
-                              (hipStream_t)stream);
-}
-
 // ---- the same pair on the bf16 step's tensors (ABI 4.11)
 extern "C" int cfsd_spiral_conv_bwd_flat_pair_bf16(const void* x, const int32_t* idx, const void* dpre,
                                                    const int32_t* inv_flat, int flat_width, const void* w,
@@ -3530,55 +3481,6 @@ static int fill_red_item(const cfsd_dw_slabs& q, int i, Item& d) {
   return CFSD_OK;
 }
 
-int cfsd::make_side_job(const cfsd_side_work* w, SideJob& J) {
-  J = SideJob{};
-  if (!w || (w->n_items <= 0 && w->n_ranges <= 0)) return CFSD_OK;
-  if (w->n_items > kSideItems || w->n_ranges > kSideRanges || w->n_items < 0 || w->n_ranges < 0)
-    return set_error(CFSD_EINVAL, "side work: %d items / %d ranges (max %d / %d)", w->n_items, w->n_ranges,
-                     kSideItems, kSideRanges);
-  if ((w->n_items && !w->items) || (w->n_ranges && !w->ranges)) return set_error(CFSD_EINVAL, "side work: null list");
-  if (w->n_ranges && !w->adam) return set_error(CFSD_EINVAL, "side work: ranges need adam = 1");
-  if (w->adam && (!w->param || !w->grad || !w->exp_avg || !w->exp_avg_sq || !w->step))
-    return set_error(CFSD_EINVAL, "side work: adam needs param / grad / exp_avg / exp_avg_sq / step");
-  int blk = 0;
-  J.n_items = w->n_items;
-  for (int i = 0; i < w->n_items; ++i) {
-    const int rc = fill_red_item(w->items[i], i, J.it[i]);
-    if (rc) return rc;
-    if (w->adam && (J.it[i].dw < w->grad || J.it[i].db < w->grad))
-      return set_error(CFSD_EINVAL, "side work: item %d outside the flat gradient", i);
-    J.it[i].blk0 = blk;
-    blk += (J.it[i].n_el + 63) / 64;
-  }
-  J.blk_items = blk;
-  J.n_ranges = w->n_ranges;
-  int rb = 0;
-  for (int r = 0; r < w->n_ranges; ++r) {
-    J.lo[r] = (long)w->ranges[2 * r];
-    J.hi[r] = (long)w->ranges[2 * r + 1];
-    if (J.hi[r] < J.lo[r]) return set_error(CFSD_EINVAL, "side work: range %d inverted", r);
-    J.rblk0[r] = rb;
-    rb += (int)((J.hi[r] - J.lo[r] + kSideRangeBlock - 1) / kSideRangeBlock);
-  }
-  J.rblk0[w->n_ranges] = rb;
-  J.n_blocks = blk + rb;
-  J.adam = w->adam;
-  J.p = w->param;
-  J.g = w->grad;
-  J.m = w->exp_avg;
-  J.v = w->exp_avg_sq;
-  J.shadow = reinterpret_cast<bf16_t*>(w->param_bf16);
-  J.step = w->step;
-  J.lr = w->lr;
-  J.b1 = w->beta1;
-  J.b2 = w->beta2;
-  J.eps = w->eps;
-  J.wd = w->weight_decay;
-  return CFSD_OK;
-}
-
-__global__ __launch_bounds__(256) void side_work_k(const SideJob J) { side_block<4>(J, blockIdx.x); }
-
 static int dw_reduce_batch_launch(const cfsd_dw_slabs* items, int n, const DwAdam* adam, long n_params,
                                   void* stream) {
   if (n <= 0 && !adam) return CFSD_OK;
@@ -3641,14 +3543,6 @@ static int dw_reduce_batch_launch(const cfsd_dw_slabs* items, int n, const DwAda
   if (blk == 0) return CFSD_OK;
   hipLaunchKernelGGL(dw_reduce_batch_k, dim3(blk), dim3(1024), 0, (hipStream_t)stream, B);
   return launch_status("dw_reduce_batch");
-}
-
-extern "C" int cfsd_side_work_run(const cfsd_side_work* side, void* stream) {
-  SideJob J;
-  const int rc = make_side_job(side, J);
-  if (rc || J.n_blocks == 0) return rc;
-  hipLaunchKernelGGL(side_work_k, dim3(J.n_blocks), dim3(256), 0, (hipStream_t)stream, J);
-  return launch_status("side_work");
 }
 
 extern "C" int cfsd_dw_reduce_batch(const cfsd_dw_slabs* items, int n, void* stream) {

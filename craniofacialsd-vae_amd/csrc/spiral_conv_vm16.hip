@@ -610,7 +610,7 @@ static int fwd16_t(const bf16_t* x, const int* idx, const bf16_t* w, const float
   constexpr size_t lds = (size_t)COUT * (kS * CIN + 8) * sizeof(bf16_t);
   auto kern = conv_fwd_vm16<CIN, COUT, ACT, TY>;
   const long tiles = (long)rows * (batch / 16);
-  static const int bpc = env_knob("CFSD_FWD16_BPC", 0);
+  constexpr int bpc = 0;
   const unsigned grid = bpc > 0 ? cu_blocks(tiles, 4, bpc)
                                 : balanced_blocks(tiles, 8, resident(kern, lds));  // >= 2 tiles per wave
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
@@ -662,55 +662,6 @@ __global__ __launch_bounds__(DW16_THREADS, 2 * DW16_WAVES / 4) void conv_bwd_row
     dw_vm16_body<float, 1>(x, idx, dpre, ws, vsrc, rows, batch, vb, nb_dw, lds_raw);
 }
 
-// The bf16 step's D3 weight-gradient slabs and the level-0 -> 1 Pool(up)^T
-// (the visiting-order SpMM over D3's data gradient, 8 channels per thread) as
-// two workgroup roles of ONE launch: independent, one MFMA-, one
-// latency-bound; both fit 80 VGPRs (two 768-thread workgroups per CU).
-template <bool UNI>
-__global__ __launch_bounds__(DW16_THREADS, 2 * DW16_WAVES / 4) void conv_dw_spmm16_pair(
-    const bf16_t* __restrict__ x, const int* __restrict__ idx, const bf16_t* __restrict__ dpre,
-    float* __restrict__ ws, int vsrc, int rows, int batch, int nb_dw, const int* __restrict__ ptr_s,
-    const int* __restrict__ col_s, const float* __restrict__ val_s, const int* __restrict__ rows_s,
-    const bf16_t* __restrict__ sx, const bf16_t* __restrict__ ey, bf16_t* __restrict__ sy, int m, int n, int c8,
-    int per, int nb_sp) {
-  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  const int bid = blockIdx.x, both = 2 * min(nb_dw, nb_sp);
-  bool is_dw;
-  int vb;
-  if (bid < both) {
-    is_dw = (bid & 1) == 0;
-    vb = bid >> 1;
-  } else {
-    is_dw = nb_dw > nb_sp;
-    vb = bid - both + both / 2;
-  }
-  if (is_dw)
-    dw_vm16_body<bf16_t, 1>(x, idx, dpre, ws, vsrc, rows, batch, vb, nb_dw, lds_raw);
-  else
-    spmm_sched_csr_body<bf16_t, bf16_t, 8, UNI>(ptr_s, col_s, val_s, rows_s, sx, ey, sy, m, n, c8, 1, batch, per, 1,
-                                                1, nb_sp, vb);
-}
-
-int launch_dw_spmm16(const bf16_t* x, const int* idx, const bf16_t* dpre, float* ws, int n_slabs, int vsrc, int rows,
-                     int batch, const int* ptr_s, const int* col_s, const float* val_s, const int* rows_s,
-                     const bf16_t* sx, const bf16_t* ey, bf16_t* sy, int m, int n, int c, hipStream_t st) {
-  if (batch % 16 || c % 8) return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_spmm_bf16: batch %% 16, c %% 8");
-  if ((long)vsrc * batch * 64 >= (long)kAbsent || (long)rows * batch * 64 >= (long)kAbsent ||
-      (long)batch * m * (c / 8) >= (1L << 31))
-    return set_error(CFSD_EINVAL, "spiral_conv_bwd_weight_spmm_bf16: operands exceed 32-bit offsets");
-  const int per = batch * m * (c / 8);
-  const int nb_sp = (per + DW16_THREADS - 1) / DW16_THREADS;
-  const dim3 grid((unsigned)(n_slabs + nb_sp));
-  const size_t lds = DW16_LDS_BYTES;
-  if ((batch * (c / 8)) % 64 == 0)
-    hipLaunchKernelGGL((conv_dw_spmm16_pair<true>), grid, dim3(DW16_THREADS), lds, st, x, idx, dpre, ws, vsrc, rows,
-                       batch, n_slabs, ptr_s, col_s, val_s, rows_s, sx, ey, sy, m, n, c / 8, per, nb_sp);
-  else
-    hipLaunchKernelGGL((conv_dw_spmm16_pair<false>), grid, dim3(DW16_THREADS), lds, st, x, idx, dpre, ws, vsrc, rows,
-                       batch, n_slabs, ptr_s, col_s, val_s, rows_s, sx, ey, sy, m, n, c / 8, per, nb_sp);
-  return launch_status("spiral_conv_bwd_weight_spmm_bf16");
-}
-
 int launch_bwd_rowsub16_pair(const bf16_t* x, const int* idx, const float* dpre, const int* flat, int width,
                              const float* w, const bf16_t* elu_y, bf16_t* dx, float* ws, int n_slabs, int vsrc,
                              int rows, int batch, hipStream_t st) {
@@ -719,7 +670,7 @@ int launch_bwd_rowsub16_pair(const bf16_t* x, const int* idx, const float* dpre,
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_rowsub_pair_bf16: operands exceed 32-bit offsets");
   constexpr size_t lds_dx = (size_t)kS * 32 * (32 + 8) * sizeof(float);
   constexpr size_t lds = lds_dx > (size_t)DW16_LDS_BYTES ? lds_dx : (size_t)DW16_LDS_BYTES;
-  static const int dxb = env_knob("CFSD_RS16PAIR_DXB", 0);  // dx workgroups (0: one per CU)
+  constexpr int dxb = 0;  // dx workgroups (0: one per CU)
   const int nb_dx = dxb > 0 ? dxb : device_cus();
 #define BV(FW_)                                                                                               \
   if (width == FW_) {                                                                                         \
@@ -740,7 +691,7 @@ int launch_bwd_vm16_pair(const bf16_t* x, const int* idx, const bf16_t* dpre, co
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair (bf16): operands exceed 32-bit offsets");
   constexpr size_t lds_dx = (size_t)kS * 32 * (32 + 8) * sizeof(bf16_t);
   constexpr size_t lds = lds_dx > (size_t)DW16_LDS_BYTES ? lds_dx : (size_t)DW16_LDS_BYTES;
-  static const int dxb = env_knob("CFSD_VM16PAIR_DXB", 0);  // dx workgroups (0: one per CU)
+  constexpr int dxb = 0;  // dx workgroups (0: one per CU)
   const int nb_dx = dxb > 0 ? dxb : device_cus();
 #define BV(FW_)                                                                                             \
   if (width == FW_) {                                                                                       \
@@ -813,7 +764,7 @@ static int dxf16_t(const TD* dpre, const int* flat, const bf16_t* w, const bf16_
   auto kern = conv_dx_flat_vm16<CIN, COUT, TD, FW>;
   const long tiles = (long)vsrc * (batch / 16);
   const int r = resident_blocks_of(kern, 512, lds);
-  static const int bpc = env_knob("CFSD_DX16_BPC", kVm16DxBpc);
+  constexpr int bpc = kVm16DxBpc;
   const unsigned grid = bpc > 0 ? cu_blocks(tiles, 8, bpc) : balanced_blocks(tiles, 8, r > 0 ? r : 1);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows,
                      batch);

@@ -664,7 +664,7 @@ static int fwd_t(const float* x, const int* idx, const float* w, const float* bi
   constexpr size_t lds = (size_t)COUT * (kS * CIN + 8) * sizeof(float);
   auto kern = conv_fwd_vm32<CIN, COUT, ACT, UPT, PD>;
   const long tiles = ((long)rows * (batch / 16) + UPT - 1) / UPT;
-  static const int bpc = env_knob("CFSD_FWD32_BPC", kVm32FwdBpc);
+  constexpr int bpc = kVm32FwdBpc;
   const unsigned grid = bpc > 0 ? cu_blocks(tiles, 4, bpc) : balanced_blocks(tiles, 4, resident(kern, 256, lds));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
   return launch_status("spiral_conv_fwd_vm32");
@@ -703,7 +703,7 @@ static int dxf_t(const float* dpre, int dpvm, int dxvm, const int* flat, const f
   constexpr size_t lds = (size_t)kS * CIN * (COUT + 8) * sizeof(float);
   auto kern = conv_dx_flat_vm32<CIN, COUT, FW, TY>;
   const long tiles = (long)vsrc * (batch / 16);
-  static const int bpc = env_knob("CFSD_DX32_BPC", kVm32DxBpc);
+  constexpr int bpc = kVm32DxBpc;
   const unsigned grid = bpc > 0 ? cu_blocks(tiles, 8, bpc) : balanced_blocks(tiles, 8, resident(kern, 512, lds));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows,
                      batch, dpvm, dxvm);
@@ -748,7 +748,7 @@ int launch_bwd_vm_pair(const float* dpre, const int* flat, int width, const floa
     return set_error(CFSD_EINVAL, "spiral_conv_bwd_flat_pair: operands exceed 32-bit offsets");
   constexpr size_t lds_dx = (size_t)kS * 32 * (32 + 8) * sizeof(float);
   constexpr size_t lds = lds_dx > DWV_LDS * sizeof(float) ? lds_dx : DWV_LDS * sizeof(float);
-  static const int dxb = env_knob("CFSD_VMPAIR_DXB", 0);  // dx workgroups (0: one per CU)
+  constexpr int dxb = 0;  // dx workgroups (0: one per CU)
   DxFlatArgs a{dpre, (const int4*)flat, w, elu_y, dx, vsrc, rows, batch, 1, 1, dxb > 0 ? dxb : device_cus()};
   const DwVmArgs d{x, idx, ws, ws_db, n_slabs};
 #define BV(FW_)                                                                                              \
@@ -797,7 +797,7 @@ static int fwd_out_t(const TX* x, const int* idx, const float* w, const float* b
   constexpr int U = kVmOutU;
   auto kern = conv_fwd_out_vm<CO, ACT, U, TX>;
   const long its = ((long)rows * (batch / 8) + U - 1) / U;
-  static const int bpc = env_knob("CFSD_FWDOUT_BPC", kVmOutFwdBpc);
+  constexpr int bpc = kVmOutFwdBpc;
   const unsigned grid = bpc > 0 ? cu_blocks(its, 4, bpc) : balanced_blocks(its, 4, resident(kern, 256, 0));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, x, idx, w, bias, y, vsrc, rows, batch, yvm);
   return launch_status("spiral_conv_fwd_out_vm");

@@ -10,7 +10,6 @@
 #include <stdio.h>
 
 #include "cfsd_common.h"
-#include "side_work.h"
 
 namespace cfsd {
 
@@ -35,14 +34,6 @@ int device_cus() {
     cus_cached = cus;
   }
   return cus_cached;
-}
-
-int env_knob(const char* name, int dflt) {
-  const char* e = getenv(name);
-  if (!e || !*e) return dflt;
-  char* end = nullptr;
-  const long v = strtol(e, &end, 10);
-  return (end && *end == 0) ? (int)v : dflt;
 }
 
 int resident_blocks(const void* kernel, int block_threads, size_t dyn_lds) {
@@ -476,13 +467,8 @@ __global__ __launch_bounds__(256) void latent_bwd_k(const float* __restrict__ mu
                                                     float* __restrict__ dmulv, int B, int L,
                                                     int train, int is_vae, int sigmoid,
                                                     const float* __restrict__ zval, int n_parts,
-                                                    int n_main, const SideJob side) {
-  const int n_side = side_grid(side);
-  if ((int)blockIdx.x < n_side) {  // side work riding in this launch (side_work.h)
-    if ((int)blockIdx.x < side.n_blocks) side_block<4>(side, (int)blockIdx.x);
-    return;
-  }
-  const int e = ((int)blockIdx.x - n_side) * blockDim.x + threadIdx.x;
+                                                    int n_main) {
+  const int e = (int)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B * L) return;
   const int i = e / L, l = e % L;
   float dzd = dz_dec[e];
@@ -1520,7 +1506,7 @@ extern "C" int cfsd_latent_bwd(const float* mulv, const float* eps, const float*
   if (is_vae && train && !eps) return set_error(CFSD_EINVAL, "latent_bwd: eps required");
   const int n = batch * latent, nb = (n + 255) / 256;
   hipLaunchKernelGGL(latent_bwd_k, dim3(nb), dim3(256), 0, (hipStream_t)stream, mulv, eps, dz_dec, dlat, dmulv,
-                     batch, latent, train, is_vae, sigmoid, z, 1, nb, SideJob{});
+                     batch, latent, train, is_vae, sigmoid, z, 1, nb);
   return launch_status("latent_bwd");
 }
 
@@ -1528,22 +1514,12 @@ extern "C" int cfsd_latent_bwd_parts(const float* mulv, const float* eps, const 
                                      const float* dz_parts, int n_parts, const float* dlat,
                                      float* dmulv, int batch, int latent, int train, int is_vae,
                                      int sigmoid, void* stream) {
-  return cfsd_latent_bwd_parts_side(mulv, eps, z, dz_parts, n_parts, dlat, dmulv, batch, latent, train, is_vae,
-                                    sigmoid, nullptr, stream);
-}
-extern "C" int cfsd_latent_bwd_parts_side(const float* mulv, const float* eps, const float* z,
-                                          const float* dz_parts, int n_parts, const float* dlat, float* dmulv,
-                                          int batch, int latent, int train, int is_vae, int sigmoid,
-                                          const cfsd_side_work* side, void* stream) {
   if (!mulv || !dz_parts || !dlat || !dmulv) return set_error(CFSD_EINVAL, "latent_bwd_parts: null pointer");
   if (n_parts <= 0) return set_error(CFSD_EINVAL, "latent_bwd_parts: n_parts %d", n_parts);
   if (is_vae && train && !eps) return set_error(CFSD_EINVAL, "latent_bwd_parts: eps required");
-  SideJob J;
-  const int rc = make_side_job(side, J);
-  if (rc) return rc;
   const int n = batch * latent, nb = (n + 255) / 256;
-  hipLaunchKernelGGL(latent_bwd_k, dim3(nb + side_grid(J)), dim3(256), 0, (hipStream_t)stream, mulv, eps, dz_parts,
-                     dlat, dmulv, batch, latent, train, is_vae, sigmoid, z, n_parts, nb, J);
+  hipLaunchKernelGGL(latent_bwd_k, dim3(nb), dim3(256), 0, (hipStream_t)stream, mulv, eps, dz_parts,
+                     dlat, dmulv, batch, latent, train, is_vae, sigmoid, z, n_parts, nb);
   return launch_status("latent_bwd_parts");
 }
 

@@ -183,26 +183,25 @@ class SDVAEEngine:
         self.vertex_major = bool(vertex_major)
         self.fuse_up = True  # coarse Deblocks: Pool(up) fused into the conv gather (False: separate SpMM)
         self.fuse_latent = True  # latent head + decoder Linear in one launch (False: two)
-        # the weight-gradient slab reductions + Adam at the end of a single-process
-        # step: "hosts" = those of finished layers ride in later latency-bound
-        # launches (ops.SideWork), the rest in one side-work launch; "final" = all
-        # in one side-work launch; "off" = cfsd_dw_reduce_batch(_adam)
-        self.side_work = "off"
+        # One default path per layer.  The attributes below select the fused
+        # launches; the separate launches they replace stay as the general
+        # fallback (shapes the fused kernels do not take) and as the bit-identity
+        # references of the GPU tests.
         # the bottleneck backward (coarsest Pool(up)^T, decoder Linear, latent
         # head, encoder Linear) as one launch (cfsd_bottleneck_bwd)
-        self.fuse_bottleneck = os.environ.get("CFSD_FUSE_BOTTLENECK", "1") != "0"
+        self.fuse_bottleneck = True
         # the feature swap and the first Enblock's conv as one launch (cfsd_spiral_conv_fwd_in_swap)
-        self.fuse_swap = os.environ.get("CFSD_FUSE_SWAP", "1") != "0"
+        self.fuse_swap = True
         # vertex-major levels whose fp32 Deblock backward runs as one dx + dW launch
         # (cfsd_spiral_conv_bwd_flat_pair): level 1 (D2: 37.8 vs 20.8 + 19.9 us,
         # step 0.563 vs 0.568 ms same-box); at level 0 the pair is slower (117.5 vs
         # 51.4 + 52.0 us: the dx role's 12-wave workgroups lose to its 2-per-CU kernel)
-        self.vm_pair_levels = {int(c) for c in os.environ.get("CFSD_VM_PAIR_LEVELS", "1") if c.isdigit()}
+        self.vm_pair_levels = {1}
         # the bf16 step's pair (cfsd_spiral_conv_bwd_flat_pair_bf16) at both vertex-major
-        # levels: D3 29.0 vs 20.0 + 19.0 us, D2 14.7 vs 10.4 + 11.6 us, step 0.427 -> 0.409 ms
-        self.rowsub_pair16 = os.environ.get("CFSD_RS16_PAIR", "1") != "0"
-        self.dw_spmm16 = os.environ.get("CFSD_DW_SPMM16", "0") != "0"
-        self.vm_pair_levels16 = {int(c) for c in os.environ.get("CFSD_VM16_PAIR_LEVELS", "01") if c.isdigit()}
+        # levels: D3 29.0 vs 20.0 + 19.0 us, D2 14.7 vs 10.4 + 11.6 us, step 0.427 -> 0.409 ms;
+        # and the bf16 Enblock's dx + dW pair (cfsd_spiral_conv_bwd_rowsub_pair_bf16)
+        self.rowsub_pair16 = True
+        self.vm_pair_levels16 = {0, 1}
         n_reg = topo.n_regions if topo.n_regions else 1
         self.region_size = self.spec.latent // n_reg if topo.n_regions else 0
         if topo.n_regions and self.w_lc and self.spec.latent % n_reg:
@@ -499,8 +498,7 @@ class SDVAEEngine:
                                          and ops.spiral_conv_bwd_flat_pair_workspace(bsz, nv[lv], T.seq[lv], cin,
                                                                                      cout) > 0)
             else:
-                b.vm_pair[("dec", i)] = (flat_ok and lv in self.vm_pair_levels16
-                                         and not (lv == 0 and self.dw_spmm16 and i > 0))
+                b.vm_pair[("dec", i)] = flat_ok and lv in self.vm_pair_levels16
         for i, (cin, cout, lv, _) in enumerate(S.dec_layers()):
             dw_region(("dec", i), nv[lv], nv[lv], T.seq[lv], cin, cout, True, lv in lp)
         for (cin, cout, lv) in S.enc_layers():
@@ -557,11 +555,11 @@ class SDVAEEngine:
             ops.spiral_conv_fwd_x(x, idx, w, w16, bias, act, out)
 
     @classmethod
-    def _spmm(cls, csr, x, m, out, elu_y=None, sched=None, uniform=0, side=None):
+    def _spmm(cls, csr, x, m, out, elu_y=None, sched=None, uniform=0):
         if cls._plain(x, out):
-            ops.spmm(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform, side=side)
+            ops.spmm(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform)
         else:
-            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform, side=side)
+            ops.spmm_x(csr, x, m, elu_y=elu_y, out=out, sched=sched, uniform=uniform)
 
     def _lin_names(self):
         n = self.spec.n
@@ -705,36 +703,15 @@ class SDVAEEngine:
         if bucket_hook is not None:
             bucket_hook(self.params.grad[:self.enc_conv_numel()])
 
-    def _grad_range(self, t):
-        """Flat [lo, hi) of a view of the gradient buffer."""
-        lo = (t.data_ptr() - self.params.grad.data_ptr()) // 4
-        return (lo, lo + t.numel())
-
     def backward_head(self, b, split=False, fuse_adam=False):
         """Losses -> decoder -> latent head -> encoder Linear.  ``split``:
         reduce the decoder conv weight gradients here (their bucket is then
         final) instead of in backward_tail's single batched reduce.
-        ``fuse_adam`` (single process, nothing between gradient and update):
-        with ``side_work`` each finished layer's Adam step rides in a later
-        launch of the backward (``b.adam_done`` lists the flat ranges already
-        updated; backward_tail updates the rest)."""
+        ``fuse_adam``: single process, nothing between gradient and update
+        (Adam then rides in backward_tail's batched reduce)."""
         T, S, P = self.topo, self.spec, self.params
         n = S.n
-        adam = self.adam_args() if fuse_adam else None
-        b.adam_done = []
-        side_items = []  # deferred slab sets not yet taken by a host launch
-
-        def take_side():
-            """Every deferred slab set so far (their layers' backward is done) as
-            side work of the next host launch, with their Adam step when fused."""
-            if self.side_work != "hosts" or not side_items:
-                return None
-            sw = ops.SideWork(side_items, adam=adam)
-            if adam is not None:
-                for _, dw, db in side_items:
-                    b.adam_done += [self._grad_range(dw), self._grad_range(db)]
-            side_items.clear()
-            return sw
+        side_items = []  # deferred weight-gradient slab sets (reduced in one launch later)
         pending, acc = getattr(b, "pending_finalize", (False, None))
         if pending:
             ops.recon_lap_bwd_finalize(b.out, b.x, b.unit, T.lapT_csr, b.dout, 1.0, self.w_lap,
@@ -771,11 +748,6 @@ class SDVAEEngine:
         for i in reversed(range(len(dec))):
             cin, cout, lv, ui = dec[i]
             w, _ = self._dec_w(i)
-            # bf16: level-0 dW slabs + this level's Pool(up)^T in one launch (after the dx)
-            fuse_up = (self.dw_spmm16 and lv == 0 and i > 0 and lv in b.xl and lv + 1 in b.xl
-                       and b.dec_up[i].dtype == torch.bfloat16 and b.dpre_dec[i - 1].dtype == torch.bfloat16
-                       and not b.vm_pair.get(("dec", i)) and cin == 32 and cout == 32
-                       and T.upT_nat[ui] is not None and self._flat_dx(b, lv, cin, cout))
             if b.vm_pair.get(("dec", i)) and b.dec_up[i].dtype == torch.bfloat16:  # bf16: the same pair
                 defer(ops.spiral_conv_bwd_flat_pair_bf16(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_flat[lv],
                                                          self._wx(f"de_layers.{i + 1}.conv.layer.weight"),
@@ -786,9 +758,8 @@ class SDVAEEngine:
                                                     w, None, None, b.g_dec_up[i],
                                                     workspace=b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
             elif lv in b.xl:  # vertex-major (bf16 or fp32) operands: dW slabs + dx
-                if not fuse_up:
-                    defer(ops.spiral_conv_bwd_weight_x(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
-                                                       b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
+                defer(ops.spiral_conv_bwd_weight_x(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
+                                                   b.ws_dw[("dec", i)]), f"de_layers.{i + 1}.conv.layer")
                 w16 = self._wx(f"de_layers.{i + 1}.conv.layer.weight")
                 if self._flat_dx(b, lv, cin, cout):  # vertex-major, batch % 16: one MFMA per list entry
                     ops.spiral_conv_bwd_data_flat(b.dpre_dec[i], T.spiral_flat[lv], w16, T.n_verts[lv],
@@ -797,12 +768,8 @@ class SDVAEEngine:
                     ops.spiral_conv_bwd_data_x(b.dpre_dec[i], T.spiral_inv[lv], w16, T.n_verts[lv],
                                                out=b.g_dec_up[i])
             elif b.paired[("dec", i)]:  # dx + dW slabs in one launch
-                # the paired launch of a ~1k-vertex layer (latency-bound, lat pair) hosts
-                # the slab reductions (+ Adam) of the layers finished before it
-                host = b.bsz * T.n_verts[lv] >= 8192
                 _, d = ops.spiral_conv_bwd(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], T.spiral_inv[lv],
-                                           w, None, None, dx=b.g_dec_up[i], workspace=b.ws_dw[("dec", i)],
-                                           side=take_side() if host else None)
+                                           w, None, None, dx=b.g_dec_up[i], workspace=b.ws_dw[("dec", i)])
                 defer(d, f"de_layers.{i + 1}.conv.layer")
             else:
                 defer(weight_grad(b.dec_up[i], T.spiral[lv], b.dpre_dec[i], None, None,
@@ -813,20 +780,11 @@ class SDVAEEngine:
             # k-th eighth of the rows (neighbouring rows share source blocks in its L2):
             # 17-19 vs 21.6 us at level 0; batch-major keeps the longest-rows-first order
             sch = T.upT_nat[ui] if lv in b.xl else T.upT_sched[ui]
-            # the coarse transposes (latency-bound) host the slab reduction (+ Adam)
-            # of every layer finished so far; the level-0/1 ones stream ~40 / 10 MB
-            # and are not hosts
-            sw = take_side() if (sch is not None and lv >= 2) else None
-            if fuse_up:
-                defer(ops.spiral_conv_bwd_weight_spmm_bf16(b.dec_up[i], T.spiral[lv], b.dpre_dec[i],
-                                                           b.ws_dw[("dec", i)], sch, b.g_dec_up[i],
-                                                           T.n_verts[lv + 1], b.dpre_dec[i - 1],
-                                                           elu_y=b.dec_out[i - 1]), f"de_layers.{i + 1}.conv.layer")
-            elif i > 0:  # through Pool(up) into the previous Deblock's ELU
+            if i > 0:  # through Pool(up) into the previous Deblock's ELU
                 self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dpre_dec[i - 1],
-                           elu_y=b.dec_out[i - 1], sched=sch, side=sw)
+                           elu_y=b.dec_out[i - 1], sched=sch)
             elif not fused_bn:
-                self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh, sched=sch, side=sw)
+                self._spmm(T.upT_csr[ui], b.g_dec_up[i], T.n_verts[lv + 1], out=b.dh, sched=sch)
         if fused_bn:  # Pool(up)^T + decoder Linear + latent head + encoder Linear: one launch
             self._bottleneck_bwd_fused(b)
             if split:
@@ -845,22 +803,7 @@ class SDVAEEngine:
                            dw=P.gview("de_layers.0.weight"), db=P.gview("de_layers.0.bias"),
                            workspace=b.lin_ws)
             dz = b.dz
-        # the latent head hosts the decoder Linear's Adam step (its gradient is
-        # final and its weight no longer read) and any slab set still pending
-        sw = None
-        if self.side_work == "hosts" and b.dz_parts is not None:
-            rng = []
-            if adam is not None:
-                lo, _ = self._grad_range(P.gview("de_layers.0.weight"))
-                _, hi = self._grad_range(P.gview("de_layers.0.bias"))
-                rng = [(lo, hi)]
-                b.adam_done.append((lo, hi))
-            if side_items:
-                sw = take_side()
-                sw.ranges += rng
-            elif rng:
-                sw = ops.SideWork(ranges=rng, adam=adam)
-        ops.latent_bwd(b.mulv, b.eps, b.z, dz, b.dlat, b.dmulv, S.latent, True, S.is_vae, S.sigmoid, side=sw)
+        ops.latent_bwd(b.mulv, b.eps, b.z, dz, b.dlat, b.dmulv, S.latent, True, S.is_vae, S.sigmoid)
         if split:
             ops.dw_reduce_batch(side_items)
             side_items.clear()
@@ -881,13 +824,13 @@ class SDVAEEngine:
                      out=b.dpre_enc[last])
 
     def _fused_bottleneck_ok(self, b):
-        """cfsd_bottleneck_bwd applies: partial-products decoder Linear, no
-        side work hosted by the latent head, the coarsest Deblock's gradient
+        """cfsd_bottleneck_bwd applies: partial-products decoder Linear, the
+        coarsest Deblock's gradient
         batch-major fp32 with 64-multiple channels, batch <= 16, latent <= 128."""
         S = self.spec
         g = b.g_dec_up[0]
         ne = S.latent * (2 if S.is_vae else 1)
-        return (self.fuse_bottleneck and b.dz_parts is not None and self.side_work != "hosts"
+        return (self.fuse_bottleneck and b.dz_parts is not None
                 and g.dtype == torch.float32 and not ops.is_vm(g) and g.is_contiguous()
                 and g.shape[2] % 64 == 0 and b.h.numel() // b.bsz <= 5120 and b.bsz <= 16 and S.latent <= 128
                 and ne <= 160)
@@ -1014,21 +957,6 @@ class SDVAEEngine:
                                          out=b.g_pooled[prev], workspace=b.ws)
                 ops.spmm(T.downT_csr[prev], b.g_pooled[prev], T.n_verts[prev], elu_y=b.enc_full[prev],
                          out=b.dpre_enc[prev])
-        done = getattr(b, "adam_done", [])
-        if fuse_adam and (done or self.side_work != "off"):
-            # Adam of everything the side work has not updated yet: the
-            # remaining slab sets' layers and the flat ranges between
-            covered = sorted(done + [self._grad_range(t) for _, dw, db in deferred for t in (dw, db)])
-            rest, cur = [], 0
-            for lo, hi in covered:
-                if lo > cur:
-                    rest.append((cur, lo))
-                cur = max(cur, hi)
-            if cur < P.numel:
-                rest.append((cur, P.numel))
-            ops.side_work_run(ops.SideWork(deferred, ranges=rest, adam=self.adam_args()))
-            b.adam_done = []
-            return
         ops.dw_reduce_batch(deferred, adam=self.adam_args() if fuse_adam else None)
 
     def adam_step(self, grad_scale=None):

@@ -224,65 +224,6 @@ def dw_reduce_batch(items, adam=None):
          float(a["beta2"]), float(a["eps"]), float(a["weight_decay"]), ptr(a.get("shadow")), stream_ptr())
 
 
-class SideWork:
-    """Side work for a host launch (``cfsd_side_work``, ABI 4.6): deferred
-    weight-gradient slab sets to reduce (``items``: (DeferredDw, dw, db) as
-    for :func:`dw_reduce_batch`) and, with ``adam`` (the dict of
-    :func:`dw_reduce_batch`), the Adam step of every reduced element and of
-    the flat ``ranges`` [(lo, hi), ...] whose gradient is final.  Runs as
-    extra workgroups of the host launch (``side=`` of :func:`spmm`,
-    :func:`spmm_x`, :func:`latent_bwd`) or alone (:func:`side_work_run`); same
-    values bit for bit as the reduce / Adam launches it replaces."""
-
-    def __init__(self, items=(), ranges=(), adam=None):
-        self.items = list(items)
-        self.ranges = [(int(a), int(b)) for a, b in ranges if int(b) > int(a)]
-        self.adam = adam
-        if len(self.items) > 12 or len(self.ranges) > 8:
-            raise ValueError(f"side work: {len(self.items)} items / {len(self.ranges)} ranges (max 12 / 8)")
-        if self.ranges and adam is None:
-            raise ValueError("side work: Adam ranges need adam=")
-
-    def __bool__(self):
-        return bool(self.items or self.ranges)
-
-    def ctype(self):
-        """The C struct (its item / range arrays are kept alive on self)."""
-        self._arr = (_abi.DwSlabs * max(len(self.items), 1))(*[d.desc(dw, db) for d, dw, db in self.items])
-        self._rng = (ctypes.c_size_t * max(2 * len(self.ranges), 2))(*[v for r in self.ranges for v in r])
-        c = _abi.SideWorkC()
-        c.items = ctypes.cast(self._arr, ctypes.c_void_p)
-        c.n_items = len(self.items)
-        c.ranges = ctypes.cast(self._rng, ctypes.c_void_p)
-        c.n_ranges = len(self.ranges)
-        a = self.adam
-        if a is not None:
-            n = a["param"].numel()
-            for t, nm in ((a["param"], "param"), (a["grad"], "grad"), (a["m"], "m"), (a["v"], "v")):
-                _need(t, (n,), name=nm)
-            if any(hi > n for _, hi in self.ranges):
-                raise ValueError("side work: range outside the flat buffers")
-            c.adam = 1
-            c.param, c.grad, c.exp_avg, c.exp_avg_sq = (a["param"].data_ptr(), a["grad"].data_ptr(),
-                                                       a["m"].data_ptr(), a["v"].data_ptr())
-            c.step = a["step"].data_ptr()
-            c.lr, c.beta1, c.beta2, c.eps, c.weight_decay = (float(a["lr"]), float(a["beta1"]), float(a["beta2"]),
-                                                            float(a["eps"]), float(a["weight_decay"]))
-            c.param_bf16 = a["shadow"].data_ptr() if a.get("shadow") is not None else None
-        self._c = c
-        return ctypes.byref(c)
-
-
-def _side_ptr(side):
-    return side.ctype() if side else None
-
-
-def side_work_run(side):
-    """The side work in a launch of its own (cfsd_side_work_run)."""
-    if side:
-        call("cfsd_side_work_run", _side_ptr(side), stream_ptr())
-
-
 def spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout):
     return int(_abi.lib().cfsd_spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout))
 
@@ -292,11 +233,9 @@ def spiral_conv_bwd_paired(bsz, vsrc, rows, seq, cin, cout):
     return bool(_abi.lib().cfsd_spiral_conv_bwd_paired(bsz, vsrc, rows, seq, cin, cout))
 
 
-def spiral_conv_bwd(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None, side=None):
+def spiral_conv_bwd(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None):
     """Fused dX (skipped when ``dx`` is None) + dW/db of one SpiralConv; same
-    results as spiral_conv_bwd_data followed by spiral_conv_bwd_weight.
-    ``side``: a :class:`SideWork` riding in the launch (the paired launch of a
-    ~1k-vertex layer; else it runs right after in a launch of its own)."""
+    results as spiral_conv_bwd_data followed by spiral_conv_bwd_weight."""
     bsz, vsrc, cin = x.shape
     rows, seq = idx.shape
     cout = dpre.shape[2]
@@ -316,14 +255,9 @@ def spiral_conv_bwd(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace
     if elu_y is not None:
         _need(elu_y, (bsz, vsrc, cin), name="elu_y")
     ws, nb = _conv_ws(workspace, x.device, spiral_conv_bwd_workspace(bsz, vsrc, rows, seq, cin, cout))
-    if side:
-        call("cfsd_spiral_conv_bwd_side", ptr(x), ptr(idx), ptr(dpre), ptr(inv_ptr), ptr(inv_row),
-             ptr(inv_head), ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb),
-             bsz, vsrc, rows, seq, cin, cout, _side_ptr(side), stream_ptr())
-    else:
-        call("cfsd_spiral_conv_bwd", ptr(x), ptr(idx), ptr(dpre), ptr(inv_ptr), ptr(inv_row),
-             ptr(inv_head), ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb),
-             bsz, vsrc, rows, seq, cin, cout, stream_ptr())
+    call("cfsd_spiral_conv_bwd", ptr(x), ptr(idx), ptr(dpre), ptr(inv_ptr), ptr(inv_row),
+         ptr(inv_head), ptr(w), ptr(elu_y), ptr(dx), ptr(dw), ptr(db), ptr(ws), ctypes.c_size_t(nb),
+         bsz, vsrc, rows, seq, cin, cout, stream_ptr())
     if dw is None:  # deferred weight gradient
         return dx, DeferredDw(ws, bsz, vsrc, rows, cin, cout, True)
     return dx
@@ -417,19 +351,16 @@ def spiral_gather(x, idx, out=None):
 
 
 # ------------------------------------------------------------------ pool / swap
-def spmm(csr, x, m, elu_y=None, out=None, order=None, uniform=0, sched=None, side=None):
+def spmm(csr, x, m, elu_y=None, out=None, order=None, uniform=0, sched=None):
     """y[b, r] = g * sum_{k in row r} val[k] x[b, col[k]]   (Pool, model.py:50-55).
     ``order``: optional row schedule (a permutation of the rows by decreasing
     length, for matrices with long skewed rows); ``uniform``: every row holds
     exactly that many entries (``topology.uniform_rows``; no row_ptr walk);
     ``sched``: the CSR re-stored in a visiting order (``topology.scheduled_csr``,
-    replaces ``csr``/``order``).  Same results bit for bit in every form.
-    ``side``: a :class:`SideWork` riding in the launch (``sched`` form only)."""
+    replaces ``csr``/``order``).  Same results bit for bit in every form."""
     row_ptr, col, val = csr
     bsz, n, c = x.shape
     _need(x, None, name="x")
-    if side and sched is None:
-        raise ValueError("side work rides only in the visiting-order (sched) SpMM")
     _need(row_ptr, (m + 1,), torch.int32, "row_ptr")
     _need(col, None, torch.int32, "col")
     _need(val, (col.numel(),), name="val")
@@ -437,7 +368,7 @@ def spmm(csr, x, m, elu_y=None, out=None, order=None, uniform=0, sched=None, sid
         _need(elu_y, (bsz, m, c), name="elu_y")
     y = _out(out, (bsz, m, c), x)
     if sched is not None:
-        _spmm_sched_csr(sched, x, elu_y, y, bsz, m, n, c, side)
+        _spmm_sched_csr(sched, x, elu_y, y, bsz, m, n, c)
         return y
     if order is not None:
         _spmm_sched(row_ptr, col, val, order, x, elu_y, y, bsz, m, n, c)
@@ -458,17 +389,13 @@ def _spmm_uniform(k, col, val, x, elu_y, y, bsz, m, n, c):
          bsz, m, n, c, stream_ptr())
 
 
-def _spmm_sched_csr(sched, x, elu_y, y, bsz, m, n, c, side=None):
-    """cfsd_spmm_sched_csr(_side) over a CSR stored in visiting order."""
+def _spmm_sched_csr(sched, x, elu_y, y, bsz, m, n, c):
+    """cfsd_spmm_sched_csr over a CSR stored in visiting order."""
     ptr_s, col_s, val_s, rows_s = sched
     _need(ptr_s, (m + 1,), torch.int32, "ptr_s")
     _need(rows_s, (m,), torch.int32, "rows_s")
     _need(col_s, None, torch.int32, "col_s")
     _need(val_s, (col_s.numel(),), name="val_s")
-    if side:
-        call("cfsd_spmm_sched_csr_side", ptr(ptr_s), ptr(col_s), ptr(val_s), ptr(rows_s), ptr(x), _st(x),
-             ptr(elu_y), ptr(y), _st(y), bsz, m, n, c, _side_ptr(side), stream_ptr())
-        return
     call("cfsd_spmm_sched_csr", ptr(ptr_s), ptr(col_s), ptr(val_s), ptr(rows_s), ptr(x), _st(x), ptr(elu_y),
          ptr(y), _st(y), bsz, m, n, c, stream_ptr())
 
@@ -747,19 +674,10 @@ def latent_linear_fwd(mulv, eps, key, z, dlat, terms, latent, region_size, train
          float(eta1), float(eta2), ptr(w), ptr(bias), ptr(out), n, stream_ptr())
 
 
-def latent_bwd(mulv, eps, z, dz_dec, dlat, dmulv, latent, train, is_vae, sigmoid, side=None):
+def latent_bwd(mulv, eps, z, dz_dec, dlat, dmulv, latent, train, is_vae, sigmoid):
     """``dz_dec`` [B, latent], or [parts, B, latent] partial products (summed
-    in part order: cfsd_latent_bwd_parts; ``side``: a :class:`SideWork`
-    riding in that launch)."""
+    in part order: cfsd_latent_bwd_parts)."""
     _need(dmulv, tuple(mulv.shape), name="dmulv")
-    if side and dz_dec.dim() != 3:
-        raise ValueError("side work rides only in the partial-products latent backward")
-    if dz_dec.dim() == 3 and side:
-        parts, bsz = dz_dec.shape[:2]
-        _need(dz_dec, (parts, bsz, latent), name="dz_parts")
-        call("cfsd_latent_bwd_parts_side", ptr(mulv), ptr(eps), ptr(z), ptr(dz_dec), parts, ptr(dlat),
-             ptr(dmulv), bsz, latent, int(train), int(is_vae), int(sigmoid), _side_ptr(side), stream_ptr())
-        return
     if dz_dec.dim() == 3:
         parts, bsz = dz_dec.shape[:2]
         _need(dz_dec, (parts, bsz, latent), name="dz_parts")
@@ -1174,38 +1092,6 @@ def spiral_conv_bwd_rowsub_pair_bf16(x, idx, dpre, flat, w, dx, elu_y=None, work
     return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2)
 
 
-def spiral_conv_bwd_weight_spmm_bf16(x, idx, dpre, workspace, sched, sx, m, out, elu_y=None):
-    """The bf16 step's D3 weight-gradient slabs (:func:`spiral_conv_bwd_weight_x`
-    deferred) and the visiting-order SpMM ``out = elu'(elu_y) * (P^T sx)``
-    (:func:`spmm_x` with ``sched``) as two roles of ONE launch
-    (``cfsd_spiral_conv_bwd_weight_spmm_bf16``, ABI 4.11); returns the
-    DeferredDw.  Every tensor bf16 vertex-major."""
-    bsz, vsrc, cin = x.shape
-    rows, seq = idx.shape
-    cout = dpre.shape[2]
-    _, n, c = sx.shape
-    for t, nm in ((x, "x"), (dpre, "dpre"), (sx, "sx"), (out, "out")):
-        _needl(t, None, nm, torch.bfloat16)
-        if not is_vm(t):
-            raise ValueError(f"spiral_conv_bwd_weight_spmm_bf16: {nm} must be vertex-major")
-    _needl(out, (bsz, m, c), "out", torch.bfloat16)
-    if elu_y is not None:
-        _needl(elu_y, (bsz, m, c), "elu_y", torch.bfloat16)
-        _same_layout(out, elu_y, "out and elu_y")
-    _need(idx, (rows, seq), torch.int32, "idx")
-    ptr_s, col_s, val_s, rows_s = sched
-    _need(ptr_s, (m + 1,), torch.int32, "ptr_s")
-    _need(rows_s, (m,), torch.int32, "rows_s")
-    _need(col_s, None, torch.int32, "col_s")
-    _need(val_s, (col_s.numel(),), name="val_s")
-    _need(workspace, None, name="workspace")
-    nbytes = workspace.numel() * workspace.element_size()
-    call("cfsd_spiral_conv_bwd_weight_spmm_bf16", ptr(x), ptr(idx), ptr(dpre), ptr(workspace),
-         ctypes.c_size_t(nbytes), bsz, vsrc, rows, seq, cin, cout, ptr(ptr_s), ptr(col_s), ptr(val_s), ptr(rows_s),
-         ptr(sx), ptr(elu_y), ptr(out), m, n, c, stream_ptr())
-    return DeferredDw(workspace, bsz, vsrc, rows, cin, cout, 2)
-
-
 def spiral_conv_bwd_x(x, idx, dpre, inv, w, dw, db, dx=None, elu_y=None, workspace=None):
     """Fused dx + dW of the xyz output conv with bf16 (or fp32) x / elu_y /
     dx in either layout."""
@@ -1271,12 +1157,10 @@ def spiral_conv_bwd_out_flat(x, idx, dpre, flat, w, dw, db, dx=None, elu_y=None,
     return dx
 
 
-def spmm_x(csr, x, m, elu_y=None, out=None, order=None, uniform=0, sched=None, side=None):
+def spmm_x(csr, x, m, elu_y=None, out=None, order=None, uniform=0, sched=None):
     """Pool SpMM with fp32 or bf16 operands (fp32 sums, file order)."""
     row_ptr, col, val = csr
     bsz, n, c = x.shape
-    if side and sched is None:
-        raise ValueError("side work rides only in the visiting-order (sched) SpMM")
     _needl(x, None, "x")
     _need(row_ptr, (m + 1,), torch.int32, "row_ptr")
     _need(col, None, torch.int32, "col")
@@ -1286,7 +1170,7 @@ def spmm_x(csr, x, m, elu_y=None, out=None, order=None, uniform=0, sched=None, s
         _needl(elu_y, (bsz, m, c), "elu_y", out.dtype)
         _same_layout(out, elu_y, "out and elu_y")
     if sched is not None:
-        _spmm_sched_csr(sched, x, elu_y, out, bsz, m, n, c, side)
+        _spmm_sched_csr(sched, x, elu_y, out, bsz, m, n, c)
         return out
     if order is not None:
         _spmm_sched(row_ptr, col, val, order, x, elu_y, out, bsz, m, n, c)

@@ -131,38 +131,6 @@ int cfsd_dw_reduce_batch_adam(const cfsd_dw_slabs* items, int n, float* param, c
                               size_t n_params, float lr, float beta1, float beta2, float eps,
                               float weight_decay, uint16_t* param_bf16, void* stream);
 
-/* Side work (ABI 4.6): slab reductions (as cfsd_dw_reduce_batch) and Adam
- * steps (as cfsd_adam) that run as EXTRA WORKGROUPS of another launch -- the
- * *_side entry points below take one -- instead of a launch of their own at
- * the end of the step (model_manager.py:315-316: the gradient of a layer is
- * final, and on one GPU its Adam step may start, once its own backward is
- * done).  Fields:
- *   items / n_items: deferred slab sets (<= 12) reduced into their dw / db;
- *   ranges / n_ranges: [lo, hi) element pairs (<= 8) of the flat buffers
- *     whose gradient is already final: Adam only (needs adam = 1);
- *   adam: 1 = apply the Adam step of cfsd_adam to every reduced element and
- *     every range element (param .. param_bf16 as in cfsd_adam; the items'
- *     dw / db must lie inside `grad`), 0 = reduce only.
- * Same values bit for bit as the reduce / Adam launches they replace.  The
- * caller guarantees that nothing in the host launch reads or writes what the
- * side work touches. */
-typedef struct {
-  const cfsd_dw_slabs* items;
-  int n_items;
-  const size_t* ranges;
-  int n_ranges;
-  int adam;
-  float* param;
-  const float* grad;
-  float* exp_avg;
-  float* exp_avg_sq;
-  const int32_t* step;
-  float lr, beta1, beta2, eps, weight_decay;
-  uint16_t* param_bf16;
-} cfsd_side_work;
-/* The side work alone, in a launch of its own (side == NULL or empty: no launch). */
-int cfsd_side_work_run(const cfsd_side_work* side, void* stream);
-
 /* Fused backward of one SpiralConv (model.py:27-41 autograd, dX and dW/db of
  * the same layer in one call): dx exactly as cfsd_spiral_conv_bwd_data
  * (skipped when dx == NULL, e.g. the first layer), dw/db exactly as
@@ -180,14 +148,6 @@ int cfsd_spiral_conv_bwd(const float* x, const int32_t* idx, const float* dpre,
                          float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows,
                          int seq, int cin, int cout, void* stream);
 size_t cfsd_spiral_conv_bwd_workspace(int batch, int vsrc, int rows, int seq, int cin, int cout);
-/* cfsd_spiral_conv_bwd with side work (ABI 4.6; side may be NULL): it rides
- * in the launch where that launch is the paired dx + dW one of a ~1k-vertex
- * layer (the level-2 Deblock), else it runs in a launch of its own after. */
-int cfsd_spiral_conv_bwd_side(const float* x, const int32_t* idx, const float* dpre,
-                              const int32_t* inv_ptr, const int32_t* inv_row, const int32_t* inv_head,
-                              const float* w, const float* elu_y, float* dx, float* dw, float* db,
-                              float* workspace, size_t workspace_bytes, int batch, int vsrc, int rows,
-                              int seq, int cin, int cout, const cfsd_side_work* side, void* stream);
 /* 1 when cfsd_spiral_conv_bwd with dx != NULL runs dx and dW as one paired
  * launch for this shape (no reference counterpart: a scheduling query). */
 int cfsd_spiral_conv_bwd_paired(int batch, int vsrc, int rows, int seq, int cin, int cout);
@@ -248,17 +208,6 @@ int cfsd_spiral_conv_bwd_rowsub_pair_bf16(const void* x, const int32_t* idx, con
                                           const int32_t* inv_flat, int flat_width, const float* w, const void* elu_y,
                                           void* dx, float* workspace, size_t workspace_bytes, int batch, int vsrc,
                                           int rows, int seq, int cin, int cout, void* stream);
-/* The bf16 step's level-0 Deblock weight-gradient slabs (as
- * cfsd_spiral_conv_bwd_weight_x deferred, fused = 2: x / dpre bf16
- * vertex-major, 32 -> 32, batch % 16 == 0) and the visiting-order Pool(up)^T
- * SpMM of cfsd_spmm_sched_csr (sx, y, elu_y bf16 vertex-major [*][batch][c],
- * c % 8 == 0) as two workgroup roles of ONE launch (ABI 4.11).  Same values
- * as the two calls. */
-int cfsd_spiral_conv_bwd_weight_spmm_bf16(const void* x, const int32_t* idx, const void* dpre, float* workspace,
-                                          size_t workspace_bytes, int batch, int vsrc, int rows, int seq, int cin,
-                                          int cout, const int32_t* ptr_s, const int32_t* col_s, const float* val_s,
-                                          const int32_t* rows_s, const void* sx, const void* elu_y, void* y, int m,
-                                          int n, int c, void* stream);
 /* The same pair on the bf16 step's tensors (ABI 4.11): x, dpre, dx, elu_y
  * bf16 vertex-major, w the bf16 weight shadow; always deferred
  * (cfsd_dw_reduce_batch item with fused = 2; workspace as
@@ -324,13 +273,6 @@ int cfsd_spmm_csr_sched(const int32_t* row_ptr, const int32_t* col, const float*
 int cfsd_spmm_sched_csr(const int32_t* ptr_s, const int32_t* col_s, const float* val_s,
                         const int32_t* rows_s, const void* x, int x_dt, const void* elu_y, void* y,
                         int y_dt, int batch, int m, int n, int c, void* stream);
-
-/* cfsd_spmm_sched_csr with side work riding in the same launch (ABI 4.6;
- * side may be NULL). */
-int cfsd_spmm_sched_csr_side(const int32_t* ptr_s, const int32_t* col_s, const float* val_s,
-                             const int32_t* rows_s, const void* x, int x_dt, const void* elu_y, void* y,
-                             int y_dt, int batch, int m, int n, int c, const cfsd_side_work* side,
-                             void* stream);
 
 /* cfsd_spmm_csr_x for a matrix whose rows all hold exactly k (1..4) entries,
  * row r's at [r*k, r*k + k) of col/val (the CSR arrays of the barycentric
@@ -524,12 +466,6 @@ int cfsd_latent_bwd(const float* mulv, const float* eps, const float* z, const f
 int cfsd_latent_bwd_parts(const float* mulv, const float* eps, const float* z,
                           const float* dz_parts, int n_parts, const float* dlat, float* dmulv,
                           int batch, int latent, int train, int is_vae, int sigmoid, void* stream);
-/* cfsd_latent_bwd_parts with side work riding in the same launch (ABI 4.6;
- * side may be NULL). */
-int cfsd_latent_bwd_parts_side(const float* mulv, const float* eps, const float* z,
-                               const float* dz_parts, int n_parts, const float* dlat, float* dmulv,
-                               int batch, int latent, int train, int is_vae, int sigmoid,
-                               const cfsd_side_work* side, void* stream);
 /* Reduce the recon partials + latent terms into out[5] = {rec, kl, lc, lap, tot}
  * (tot = rec + w_kl*kl + w_lc*lc + w_lap*lap, model_manager.py:308-312) and,
  * when acc != NULL, add them to acc[0..4] and 1 to acc[5] (per-epoch sums on

@@ -484,33 +484,3 @@ def test_bwd_rowsub_pair_bf16(mods, dtopo, with_elu):
     assert torch.equal(dx_a, dx_b)
     assert torch.equal(dw_a, dw_b) and torch.equal(db_a, db_b)
 
-
-@pytest.mark.parametrize("with_elu", [False, True])
-def test_bwd_weight_spmm_bf16(mods, dtopo, with_elu):
-    """cfsd_spiral_conv_bwd_weight_spmm_bf16 (ABI 4.11: the bf16 level-0 dW
-    slabs and the visiting-order Pool(up)^T SpMM as two roles of one launch)
-    == the deferred cfsd_spiral_conv_bwd_weight_x + spmm_x(sched=upT_nat),
-    bit for bit (the SpMM output, and dW / db through the batched reduce)."""
-    _, ops, _ = mods
-    if dtopo.upT_nat[0] is None:
-        pytest.skip("no visiting-order schedule at level 0")
-    g = torch.Generator().manual_seed(51 + with_elu)
-    bsz, v, m = 16, dtopo.n_verts[0], dtopo.n_verts[1]
-    idx = dtopo.spiral[0]
-    x = ops.to_vm(torch.randn(bsz, v, 32, generator=g).to(DEV).bfloat16())
-    dpre = ops.to_vm(torch.randn(bsz, v, 32, generator=g).to(DEV).bfloat16())
-    sx = ops.to_vm(torch.randn(bsz, v, 32, generator=g).to(DEV).bfloat16())
-    ey = ops.to_vm(torch.nn.functional.elu(torch.randn(bsz, m, 32, generator=g)).to(DEV).bfloat16()) if with_elu else None
-    nb = ops.spiral_conv_bwd_weight_x_workspace(bsz, v, 9, 32, 32)
-    ws_a = torch.zeros(nb // 4 + 64, device=DEV)
-    ws_b = torch.zeros_like(ws_a)
-    y_a = ops.vm_empty(bsz, m, 32, dtype=torch.bfloat16, device=DEV)
-    y_b = ops.vm_empty(bsz, m, 32, dtype=torch.bfloat16, device=DEV)
-    d_a = ops.spiral_conv_bwd_weight_spmm_bf16(x, idx, dpre, ws_a, dtopo.upT_nat[0], sx, m, y_a, elu_y=ey)
-    d_b = ops.spiral_conv_bwd_weight_x(x, idx, dpre, None, None, ws_b)
-    ops.spmm_x(dtopo.upT_csr[0], sx, m, elu_y=ey, out=y_b, sched=dtopo.upT_nat[0])
-    dw_a, db_a = torch.empty(32, 288, device=DEV), torch.empty(32, device=DEV)
-    dw_b, db_b = torch.empty_like(dw_a), torch.empty_like(db_a)
-    ops.dw_reduce_batch([(d_a, dw_a, db_a), (d_b, dw_b, db_b)])
-    assert torch.equal(y_a, y_b)
-    assert torch.equal(dw_a, dw_b) and torch.equal(db_a, db_b)

@@ -465,21 +465,17 @@ def test_train_step_deterministic(dtopo):
 
 @pytest.mark.parametrize("precision,vertex_major", [("fp32", True), ("fp32", False), ("bf16", True)])
 def test_fused_reduce_adam_matches_separate(dtopo, precision, vertex_major):
-    """The single-process step's fused updates == cfsd_dw_reduce_batch +
-    cfsd_adam, bit for bit: parameters, gradients, both Adam moments and
-    (bf16) the weight shadow after two steps.  Fused two ways: the side work
-    (ABI 4.6: slab reductions + Adam of finished layers riding in the
-    up-sampling transposes and the latent backward, the rest in one side-work
-    launch) and, with side_work off, cfsd_dw_reduce_batch_adam; in bf16 also
-    the bf16-MFMA weight-gradient items."""
+    """The single-process step's fused update (cfsd_dw_reduce_batch_adam)
+    == cfsd_dw_reduce_batch + cfsd_adam, bit for bit: parameters, gradients,
+    both Adam moments and (bf16) the weight shadow after two steps; in bf16
+    also the bf16-MFMA weight-gradient items."""
     w = recipe.golden_weights()
     x = torch.from_numpy(O.swap_features(recipe.normalized_meshes(4), [np.asarray(r) for r in
                                          O.Topology(recipe.load_topology()).region_features], 2)).to(DEV)
     eps = torch.from_numpy(recipe.train_eps(0)).to(DEV)
     outs = []
-    for mode in ("hosts", "final", "off", "separate"):
+    for mode in ("fused", "separate"):
         eng = make_engine(dtopo, w, precision=precision, vertex_major=vertex_major)
-        eng.side_work = "off" if mode == "separate" else mode
         for _ in range(2):
             b = eng.set_batch(x, key_index=2, eps=eps)
             if mode != "separate":

@@ -1031,7 +1031,11 @@ class SDVAEEngine:
 
     def load_batch(self, b, data):
         """The step's input from the picked base meshes: the on-device feature
-        swap (bs -> bs^2) or, with ``swap_features`` False, the bs meshes."""
+        swap (bs -> bs^2) or, with ``swap_features`` False, the bs meshes.
+        With the swap fused into the first Enblock's conv (the default,
+        ``_swap_in_conv_ok``) nothing is written here: ``b.x`` holds the
+        swapped batch only after :meth:`encode` / :meth:`forward` ran (that
+        launch writes it); ``b.swap_from`` marks the pending swap."""
         b.swap_from = None
         if self.swap and self._swap_in_conv_ok(b, data):
             b.swap_from = data.meshes  # the swap rides in the first Enblock's conv launch (encode)

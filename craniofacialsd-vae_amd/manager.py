@@ -187,6 +187,10 @@ class ModelManager:
         b = self.engine.buffers(self.engine.step_rows)
         acc = self.engine.loss_acc if train else self.val_acc
         acc.zero_()
+        # writes made through ``net`` (a torch optimizer on its parameters,
+        # net.load_state_dict) reach the fp32 master but not the bf16 shadow
+        # the bf16 kernels read: refresh it once per epoch (one cast launch)
+        self.engine.sync_shadow()
         steps_done = 0
         while steps_done < data.n_batches:
             if train:
@@ -227,10 +231,19 @@ class ModelManager:
         ``nn.Parameter``s are views of the flat buffer, so the engine's Adam
         updates are what it computes with.  Autograd runs through libcfsd
         (``model.py`` autograd Functions); parameter gradients it produces
-        land in the module's own ``.grad`` tensors, not in the engine's."""
+        land in the module's own ``.grad`` tensors, not in the engine's.
+        Read-mostly: a write through it (an optimizer step on its parameters,
+        ``load_state_dict``) updates the fp32 master; in bf16 mode call
+        :meth:`sync_from_net` afterwards (``run_epoch`` also refreshes the
+        bf16 shadow at every epoch start)."""
         if getattr(self, "_net", None) is None:
             self._net = _engine_model(self.engine, self.topology_arrays, self._model_params, self.device)
         return self._net
+
+    def sync_from_net(self):
+        """Refresh the engine's bf16 weight shadow after writes made through
+        :attr:`net` (no-op in fp32)."""
+        self.engine.sync_shadow()
 
     def forward(self, data):
         """``ModelManager.forward`` (``model_manager.py:240-241``):

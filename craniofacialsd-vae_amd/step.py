@@ -40,6 +40,14 @@ import torch
 
 from . import ops
 
+# Capture in thread-local mode: with the default ("global") mode a CUDA/HIP
+# call from ANY thread that is unsafe during capture fails -- and the RCCL
+# process group's watchdog thread polls the events of finished collectives
+# (cudaEventQuery) at its own pace, so a capture that overlaps one of its
+# polls aborted the process (a watchdog exception in one of round 6's
+# one-rank RCCL capture tests).  The capturing thread itself is still checked.
+_CAPTURE_MODE = "thread_local"
+
 
 class TrainStep:
     """``TrainStep(engine, data, averager=None, acc=None)``.
@@ -131,13 +139,13 @@ class TrainStep:
         torch.cuda.synchronize(dev)
         if self.one_graph:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                 self.eager_step()
             self.graphs = [g]
         else:
             self.graphs = [torch.cuda.CUDAGraph() for _ in range(3)]
             for g, fn in zip(self.graphs, (self.part_a, self.part_b, self.part_c)):
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                     fn()
 
     def capture_multi(self):
@@ -147,7 +155,7 @@ class TrainStep:
         many steps.  Nothing runs while recording."""
         if self.graph_multi is None and self.graphs is not None and self.one_graph:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                 for _ in range(self.steps_per_graph):
                     self.eager_step()
             self.graph_multi = g

@@ -49,7 +49,10 @@ def _run(tmp_path, script, nproc, *args, env_extra=None, timeout=600):
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(wfile), ROOT, str(out), *args]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    if r.returncode != 0:  # the first error lines (a C++ exception's what() precedes its long trace)
+        errs = [ln for ln in (r.stdout + r.stderr).splitlines()
+                if any(k in ln for k in ("Error", "error", "what()", "Exception", "failed"))][:20]
+        raise AssertionError("\n".join(errs) + "\n---\n" + r.stderr[-2000:])
     return json.loads(out.read_text())
 
 

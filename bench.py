@@ -811,6 +811,7 @@ def main():
                        "parallelism": f"dp{world}", "graph": runner.use_graph,
                        "step_graph": ("one graph per step" if runner.ts.one_graph else "three graphs") +
                                      (", collectives captured" if (world > 1 and runner.ts.one_graph) else ""),
+                       "step_graph_fallback": runner.ts.fallback,
                        "collective": None if world == 1 else
                        (("rccl" if backend == "nccl" else backend) + " all_reduce, 2 buckets overlapped")},
             "roofline": roof,

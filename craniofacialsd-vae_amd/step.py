@@ -79,6 +79,7 @@ class TrainStep:
         # backend cannot be captured or the three-graph structure is forced
         self.one_graph = self.avg is None or (os.environ.get("CFSD_DP_GRAPH", "one") != "three"
                                               and self.avg.capturable)
+        self.fallback = None  # why a capturable backend ended up with the three-graph structure
 
     @property
     def world(self):
@@ -138,27 +139,46 @@ class TrainStep:
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         if self.one_graph:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
-                self.eager_step()
-            self.graphs = [g]
-        else:
-            self.graphs = [torch.cuda.CUDAGraph() for _ in range(3)]
-            for g, fn in zip(self.graphs, (self.part_a, self.part_b, self.part_c)):
+            try:
+                g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
-                    fn()
+                    self.eager_step()
+                self.graphs = [g]
+                return
+            except RuntimeError as e:
+                # a collective the backend refused to record (nothing ran
+                # during the capture): fall back to the three-graph structure,
+                # the collectives issued by the host between the replays
+                if self.avg is None:
+                    raise
+                self.avg._works.clear()
+                self.fallback = f"collectives not capturable: {e!r}"[:300]
+                self.one_graph = False
+                torch.cuda.synchronize(dev)
+        self.graphs = [torch.cuda.CUDAGraph() for _ in range(3)]
+        for g, fn in zip(self.graphs, (self.part_a, self.part_b, self.part_c)):
+            with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+                fn()
 
     def capture_multi(self):
         """Record (once) the graph holding ``steps_per_graph`` whole steps,
         which :meth:`run` replays k // steps_per_graph times: the per-replay
         host gap (~8 us between consecutive replays) is paid once per that
         many steps.  Nothing runs while recording."""
-        if self.graph_multi is None and self.graphs is not None and self.one_graph:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
-                for _ in range(self.steps_per_graph):
-                    self.eager_step()
-            self.graph_multi = g
+        if self.graph_multi is None and self.graphs is not None and self.one_graph and self.steps_per_graph > 1:
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+                    for _ in range(self.steps_per_graph):
+                        self.eager_step()
+                self.graph_multi = g
+            except RuntimeError as e:  # keep replaying the one-step graph
+                if self.avg is None:
+                    raise
+                self.avg._works.clear()
+                self.fallback = f"multi-step graph not capturable: {e!r}"[:300]
+                self.steps_per_graph = 1
+                torch.cuda.synchronize(self.eng.device)
 
     capture_pair = capture_multi  # (round-4 name)
 
@@ -181,12 +201,14 @@ class TrainStep:
         """``k`` training steps (the same steps as ``k`` calls of :meth:`step`);
         a one-graph runner replays the multi-step graph."""
         if self.graphs is not None and self.one_graph:
-            n = self.steps_per_graph
-            if k >= n:
+            if k >= self.steps_per_graph > 1:
                 self.capture_multi()
-            for _ in range(k // n):
-                self.graph_multi.replay()
-            for _ in range(k % n):
+            n = self.steps_per_graph if self.graph_multi is not None else 1
+            if n > 1:
+                for _ in range(k // n):
+                    self.graph_multi.replay()
+                k %= n
+            for _ in range(k):
                 self.graphs[0].replay()
             return
         for _ in range(k):

@@ -250,20 +250,38 @@ def state(eng):
         out.append(P.shadow)
     return [t.detach().cpu().clone() for t in out]
 
+import craniofacialsd_vae_amd.step as S
+real_graph = torch.cuda.graph
+
+class RefusingGraph:  # a backend that refuses the first capture (the fallback path)
+    calls = 0
+    def __init__(self, *a, **k):
+        self.inner = real_graph(*a, **k)
+    def __enter__(self):
+        RefusingGraph.calls += 1
+        if RefusingGraph.calls == 1:
+            raise RuntimeError("simulated: collective not capturable")
+        return self.inner.__enter__()
+    def __exit__(self, *exc):
+        return self.inner.__exit__(*exc)
+
 runs = {}
-for mode in ("single", "rccl_one_graph", "rccl_three_graphs"):
+for mode in ("single", "rccl_one_graph", "rccl_three_graphs", "rccl_fallback"):
     eng, data = make()
     avg = None if mode == "single" else D.GradientAverager(1, always=True)
     ts = TrainStep(eng, data, avg)
     ts.steps_per_graph = 4
     if mode == "rccl_three_graphs":
         ts.one_graph = False
+    S.torch.cuda.graph = RefusingGraph if mode == "rccl_fallback" else real_graph
     ts.capture()                     # step 1 (eager, RCCL communicator warm)
+    S.torch.cuda.graph = real_graph
     ts.step()                        # step 2: one replay
     ts.run(8)                        # steps 3-10: multi-step graph (one-graph modes)
     torch.cuda.synchronize()
     runs[mode] = {"state": state(eng), "one_graph": ts.one_graph, "dp": ts.avg is not None,
-                  "multi": ts.graph_multi is not None, "loss_acc": eng.loss_acc.cpu().clone()}
+                  "multi": ts.graph_multi is not None, "loss_acc": eng.loss_acc.cpu().clone(),
+                  "fallback": ts.fallback}
 names = ["data", "grad", "exp_avg", "exp_avg_sq", "step", "counter", "shadow"]
 res = {"backend": dist.get_backend(), "world": dist.get_world_size()}
 try:
@@ -272,9 +290,9 @@ except Exception as e:  # version query only
     res["nccl_version"] = repr(e)
 with open("/proc/self/maps") as f:
     res["rccl_libs"] = sorted({ln.split()[-1] for ln in f if "rccl" in ln.split()[-1]})
-for mode in ("rccl_one_graph", "rccl_three_graphs"):
+for mode in ("rccl_one_graph", "rccl_three_graphs", "rccl_fallback"):
     a, s = runs[mode], runs["single"]
-    res[mode] = {"one_graph": a["one_graph"], "dp": a["dp"], "multi": a["multi"],
+    res[mode] = {"one_graph": a["one_graph"], "dp": a["dp"], "multi": a["multi"], "fallback": a["fallback"],
                  "equal_single": all(torch.equal(x, y) for x, y in zip(a["state"], s["state"])),
                  "differs": [n for n, x, y in zip(names, a["state"], s["state"]) if not torch.equal(x, y)],
                  "loss_equal": bool(torch.equal(a["loss_acc"], s["loss_acc"]))}
@@ -299,3 +317,6 @@ def test_rccl_world1_dp_step_bitequal(tmp_path, precision):
     assert three["dp"] and not three["one_graph"], three
     assert one["equal_single"] and one["loss_equal"], one
     assert three["equal_single"] and three["loss_equal"], three
+    fb = res["rccl_fallback"]  # a refused capture falls back to the three-graph structure
+    assert fb["dp"] and not fb["one_graph"] and "simulated" in (fb["fallback"] or ""), fb
+    assert fb["equal_single"] and fb["loss_equal"], fb

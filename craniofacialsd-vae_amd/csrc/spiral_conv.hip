@@ -1078,16 +1078,12 @@ struct DxLatArgs {
 };
 template <int CIN, int COUT, int CTW>
 __global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, const DwLatArgs d) {
-  const int bid = (int)blockIdx.x, both = 2 * min(a.nb, d.nb);
-  bool is_dx;
-  int vb;
-  if (bid < both) {
-    is_dx = (bid & 1) == 0;
-    vb = bid >> 1;
-  } else {
-    is_dx = a.nb > d.nb;
-    vb = bid - both + both / 2;
-  }
+  // the data-gradient role first: it is the longer one, and the dW
+  // workgroups fill the slots its retiring waves free (alternating the
+  // roles: D1 27.4 vs 25.8 us, D0 24.2 vs 19.6 us, same box)
+  const int bid = (int)blockIdx.x;
+  const bool is_dx = bid < a.nb;
+  const int vb = is_dx ? bid : bid - a.nb;
   __shared__ float red[lat_red_floats(4)];
   if (is_dx)
     conv_dx_lat_body<CIN, COUT, CTW>(vb, a.nb, a.dpre, a.inv_ptr, a.inv_row, a.inv_head, a.w,
@@ -1195,16 +1191,12 @@ template <int CIN, int COUT>
 __global__ __launch_bounds__(256) void conv_bwd_rowsub_pair(const DgArgs a, const DwLatArgs d) {
   extern __shared__ float wl[];
   __shared__ float red[lat_red_floats(4)];
-  const int bid = blockIdx.x, both = 2 * min(a.nb, d.nb);
-  bool is_dg;
-  int vb;
-  if (bid < both) {
-    is_dg = (bid & 1) == 0;
-    vb = bid >> 1;
-  } else {
-    is_dg = a.nb > d.nb;
-    vb = bid - both + both / 2;
-  }
+  // the data-gradient role first: it is the longer one, and the dW
+  // workgroups fill the slots its retiring waves free (alternating the
+  // roles: D1 27.4 vs 25.8 us, D0 24.2 vs 19.6 us, same box)
+  const int bid = (int)blockIdx.x;
+  const bool is_dg = bid < a.nb;
+  const int vb = is_dg ? bid : bid - a.nb;
   if (is_dg)
     conv_dg_body<CIN, COUT>(vb, a.nb, a, wl);
   else

@@ -416,16 +416,12 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_dx_ks(co
 template <int CIN, int COUT, int NSG, int RT>
 __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_bwd_ks_pair(const DxKsArgs a, const DwLatArgs d,
                                                                               int nb_dx) {
-  const int bid = blockIdx.x, both = 2 * min(nb_dx, d.nb);
-  bool is_dx;
-  int vb;
-  if (bid < both) {
-    is_dx = (bid & 1) == 0;
-    vb = bid >> 1;
-  } else {
-    is_dx = nb_dx > d.nb;
-    vb = bid - both + both / 2;
-  }
+  // the data-gradient role first: it is the longer one, and the dW
+  // workgroups fill the slots its retiring waves free (alternating the
+  // roles: D1 27.4 vs 25.8 us, D0 24.2 vs 19.6 us, same box)
+  const int bid = (int)blockIdx.x;
+  const bool is_dx = bid < nb_dx;
+  const int vb = is_dx ? bid : bid - nb_dx;
   // one LDS array for both roles (the dW role's chunk-group sums alias the dx partials)
   __shared__ f32x4 part4[dx_ks_lds_f4<CIN, NSG, RT>()];
   static_assert(dx_ks_lds_f4<CIN, NSG, RT>() * 4 >= lat_red_floats(NSG), "dW chunk-group LDS");

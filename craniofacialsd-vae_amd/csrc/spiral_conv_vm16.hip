@@ -580,16 +580,10 @@ __global__ __launch_bounds__(DW16_THREADS, 2 * DW16_WAVES / 4) void conv_bwd_vm1
     const int4* __restrict__ flat, const bf16_t* __restrict__ w, const bf16_t* __restrict__ elu_y,
     bf16_t* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, int batch, int nb_dx, int nb_dw) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  const int bid = blockIdx.x, both = 2 * min(nb_dx, nb_dw);
-  bool is_dx;
-  int vb;
-  if (bid < both) {
-    is_dx = (bid & 1) == 0;
-    vb = bid >> 1;
-  } else {
-    is_dx = nb_dx > nb_dw;
-    vb = bid - both + both / 2;
-  }
+  // the data-gradient role first (see conv_bwd_lat_pair)
+  const int bid = (int)blockIdx.x;
+  const bool is_dx = bid < nb_dx;
+  const int vb = is_dx ? bid : bid - nb_dx;
   if (is_dx)
     dx_flat_vm16_body<32, 32, bf16_t, FW, DW16_WAVES>(dpre, flat, w, elu_y, dx, vsrc, rows, batch, vb, nb_dx,
                                                       reinterpret_cast<bf16_t*>(lds_raw));
@@ -645,16 +639,10 @@ __global__ __launch_bounds__(DW16_THREADS, 2 * DW16_WAVES / 4) void conv_bwd_row
     const int4* __restrict__ flat, const float* __restrict__ w, const bf16_t* __restrict__ elu_y,
     bf16_t* __restrict__ dx, float* __restrict__ ws, int vsrc, int rows, int batch, int nb_dx, int nb_dw) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  const int bid = blockIdx.x, both = 2 * min(nb_dx, nb_dw);
-  bool is_dx;
-  int vb;
-  if (bid < both) {
-    is_dx = (bid & 1) == 0;
-    vb = bid >> 1;
-  } else {
-    is_dx = nb_dx > nb_dw;
-    vb = bid - both + both / 2;
-  }
+  // the data-gradient role first (see conv_bwd_lat_pair)
+  const int bid = (int)blockIdx.x;
+  const bool is_dx = bid < nb_dx;
+  const int vb = is_dx ? bid : bid - nb_dx;
   if (is_dx)
     vm32::dx_flat_body<32, 32, FW, bf16_t, DW16_WAVES>(dpre, flat, w, elu_y, dx, vsrc, rows, batch, 0, 1, vb, nb_dx,
                                                        reinterpret_cast<float*>(lds_raw));

@@ -165,16 +165,10 @@ struct DxFlatArgs {
 template <int CIN, int COUT, int FW>
 __global__ __launch_bounds__(512) void conv_bwd_flat_pair(const DxFlatArgs a, const DwLatArgs d) {
   extern __shared__ float lwt[];
-  const int bid = blockIdx.x, both = 2 * min(a.nb, d.nb);
-  bool is_dx;
-  int vb;
-  if (bid < both) {
-    is_dx = (bid & 1) == 0;
-    vb = bid >> 1;
-  } else {
-    is_dx = a.nb > d.nb;
-    vb = bid - both + both / 2;
-  }
+  // the data-gradient role first (see conv_bwd_lat_pair)
+  const int bid = (int)blockIdx.x;
+  const bool is_dx = bid < a.nb;
+  const int vb = is_dx ? bid : bid - a.nb;
   if (is_dx)
     dx_flat_body<CIN, COUT, FW>(a.dpre, a.flat, a.w, a.elu_y, a.dx, a.vsrc, a.rows, a.batch, a.dpvm, a.dxvm, vb,
                                 a.nb, lwt);

@@ -916,6 +916,7 @@ static_assert(kBnSyncErr == CFSD_BN_SYNC_ERR, "cfsd.h documents the error word")
 constexpr int kBnDwRows = 4;  // encoder dW rows per E workgroup (x loaded once for all of them)
 constexpr int kBnWPer = kLinSplitN * kLinSplitK / 256;  // W-slice floats per thread of an A workgroup
 constexpr int kBnMaxParts = 80;                          // decoder-Linear partials (nd <= 80 x 64)
+constexpr int kBnWT = kLinSplitN + 4;  // row stride of the A role's transposed W slice (16-B aligned rows)
 
 __device__ __forceinline__ void bn_arrive(int* ctr) {
   __syncthreads();
@@ -950,11 +951,61 @@ __device__ __forceinline__ float bn_ld(const float* p) { return *p; }
 
 // dst[i * ds + c] = dh[i][c0 + c], c < nc (nc <= cup, inside one coarse vertex):
 // the transposed Pool's sequential fold of spmm_fold_prefetch (acc = acc +
-// x * v over the row's entries in order, contraction off)
-__device__ __forceinline__ void bn_fold_dh(const BneckArgs& a, int c0, int nc, float* dst, int ds) {
+// x * v over the row's entries in order, contraction off).
+// The row (one coarse vertex: workgroup-uniform) is read ONCE per wave -- lane
+// e holds entry e's column / value (bn_fold_row, issued before the caller
+// parks its own operands), read back by v_readlane -- so the x gathers of 16
+// entries at a time depend on that one load only.  The per-8-entry
+// column -> x round trips of the plain walk (up to 9 dependent trips for the
+// 29-entry rows at level 3) were the A role's critical path.
+constexpr int kBnFoldLanes = 64;  // longest row held in one wave's lanes (level 3: 29)
+constexpr int kBnFoldBatch = 16;  // x gathers in flight per thread
+struct BnRow {
+  int beg, n, col;
+  float val;
+};
+__device__ __forceinline__ BnRow bn_fold_row(const BneckArgs& a, int c0) {
+  const int v = c0 / a.cup;
+  BnRow r;
+  r.beg = a.up_ptr[v];
+  r.n = a.up_ptr[v + 1] - r.beg;
+  const int lane = threadIdx.x & 63;
+  const bool in = lane < r.n && r.n <= kBnFoldLanes;
+  r.col = in ? a.up_col[r.beg + lane] : 0;
+  r.val = in ? a.up_val[r.beg + lane] : 0.f;
+  return r;
+}
+__device__ __forceinline__ void bn_fold_dh(const BneckArgs& a, const BnRow& r, int c0, int nc, float* dst, int ds) {
 #pragma clang fp contract(off)
   const int v = c0 / a.cup, ch0 = c0 - v * a.cup, q4 = nc / 4;
-  const int beg = a.up_ptr[v], end = a.up_ptr[v + 1];
+  if (r.n <= kBnFoldLanes) {
+    for (int t = threadIdx.x; t < a.m * q4; t += blockDim.x) {
+      const int i = t / q4, q = t - i * q4;
+      const float* xb = a.g + (long)i * a.n_up * a.cup + ch0 + 4 * q;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int e0 = 0; e0 < r.n; e0 += kBnFoldBatch) {  // uniform
+        f32x4 xv[kBnFoldBatch];
+#pragma unroll
+        for (int j = 0; j < kBnFoldBatch; ++j) {
+          const int e = min(e0 + j, r.n - 1);
+          xv[j] = ld4(xb + (long)__builtin_amdgcn_readlane(r.col, e) * a.cup);
+        }
+#pragma unroll
+        for (int j = 0; j < kBnFoldBatch; ++j) {
+          if (e0 + j < r.n) {
+            const float vv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r.val), e0 + j));
+            acc.x = acc.x + xv[j].x * vv;
+            acc.y = acc.y + xv[j].y * vv;
+            acc.z = acc.z + xv[j].z * vv;
+            acc.w = acc.w + xv[j].w * vv;
+          }
+        }
+      }
+      st4(dst + i * ds + 4 * q, acc);
+    }
+    return;
+  }
+  const int beg = r.beg, end = r.beg + r.n;  // (rows longer than a wave: the plain walk)
   for (int t = threadIdx.x; t < a.m * q4; t += blockDim.x) {
     const int i = t / q4, q = t - i * q4;
     const float* xb = a.g + (long)i * a.n_up * a.cup + ch0 + 4 * q;
@@ -982,16 +1033,37 @@ __device__ __forceinline__ void bn_fold_dh(const BneckArgs& a, int c0, int nc, f
   }
 }
 
+#ifdef CFSD_BN_STAMPS
+// diagnostic build only (tools/kbench.py KB_BNSTAMPS): per-workgroup role,
+// start, two phase marks and end times (wall_clock64, 100 MHz)
+__device__ unsigned long long g_bn_stamps[4096 * 5];
+#define BN_T0 const unsigned long long bn_t0 = wall_clock64(); unsigned long long bn_t1 = bn_t0, bn_t2 = 0;
+#define BN_T1 bn_t1 = wall_clock64();
+#define BN_T2 bn_t2 = wall_clock64();
+#define BN_OUT(role) \
+  if (threadIdx.x == 0 && bid < 4096) { \
+    g_bn_stamps[5 * bid] = role; g_bn_stamps[5 * bid + 1] = bn_t0; g_bn_stamps[5 * bid + 2] = bn_t1; \
+    g_bn_stamps[5 * bid + 3] = bn_t2 ? bn_t2 : bn_t1; g_bn_stamps[5 * bid + 4] = wall_clock64(); }
+extern "C" int cfsd_debug_bn_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bn_stamps), sizeof(g_bn_stamps), 0, hipMemcpyDeviceToHost);
+}
+#else
+#define BN_T0
+#define BN_T1
+#define BN_T2
+#define BN_OUT(role)
+#endif
 __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
   extern __shared__ float bn_lds[];
   const int bid = blockIdx.x;
+  BN_T0
   const int b_lat = a.ndx_d, b_dwd = b_lat + a.nb_lat, b_enc = b_dwd + a.ndw_d;
   const int n_enc = a.ndx_e + a.ndw_x * a.ndw_g;
   const int m = a.m;
   if (bid < b_lat) {  // A: parts[bid][i][kk] = sum_{c in slice} dy[i][c] W_d[c][kk]
-    float* wl = bn_lds;                    // [64][kd]
-    float* dl = bn_lds + kLinSplitN * a.kd;  // [m][64]
-    const int c0 = bid * kLinSplitN, nc = min(kLinSplitN, a.nd - c0);
+    float* wt = bn_lds;                      // W slice transposed: [kd][kBnWT] (c contiguous)
+    float* dl = bn_lds + kBnWT * a.kd;       // [m][64]
+    const int c0 = bid * kLinSplitN, nc = kLinSplitN;  // (nd % 64 == 0: whole slices, host-checked)
     // the W slice's loads go out first and land while the dh fold's own
     // gathers are in flight (one memory round trip for both, not 3 + 2)
     const float* ws = a.wd + (long)c0 * a.kd;
@@ -1002,24 +1074,61 @@ __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
       const int e = j * 256 + (int)threadIdx.x;
       wv[j] = e < nw ? ws[e] : 0.f;
     }
-    bn_fold_dh(a, c0, nc, dl, kLinSplitN);
+    const BnRow row = bn_fold_row(a, c0);
+    // (the W slice is parked while the row's column / value loads land; its
+    // registers are free again before the gathers)
 #pragma unroll
     for (int j = 0; j < kBnWPer; ++j) {
       const int e = j * 256 + (int)threadIdx.x;
-      if (e < nw) wl[e] = wv[j];
+      if (e < nw) {
+        const int c = e / a.kd;
+        wt[(e - c * a.kd) * kBnWT + c] = wv[j];
+      }
     }
+    bn_fold_dh(a, row, c0, nc, dl, kLinSplitN);
     __syncthreads();
-    for (int e = threadIdx.x; e < m * a.kd; e += blockDim.x) {
-      const int i = e / a.kd, kk = e % a.kd;
-      float acc = 0.f;
-      for (int c = 0; c < nc; ++c) acc = fmaf(dl[i * kLinSplitN + c], wl[c * a.kd + kk], acc);
-      a.parts[(long)bid * a.pstride + e] = acc;
+    BN_T1
+    // register blocks of 4 meshes x 2 columns: per 4 terms c, four 16-B dl
+    // reads and two 16-B W reads feed 32 fmaf (one 64-term LDS chain per
+    // output with two 4-B reads per fmaf took ~5 us); per output the same
+    // fmaf chain over c ascending as linear_bwd_split_k
+    const int nkp = (a.kd + 1) / 2, nblk = ((m + 3) / 4) * nkp;
+    for (int t = threadIdx.x; t < nblk; t += blockDim.x) {
+      const int ib = t / nkp, kp = t - ib * nkp;
+      const int i0 = ib * 4, k0 = 2 * kp, k1 = min(k0 + 1, a.kd - 1);
+      float acc[4][2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = 0.f;
+#pragma unroll 2
+      for (int c = 0; c < kLinSplitN; c += 4) {
+        f32x4 d[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d[r] = ld4(dl + min(i0 + r, m - 1) * kLinSplitN + c);
+        const f32x4 w0 = ld4(wt + k0 * kBnWT + c), w1 = ld4(wt + k1 * kBnWT + c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            acc[r][0] = fmaf(d[r][q], w0[q], acc[r][0]);
+            acc[r][1] = fmaf(d[r][q], w1[q], acc[r][1]);
+          }
+      }
+      float* pp = a.parts + (long)bid * a.pstride;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (i0 + r < m) {
+          pp[(i0 + r) * a.kd + k0] = acc[r][0];
+          if (k0 + 1 < a.kd) pp[(i0 + r) * a.kd + k0 + 1] = acc[r][1];
+        }
     }
+    BN_T2
     bn_arrive(a.sync + kBnSyncA);
+    BN_OUT(0)
     return;
   }
   if (bid < b_dwd) {  // L: latent_bwd_k's per-element arithmetic, lat_rows whole dmulv rows per workgroup
     bn_wait(a.sync + kBnSyncA, a.ndx_d, a.sync + kBnSyncErr, 1);
+    BN_T1
     const int B = m, L = a.L;
     const int i = (bid - b_lat) * a.lat_rows + (int)threadIdx.x / L, l = (int)threadIdx.x % L;
     if ((int)threadIdx.x < a.lat_rows * L && i < B) {
@@ -1060,15 +1169,18 @@ __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
       for (int g = 0; g < kBnGroups && g < n_enc; ++g)
         __hip_atomic_store(a.sync + kBnSyncFlag + kBnSyncLine * g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    BN_OUT(1)
     return;
   }
   if (bid < b_enc) {  // D: dW_d / db_d rows c0 .. c0 + 15 (linear_bwd_split_k's dW body)
     float* xl = bn_lds;              // [m][kd]
     float* dl = bn_lds + m * a.kd;   // [m][16]
     const int c0 = (bid - b_dwd) * kLinDwRows, nc = min(kLinDwRows, a.nd - c0);
+    const BnRow row = bn_fold_row(a, c0);
     stage_lds(a.z, xl, m * a.kd);
-    bn_fold_dh(a, c0, nc, dl, kLinDwRows);
+    bn_fold_dh(a, row, c0, nc, dl, kLinDwRows);
     __syncthreads();
+    BN_T1
     for (int e = threadIdx.x; e < nc * a.kd; e += blockDim.x) {
       const int c = e / a.kd, kk = e % a.kd;
       float acc = 0.f;
@@ -1080,6 +1192,7 @@ __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
       for (int i = 0; i < m; ++i) acc += dl[i * kLinDwRows + c];
       a.dbd[c0 + c] = acc;
     }
+    BN_OUT(2)
     return;
   }
   // E: encoder Linear, operands loaded before the wait for dmulv
@@ -1100,6 +1213,7 @@ __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
 #pragma unroll
     for (int u = 0; u < kLinDxChunk; ++u) wv[u] = c0 + u < c1 ? a.we[(long)(c0 + u) * k + kc] : 0.f;
     bn_wait(a.sync + kBnSyncFlag + kBnSyncLine * (ej % kBnGroups), 1, a.sync + kBnSyncErr, 2);
+    BN_T1
     for (int e = threadIdx.x; e < mr * n; e += blockDim.x)
       ds[e] = bn_ld(a.xdmulv + (long)(i0 + e / n) * a.dstride + e % n);
     __syncthreads();
@@ -1129,6 +1243,7 @@ __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
 #pragma unroll
     for (int i = 0; i < kLinSplitM; ++i) xv[i] = (on && i < m) ? a.xe[(long)i * k + kk] : 0.f;
     bn_wait(a.sync + kBnSyncFlag + kBnSyncLine * (ej % kBnGroups), 1, a.sync + kBnSyncErr, 4);
+    BN_T1
     // the block's dmulv columns [m][8] in ONE round of vector loads (per-row
     // scalar loads were 8 dependent trips to memory: 40 us for this phase)
     float* dl = bn_lds;  // [m][kBnDwRows]
@@ -1154,6 +1269,7 @@ __global__ __launch_bounds__(256) void bottleneck_bwd_k(const BneckArgs a) {
       }
     }
   }
+  BN_OUT(ej < a.ndx_e ? 3 : 4)
   // the last E workgroup resets the counters for the next launch.  Counted in
   // two levels (8 group counters on their own cache lines, then one top
   // counter): 591 RMWs on ONE address serialise at its memory channel (the E
@@ -1683,7 +1799,7 @@ extern "C" int cfsd_bottleneck_bwd(const int32_t* up_ptr, const int32_t* up_col,
   a.ndw_g = (ne + kBnDwRows - 1) / kBnDwRows;
   a.sync = sync;
   const int nb = a.ndx_d + a.nb_lat + a.ndw_d + a.ndx_e + a.ndw_x * a.ndw_g;
-  size_t lds = (size_t)kLinSplitN * kd + (size_t)m * kLinSplitN;
+  size_t lds = (size_t)kBnWT * kd + (size_t)m * kLinSplitN;
   lds = std::max(lds, (size_t)m * kd + (size_t)m * kLinDwRows);
   lds = std::max(lds, (size_t)4 * ne + 16 * 64);
   lds = std::max(lds, (size_t)m * kBnDwRows);

@@ -381,6 +381,25 @@ def main():
                              "spmm_up0T", "e0_fwd", "e0_dw"]
     iters = int(os.environ.get("KB_ITERS", "50"))
     cases, names, b = build_cases(names)
+    if os.environ.get("KB_BNSTAMPS"):  # diagnostic library built with -DCFSD_BN_STAMPS
+        import ctypes
+        from craniofacialsd_vae_amd import _abi
+        for _ in range(5):
+            cases["bneck"]()
+        torch.cuda.synchronize()
+        buf = (ctypes.c_ulonglong * (4096 * 5))()
+        rc = _abi.lib().cfsd_debug_bn_stamps(buf)
+        st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 5).astype(np.int64)
+        st = st[st[:, 1] > 0]
+        t0 = st[:, 1].min()
+        print(f"bneck stamps rc {rc}: {len(st)} workgroups, span {(st[:, 4].max() - t0) / 100:.2f} us (100 MHz clock)")
+        for role, nm in enumerate(["A dz parts", "L latent", "D dW_d", "E dx", "E dW"]):
+            r = st[st[:, 0] == role]
+            if len(r) == 0:
+                continue
+            q = lambda c: np.percentile((r[:, c] - t0) / 100.0, [0, 50, 100])
+            print(f"  {nm:11s} n={len(r):4d}  start {q(1)}  mark1 {q(2)}  mark2 {q(3)}  end {q(4)}")
+        return
     if os.environ.get("KB_STAMPS"):
         for n in names:
             b.ws.zero_()

@@ -384,8 +384,9 @@ def main():
     if os.environ.get("KB_BNSTAMPS"):  # diagnostic library built with -DCFSD_BN_STAMPS
         import ctypes
         from craniofacialsd_vae_amd import _abi
+        bn_case = os.environ.get("KB_BNCASE", "bneck")
         for _ in range(5):
-            cases["bneck"]()
+            cases[bn_case]()
         torch.cuda.synchronize()
         buf = (ctypes.c_ulonglong * (4096 * 5))()
         rc = _abi.lib().cfsd_debug_bn_stamps(buf)

@@ -188,8 +188,13 @@ class SDVAEEngine:
         # fallback (shapes the fused kernels do not take) and as the bit-identity
         # references of the GPU tests.
         # the bottleneck backward (coarsest Pool(up)^T, decoder Linear, latent
-        # head, encoder Linear) as one launch (cfsd_bottleneck_bwd)
-        self.fuse_bottleneck = True
+        # head, encoder Linear) as one launch (cfsd_bottleneck_bwd).  Its
+        # workgroups wait on counters for lower-index workgroups, which is
+        # deadlock-free only while no OTHER such launch holds the device's
+        # slots: ranks sharing one GPU (CFSD_SHARE_DEVICE rehearsals) take the
+        # four bit-identical launches instead (a world-2 shared-device bench hit
+        # the kernel's timed-out-wait guard)
+        self.fuse_bottleneck = not os.environ.get("CFSD_SHARE_DEVICE")
         # the feature swap and the first Enblock's conv as one launch (cfsd_spiral_conv_fwd_in_swap)
         self.fuse_swap = True
         # vertex-major levels whose fp32 Deblock backward runs as one dx + dW launch

@@ -45,7 +45,10 @@ def _run(tmp_path, script, nproc, *args, env_extra=None, timeout=600):
     wfile = tmp_path / "worker.py"
     wfile.write_text(script)
     out = tmp_path / "res.json"
-    env = dict(os.environ, OMP_NUM_THREADS="1", **(env_extra or {}))
+    # (nproc > 1: every rank on the one test GPU -- the engine then avoids the
+    # spin-waiting one-launch bottleneck, whose forward progress needs the device to itself)
+    env = dict(os.environ, OMP_NUM_THREADS="1", **({"CFSD_SHARE_DEVICE": "1"} if nproc > 1 else {}),
+               **(env_extra or {}))
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(wfile), ROOT, str(out), *args]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)

@@ -97,7 +97,9 @@ def _run2(tmp_path, script, *args):
     wfile = tmp_path / "dp_worker.py"
     wfile.write_text(script)
     out = tmp_path / "res.json"
-    env = dict(os.environ, CFSD_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    # both ranks on the one test GPU (CFSD_SHARE_DEVICE: the engine then avoids the
+    # spin-waiting one-launch bottleneck, whose forward progress needs the device to itself)
+    env = dict(os.environ, CFSD_DIST_BACKEND="gloo", CFSD_SHARE_DEVICE="1", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(wfile), ROOT, str(out),
            *args]

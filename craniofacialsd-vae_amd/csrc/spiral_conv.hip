@@ -697,7 +697,7 @@ __global__ __launch_bounds__(256) void conv_fwd_lat(const float* __restrict__ x,
 // strided dwords per 4-chunk of o; W is L2-resident), in flight with A.
 // (body shared by the conv_dx_lat kernel and the dx half of
 // conv_bwd_lat_pair; vb / vnb = this workgroup's number / count in its grid)
-template <int CIN, int COUT, int CTW>
+template <int CIN, int COUT, int CTW, int DSB = kDxLatSb>
 __device__ __forceinline__ void conv_dx_lat_body(int vb, int vnb, const float* __restrict__ dpre,
                                                  const int* __restrict__ inv_ptr,
                                                  const int* __restrict__ inv_row,
@@ -707,7 +707,6 @@ __device__ __forceinline__ void conv_dx_lat_body(int vb, int vnb, const float* _
                                                  float* __restrict__ dx, int vsrc, int rows,
                                                  long total_rows) {
   constexpr int CH = COUT / 16, NCT = CIN / 16, K = kSeq * CIN, NTW = NCT / CTW;
-  constexpr int DSB = kDxLatSb;
   static_assert(kSeq % DSB == 0, "slot batches");
   static_assert(NCT % CTW == 0, "column tiles per wave");
   const int lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
@@ -1076,8 +1075,25 @@ struct DxLatArgs {
   long total_rows;
   int nb;
 };
+#ifdef CFSD_LAT_STAMPS
+// diagnostic build only (tools/kbench.py KB_LATSTAMPS): per-workgroup role, start, end
+__device__ unsigned long long g_lat_stamps[4096 * 3];
+extern "C" int cfsd_debug_lat_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lat_stamps), sizeof(g_lat_stamps), 0, hipMemcpyDeviceToHost);
+}
+#endif
+// The pair's data-gradient role gathers ONE slot per trip (the standalone
+// conv_dx_lat three): 94 VGPRs + 32 AGPRs instead of 162 + 32, so four waves
+// per SIMD fit and BOTH roles are resident from the start.  At 196 registers
+// (two waves per SIMD) D1's 533 dx workgroups alone filled the chip and its
+// 486 dW workgroups were dispatched only as dx ones retired (per-workgroup
+// stamps: dW starts 9.0-15.8 us, span 24.4 us); now every workgroup starts
+// by 0.6 us, span 22.6 us.  Same slot order: bit-identical.  D1 pair 25.9 ->
+// 24.1 us, step fp32 -1..-7 us, bf16 -3 us (profiles/round8j_*).
+constexpr int kPairDxSb = 1;
+constexpr int kPairMinWaves = 4;
 template <int CIN, int COUT, int CTW>
-__global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, const DwLatArgs d) {
+__global__ __launch_bounds__(256, kPairMinWaves) void conv_bwd_lat_pair(const DxLatArgs a, const DwLatArgs d) {
   // the data-gradient role first: it is the longer one, and the dW
   // workgroups fill the slots its retiring waves free (alternating the
   // roles: D1 27.4 vs 25.8 us, D0 24.2 vs 19.6 us, same box)
@@ -1085,12 +1101,23 @@ __global__ __launch_bounds__(256) void conv_bwd_lat_pair(const DxLatArgs a, cons
   const bool is_dx = bid < a.nb;
   const int vb = is_dx ? bid : bid - a.nb;
   __shared__ float red[lat_red_floats(4)];
+#ifdef CFSD_LAT_STAMPS
+  const unsigned long long t0 = wall_clock64();
+#endif
   if (is_dx)
-    conv_dx_lat_body<CIN, COUT, CTW>(vb, a.nb, a.dpre, a.inv_ptr, a.inv_row, a.inv_head, a.w,
-                                     a.elu_y, a.dx, a.vsrc, a.rows, a.total_rows);
+    conv_dx_lat_body<CIN, COUT, CTW, kPairDxSb>(vb, a.nb, a.dpre, a.inv_ptr, a.inv_row, a.inv_head, a.w,
+                                                a.elu_y, a.dx, a.vsrc, a.rows, a.total_rows);
   else
     conv_dw_lat_body<CIN, COUT>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows,
                                 d.total_rows, d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm, red);
+#ifdef CFSD_LAT_STAMPS
+  __syncthreads();
+  if (threadIdx.x == 0 && bid < 4096) {
+    g_lat_stamps[3 * bid] = is_dx ? 1 : 2;
+    g_lat_stamps[3 * bid + 1] = t0;
+    g_lat_stamps[3 * bid + 2] = wall_clock64();
+  }
+#endif
 }
 
 // ==========================================================================

@@ -381,6 +381,24 @@ def main():
                              "spmm_up0T", "e0_fwd", "e0_dw"]
     iters = int(os.environ.get("KB_ITERS", "50"))
     cases, names, b = build_cases(names)
+    if os.environ.get("KB_LATSTAMPS"):  # library built with -DCFSD_LAT_STAMPS: conv_bwd_lat_pair roles
+        import ctypes
+        from craniofacialsd_vae_amd import _abi
+        case = os.environ["KB_LATSTAMPS"]
+        for _ in range(5):
+            cases[case]()
+        torch.cuda.synchronize()
+        buf = (ctypes.c_ulonglong * (4096 * 3))()
+        rc = _abi.lib().cfsd_debug_lat_stamps(buf)
+        st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 3).astype(np.int64)
+        st = st[st[:, 0] > 0]
+        t0 = st[:, 1].min()
+        print(f"{case} lat-pair stamps rc {rc}: {len(st)} workgroups, span {(st[:, 2].max() - t0) / 100:.2f} us")
+        for role, nm in ((1, "dx"), (2, "dW")):
+            r = st[st[:, 0] == role]
+            q = lambda c: np.round(np.percentile((r[:, c] - t0) / 100.0, [0, 10, 50, 90, 100]), 2)
+            print(f"  {nm} n={len(r)}  start {q(1)}  end {q(2)}  dur p50 {np.median((r[:, 2] - r[:, 1]) / 100):.2f}")
+        return
     if os.environ.get("KB_BNSTAMPS"):  # diagnostic library built with -DCFSD_BN_STAMPS
         import ctypes
         from craniofacialsd_vae_amd import _abi

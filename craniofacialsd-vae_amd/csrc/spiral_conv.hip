@@ -2483,14 +2483,25 @@ int dw_mfma_slabs(int cin, int cout, int gx) {
 }
 
 constexpr int kDwLatWaves = 2048;
-// one wave per (dW unit, row chunk), ~2k waves (the few-row layers)
+// one wave per (dW unit, row chunk), ~2k waves (the few-row layers).
+// The 64 -> 64 few-tile layer (D0) pairs its dW slabs with the slot-group
+// dx (coarse::conv_bwd_ks_pair: 9-wave workgroups, ONE per CU at its 160
+// VGPRs), so its dW waves are sized to the CUs the dx role leaves: with
+// 2048 waves (252 workgroups + 134 dx) half the dW workgroups were
+// dispatched only as dx ones retired (stamps: starts up to 11.4 us, span
+// 17.9 us); sized to fit, every workgroup of the launch starts at once.
 DwGeom lat_geom(int batch, int rows, int cin, int cout) {
   DwGeom g{kDwLat, 0, 0, 0};
   const long M = (long)batch * rows;
   const long U = (long)dw_units(cin, cout);
-  constexpr int lat_waves = kDwLatWaves;
-  long R = (M * U / lat_waves + 15) / 16 * 16;
+  long R = (M * U / kDwLatWaves + 15) / 16 * 16;
   R = R < 32 ? 32 : (R > 512 ? 512 : R);
+  if (cin == 64 && cout == 64 && M < coarse::kMaxTilesFew * 16) {
+    // longer row chunks until the pair's dW workgroups (8 waves each, whole
+    // chunk groups) fit beside its dx workgroups (rows == dx rows there)
+    const long nb_dx = ((M + 15) / 16 + 1) / 2, free_wg = device_cus() - nb_dx;
+    while (R < 512 && (lat_tasks((int)((M + R - 1) / R), (int)U) + 7) / 8 > free_wg) R += 16;
+  }
   g.rchunk = (int)R;
   g.gx = (int)((M + R - 1) / R);
   g.ws_floats = (size_t)g.gx * U * 1024 + (size_t)g.gx * cout;

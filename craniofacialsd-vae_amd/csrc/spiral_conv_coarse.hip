@@ -413,9 +413,19 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_dx_ks(co
 // launch (they are independent and each alone leaves most of the chip idle):
 // workgroups alternate between the two halves while both last; the dW half
 // is conv_dw_lat_body with NSG waves per workgroup (same slabs, same values).
+#ifdef CFSD_LAT_STAMPS
+// diagnostic build only (tools/kbench.py KB_KSSTAMPS): per-workgroup role, start, end
+__device__ unsigned long long g_ks_stamps[4096 * 3];
+extern "C" int cfsd_debug_ks_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ks_stamps), sizeof(g_ks_stamps), 0, hipMemcpyDeviceToHost);
+}
+#endif
 template <int CIN, int COUT, int NSG, int RT>
 __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_bwd_ks_pair(const DxKsArgs a, const DwLatArgs d,
                                                                               int nb_dx) {
+#ifdef CFSD_LAT_STAMPS
+  const unsigned long long t0 = wall_clock64();
+#endif
   // the data-gradient role first: it is the longer one, and the dW
   // workgroups fill the slots its retiring waves free (alternating the
   // roles: D1 27.4 vs 25.8 us, D0 24.2 vs 19.6 us, same box)
@@ -430,6 +440,14 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_bwd_ks_p
   else
     conv_dw_lat_body<CIN, COUT, NSG>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows, d.total_rows,
                                      d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm, reinterpret_cast<float*>(part4));
+#ifdef CFSD_LAT_STAMPS
+  __syncthreads();
+  if (threadIdx.x == 0 && bid < 4096) {
+    g_ks_stamps[3 * bid] = is_dx ? 1 : 2;
+    g_ks_stamps[3 * bid + 1] = t0;
+    g_ks_stamps[3 * bid + 2] = wall_clock64();
+  }
+#endif
 }
 
 // ------------------------------------------------------------------ host side

@@ -389,7 +389,8 @@ def main():
             cases[case]()
         torch.cuda.synchronize()
         buf = (ctypes.c_ulonglong * (4096 * 3))()
-        rc = _abi.lib().cfsd_debug_lat_stamps(buf)
+        fn = os.environ.get("KB_STAMPFN", "cfsd_debug_lat_stamps")  # cfsd_debug_ks_stamps: the coarse ks pair
+        rc = getattr(_abi.lib(), fn)(buf)
         st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 3).astype(np.int64)
         st = st[st[:, 0] > 0]
         t0 = st[:, 1].min()

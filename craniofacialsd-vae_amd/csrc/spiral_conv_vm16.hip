@@ -574,6 +574,13 @@ __global__ __launch_bounds__(DW16_THREADS) void conv_dw_vm16(const bf16_t* __res
 // workgroups (12 waves) and weight-gradient workgroups (one unit in flight,
 // one slab each) interleaved; both fit 80 VGPRs, so a CU holds one of each
 // (as vm32::conv_bwd_vm_pair for fp32).  Same values as the two kernels.
+#ifdef CFSD_LAT_STAMPS
+// diagnostic build only (tools/kbench.py KB_STAMPFN=cfsd_debug_vm16_stamps): role, start, end
+__device__ unsigned long long g_vm16_stamps[4096 * 3];
+extern "C" int cfsd_debug_vm16_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_vm16_stamps), sizeof(g_vm16_stamps), 0, hipMemcpyDeviceToHost);
+}
+#endif
 template <int FW>
 __global__ __launch_bounds__(DW16_THREADS, 2 * DW16_WAVES / 4) void conv_bwd_vm16_pair(
     const bf16_t* __restrict__ x, const int* __restrict__ idx, const bf16_t* __restrict__ dpre,
@@ -584,11 +591,22 @@ __global__ __launch_bounds__(DW16_THREADS, 2 * DW16_WAVES / 4) void conv_bwd_vm1
   const int bid = (int)blockIdx.x;
   const bool is_dx = bid < nb_dx;
   const int vb = is_dx ? bid : bid - nb_dx;
+#ifdef CFSD_LAT_STAMPS
+  const unsigned long long t0 = wall_clock64();
+#endif
   if (is_dx)
     dx_flat_vm16_body<32, 32, bf16_t, FW, DW16_WAVES>(dpre, flat, w, elu_y, dx, vsrc, rows, batch, vb, nb_dx,
                                                       reinterpret_cast<bf16_t*>(lds_raw));
   else
     dw_vm16_body<bf16_t, 1>(x, idx, dpre, ws, vsrc, rows, batch, vb, nb_dw, lds_raw);
+#ifdef CFSD_LAT_STAMPS
+  __syncthreads();
+  if (threadIdx.x == 0 && bid < 4096) {
+    g_vm16_stamps[3 * bid] = is_dx ? 1 : 2;
+    g_vm16_stamps[3 * bid + 1] = t0;
+    g_vm16_stamps[3 * bid + 2] = wall_clock64();
+  }
+#endif
 }
 
 // ------------------------------------------------------------------ launchers

@@ -162,6 +162,13 @@ struct DxFlatArgs {
   float* dx;
   int vsrc, rows, batch, dpvm, dxvm, nb;
 };
+#ifdef CFSD_LAT_STAMPS
+// diagnostic build only (tools/kbench.py KB_STAMPFN=cfsd_debug_flat_stamps): role, start, end
+__device__ unsigned long long g_flat_stamps[4096 * 3];
+extern "C" int cfsd_debug_flat_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_flat_stamps), sizeof(g_flat_stamps), 0, hipMemcpyDeviceToHost);
+}
+#endif
 template <int CIN, int COUT, int FW>
 __global__ __launch_bounds__(512) void conv_bwd_flat_pair(const DxFlatArgs a, const DwLatArgs d) {
   extern __shared__ float lwt[];
@@ -169,12 +176,23 @@ __global__ __launch_bounds__(512) void conv_bwd_flat_pair(const DxFlatArgs a, co
   const int bid = (int)blockIdx.x;
   const bool is_dx = bid < a.nb;
   const int vb = is_dx ? bid : bid - a.nb;
+#ifdef CFSD_LAT_STAMPS
+  const unsigned long long t0 = wall_clock64();
+#endif
   if (is_dx)
     dx_flat_body<CIN, COUT, FW>(a.dpre, a.flat, a.w, a.elu_y, a.dx, a.vsrc, a.rows, a.batch, a.dpvm, a.dxvm, vb,
                                 a.nb, lwt);
   else
     conv_dw_lat_body<CIN, COUT, 8>(vb, d.nb, d.x, d.idx, d.dpre, d.ws, d.ws_db, d.vsrc, d.rows, d.total_rows,
                                    d.rchunk, d.n_chunks, d.batch, d.xvm, d.dpvm, lwt);  // lwt >= lat_red_floats(8)
+#ifdef CFSD_LAT_STAMPS
+  __syncthreads();
+  if (threadIdx.x == 0 && bid < 4096) {
+    g_flat_stamps[3 * bid] = is_dx ? 1 : 2;
+    g_flat_stamps[3 * bid + 1] = t0;
+    g_flat_stamps[3 * bid + 2] = wall_clock64();
+  }
+#endif
 }
 
 

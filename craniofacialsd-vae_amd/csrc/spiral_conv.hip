@@ -1363,13 +1363,13 @@ __device__ __forceinline__ void adam_at4(const DwAdam& a, const float* gp, const
 #define CFSD_RED_LOADS 8
 #endif
 constexpr int kRedLoads = CFSD_RED_LOADS;
-__global__ __launch_bounds__(1024, kRedLoads <= 8 ? 8 : 4) void dw_reduce_batch_k(const DwRedBatch B) {
+__device__ __forceinline__ void dw_reduce_batch_body(const DwRedBatch& B, const int vb) {
   const bool fuse = B.adam.p != nullptr;
-  if (fuse && (int)blockIdx.x >= B.blk_end) {  // Adam on the elements no item covers
+  if (fuse && vb >= B.blk_end) {  // Adam on the elements no item covers
     const DwAdam& a = B.adam;
     float step_size, sqrt_bc2;
     adam_consts(a, step_size, sqrt_bc2);
-    const int rb = (int)blockIdx.x - B.blk_end;
+    const int rb = vb - B.blk_end;
     int ri = 0;
     while (ri + 1 < a.n_rest && rb >= a.rest_blk0[ri + 1]) ++ri;
     const long base = a.rest_lo[ri] + (long)(rb - a.rest_blk0[ri]) * 4096;
@@ -1397,7 +1397,7 @@ __global__ __launch_bounds__(1024, kRedLoads <= 8 ? 8 : 4) void dw_reduce_batch_
     return;
   }
   int li = 0;
-  while (li + 1 < B.n && (int)blockIdx.x >= B.it[li + 1].blk0) ++li;
+  while (li + 1 < B.n && vb >= B.it[li + 1].blk0) ++li;
   const DwRedItem d = B.it[li];
   __shared__ f32x4 part[16][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1405,7 +1405,7 @@ __global__ __launch_bounds__(1024, kRedLoads <= 8 ? 8 : 4) void dw_reduce_batch_
   const int nw = d.n_el - d.cout;  // kind 0: dW part of a slab
   const bool vec = d.kind == 0;     // n_el, nw and cout are multiples of 4
   const int per_blk = vec ? 256 : 64;
-  int f = ((int)blockIdx.x - d.blk0) * per_blk + (vec ? 4 * lane : lane);
+  int f = (vb - d.blk0) * per_blk + (vec ? 4 * lane : lane);
   const bool valid = f < d.n_el;
   if (!valid) f = vec ? d.n_el - 4 : d.n_el - 1;
   const float* src;
@@ -1474,6 +1474,33 @@ __global__ __launch_bounds__(1024, kRedLoads <= 8 ? 8 : 4) void dw_reduce_batch_
       if (fuse) adam_at4(B.adam, dst, t, step_size, sqrt_bc2);
     }
   }
+}
+#ifdef CFSD_LAT_STAMPS
+// diagnostic build only (tools/kbench.py KB_STAMPFN=cfsd_debug_red_stamps): role (1 reduce, 2 Adam rest), start, end
+__device__ unsigned long long g_red_stamps[4096 * 3];
+extern "C" int cfsd_debug_red_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_red_stamps), sizeof(g_red_stamps), 0, hipMemcpyDeviceToHost);
+}
+#endif
+__global__ __launch_bounds__(1024, kRedLoads <= 8 ? 8 : 4) void dw_reduce_batch_k(const DwRedBatch B) {
+#ifdef CFSD_LAT_STAMPS
+  const unsigned long long t0 = wall_clock64();
+#endif
+  // the Adam-only workgroups (the elements no item covers: the Linears) are
+  // dispatched FIRST: the launch is 704 workgroups at two per CU, and as the
+  // last of the grid they waited ~7 us for slots the slab reductions held
+  // (role stamps, profiles/round8o_*), then ran their own trips at the end
+  const int nrest = (B.adam.p != nullptr) ? (int)gridDim.x - B.blk_end : 0;
+  const int vb = (int)blockIdx.x < nrest ? B.blk_end + (int)blockIdx.x : (int)blockIdx.x - nrest;
+  dw_reduce_batch_body(B, vb);
+#ifdef CFSD_LAT_STAMPS
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {
+    g_red_stamps[3 * blockIdx.x] = vb >= B.blk_end ? 2 : 1;
+    g_red_stamps[3 * blockIdx.x + 1] = t0;
+    g_red_stamps[3 * blockIdx.x + 2] = wall_clock64();
+  }
+#endif
 }
 
 // Backward weight, small input (CS <= 4; first Enblock): lane = output

@@ -333,6 +333,13 @@ struct DwVmArgs {
   float* ws_db;
   int nb;
 };
+#ifdef CFSD_LAT_STAMPS
+// diagnostic build only (tools/kbench.py KB_STAMPFN=cfsd_debug_vmp_stamps): role, start, end
+__device__ unsigned long long g_vmp_stamps[4096 * 3];
+extern "C" int cfsd_debug_vmp_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_vmp_stamps), sizeof(g_vmp_stamps), 0, hipMemcpyDeviceToHost);
+}
+#endif
 template <int FW>
 __global__ __launch_bounds__(DWV_THREADS, 2 * DWV_WAVES / 4) void conv_bwd_vm_pair(const DxFlatArgs a,
                                                                                 const DwVmArgs d) {
@@ -347,11 +354,22 @@ __global__ __launch_bounds__(DWV_THREADS, 2 * DWV_WAVES / 4) void conv_bwd_vm_pa
     is_dx = a.nb > d.nb;
     vb = bid - both + both / 2;
   }
+#ifdef CFSD_LAT_STAMPS
+  const unsigned long long t0 = wall_clock64();
+#endif
   if (is_dx)
     dx_flat_body<32, 32, FW, float, DWV_WAVES>(a.dpre, a.flat, a.w, a.elu_y, a.dx, a.vsrc, a.rows, a.batch, 1, 1,
                                                vb, a.nb, lds);
   else
     dw_vm32_body<0>(d.x, d.idx, a.dpre, d.ws, d.ws_db, a.vsrc, a.rows, a.batch, vb, d.nb, lds);
+#ifdef CFSD_LAT_STAMPS
+  __syncthreads();
+  if (threadIdx.x == 0 && bid < 4096) {
+    g_vmp_stamps[3 * bid] = is_dx ? 1 : 2;
+    g_vmp_stamps[3 * bid + 1] = t0;
+    g_vmp_stamps[3 * bid + 2] = wall_clock64();
+  }
+#endif
 }
 
 

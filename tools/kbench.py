@@ -285,6 +285,10 @@ def build_cases(names=()):
                                                                out=v.g_dec_up[2])
     cases["dw_d2_vm"] = lambda: ops.spiral_conv_bwd_weight_x(v.dec_up[2], T.spiral[1], v.dpre_dec[2], None, None,
                                                              v.ws_dw[("dec", 2)])
+    # the fp32 step's D2 backward: flat dx + vm32 dW slabs in one launch (conv_bwd_vm_pair)
+    cases["pair_d2_vm"] = lambda: ops.spiral_conv_bwd_flat_pair(v.dec_up[2], T.spiral[1], v.dpre_dec[2],
+                                                                T.spiral_flat[1], w2v, None, None, v.g_dec_up[2],
+                                                                workspace=v.ws_dw[("dec", 2)])
     wov, bov = ev.params.view("de_layers.5.layer.weight"), ev.params.view("de_layers.5.layer.bias")
     cases["dout_fwd_vm"] = lambda: ops.spiral_conv_fwd_x(v.dec_out[3], T.spiral[0], wov, None, bov, 0, v.out)
     cases["dout_bwd_vm"] = lambda: ops.spiral_conv_bwd_x(v.dec_out[3], T.spiral[0], v.dout, T.spiral_inv[0], wov,

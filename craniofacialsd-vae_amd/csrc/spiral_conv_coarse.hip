@@ -159,8 +159,21 @@ __global__ __launch_bounds__(64 * NSG, ks_min_waves(NSG, RT)) void conv_fwd_ks(c
 // row -- the 3 coarse columns / values of every spiral neighbour, a static
 // table) is in flight during this tile's MFMAs and its gathers during this
 // tile's combine; partials double-buffered in LDS (one barrier per tile).
+#ifdef CFSD_LAT_STAMPS
+// diagnostic build only (tools/kbench.py KB_PTSTAMPS): per-workgroup phases of conv_fwd_pt's first tile
+__device__ unsigned long long g_pt_stamps[2048 * 6];
+extern "C" int cfsd_debug_pt_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pt_stamps), sizeof(g_pt_stamps), 0, hipMemcpyDeviceToHost);
+}
+#define PT_T(v) v = wall_clock64();
+#else
+#define PT_T(v)
+#endif
 template <int CIN, int COUT, int UP>
 __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
+#ifdef CFSD_LAT_STAMPS
+  unsigned long long pt0 = wall_clock64(), pt1 = 0, pt2 = 0, pt3 = 0, pt4 = 0;
+#endif
   constexpr int CH = CIN / 16, NCT = COUT / 16, K = kSeq * CIN, LDC = COUT + 4;
   constexpr int PB = 9 * 16 * LDC;  // floats per partial buffer
   __shared__ f32x4 part4[2 * PB / 4];
@@ -178,6 +191,10 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
   for (int c = 0; c < CH; ++c)
 #pragma unroll
     for (int t = 0; t < NCT; ++t) bw[c][t] = ld4(wb + (long)t * 16 * K + 16 * c);
+#ifdef CFSD_LAT_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PT_T(pt1)
+#endif
   // per tile: this lane's mesh b and spiral neighbour (UP: its 3 taps)
   struct Src {
     int b, v;
@@ -218,8 +235,16 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
   if (t0 >= t1) return;  // (grid <= tiles: never taken)
   Src cur;
   load_src(t0, cur);
+#ifdef CFSD_LAT_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PT_T(pt2)
+#endif
   f32x4 av[CH];
   load_x(cur, av);
+#ifdef CFSD_LAT_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PT_T(pt3)
+#endif
   for (long tile = t0; tile < t1; ++tile) {
     const bool more = tile + 1 < t1;  // uniform
     Src nxt;
@@ -279,7 +304,16 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
       st4(a.y + yo * COUT + 4 * c4, v);
     }
     cur = nxt;
+#ifdef CFSD_LAT_STAMPS
+    if (tile == t0) PT_T(pt4)
+#endif
   }
+#ifdef CFSD_LAT_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 2048) {
+    unsigned long long* o = g_pt_stamps + 6 * blockIdx.x;
+    o[0] = pt0; o[1] = pt1; o[2] = pt2; o[3] = pt3; o[4] = pt4; o[5] = wall_clock64();
+  }
+#endif
 }
 
 // Backward data, same geometry: a workgroup owns RT 16-row tiles of SOURCE

@@ -385,6 +385,22 @@ def main():
                              "spmm_up0T", "e0_fwd", "e0_dw"]
     iters = int(os.environ.get("KB_ITERS", "50"))
     cases, names, b = build_cases(names)
+    if os.environ.get("KB_PTSTAMPS"):  # -DCFSD_LAT_STAMPS build: conv_fwd_pt first-tile phases (wave 0)
+        import ctypes
+        from craniofacialsd_vae_amd import _abi
+        case = os.environ["KB_PTSTAMPS"]
+        for _ in range(5):
+            cases[case]()
+        torch.cuda.synchronize()
+        buf = (ctypes.c_ulonglong * (2048 * 6))()
+        rc = _abi.lib().cfsd_debug_pt_stamps(buf)
+        st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 6).astype(np.int64)
+        st = st[st[:, 0] > 0]
+        t0 = st[:, 0].min()
+        print(f"{case} conv_fwd_pt stamps rc {rc}: {len(st)} workgroups (us from the first start; min p10 p50 p90 max)")
+        for c, nm in enumerate(["start", "W slice in", "tables in", "x taps in", "tile 1 done", "end"]):
+            print(f"  {nm:12s} {np.round(np.percentile((st[:, c] - t0) / 100.0, [0, 10, 50, 90, 100]), 2)}")
+        return
     if os.environ.get("KB_LATSTAMPS"):  # library built with -DCFSD_LAT_STAMPS: conv_bwd_lat_pair roles
         import ctypes
         from craniofacialsd_vae_amd import _abi

@@ -182,7 +182,17 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const long M = a.total_rows, n_rt = (M + 15) / 16;
   const int nb = gridDim.x, blk = xcd_block();
-  const long t0 = n_rt * blk / nb, t1 = n_rt * (blk + 1) / nb;
+  // every workgroup walks `full` whole tiles; the rem leftover tiles are cut
+  // into S column groups of NCT / S column tiles each (S the largest split
+  // with rem * S <= nb), at most one such unit per workgroup: the launch's
+  // tail is a fraction of a tile's MFMAs instead of a whole extra tile
+  const long full = n_rt / nb, rem = n_rt - full * nb;
+  int S = NCT;
+  while (S > 1 && rem * S > nb) S >>= 1;
+  const long t0 = full * blk;
+  const long nitems = full + (blk < rem * S ? 1 : 0);
+  const int cw = NCT / S, clo_last = (blk % S) * cw;  // the unit's column tiles
+  auto item_tile = [&](long i) { return i < full ? t0 + i : full * nb + blk / S; };
   const int nv_x = UP ? a.n_coarse : a.vsrc;
   const Lay lx = make_lay(a.xvm, a.batch, nv_x);
   f32x4 bw[CH][NCT];
@@ -232,9 +242,9 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
       for (int c = 0; c < CH; ++c) av[c] = ld4(xb + (long)sr.v * lx.vs * CIN + 16 * c);
     }
   };
-  if (t0 >= t1) return;  // (grid <= tiles: never taken)
+  if (nitems == 0) return;  // (grid <= tiles: never taken)
   Src cur;
-  load_src(t0, cur);
+  load_src(item_tile(0), cur);
 #ifdef CFSD_LAT_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PT_T(pt2)
@@ -245,26 +255,43 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PT_T(pt3)
 #endif
-  for (long tile = t0; tile < t1; ++tile) {
-    const bool more = tile + 1 < t1;  // uniform
+  for (long it = 0; it < nitems; ++it) {
+    const long tile = item_tile(it);
+    const bool whole = it < full;  // uniform
+    const int clo = whole ? 0 : clo_last, chi = whole ? NCT : clo_last + cw;
+    const bool more = it + 1 < nitems;  // uniform
     Src nxt;
-    if (more) load_src(tile + 1, nxt);
+    if (more) load_src(item_tile(it + 1), nxt);
     f32x4 acc[NCT];
 #pragma unroll
     for (int t = 0; t < NCT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (whole) {
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
+      for (int c = 0; c < CH; ++c) {
 #pragma unroll
-      for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].x, bw[c][t].x, acc[t]);
+        for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].x, bw[c][t].x, acc[t]);
 #pragma unroll
-      for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].y, bw[c][t].y, acc[t]);
+        for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].y, bw[c][t].y, acc[t]);
 #pragma unroll
-      for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].z, bw[c][t].z, acc[t]);
+        for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].z, bw[c][t].z, acc[t]);
 #pragma unroll
-      for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].w, bw[c][t].w, acc[t]);
+        for (int t = 0; t < NCT; ++t) acc[t] = mfma16(av[c].w, bw[c][t].w, acc[t]);
+      }
+    } else {  // a leftover unit: the same per-column chains, its columns only
+#pragma unroll
+      for (int t = 0; t < NCT; ++t)
+        if (t >= clo && t < chi) {
+#pragma unroll
+          for (int c = 0; c < CH; ++c) {
+            acc[t] = mfma16(av[c].x, bw[c][t].x, acc[t]);
+            acc[t] = mfma16(av[c].y, bw[c][t].y, acc[t]);
+            acc[t] = mfma16(av[c].z, bw[c][t].z, acc[t]);
+            acc[t] = mfma16(av[c].w, bw[c][t].w, acc[t]);
+          }
+        }
     }
     if constexpr (UP) {  // slot 0 = the vertex itself: the tile's up-sampled rows
-      if (g == 0 && a.yup) {
+      if (g == 0 && a.yup && clo == 0) {
         const long m = tile * 16 + r16;
         if (m < M) {
 #pragma unroll
@@ -272,17 +299,18 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
         }
       }
     }
-    float* pb = part + ((tile - t0) & 1) * PB;
+    float* pb = part + (it & 1) * PB;
 #pragma unroll
     for (int t = 0; t < NCT; ++t)
+      if (t >= clo && t < chi)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) pb[(g * 16 + 4 * kg + rr) * LDC + t * 16 + r16] = acc[t][rr];
+        for (int rr = 0; rr < 4; ++rr) pb[(g * 16 + 4 * kg + rr) * LDC + t * 16 + r16] = acc[t][rr];
     if (more) load_x(nxt, av);  // next tile's gathers in flight during the combine
     __syncthreads();
     const f32x4* pb4 = reinterpret_cast<const f32x4*>(pb);
-    constexpr int N4 = 16 * COUT / 4;
+    const int lg = __builtin_ctz((chi - clo) * 4), N4 = 16 << lg;  // (column tiles: a power of two)
     for (int q = threadIdx.x; q < N4; q += 576) {
-      const int row = q / (COUT / 4), c4 = q % (COUT / 4);
+      const int row = q >> lg, c4 = clo * 4 + (q & ((1 << lg) - 1));
       const long m = tile * 16 + row;
       if (m >= M) continue;
       f32x4 v = pb4[row * (LDC / 4) + c4];
@@ -305,7 +333,7 @@ __global__ __launch_bounds__(576, 3) void conv_fwd_pt(const FwdKsArgs a) {
     }
     cur = nxt;
 #ifdef CFSD_LAT_STAMPS
-    if (tile == t0) PT_T(pt4)
+    if (it == 0) PT_T(pt4)
 #endif
   }
 #ifdef CFSD_LAT_STAMPS
